@@ -1,0 +1,145 @@
+"""ctypes mirror of include/flinkwin.h (the C-ABI of libflinkwin).
+
+Only plain data types live here so both the product bindings (flink_amd._native) and the
+test-side oracle wrapper can build the same ``fw_config`` structure.
+"""
+import ctypes as C
+
+FW_ABI_VERSION = 1
+FW_MAX_AGGS = 8
+FW_MAX_COLS = 8
+
+FW_OK = 0
+FW_E_INVALID = -1
+FW_E_DEVICE = -2
+FW_E_CAPACITY = -3
+FW_E_STATE = -4
+FW_E_NOMEM = -5
+
+# fw_api_kind
+API_SQL = 0
+API_DATASTREAM = 1
+# fw_window_kind
+WIN_TUMBLE = 0
+WIN_HOP = 1
+WIN_CUMULATE = 2
+# fw_agg_kind
+AGG_COUNT_STAR = 0
+AGG_COUNT = 1
+AGG_SUM = 2
+AGG_MIN = 3
+AGG_MAX = 4
+AGG_AVG = 5
+# fw_value_type
+T_I64 = 0
+T_F64 = 1
+T_I32 = 2
+# fw_key_hash_kind
+KEYHASH_LONG = 0
+KEYHASH_INT = 1
+KEYHASH_BINROW_BIGINT = 2
+KEYHASH_BINROW_INT = 3
+KEYHASH_PRECOMPUTED = 4
+
+AGG_NAMES = {"COUNT_STAR": AGG_COUNT_STAR, "COUNT": AGG_COUNT, "SUM": AGG_SUM,
+             "MIN": AGG_MIN, "MAX": AGG_MAX, "AVG": AGG_AVG}
+TYPE_NAMES = {"BIGINT": T_I64, "DOUBLE": T_F64, "INT": T_I32}
+WINDOW_NAMES = {"TUMBLE": WIN_TUMBLE, "HOP": WIN_HOP, "CUMULATE": WIN_CUMULATE}
+
+
+class fw_agg_desc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("input_col", C.c_int32), ("type", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class fw_config(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32),
+        ("api", C.c_int32),
+        ("window_kind", C.c_int32),
+        ("key_hash", C.c_int32),
+        ("size_ms", C.c_int64),
+        ("slide_ms", C.c_int64),
+        ("offset_ms", C.c_int64),
+        ("n_aggs", C.c_int32),
+        ("count_star_index", C.c_int32),
+        ("aggs", fw_agg_desc * FW_MAX_AGGS),
+        ("n_value_cols", C.c_int32),
+        ("value_col_types", C.c_int32 * FW_MAX_COLS),
+        ("max_parallelism", C.c_int32),
+        ("parallelism", C.c_int32),
+        ("subtask_index", C.c_int32),
+        ("device", C.c_int32),
+        ("state_capacity", C.c_int64),
+        ("max_batch_rows", C.c_int64),
+        ("output_capacity", C.c_int64),
+    ]
+
+
+class fw_host_cols(C.Structure):
+    _fields_ = [("key", C.POINTER(C.c_int64)), ("ts", C.POINTER(C.c_int64)),
+                ("key_hash", C.POINTER(C.c_int32)),
+                ("values", C.POINTER(C.c_int64) * FW_MAX_COLS)]
+
+
+class fw_result(C.Structure):
+    _fields_ = [("n", C.c_int64), ("key", C.POINTER(C.c_int64)),
+                ("window_start", C.POINTER(C.c_int64)), ("window_end", C.POINTER(C.c_int64)),
+                ("values", C.POINTER(C.c_int64) * FW_MAX_AGGS),
+                ("null_mask", C.POINTER(C.c_uint32))]
+
+
+class fw_stats(C.Structure):
+    _fields_ = [("current_watermark", C.c_int64), ("next_trigger_progress", C.c_int64),
+                ("num_late_records_dropped", C.c_int64), ("live_state_entries", C.c_int64),
+                ("pending_rows", C.c_int64), ("results_available", C.c_int64),
+                ("num_fired_windows", C.c_int64), ("error_flags", C.c_int32),
+                ("num_superbuckets", C.c_int32)]
+
+
+class fw_gen_params(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("t0_ms", C.c_int64), ("rate_per_s", C.c_int64),
+                ("ooo_ms", C.c_int64), ("key_base", C.c_int64), ("key_count", C.c_int64),
+                ("key_dist", C.c_int32), ("value_kind", C.c_int32),
+                ("zipf_cdf", C.c_void_p)]
+
+
+def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, offset_ms=0,
+                aggs=(), count_star_index=-1, value_col_types=(), key_hash=KEYHASH_BINROW_BIGINT,
+                max_parallelism=128, parallelism=1, subtask_index=0, device=0,
+                state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22):
+    """Build an fw_config.  ``aggs`` is a sequence of (kind, input_col, type)."""
+    if len(aggs) > FW_MAX_AGGS or len(value_col_types) > FW_MAX_COLS:
+        raise ValueError("too many aggregates or value columns")
+    c = fw_config()
+    c.abi_version = FW_ABI_VERSION
+    c.api = api
+    c.window_kind = window_kind
+    c.key_hash = key_hash
+    c.size_ms = size_ms
+    c.slide_ms = slide_ms
+    c.offset_ms = offset_ms
+    c.n_aggs = len(aggs)
+    c.count_star_index = count_star_index
+    for i, (kind, col, typ) in enumerate(aggs):
+        c.aggs[i].kind = kind
+        c.aggs[i].input_col = col
+        c.aggs[i].type = typ
+    c.n_value_cols = len(value_col_types)
+    for i, t in enumerate(value_col_types):
+        c.value_col_types[i] = t
+    c.max_parallelism = max_parallelism
+    c.parallelism = parallelism
+    c.subtask_index = subtask_index
+    c.device = device
+    c.state_capacity = state_capacity
+    c.max_batch_rows = max_batch_rows
+    c.output_capacity = output_capacity
+    return c
+
+
+def result_is_double(kind, typ):
+    """Whether an aggregate's SQL/DataStream result column is DOUBLE."""
+    if kind in (AGG_COUNT_STAR, AGG_COUNT):
+        return False
+    return typ == T_F64

@@ -1,0 +1,245 @@
+/*
+ * flinkwin.h -- C-ABI of libflinkwin, the MI355X-native windowed keyed-aggregation
+ * operator core that sits behind Flink's own window-operator seams.
+ *
+ * One fw_handle == one operator subtask (one Flink WindowAggOperator / WindowOperator
+ * instance).  All calls on a handle must come from one thread (Flink's mailbox thread,
+ * flink-runtime/.../tasks/mailbox/MailboxProcessor.java:58-91).  Every entry point
+ * returns 0 on success and a negative FW_E_* code on failure; the message is then
+ * available from fw_last_error() (thread-local).  No torch / HIP types appear here:
+ * device buffers are plain pointers, streams are opaque void*.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the Flink tree,
+ * TR = flink-table/flink-table-runtime/src/main/java/org/apache/flink/table/runtime,
+ * FR = flink-runtime/src/main/java/org/apache/flink):
+ *
+ *   fw_create        SlicingSyncStateWindowProcessor construction in
+ *                    WindowAggOperatorBuilder.buildSlicingWindowProcessor
+ *                    (TR/operators/aggregate/window/WindowAggOperatorBuilder.java:220-260)
+ *                    + WindowProcessor.open (TR/operators/window/tvf/common/WindowProcessor.java:42);
+ *                    DataStream: WindowOperatorBuilder.buildWindowOperator
+ *                    (FR/streaming/runtime/operators/windowing/WindowOperatorBuilder.java:432-446)
+ *   fw_initialize_watermark
+ *                    WindowProcessor.initializeWatermark (WindowProcessor.java:48) /
+ *                    InternalTimerServiceImpl.initializeWatermark
+ *   fw_reserve/fw_commit, fw_push_device
+ *                    SyncStateWindowProcessor.processElement(key,row) -> dropped
+ *                    (TR/operators/window/tvf/common/SyncStateWindowProcessor.java:37),
+ *                    i.e. AbstractSliceSyncStateWindowAggProcessor.processElement :96-126
+ *                    + RecordsWindowBuffer.addElement :81; DataStream WindowOperator.processElement
+ *                    (FR/.../windowing/WindowOperator.java:293-447). Batched: one call per
+ *                    columnar batch buffered between watermarks.
+ *   fw_advance       WindowAggOperator.processWatermark (TR/.../tvf/common/WindowAggOperator.java:227)
+ *                    = advanceProgress (flush, AbstractSliceSyncStateWindowAggProcessor.java:139)
+ *                    + InternalTimerServiceImpl.tryAdvanceWatermark (FR/streaming/api/operators/
+ *                    InternalTimerServiceImpl.java:328) -> onTimer -> fireWindow/clearWindow.
+ *                    Results for W are produced before the call returns (the caller forwards W
+ *                    afterwards, AbstractStreamOperator.java:700-702).
+ *   fw_flush         prepareCheckpoint (WindowAggOperator.prepareSnapshotPreBarrier :268 ->
+ *                    AbstractSliceSyncStateWindowAggProcessor.prepareCheckpoint :156)
+ *   fw_snapshot/fw_restore
+ *                    keyed-state + timer snapshot of the operator (HeapSnapshotStrategy /
+ *                    InternalTimerServiceImpl.snapshotTimersForKeyGroup :360) and the union-list
+ *                    watermark state (WindowAggOperator.java:183-206)
+ *   fw_get_stats     numLateRecordsDropped (WindowAggOperator.java:101,164; WindowOperator.java:144)
+ *   fw_assign_key_groups
+ *                    KeyGroupRangeAssignment.assignToKeyGroup / computeOperatorIndexForKeyGroup
+ *                    (FR/runtime/state/KeyGroupRangeAssignment.java:63-127) as used by
+ *                    KeyGroupStreamPartitioner.selectChannel (FR/streaming/runtime/partitioner/
+ *                    KeyGroupStreamPartitioner.java:55-65)
+ *   fw_partition_by_dest
+ *                    the keyBy exchange's record routing (ChannelSelectorRecordWriter.emit,
+ *                    FR/runtime/io/network/api/writer/ChannelSelectorRecordWriter.java:54): rows
+ *                    bucketed per destination subtask, ready for an RCCL all-to-all.
+ */
+#ifndef FLINKWIN_H_
+#define FLINKWIN_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FW_ABI_VERSION 1
+#define FW_MAX_AGGS 8
+#define FW_MAX_COLS 8
+
+/* ---- error codes ---------------------------------------------------------------- */
+#define FW_OK 0
+#define FW_E_INVALID (-1)       /* bad argument / unsupported configuration            */
+#define FW_E_DEVICE (-2)        /* HIP runtime error                                    */
+#define FW_E_CAPACITY (-3)      /* a device table / buffer capacity was exceeded        */
+#define FW_E_STATE (-4)         /* call not allowed in the current state               */
+#define FW_E_NOMEM (-5)
+
+/* ---- configuration ----------------------------------------------------------------- */
+typedef enum {
+    FW_API_SQL = 0,         /* Table/SQL slicing WindowAggOperator (window TVF aggregate) */
+    FW_API_DATASTREAM = 1   /* DataStream WindowOperator + EventTimeTrigger, lateness 0  */
+} fw_api_kind;
+
+typedef enum {
+    FW_WIN_TUMBLE = 0,      /* SQL TUMBLE / DataStream TumblingEventTimeWindows         */
+    FW_WIN_HOP = 1,         /* SQL HOP / DataStream SlidingEventTimeWindows (size%slide==0) */
+    FW_WIN_CUMULATE = 2     /* SQL CUMULATE                                             */
+} fw_window_kind;
+
+typedef enum {
+    FW_AGG_COUNT_STAR = 0,  /* COUNT(*)            Count1AggFunction                    */
+    FW_AGG_COUNT = 1,       /* COUNT(col)          CountAggFunction (non-null inputs)   */
+    FW_AGG_SUM = 2,         /* SUM(col)            SumAggFunction / SumAggregator        */
+    FW_AGG_MIN = 3,         /* MIN(col)            MinAggFunction / ComparableAggregator */
+    FW_AGG_MAX = 4,         /* MAX(col)            MaxAggFunction / ComparableAggregator */
+    FW_AGG_AVG = 5          /* AVG(col)            AvgAggFunction                        */
+} fw_agg_kind;
+
+typedef enum {
+    FW_T_I64 = 0,           /* BIGINT / long                                            */
+    FW_T_F64 = 1,           /* DOUBLE / double (values passed as IEEE-754 bits)          */
+    FW_T_I32 = 2            /* INT / int, passed sign-extended in an int64 column; SUM
+                               wraps at 32 bits, AVG result is INT                      */
+} fw_value_type;
+
+typedef enum {
+    FW_KEYHASH_LONG = 0,         /* DataStream Long key: Long.hashCode = (int)(v ^ v>>>32)      */
+    FW_KEYHASH_INT = 1,          /* DataStream Integer key: Integer.hashCode = v                */
+    FW_KEYHASH_BINROW_BIGINT = 2,/* SQL key row (BIGINT): BinaryRowData.hashCode, 16-byte row  */
+    FW_KEYHASH_BINROW_INT = 3,   /* SQL key row (INT):    BinaryRowData.hashCode, 16-byte row   */
+    FW_KEYHASH_PRECOMPUTED = 4   /* key column holds an opaque id; the Java hashCode of the real
+                                    key is passed in the key_hash column (VARCHAR, composite)   */
+} fw_key_hash_kind;
+
+typedef struct {
+    int32_t kind;        /* fw_agg_kind                                   */
+    int32_t input_col;   /* value column index (ignored for COUNT_STAR)   */
+    int32_t type;        /* fw_value_type of the input column             */
+    int32_t reserved;
+} fw_agg_desc;
+
+typedef struct {
+    int32_t abi_version;      /* must be FW_ABI_VERSION                                    */
+    int32_t api;              /* fw_api_kind                                               */
+    int32_t window_kind;      /* fw_window_kind                                            */
+    int32_t key_hash;         /* fw_key_hash_kind                                          */
+    int64_t size_ms;          /* TUMBLE size, HOP size, CUMULATE max size                  */
+    int64_t slide_ms;         /* HOP slide, CUMULATE step (0 for TUMBLE)                   */
+    int64_t offset_ms;        /* window offset (withOffset)                                */
+    int32_t n_aggs;
+    int32_t count_star_index; /* SQL indexOfCountStar: agg index whose value is COUNT(*),
+                                 -1 if none (required for HOP, as in the reference)        */
+    fw_agg_desc aggs[FW_MAX_AGGS];
+    int32_t n_value_cols;
+    int32_t value_col_types[FW_MAX_COLS];
+    int32_t max_parallelism;  /* number of key groups (pipeline.max-parallelism)           */
+    int32_t parallelism;      /* operator parallelism p                                    */
+    int32_t subtask_index;    /* this subtask: owns computeKeyGroupRangeForOperatorIndex   */
+    int32_t device;           /* HIP device ordinal                                        */
+    int64_t state_capacity;   /* expected max live (key, slice) state entries (sizing hint) */
+    int64_t max_batch_rows;   /* max rows per fw_commit / fw_push_device call              */
+    int64_t output_capacity;  /* result rows kept between fw_results_reset calls           */
+} fw_config;
+
+typedef struct fw_handle fw_handle;
+
+/* Pinned host staging columns returned by fw_reserve (valid until fw_commit). */
+typedef struct {
+    int64_t* key;
+    int64_t* ts;                       /* event time, epoch ms (rowtime)               */
+    int32_t* key_hash;                 /* only for FW_KEYHASH_PRECOMPUTED              */
+    int64_t* values[FW_MAX_COLS];      /* int64 or double bits, per value_col_types     */
+} fw_host_cols;
+
+/* Window results: SQL rows are key ++ aggs ++ (window_start, window_end); DataStream
+   records are (key, agg) with record timestamp window.maxTimestamp() = window_end - 1. */
+typedef struct {
+    int64_t n;
+    int64_t* key;
+    int64_t* window_start;
+    int64_t* window_end;
+    int64_t* values[FW_MAX_AGGS];      /* per agg: int64, or double bits for DOUBLE results */
+    uint32_t* null_mask;               /* bit a set => agg a is SQL NULL                */
+} fw_result;
+
+typedef struct {
+    int64_t current_watermark;         /* operator currentWatermark / processor currentProgress */
+    int64_t next_trigger_progress;
+    int64_t num_late_records_dropped;
+    int64_t live_state_entries;
+    int64_t pending_rows;              /* rows buffered (not yet flushed into state)    */
+    int64_t results_available;
+    int64_t num_fired_windows;         /* numFiredTimers analogue                       */
+    int32_t error_flags;
+    int32_t num_superbuckets;
+} fw_stats;
+
+/* ---- lifecycle ------------------------------------------------------------------- */
+int fw_create(const fw_config* cfg, fw_handle** out);
+int fw_destroy(fw_handle* h);
+const char* fw_last_error(void);
+int fw_abi_version(void);
+/* hipStream_t of the handle, as void* (so a caller can order its own work with it). */
+void* fw_get_stream(fw_handle* h);
+int fw_sync(fw_handle* h);
+
+int fw_initialize_watermark(fw_handle* h, int64_t watermark);
+
+/* ---- ingest ------------------------------------------------------------------------ */
+int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out);
+int fw_commit(fw_handle* h, int64_t n);
+/* Device-resident columns (caller-owned device memory, ordered on the handle stream).
+   d_values[c] points at n 8-byte words of value column c; d_key_hash may be NULL unless
+   key_hash == FW_KEYHASH_PRECOMPUTED. */
+int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t* d_ts,
+                   const int32_t* d_key_hash, const void* const* d_values);
+
+/* ---- progress / output --------------------------------------------------------------- */
+int fw_advance(fw_handle* h, int64_t watermark);
+int fw_flush(fw_handle* h);
+/* copy_to_host != 0: host arrays owned by the handle, valid until the next call;
+   otherwise device pointers. */
+int fw_results(fw_handle* h, fw_result* out, int copy_to_host);
+int fw_results_reset(fw_handle* h);
+int fw_get_stats(fw_handle* h, fw_stats* out);
+
+/* ---- checkpoint -------------------------------------------------------------------- */
+/* Flushes, then serialises watermark + state + timers.  *size receives the byte count;
+   call with buf == NULL to query it. */
+int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size);
+int fw_restore(fw_handle* h, const void* buf, int64_t size);
+
+/* ---- stand-alone device kernels (partitioner, tests) ---------------------------------- */
+/* d_kg[i] = key group, d_dest[i] = computeOperatorIndexForKeyGroup(maxP, p, kg). */
+int fw_assign_key_groups(const int64_t* d_key, const int32_t* d_key_hash, int64_t n,
+                         int32_t key_hash_kind, int32_t max_parallelism, int32_t parallelism,
+                         int32_t* d_kg, int32_t* d_dest, void* stream);
+/* Counting-sort rows by destination subtask.  d_counts[p] receives rows per destination;
+   output columns are grouped by destination in ascending order. n_cols value columns. */
+int fw_partition_by_dest(const int64_t* d_key, const int64_t* d_ts, const void* const* d_values,
+                         int32_t n_cols, int64_t n, int32_t key_hash_kind,
+                         int32_t max_parallelism, int32_t parallelism,
+                         int64_t* d_out_key, int64_t* d_out_ts, void* const* d_out_values,
+                         int64_t* d_counts, void* d_workspace, int64_t workspace_bytes,
+                         void* stream);
+int64_t fw_partition_workspace_bytes(int64_t n, int32_t parallelism);
+
+/* Synthetic Nexmark-shaped generator: event i in [i0, i0+n). */
+typedef struct {
+    uint64_t seed;
+    int64_t t0_ms;
+    int64_t rate_per_s;        /* events per second of event time                 */
+    int64_t ooo_ms;            /* out-of-orderness J                              */
+    int64_t key_base;
+    int64_t key_count;
+    int32_t key_dist;          /* 0 uniform: key_base + (u>>20) % key_count; 1 zipf    */
+    int32_t value_kind;        /* 0: 1 + u % 1e9 (int64); 1: 1000*(u>>11)*2^-53 (double);
+                                  2: u % 1e6 (int64)                                */
+    const double* zipf_cdf;    /* device pointer, key_count entries (key_dist == 1) */
+} fw_gen_params;
+int fw_generate(const fw_gen_params* gp, int64_t i0, int64_t n, int64_t* d_key, int64_t* d_ts,
+                int64_t* d_value, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLINKWIN_H_ */

@@ -1,0 +1,737 @@
+// ORACLE -- TEST INFRASTRUCTURE ONLY.
+//
+// A CPU restatement of Apache Flink's windowed keyed-aggregation semantics (reference tree
+// mounted at /root/reference, Flink 2.3-SNAPSHOT), used ONLY by tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg as the checker.  The product (libflinkwin, flink_amd/) never
+// links, imports or calls anything in this directory.
+//
+// It restates, record by record and timer by timer, the reference algorithms:
+//   TR = flink-table/flink-table-runtime/src/main/java/org/apache/flink/table/runtime
+//   FR = flink-runtime/src/main/java/org/apache/flink
+//   * hashing             flink-core/.../util/MathUtils.java:137-200 (murmurHash, bitMix)
+//                         FR/runtime/state/KeyGroupRangeAssignment.java:63-147
+//                         flink-table-common/.../data/binary/MurmurHashUtils.java:70-170
+//                         + BinaryRowData.java:69-124,459 (hashByWords, seed 42)
+//   * window math         FR/streaming/api/windowing/windows/TimeWindow.java:84,264-272
+//                         TR/operators/window/tvf/slicing/SliceAssigners.java:140-757
+//                         TR/util/TimeWindowUtil.java:52-211 (UTC shift zone only)
+//   * SQL operator        TR/operators/window/tvf/common/WindowAggOperator.java:216-265
+//                         TR/operators/aggregate/window/processors/
+//                           AbstractSliceSyncStateWindowAggProcessor.java:96-167
+//                           SliceUnsharedSyncStateWindowAggProcessor.java:54-71
+//                           SliceSharedSyncStateWindowAggProcessor.java:65-132
+//                           AbstractSyncStateWindowAggProcessor.java:92-118 (WindowIsEmptySupplier)
+//                         TR/operators/aggregate/window/buffers/RecordsWindowBuffer.java:81-126
+//                         TR/operators/aggregate/window/combines/AggCombiner.java:76-115
+//                         FR/streaming/api/operators/InternalTimerServiceImpl.java:249,328-348
+//   * SQL aggregates      flink-table-planner/.../functions/aggfunctions/
+//                           {Count1,Count,Sum,Max,Min,Avg}AggFunction.java
+//   * DataStream operator FR/streaming/runtime/operators/windowing/WindowOperator.java:293-682
+//                         FR/streaming/api/windowing/triggers/EventTimeTrigger.java:37-52
+//                         FR/streaming/api/windowing/assigners/{Tumbling,Sliding}EventTimeWindows.java
+//                         FR/streaming/api/functions/aggregation/{SumAggregator,ComparableAggregator,
+//                           Comparator}.java
+// Java `long`/`int` wrap-around is reproduced with unsigned arithmetic; Java `%` truncates.
+#include "../include/flinkwin.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <set>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------------------------
+// Java arithmetic helpers
+// ------------------------------------------------------------------------------------
+inline int32_t jmul32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+inline int32_t jadd32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+inline int32_t rotl32(int32_t x, int r) { uint32_t u = (uint32_t)x; return (int32_t)((u << r) | (u >> (32 - r))); }
+inline int32_t ushr32(int32_t x, int r) { return (int32_t)((uint32_t)x >> r); }
+inline int64_t jadd64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+inline int64_t jsub64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+
+// MathUtils.bitMix (MathUtils.java:194-200)
+int32_t bit_mix(int32_t in) {
+    in ^= ushr32(in, 16);
+    in = jmul32(in, (int32_t)0x85ebca6b);
+    in ^= ushr32(in, 13);
+    in = jmul32(in, (int32_t)0xc2b2ae35);
+    in ^= ushr32(in, 16);
+    return in;
+}
+
+// MathUtils.murmurHash (MathUtils.java:137-155)
+int32_t murmur_hash(int32_t code) {
+    code = jmul32(code, (int32_t)0xcc9e2d51);
+    code = rotl32(code, 15);
+    code = jmul32(code, (int32_t)0x1b873593);
+    code = rotl32(code, 13);
+    code = jadd32(jmul32(code, 5), (int32_t)0xe6546b64);
+    code ^= 4;
+    code = bit_mix(code);
+    if (code >= 0) return code;
+    if (code != INT32_MIN) return -code;
+    return 0;
+}
+
+// MurmurHashUtils.mixK1 / mixH1 / fmix (MurmurHashUtils.java:143-170)
+int32_t mix_k1(int32_t k1) {
+    k1 = jmul32(k1, (int32_t)0xcc9e2d51);
+    k1 = rotl32(k1, 15);
+    return jmul32(k1, (int32_t)0x1b873593);
+}
+int32_t mix_h1(int32_t h1, int32_t k1) {
+    h1 ^= k1;
+    h1 = rotl32(h1, 13);
+    return jadd32(jmul32(h1, 5), (int32_t)0xe6546b64);
+}
+int32_t fmix32(int32_t h) {
+    h ^= ushr32(h, 16);
+    h = jmul32(h, (int32_t)0x85ebca6b);
+    h ^= ushr32(h, 13);
+    h = jmul32(h, (int32_t)0xc2b2ae35);
+    h ^= ushr32(h, 16);
+    return h;
+}
+
+// BinaryRowData.hashCode of a one-field key row (BinaryRowData.java:459 ->
+// BinarySegmentUtils.hashByWords -> MurmurHashUtils.hashBytesByWords, seed 42).
+// Row layout (BinaryRowData.java:69-124; BinaryRowWriter.reset zeroes the 8-byte header):
+// [header/null-bits 8 B = 0][field slot 8 B little endian]; an INT writes 4 bytes only.
+int32_t binrow_hash_words(const int32_t* words, int nwords) {
+    int32_t h1 = 42;
+    for (int i = 0; i < nwords; i++) h1 = mix_h1(h1, mix_k1(words[i]));
+    return fmix32(h1 ^ (nwords * 4));
+}
+
+int32_t java_key_hash(int kind, int64_t key, int32_t precomputed) {
+    switch (kind) {
+        case FW_KEYHASH_LONG: return (int32_t)(key ^ (int64_t)((uint64_t)key >> 32));  // Long.hashCode
+        case FW_KEYHASH_INT: return (int32_t)key;                                       // Integer.hashCode
+        case FW_KEYHASH_BINROW_BIGINT: {
+            int32_t w[4] = {0, 0, (int32_t)(uint32_t)(uint64_t)key, (int32_t)(uint32_t)((uint64_t)key >> 32)};
+            return binrow_hash_words(w, 4);
+        }
+        case FW_KEYHASH_BINROW_INT: {
+            int32_t w[4] = {0, 0, (int32_t)key, 0};
+            return binrow_hash_words(w, 4);
+        }
+        default: return precomputed;
+    }
+}
+
+// KeyGroupRangeAssignment.computeKeyGroupForKeyHash (:75) / computeOperatorIndexForKeyGroup (:124)
+int32_t key_group_for_hash(int32_t h, int32_t max_p) { return murmur_hash(h) % max_p; }
+int32_t operator_index_for_kg(int32_t max_p, int32_t p, int32_t kg) { return kg * p / max_p; }
+
+// ------------------------------------------------------------------------------------
+// window math
+// ------------------------------------------------------------------------------------
+// TimeWindow.getWindowStartWithOffset (TimeWindow.java:264-272), Java long semantics.
+int64_t window_start_with_offset(int64_t ts, int64_t offset, int64_t size) {
+    const int64_t remainder = jsub64(ts, offset) % size;  // C++ % truncates like Java
+    if (remainder < 0) return jsub64(ts, jadd64(remainder, size));
+    return jsub64(ts, remainder);
+}
+
+// TimeWindowUtil.isWindowFired (TimeWindowUtil.java:175-183), UTC shift zone.
+bool is_window_fired(int64_t window_end, int64_t progress) {
+    if (window_end == INT64_MAX) return false;
+    return progress >= jsub64(window_end, 1);
+}
+
+// TimeWindowUtil.getNextTriggerWatermark (TimeWindowUtil.java:186-211), no DST.
+int64_t next_trigger_watermark(int64_t wm, int64_t interval) {
+    if (wm == INT64_MAX) return wm;
+    int64_t start = window_start_with_offset(wm, 0, interval);
+    int64_t trig = jsub64(jadd64(start, interval), 1);
+    return trig > wm ? trig : jadd64(trig, interval);
+}
+
+int64_t gcd64(int64_t a, int64_t b) {  // commons-math3 ArithmeticUtils.gcd for positive args
+    while (b != 0) { int64_t t = a % b; a = b; b = t; }
+    return a < 0 ? -a : a;
+}
+
+// ------------------------------------------------------------------------------------
+// accumulators: SQL built-in aggregate functions (declarative expressions) and the
+// DataStream SumAggregator / ComparableAggregator.
+// ------------------------------------------------------------------------------------
+struct AggState {
+    int64_t i = 0;        // integer sum / min / max / count / avg-sum(int)
+    double d = 0.0;       // double sum / min / max / avg-sum(double)
+    int64_t cnt = 0;      // AVG count
+    bool is_null = true;  // SUM/MIN/MAX null flag (SQL); COUNT never null
+};
+
+struct Row {
+    AggState a[FW_MAX_AGGS];
+};
+
+struct OutRow {
+    int64_t key, ws, we;
+    uint64_t v[FW_MAX_AGGS];
+    uint32_t null_mask;
+    int64_t epoch;  // index of the watermark call that produced it
+};
+
+inline double bits_to_double(uint64_t b) { double d; std::memcpy(&d, &b, 8); return d; }
+inline uint64_t double_to_bits(double d) { uint64_t b; std::memcpy(&b, &d, 8); return b; }
+
+// Double.compare (JDK): total order with -0.0 < 0.0 and NaN greatest.
+int java_double_compare(double a, double b) {
+    if (a < b) return -1;
+    if (a > b) return 1;
+    // doubleToLongBits canonicalises NaN
+    const int64_t x = std::isnan(a) ? 0x7ff8000000000000LL : (int64_t)double_to_bits(a);
+    const int64_t y = std::isnan(b) ? 0x7ff8000000000000LL : (int64_t)double_to_bits(b);
+    return x == y ? 0 : (x < y ? -1 : 1);
+}
+
+struct Config {
+    fw_config c;
+    int64_t interval;  // slice size (SliceAssigner.getSliceEndInterval)
+    int n_slices;      // HOP slices per window
+};
+
+struct Oracle {
+    Config cfg;
+    bool ds;  // DataStream operator
+    // operator / processor progress
+    int64_t current_watermark = INT64_MIN;      // WindowAggOperator.currentWatermark
+    int64_t current_progress = INT64_MIN;       // WindowAggProcessorBase.currentProgress
+    int64_t next_trigger_progress = INT64_MIN;  // AbstractSliceSyncStateWindowAggProcessor
+    int64_t timer_watermark = INT64_MIN;        // InternalTimerServiceImpl.currentWatermark
+    int64_t late_dropped = 0;
+    int64_t fired = 0;
+    int64_t epoch = 0;
+
+    // RecordsWindowBuffer: (sliceEnd, key) -> records in insertion order
+    struct BufRec { uint64_t vals[FW_MAX_COLS]; };
+    std::vector<std::pair<std::pair<int64_t, int64_t>, std::vector<BufRec>>> buffer;
+    std::map<std::pair<int64_t, int64_t>, size_t> buffer_index;
+    int64_t min_slice_end = INT64_MAX;
+
+    // keyed state: (key, namespace) -> accumulator row
+    std::map<std::pair<int64_t, int64_t>, Row> state;
+    // event-time timers: (timestamp, key, namespace) -- a set, so registration dedups
+    std::set<std::tuple<int64_t, int64_t, int64_t>> timers;
+
+    std::vector<OutRow> out;
+
+    // -------------------------------------------------------------------------------
+    // aggregate function expressions
+    // -------------------------------------------------------------------------------
+    Row create_accumulators() const { return Row(); }
+
+    void accumulate(Row& r, const uint64_t* vals) const {
+        for (int a = 0; a < cfg.c.n_aggs; a++) {
+            const fw_agg_desc& g = cfg.c.aggs[a];
+            AggState& s = r.a[a];
+            const uint64_t raw = g.kind == FW_AGG_COUNT_STAR ? 0 : vals[g.input_col];
+            const bool isf = g.type == FW_T_F64;
+            const int64_t iv = (int64_t)raw;
+            const double dv = bits_to_double(raw);
+            switch (g.kind) {
+                case FW_AGG_COUNT_STAR:  // Count1AggFunction: count + 1
+                case FW_AGG_COUNT:       // CountAggFunction: inputs are NOT NULL here
+                    s.i = jadd64(s.i, 1);
+                    s.is_null = false;
+                    break;
+                case FW_AGG_SUM:  // SumAggFunction: isNull(sum) ? operand : sum + operand
+                    if (isf) s.d = s.is_null ? dv : s.d + dv;
+                    else if (g.type == FW_T_I32) s.i = s.is_null ? (int32_t)iv : (int32_t)jadd32((int32_t)s.i, (int32_t)iv);
+                    else s.i = s.is_null ? iv : jadd64(s.i, iv);
+                    s.is_null = false;
+                    break;
+                case FW_AGG_MAX:
+                case FW_AGG_MIN: {
+                    const bool mx = g.kind == FW_AGG_MAX;
+                    if (s.is_null) {
+                        if (isf) s.d = dv; else s.i = iv;
+                    } else if (isf) {
+                        if (ds) {  // ComparableAggregator + Comparator: Double.compareTo
+                            int c = java_double_compare(dv, s.d);
+                            if (mx ? c > 0 : c < 0) s.d = dv;
+                        } else {   // MaxAggFunction: operand > max ; MinAggFunction: operand < min
+                            if (mx ? dv > s.d : dv < s.d) s.d = dv;
+                        }
+                    } else {
+                        if (mx ? iv > s.i : iv < s.i) s.i = iv;
+                    }
+                    s.is_null = false;
+                    break;
+                }
+                case FW_AGG_AVG:  // AvgAggFunction: sum + operand, count + 1
+                    if (isf) s.d = s.d + dv; else s.i = jadd64(s.i, iv);
+                    s.cnt = jadd64(s.cnt, 1);
+                    s.is_null = false;
+                    break;
+            }
+        }
+    }
+
+    // mergeExpressions of the same functions
+    void merge(Row& r, const Row& o) const {
+        for (int a = 0; a < cfg.c.n_aggs; a++) {
+            const fw_agg_desc& g = cfg.c.aggs[a];
+            AggState& s = r.a[a];
+            const AggState& t = o.a[a];
+            const bool isf = g.type == FW_T_F64;
+            switch (g.kind) {
+                case FW_AGG_COUNT_STAR:
+                case FW_AGG_COUNT:
+                    s.i = jadd64(s.i, t.i);
+                    s.is_null = false;
+                    break;
+                case FW_AGG_SUM:
+                    if (t.is_null) break;
+                    if (isf) s.d = s.is_null ? t.d : s.d + t.d;
+                    else if (g.type == FW_T_I32) s.i = s.is_null ? t.i : (int32_t)jadd32((int32_t)s.i, (int32_t)t.i);
+                    else s.i = s.is_null ? t.i : jadd64(s.i, t.i);
+                    s.is_null = false;
+                    break;
+                case FW_AGG_MAX:
+                case FW_AGG_MIN: {
+                    if (t.is_null) break;
+                    const bool mx = g.kind == FW_AGG_MAX;
+                    if (s.is_null) { s.i = t.i; s.d = t.d; }
+                    else if (isf) {
+                        if (ds) { int c = java_double_compare(t.d, s.d); if (mx ? c > 0 : c < 0) s.d = t.d; }
+                        else if (mx ? t.d > s.d : t.d < s.d) s.d = t.d;
+                    } else if (mx ? t.i > s.i : t.i < s.i) s.i = t.i;
+                    s.is_null = false;
+                    break;
+                }
+                case FW_AGG_AVG:
+                    if (isf) s.d = s.d + t.d; else s.i = jadd64(s.i, t.i);
+                    s.cnt = jadd64(s.cnt, t.cnt);
+                    s.is_null = false;
+                    break;
+            }
+        }
+    }
+
+    // getValueExpression; returns value words + null mask
+    void get_value(const Row& r, uint64_t* v, uint32_t* nm) const {
+        *nm = 0;
+        for (int a = 0; a < cfg.c.n_aggs; a++) {
+            const fw_agg_desc& g = cfg.c.aggs[a];
+            const AggState& s = r.a[a];
+            const bool isf = g.type == FW_T_F64;
+            v[a] = 0;
+            switch (g.kind) {
+                case FW_AGG_COUNT_STAR:
+                case FW_AGG_COUNT: v[a] = (uint64_t)s.i; break;
+                case FW_AGG_SUM:
+                case FW_AGG_MAX:
+                case FW_AGG_MIN:
+                    if (s.is_null) { *nm |= 1u << a; break; }
+                    v[a] = isf ? double_to_bits(s.d) : (uint64_t)s.i;
+                    break;
+                case FW_AGG_AVG:  // count == 0 ? null : cast(sum / count)
+                    if (s.cnt == 0) { *nm |= 1u << a; break; }
+                    if (isf) v[a] = double_to_bits(s.d / (double)s.cnt);
+                    else {
+                        int64_t q = (s.i == INT64_MIN && s.cnt == -1) ? INT64_MIN : s.i / s.cnt;
+                        if (g.type == FW_T_I32) q = (int32_t)q;
+                        v[a] = (uint64_t)q;
+                    }
+                    break;
+            }
+        }
+    }
+
+    int64_t count_star(const Row& r) const {
+        int idx = cfg.c.count_star_index;
+        return r.a[idx].i;
+    }
+
+    // -------------------------------------------------------------------------------
+    // SliceAssigner (SliceAssigners.java)
+    // -------------------------------------------------------------------------------
+    int64_t assign_slice_end(int64_t ts) const {
+        const fw_config& c = cfg.c;
+        const int64_t step = cfg.interval;
+        return jadd64(window_start_with_offset(ts, c.offset_ms, step), step);
+    }
+    int64_t get_window_start(int64_t we) const {
+        const fw_config& c = cfg.c;
+        if (c.window_kind == FW_WIN_CUMULATE)
+            return window_start_with_offset(jsub64(we, 1), c.offset_ms, c.size_ms);
+        return jsub64(we, c.size_ms);
+    }
+    int64_t get_last_window_end(int64_t slice_end) const {
+        const fw_config& c = cfg.c;
+        switch (c.window_kind) {
+            case FW_WIN_TUMBLE: return slice_end;
+            case FW_WIN_HOP: return jadd64(jsub64(slice_end, cfg.interval), c.size_ms);
+            default: return jadd64(get_window_start(slice_end), c.size_ms);
+        }
+    }
+    // sliceStateMergeTarget: unshared -> itself; hop -> itself (null merge target);
+    // cumulate -> first slice of the window (mergeSlices callback target).
+    int64_t merge_target(int64_t slice_end) const {
+        if (cfg.c.window_kind == FW_WIN_CUMULATE) return jadd64(get_window_start(slice_end), cfg.interval);
+        return slice_end;
+    }
+
+    void register_timer(int64_t key, int64_t window) {
+        // SlicingWindowTimerServiceImpl.registerEventTimeWindowTimer: ts = window - 1 (UTC)
+        timers.insert(std::make_tuple(jsub64(window, 1), key, window));
+    }
+
+    // -------------------------------------------------------------------------------
+    // SQL: AbstractSliceSyncStateWindowAggProcessor.processElement (:96-126)
+    // -------------------------------------------------------------------------------
+    bool sql_process_element(int64_t key, int64_t ts, const uint64_t* vals) {
+        const int64_t slice_end = assign_slice_end(ts);
+        if (is_window_fired(slice_end, current_progress)) {
+            const int64_t last = get_last_window_end(slice_end);
+            if (is_window_fired(last, current_progress)) return true;  // dropped
+            buffer_add(key, merge_target(slice_end), vals);
+            int64_t unfired = slice_end;
+            while (is_window_fired(unfired, current_progress)) unfired = jadd64(unfired, cfg.interval);
+            register_timer(key, unfired);
+            return false;
+        }
+        buffer_add(key, slice_end, vals);
+        return false;
+    }
+
+    void buffer_add(int64_t key, int64_t slice, const uint64_t* vals) {
+        auto wk = std::make_pair(slice, key);
+        auto it = buffer_index.find(wk);
+        size_t gi;
+        if (it == buffer_index.end()) {
+            gi = buffer.size();
+            buffer_index.emplace(wk, gi);
+            buffer.push_back({wk, {}});
+        } else {
+            gi = it->second;
+        }
+        BufRec r;
+        std::memcpy(r.vals, vals, sizeof(r.vals));
+        buffer[gi].second.push_back(r);
+        min_slice_end = std::min(min_slice_end, slice);
+    }
+
+    // RecordsWindowBuffer.flush (:115-126) -> AggCombiner.combine (:76-115)
+    void flush() {
+        for (auto& g : buffer) {
+            const int64_t slice = g.first.first, key = g.first.second;
+            auto sk = std::make_pair(key, slice);
+            auto it = state.find(sk);
+            Row acc = it == state.end() ? create_accumulators() : it->second;
+            for (auto& rec : g.second) accumulate(acc, rec.vals);
+            state[sk] = acc;
+            if (!is_window_fired(slice, timer_watermark)) register_timer(key, slice);
+        }
+        buffer.clear();
+        buffer_index.clear();
+        min_slice_end = INT64_MAX;
+    }
+
+    void emit(int64_t key, int64_t we, const Row& acc) {
+        OutRow o;
+        o.key = key;
+        o.we = we;
+        o.ws = ds ? jsub64(we, cfg.c.size_ms) : get_window_start(we);
+        get_value(acc, o.v, &o.null_mask);
+        o.epoch = epoch;
+        out.push_back(o);
+    }
+
+    bool is_empty(const Row& acc) const {  // WindowIsEmptySupplier.get
+        if (cfg.c.count_star_index < 0) return false;
+        return count_star(acc) == 0;
+    }
+
+    void sql_fire_window(int64_t key, int64_t we) {
+        const fw_config& c = cfg.c;
+        if (c.window_kind == FW_WIN_TUMBLE) {  // SliceUnsharedSyncStateWindowAggProcessor.fireWindow
+            auto it = state.find({key, we});
+            Row acc = it == state.end() ? create_accumulators() : it->second;
+            if (is_empty(acc)) return;
+            emit(key, we, acc);
+            return;
+        }
+        // SliceSharedSyncStateWindowAggProcessor.fireWindow -> mergeSlices -> merge
+        Row acc;
+        if (c.window_kind == FW_WIN_HOP) {
+            acc = create_accumulators();  // null merge target: heap accumulator
+            int64_t s = we;
+            for (int i = 0; i < cfg.n_slices; i++) {  // HoppingSlicesIterable
+                auto it = state.find({key, s});
+                if (it != state.end()) merge(acc, it->second);
+                s = jsub64(s, cfg.interval);
+            }
+        } else {
+            const int64_t first = jadd64(get_window_start(we), cfg.interval);
+            auto it = state.find({key, first});
+            acc = it == state.end() ? create_accumulators() : it->second;
+            if (we != first) {
+                auto jt = state.find({key, we});
+                if (jt != state.end()) merge(acc, jt->second);
+            }
+            state[{key, first}] = acc;  // windowState.update(mergeResult, acc)
+        }
+        const bool empty = is_empty(acc);
+        if (!empty) emit(key, we, acc);
+        // nextTriggerWindow
+        if (c.window_kind == FW_WIN_HOP) {
+            if (!empty) register_timer(key, jadd64(we, cfg.interval));
+        } else {
+            const int64_t next = jadd64(we, cfg.interval);
+            const int64_t max_we = jadd64(get_window_start(we), c.size_ms);
+            if (!(next > max_we)) register_timer(key, next);
+        }
+    }
+
+    // AbstractSliceSyncStateWindowAggProcessor.clearWindow -> expiredSlices
+    void sql_clear_window(int64_t key, int64_t we) {
+        const fw_config& c = cfg.c;
+        if (c.window_kind == FW_WIN_TUMBLE) {
+            state.erase({key, we});
+        } else if (c.window_kind == FW_WIN_HOP) {
+            state.erase({key, jadd64(jsub64(we, c.size_ms), cfg.interval)});
+        } else {
+            const int64_t ws = get_window_start(we);
+            const int64_t first = jadd64(ws, cfg.interval);
+            const int64_t last = jadd64(ws, c.size_ms);
+            if (we == first) {
+            } else if (we == last) {
+                state.erase({key, we});
+                state.erase({key, first});
+            } else {
+                state.erase({key, we});
+            }
+        }
+    }
+
+    // InternalTimerServiceImpl.tryAdvanceWatermark (:328-348)
+    void advance_timers(int64_t wm) {
+        timer_watermark = wm;
+        while (!timers.empty()) {
+            auto t = *timers.begin();
+            if (std::get<0>(t) > wm) break;
+            timers.erase(timers.begin());
+            fired++;
+            const int64_t key = std::get<1>(t), ns = std::get<2>(t);
+            if (ds) {
+                ds_on_event_time(key, ns, std::get<0>(t));
+            } else {  // WindowAggOperator.onTimer: fireWindow then clearWindow
+                sql_fire_window(key, ns);
+                sql_clear_window(key, ns);
+            }
+        }
+    }
+
+    // WindowAggOperator.processWatermark (:227-238)
+    void sql_process_watermark(int64_t wm) {
+        if (wm > current_watermark) {
+            // AbstractSliceSyncStateWindowAggProcessor.advanceProgress (:139-153)
+            if (wm > current_progress) {
+                current_progress = wm;
+                if (current_progress >= next_trigger_progress) {
+                    // RecordsWindowBuffer.advanceProgress (:107-112)
+                    if (is_window_fired(min_slice_end, current_progress)) flush();
+                    next_trigger_progress = next_trigger_watermark(current_progress, cfg.interval);
+                }
+            }
+            current_watermark = wm;
+            advance_timers(wm);
+        }
+    }
+
+    // -------------------------------------------------------------------------------
+    // DataStream: WindowOperator.processElement (non-merging branch :405-446) with
+    // EventTimeTrigger, allowedLateness = 0, no late side output.
+    // -------------------------------------------------------------------------------
+    bool ds_process_element(int64_t key, int64_t ts, const uint64_t* vals) {
+        const fw_config& c = cfg.c;
+        std::vector<int64_t> starts;
+        if (c.window_kind == FW_WIN_TUMBLE) {
+            // TumblingEventTimeWindows.assignWindows (:69-87), stagger offset 0
+            starts.push_back(window_start_with_offset(ts, c.offset_ms % c.size_ms, c.size_ms));
+        } else {
+            // SlidingEventTimeWindows.assignWindows (:77-90)
+            const int64_t last_start = window_start_with_offset(ts, c.offset_ms, c.slide_ms);
+            for (int64_t s = last_start; s > jsub64(ts, c.size_ms); s = jsub64(s, c.slide_ms)) starts.push_back(s);
+        }
+        bool skipped = true;
+        for (int64_t s : starts) {
+            const int64_t end = jadd64(s, c.size_ms);
+            const int64_t max_ts = jsub64(end, 1);
+            if (max_ts <= timer_watermark) continue;  // isWindowLate: cleanupTime <= currentWatermark
+            skipped = false;
+            auto sk = std::make_pair(key, end);
+            auto it = state.find(sk);
+            Row acc = it == state.end() ? create_accumulators() : it->second;
+            accumulate(acc, vals);  // HeapReducingState.add / HeapAggregatingState.add
+            state[sk] = acc;
+            // EventTimeTrigger.onElement: maxTs > watermark -> registerEventTimeTimer(maxTs);
+            // registerCleanupTimer(window) registers the same (key, window, maxTs) timer.
+            timers.insert(std::make_tuple(max_ts, key, end));
+        }
+        if (skipped && ts <= timer_watermark) return true;  // isElementLate -> numLateRecordsDropped
+        return false;
+    }
+
+    // WindowOperator.onEventTime (:450-494)
+    void ds_on_event_time(int64_t key, int64_t end, int64_t time) {
+        const int64_t max_ts = jsub64(end, 1);
+        if (time == max_ts) {  // EventTimeTrigger.onEventTime -> FIRE
+            auto it = state.find({key, end});
+            if (it != state.end()) emit(key, end, it->second);  // emitWindowContents, ts = maxTimestamp
+        }
+        if (time == max_ts) state.erase({key, end});  // isCleanupTime -> clearAllState
+    }
+
+    void ds_process_watermark(int64_t wm) {
+        if (wm > timer_watermark) advance_timers(wm);
+        current_watermark = std::max(current_watermark, wm);
+        current_progress = current_watermark;
+    }
+
+    void process_watermark(int64_t wm) {
+        if (ds) ds_process_watermark(wm); else sql_process_watermark(wm);
+        epoch++;
+    }
+
+    // prepareSnapshotPreBarrier -> windowBuffer.flush(); then a restored operator starts with
+    // nextTriggerProgress = Long.MIN_VALUE and the watermark from union-list state.
+    void snapshot_restore() {
+        if (!ds) flush();
+        next_trigger_progress = INT64_MIN;
+    }
+};
+
+thread_local char g_err[256];
+
+}  // namespace
+
+// ======================================================================================
+// C ABI (tests only)
+// ======================================================================================
+extern "C" {
+
+const char* or_last_error(void) { return g_err; }
+
+void* or_create(const fw_config* c) {
+    if (!c || c->n_aggs < 0 || c->n_aggs > FW_MAX_AGGS) { snprintf(g_err, sizeof g_err, "bad config"); return nullptr; }
+    Oracle* o = new Oracle();
+    o->cfg.c = *c;
+    o->ds = c->api == FW_API_DATASTREAM;
+    if (c->window_kind == FW_WIN_TUMBLE) { o->cfg.interval = c->size_ms; o->cfg.n_slices = 1; }
+    else if (c->window_kind == FW_WIN_HOP) {
+        o->cfg.interval = gcd64(c->size_ms, c->slide_ms);
+        o->cfg.n_slices = (int)(c->size_ms / o->cfg.interval);
+    } else { o->cfg.interval = c->slide_ms; o->cfg.n_slices = (int)(c->size_ms / c->slide_ms); }
+    return o;
+}
+
+void or_destroy(void* h) { delete (Oracle*)h; }
+
+void or_initialize_watermark(void* h, int64_t wm) {
+    Oracle* o = (Oracle*)h;
+    o->current_watermark = wm;
+    o->current_progress = wm;
+    o->timer_watermark = wm;
+}
+
+// Row-major value columns: vals[col * n + i] (8-byte words).
+int64_t or_process_batch(void* h, int64_t n, const int64_t* key, const int64_t* ts, const uint64_t* vals, int32_t ncols) {
+    Oracle* o = (Oracle*)h;
+    int64_t dropped = 0;
+    uint64_t row[FW_MAX_COLS] = {0};
+    for (int64_t i = 0; i < n; i++) {
+        for (int c = 0; c < ncols; c++) row[c] = vals[(int64_t)c * n + i];
+        bool d = o->ds ? o->ds_process_element(key[i], ts[i], row) : o->sql_process_element(key[i], ts[i], row);
+        if (d) dropped++;
+    }
+    o->late_dropped += dropped;
+    return dropped;
+}
+
+void or_process_watermark(void* h, int64_t wm) { ((Oracle*)h)->process_watermark(wm); }
+void or_flush(void* h) { Oracle* o = (Oracle*)h; if (!o->ds) o->flush(); }
+void or_snapshot_restore(void* h) { ((Oracle*)h)->snapshot_restore(); }
+int64_t or_late_dropped(void* h) { return ((Oracle*)h)->late_dropped; }
+int64_t or_state_size(void* h) { return (int64_t)((Oracle*)h)->state.size(); }
+int64_t or_timer_count(void* h) { return (int64_t)((Oracle*)h)->timers.size(); }
+int64_t or_current_watermark(void* h) { return ((Oracle*)h)->current_watermark; }
+
+int64_t or_num_results(void* h) { return (int64_t)((Oracle*)h)->out.size(); }
+// Copies results into SoA arrays (each may be NULL): vals[a * n + i].
+void or_get_results(void* h, int64_t* key, int64_t* ws, int64_t* we, uint64_t* vals, uint32_t* nm, int64_t* epoch) {
+    Oracle* o = (Oracle*)h;
+    const int64_t n = (int64_t)o->out.size();
+    for (int64_t i = 0; i < n; i++) {
+        const OutRow& r = o->out[i];
+        if (key) key[i] = r.key;
+        if (ws) ws[i] = r.ws;
+        if (we) we[i] = r.we;
+        if (nm) nm[i] = r.null_mask;
+        if (epoch) epoch[i] = r.epoch;
+        if (vals) for (int a = 0; a < o->cfg.c.n_aggs; a++) vals[(int64_t)a * n + i] = r.v[a];
+    }
+}
+void or_clear_results(void* h) { ((Oracle*)h)->out.clear(); }
+
+// Hash / key-group restatements.
+int32_t or_murmur_hash(int32_t code) { return murmur_hash(code); }
+int32_t or_java_key_hash(int32_t kind, int64_t key, int32_t pre) { return java_key_hash(kind, key, pre); }
+int32_t or_key_group(int32_t kind, int64_t key, int32_t pre, int32_t max_p) {
+    return key_group_for_hash(java_key_hash(kind, key, pre), max_p);
+}
+int32_t or_operator_index(int32_t max_p, int32_t p, int32_t kg) { return operator_index_for_kg(max_p, p, kg); }
+void or_key_group_range(int32_t max_p, int32_t p, int32_t idx, int32_t* start, int32_t* end) {
+    // computeKeyGroupRangeForOperatorIndex (:93-106)
+    *start = (idx * max_p + p - 1) / p;
+    *end = ((idx + 1) * max_p - 1) / p;
+}
+int64_t or_window_start_with_offset(int64_t ts, int64_t off, int64_t size) { return window_start_with_offset(ts, off, size); }
+int64_t or_next_trigger_watermark(int64_t wm, int64_t interval) { return next_trigger_watermark(wm, interval); }
+
+// Synthetic generator, same definition as the device generator.
+static inline uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+void or_generate(const fw_gen_params* gp, const double* zipf_cdf, int64_t i0, int64_t n,
+                 int64_t* key, int64_t* ts, int64_t* val) {
+    for (int64_t j = 0; j < n; j++) {
+        const uint64_t i = (uint64_t)(i0 + j);
+        const uint64_t u = splitmix64(gp->seed ^ (i * 0x9E3779B97F4A7C15ULL));
+        const int64_t t = gp->t0_ms + (int64_t)((__int128)i * 1000 / gp->rate_per_s) - (int64_t)(u % (uint64_t)gp->ooo_ms);
+        int64_t k;
+        if (gp->key_dist == 0) {
+            k = gp->key_base + (int64_t)((u >> 20) % (uint64_t)gp->key_count);
+        } else {
+            const double x = (double)(u >> 11) * (1.0 / 9007199254740992.0);
+            int64_t lo = 0, hi = gp->key_count - 1;  // first index with cdf > x
+            while (lo < hi) { int64_t mid = (lo + hi) >> 1; if (zipf_cdf[mid] > x) hi = mid; else lo = mid + 1; }
+            k = gp->key_base + lo;
+        }
+        uint64_t v;
+        if (gp->value_kind == 0) v = 1 + u % 1000000000ULL;
+        else if (gp->value_kind == 1) { double d = 1000.0 * (double)(u >> 11) * (1.0 / 9007199254740992.0); std::memcpy(&v, &d, 8); }
+        else v = u % 1000000ULL;
+        if (key) key[j] = k;
+        if (ts) ts[j] = t;
+        if (val) val[j] = (int64_t)v;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper around oracle/liboracle.so, the CPU restatement of the reference window
+operators (see flinkwin_oracle.cpp for the file:line map).  Imported only by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from flink_amd import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
+        L.or_create.restype = vp
+        L.or_create.argtypes = [C.POINTER(abi.fw_config)]
+        L.or_destroy.argtypes = [vp]
+        L.or_initialize_watermark.argtypes = [vp, i64]
+        L.or_process_batch.restype = i64
+        L.or_process_batch.argtypes = [vp, i64, vp, vp, vp, i32]
+        L.or_process_watermark.argtypes = [vp, i64]
+        L.or_flush.argtypes = [vp]
+        L.or_snapshot_restore.argtypes = [vp]
+        for f in ("or_late_dropped", "or_state_size", "or_timer_count", "or_num_results",
+                  "or_current_watermark"):
+            getattr(L, f).restype = i64
+            getattr(L, f).argtypes = [vp]
+        L.or_get_results.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.or_clear_results.argtypes = [vp]
+        L.or_murmur_hash.restype = i32
+        L.or_murmur_hash.argtypes = [i32]
+        L.or_java_key_hash.restype = i32
+        L.or_java_key_hash.argtypes = [i32, i64, i32]
+        L.or_key_group.restype = i32
+        L.or_key_group.argtypes = [i32, i64, i32, i32]
+        L.or_operator_index.restype = i32
+        L.or_operator_index.argtypes = [i32, i32, i32]
+        L.or_key_group_range.argtypes = [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]
+        L.or_window_start_with_offset.restype = i64
+        L.or_window_start_with_offset.argtypes = [i64, i64, i64]
+        L.or_next_trigger_watermark.restype = i64
+        L.or_next_trigger_watermark.argtypes = [i64, i64]
+        L.or_generate.argtypes = [C.POINTER(abi.fw_gen_params), vp, i64, i64, vp, vp, vp]
+        _LIB = L
+    return _LIB
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class OracleOperator:
+    """One reference window operator subtask (SQL WindowAggOperator or DataStream
+    WindowOperator), driven record-by-record exactly as the reference harness does."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.h = lib().or_create(C.byref(cfg))
+        if not self.h:
+            raise RuntimeError("oracle create failed")
+
+    def close(self):
+        if self.h:
+            lib().or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def initialize_watermark(self, wm):
+        lib().or_initialize_watermark(self.h, int(wm))
+
+    def process_batch(self, keys, ts, values):
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        n = len(keys)
+        ncols = len(values)
+        vals = np.zeros((max(ncols, 1), n), dtype=np.uint64)
+        for c, v in enumerate(values):
+            v = np.asarray(v)
+            vals[c] = v.view(np.uint64) if v.dtype in (np.float64, np.int64, np.uint64) else v.astype(np.int64).view(np.uint64)
+        return lib().or_process_batch(self.h, n, _ptr(keys), _ptr(ts), _ptr(vals), ncols)
+
+    def process_watermark(self, wm):
+        lib().or_process_watermark(self.h, int(wm))
+
+    def flush(self):
+        lib().or_flush(self.h)
+
+    def snapshot_restore(self):
+        lib().or_snapshot_restore(self.h)
+
+    @property
+    def late_dropped(self):
+        return lib().or_late_dropped(self.h)
+
+    @property
+    def state_size(self):
+        return lib().or_state_size(self.h)
+
+    def results(self, clear=True):
+        L = lib()
+        n = L.or_num_results(self.h)
+        na = self.cfg.n_aggs
+        key = np.empty(n, np.int64)
+        ws = np.empty(n, np.int64)
+        we = np.empty(n, np.int64)
+        vals = np.empty((max(na, 1), n), np.uint64)
+        nm = np.empty(n, np.uint32)
+        ep = np.empty(n, np.int64)
+        if n:
+            L.or_get_results(self.h, _ptr(key), _ptr(ws), _ptr(we), _ptr(vals), _ptr(nm), _ptr(ep))
+        if clear:
+            L.or_clear_results(self.h)
+        return {"key": key, "window_start": ws, "window_end": we,
+                "values": [vals[a] for a in range(na)], "null_mask": nm, "epoch": ep}
+
+
+def murmur_hash(code):
+    return lib().or_murmur_hash(int(np.int32(code)))
+
+
+def java_key_hash(kind, key, pre=0):
+    return lib().or_java_key_hash(kind, int(key), int(pre))
+
+
+def key_group(kind, key, max_p, pre=0):
+    return lib().or_key_group(kind, int(key), int(pre), max_p)
+
+
+def operator_index(max_p, p, kg):
+    return lib().or_operator_index(max_p, p, kg)
+
+
+def key_group_range(max_p, p, idx):
+    s, e = C.c_int32(), C.c_int32()
+    lib().or_key_group_range(max_p, p, idx, C.byref(s), C.byref(e))
+    return s.value, e.value
+
+
+def window_start_with_offset(ts, off, size):
+    return lib().or_window_start_with_offset(int(ts), int(off), int(size))
+
+
+def next_trigger_watermark(wm, interval):
+    return lib().or_next_trigger_watermark(int(wm), int(interval))
+
+
+def generate(gp, i0, n, zipf_cdf=None):
+    key = np.empty(n, np.int64)
+    ts = np.empty(n, np.int64)
+    val = np.empty(n, np.int64)
+    lib().or_generate(C.byref(gp), _ptr(zipf_cdf), int(i0), int(n), _ptr(key), _ptr(ts), _ptr(val))
+    return key, ts, val
+
+
+def zipf_cdf(n, s):
+    """Inverse-CDF table for Zipf(s) over n keys."""
+    w = 1.0 / np.power(np.arange(1, n + 1, dtype=np.float64), s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    return cdf

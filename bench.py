@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""Windowed keyed-aggregation benchmark (BASELINE.json metric: windowed-agg events/sec, whole
+node, at 1/2/4/8 GPUs, + % of HBM peak of the segmented-reduce kernel).
+
+One "step" = one watermark interval of the hot path: ingest one batch of B = 2^22 synthetic
+Nexmark-shaped events already resident in HBM (slice assignment + LDS segmented reduce), then
+processWatermark (flush into the HBM slice table + fire/emit due windows).  Default workload is
+CFG2 (Nexmark Q7-style TUMBLE 10 s MAX(price) GROUP BY auction, 10^6 auctions) for 24 steps
+= 100.7 M events, the configuration BASELINE.json quotes the metric on (configs[1]).
+
+N > 1 (torchrun, one rank per GPU, RCCL): every rank generates its slice of each global batch,
+routes rows to the key-group owner with fw_partition_by_dest + an all-to-all over xGMI (the
+keyBy exchange), min-reduces the watermark, then runs its own operator subtask.  Weak scaling:
+per-GPU events, keys and event rate stay fixed as N grows.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+B = 1 << 22                    # events per watermark interval
+T0 = 1_599_998_400_000         # hour-aligned UTC start
+J = 4000                       # out-of-orderness (nexmark.sql WATERMARK -4 s)
+HBM_PEAK_GBPS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # name: (description, window, aggs, keys per GPU, rate per GPU, value kind, key dist, input B/event)
+    "cfg2": dict(desc="Nexmark Q7-style TUMBLE(10 s) MAX(price) GROUP BY auction",
+                 window=("TUMBLE", 10_000, 0), aggs=[("MAX", 0, "BIGINT")], count_star=-1,
+                 keys=1_000_000, key_base=1000, rate=1_000_000, value_kind=0, dist=0, w_in=24,
+                 value_cols=["BIGINT"], nw=1, state_per_key=2),
+    "cfg3": dict(desc="Nexmark Q5-style HOP(2 s slide, 10 s size) COUNT(*) GROUP BY auction",
+                 window=("HOP", 10_000, 2_000), aggs=[("COUNT_STAR", 0, "BIGINT")], count_star=0,
+                 keys=1_000_000, key_base=1000, rate=1_000_000, value_kind=0, dist=0, w_in=16,
+                 value_cols=[], nw=1, state_per_key=8),
+    "cfg4": dict(desc="TUMBLE(10 s) SUM(v), AVG(v) DOUBLE over 10^7 keys (1.25 M per GPU at N=8)",
+                 window=("TUMBLE", 10_000, 0), aggs=[("SUM", 0, "DOUBLE"), ("AVG", 0, "DOUBLE")],
+                 count_star=-1, keys=1_250_000, key_base=0, rate=1_000_000, value_kind=1, dist=0, w_in=24,
+                 value_cols=["DOUBLE"], nw=2, state_per_key=2),
+    "cfg5": dict(desc="CUMULATE(1 min step, 1 h) COUNT(*), SUM, MIN, MAX, Zipf(1.1) keys",
+                 window=("CUMULATE", 3_600_000, 60_000),
+                 aggs=[("COUNT_STAR", 0, "BIGINT"), ("SUM", 0, "BIGINT"), ("MIN", 0, "BIGINT"), ("MAX", 0, "BIGINT")],
+                 count_star=0, keys=1_000_000, key_base=0, rate=27_778, value_kind=2, dist=1, w_in=24,
+                 zipf_s=1.1, keys_fixed=True, value_cols=["BIGINT"], nw=4, state_per_key=3),
+}
+
+
+def watermark(b, rate_per_gpu):
+    # W_b = T0 + floor((b+1) * B * 1000 / R) - J - 1 (per-GPU rate; N ranks x B events per step)
+    return T0 + ((b + 1) * B * 1000) // rate_per_gpu - J - 1
+
+
+def build_config(wl, world, rank, keys_total, out_cap):
+    from flink_amd import abi
+    kind, size, slide = wl["window"]
+    return abi.make_config(
+        api=abi.API_SQL, window_kind=abi.WINDOW_NAMES[kind], size_ms=size, slide_ms=slide,
+        aggs=[(abi.AGG_NAMES[k], c, abi.TYPE_NAMES[t]) for k, c, t in wl["aggs"]],
+        count_star_index=wl["count_star"],
+        value_col_types=[abi.TYPE_NAMES[t] for t in wl["value_cols"]],
+        key_hash=abi.KEYHASH_BINROW_BIGINT, max_parallelism=128, parallelism=world,
+        subtask_index=rank, state_capacity=int(keys_total * wl["state_per_key"]),
+        max_batch_rows=2 * B, output_capacity=out_cap)
+
+
+def gen_params(wl, world, zipf_ptr):
+    from flink_amd import abi
+    keys_total = wl["keys"] if wl.get("keys_fixed") else wl["keys"] * world
+    return abi.fw_gen_params(seed=42, t0_ms=T0, rate_per_s=wl["rate"] * world, ooo_ms=J,
+                             key_base=wl["key_base"], key_count=keys_total, key_dist=wl["dist"],
+                             value_kind=wl["value_kind"], zipf_cdf=zipf_ptr), keys_total
+
+
+def cpu_baseline(wl, sample_events):
+    """Oracle (CPU restatement, single thread) on the first `sample_events` events of the same
+    stream with the same watermarks; returns events/s of the record + watermark processing."""
+    from flink_amd import abi
+    from oracle import oracle as O
+    zcdf = O.zipf_cdf(wl["keys"], wl["zipf_s"]) if wl["dist"] == 1 else None
+    gp = abi.fw_gen_params(seed=42, t0_ms=T0, rate_per_s=wl["rate"], ooo_ms=J, key_base=wl["key_base"],
+                           key_count=wl["keys"], key_dist=wl["dist"], value_kind=wl["value_kind"], zipf_cdf=None)
+    cfg = build_config(wl, 1, 0, wl["keys"], 1 << 22)
+    op = O.OracleOperator(cfg)
+    steps = max(1, sample_events // B)
+    batches = [O.generate(gp, b * B, B, zcdf) for b in range(steps)]
+    t0 = time.perf_counter()
+    n_out = 0
+    for b, (k, t, v) in enumerate(batches):
+        op.process_batch(k, t, [v] if cfg.n_value_cols else [])
+        op.process_watermark(watermark(b, wl["rate"]))
+        n_out += len(op.results(clear=True)["key"])
+    dt = time.perf_counter() - t0
+    op.close()
+    return steps * B / dt, steps * B, dt, n_out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-sample", type=int, default=4 * B, help="events for the CPU baseline leg")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from flink_amd import _native, abi
+    from flink_amd.runtime.handle import WindowAggHandle
+    L = _native.lib()
+    wl = WORKLOADS[args.workload]
+    nv = len(wl["value_cols"])
+
+    # ---------------- synthetic input, resident in HBM before timing --------------------
+    zipf_t = None
+    if wl["dist"] == 1:
+        w = 1.0 / np.power(np.arange(1, wl["keys"] + 1, dtype=np.float64), wl["zipf_s"])
+        cdf = np.cumsum(w)
+        cdf /= cdf[-1]
+        zipf_t = torch.tensor(cdf, device=dev)
+    gp, keys_total = gen_params(wl, world, zipf_t.data_ptr() if zipf_t is not None else None)
+    total_steps = args.warmup + args.steps
+    gk = torch.empty((total_steps, B), dtype=torch.int64, device=dev)
+    gt = torch.empty_like(gk)
+    gv = torch.empty_like(gk)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for b in range(total_steps):
+        i0 = (b * world + rank) * B     # this rank's slice of global batch b
+        _native.check(L.fw_generate(C.byref(gp), i0, B, gk[b].data_ptr(), gt[b].data_ptr(), gv[b].data_ptr(), s))
+    torch.cuda.synchronize(dev)
+
+    # ---------------- keyBy exchange (N > 1) ----------------------------------------------
+    ws_bytes = L.fw_partition_workspace_bytes(B, world)
+    workspace = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
+    pk = torch.empty(B, dtype=torch.int64, device=dev)
+    pt = torch.empty_like(pk)
+    pv = torch.empty_like(pk)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+
+    def exchange(b):
+        if world == 1:
+            return gk[b], gt[b], gv[b]
+        vin = (C.c_void_p * abi.FW_MAX_COLS)(gv[b].data_ptr())
+        vout = (C.c_void_p * abi.FW_MAX_COLS)(pv.data_ptr())
+        _native.check(L.fw_partition_by_dest(gk[b].data_ptr(), gt[b].data_ptr(), vin, 1, B, abi.KEYHASH_BINROW_BIGINT,
+                                             128, world, pk.data_ptr(), pt.data_ptr(), vout, counts.data_ptr(),
+                                             workspace.data_ptr(), workspace.numel(), torch.cuda.current_stream(dev).cuda_stream))
+        rc = torch.empty_like(counts)
+        dist.all_to_all_single(rc, counts)
+        send = counts.tolist()
+        recv = rc.tolist()
+        n = sum(recv)
+        rk = torch.empty(n, dtype=torch.int64, device=dev)
+        rt = torch.empty_like(rk)
+        rv = torch.empty_like(rk)
+        dist.all_to_all_single(rk, pk, recv, send)
+        dist.all_to_all_single(rt, pt, recv, send)
+        if nv:
+            dist.all_to_all_single(rv, pv, recv, send)
+        return rk, rt, rv
+
+    def global_watermark(b):
+        w = torch.tensor([watermark(b, wl["rate"])], dtype=torch.int64, device=dev)
+        if world > 1:  # StatusWatermarkValve: min over input channels
+            dist.all_reduce(w, op=dist.ReduceOp.MIN)
+            return int(w.item())
+        return int(w[0])
+
+    out_cap = 2 * keys_total // world + (1 << 20)
+    if wl["window"][0] == "CUMULATE":
+        out_cap = keys_total + (1 << 20)
+
+    def run(first, nsteps, handle, timed):
+        ext = torch.cuda.ExternalStream(handle.stream_ptr, device=dev)
+        ev = []
+        for b in range(first, first + nsteps):
+            k, t, v = exchange(b)
+            wm = global_watermark(b)
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e2 = torch.cuda.Event(enable_timing=True)
+                ext.wait_stream(torch.cuda.current_stream(dev))
+                e0.record(ext)
+            handle.push_device(k, t, [v] if nv else [])
+            if timed:
+                e1.record(ext)
+            handle.reset_results()       # blackhole sink: results of the previous watermark consumed
+            handle.advance(wm)
+            if timed:
+                e2.record(ext)
+                ev.append((e0, e1, e2))
+        return ev
+
+    cfg = build_config(wl, world, rank, keys_total, out_cap)
+    # warmup on its own operator instance (first batches of the same stream)
+    if args.warmup:
+        hw = WindowAggHandle(cfg)
+        run(0, args.warmup, hw, False)
+        hw.sync()
+        hw.close()
+    h = WindowAggHandle(cfg)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    events = run(args.warmup, args.steps, h, True)
+    h.sync()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    st = h.stats()
+    ingest_ms = [a.elapsed_time(b_) for a, b_, _ in events]
+    fire_ms = [b_.elapsed_time(c) for _, b_, c in events]
+    if st["error_flags"]:
+        raise SystemExit(f"device error flags {st['error_flags']}")
+
+    n_total = args.steps * B * world
+    value = n_total / elapsed
+    # ---------------- roofline of the segmented-reduce (ingest) kernel ----------------------
+    w_partial = 8 * (2 + wl["nw"])   # partial = key, slice, accumulator words (8 B each)
+    g_per = st["partials_emitted"] / args.steps
+    n_per = st["rows_ingested"] / args.steps if "rows_ingested" in st else B
+    bytes_per_launch = n_per * wl["w_in"] + g_per * w_partial
+    avg_ingest_s = float(np.mean(ingest_ms)) / 1e3
+    achieved = bytes_per_launch / avg_ingest_s / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("workload") == args.workload:
+                traffic = tj.get("k_ingest_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        v, n, dt, _ = cpu_baseline(wl, args.cpu_sample)
+        cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
+               "sample": f"first {n} events of the same {args.workload} stream through the C++ oracle "
+                         f"(oracle/flinkwin_oracle.cpp, single thread), {dt:.1f} s"}
+
+    if rank == 0:
+        line = {
+            "metric": "windowed-agg events/sec (whole node) at 1/2/4/8 GPU + % of HBM peak",
+            "value": value, "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64" if wl["value_kind"] != 1 else "f64",
+            "data": "synthetic (SplitMix64 Nexmark-shaped generator, seed 42, device-resident)",
+            "config": {"workload": f"{args.workload}: {wl['desc']}", "events_per_gpu_per_step": B,
+                       "keys_total": keys_total, "rate_per_gpu_ev_s": wl["rate"],
+                       "parallelism": f"key-group sharded x{world}" + (" + RCCL all-to-all" if world > 1 else ""),
+                       "max_parallelism": 128, "superbuckets": st["num_superbuckets"]},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "kernel": "k_ingest (slice assign + LDS segmented reduce + partition)",
+                         "algorithmic_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ingest_s * 1e6},
+            "cpu_baseline": cpu,
+            "breakdown_ms_per_step": {"ingest": float(np.mean(ingest_ms)), "watermark_fire": float(np.mean(fire_ms))},
+        }
+        print(json.dumps(line), flush=True)
+    h.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,85 @@
+"""ctypes binding of libflinkwin.so (the HIP/gfx950 library built in-tree from flink_amd/csrc).
+
+There is no CPU fallback: if the library is missing or cannot be loaded this module raises,
+so a GPU run can never silently take another path.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libflinkwin.so")
+
+
+class FlinkWinError(RuntimeError):
+    """Raised for any non-zero libflinkwin status (the Java shim maps this to Exception)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libflinkwin error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not found: build it with `make -C flink_amd/csrc` "
+                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
+    P = C.POINTER
+    sig = {
+        "fw_create": (i32, [P(abi.fw_config), P(vp)]),
+        "fw_destroy": (i32, [vp]),
+        "fw_last_error": (C.c_char_p, []),
+        "fw_abi_version": (i32, []),
+        "fw_get_stream": (vp, [vp]),
+        "fw_sync": (i32, [vp]),
+        "fw_initialize_watermark": (i32, [vp, i64]),
+        "fw_reserve": (i32, [vp, i64, P(abi.fw_host_cols)]),
+        "fw_commit": (i32, [vp, i64]),
+        "fw_push_device": (i32, [vp, i64, vp, vp, vp, vp]),
+        "fw_advance": (i32, [vp, i64]),
+        "fw_flush": (i32, [vp]),
+        "fw_results": (i32, [vp, P(abi.fw_result), i32]),
+        "fw_results_reset": (i32, [vp]),
+        "fw_get_stats": (i32, [vp, P(abi.fw_stats)]),
+        "fw_snapshot": (i32, [vp, vp, i64, P(i64)]),
+        "fw_restore": (i32, [vp, vp, i64]),
+        "fw_assign_key_groups": (i32, [vp, vp, i64, i32, i32, i32, vp, vp, vp]),
+        "fw_partition_by_dest": (i32, [vp, vp, vp, i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp]),
+        "fw_partition_workspace_bytes": (i64, [i64, i32]),
+        "fw_generate": (i32, [P(abi.fw_gen_params), i64, i64, vp, vp, vp, vp]),
+        "fw_host_key_group": (i32, [i32, i64, i32, i32]),
+        "fw_host_window_start": (i64, [i64, i64, i64]),
+        "fw_host_next_trigger_watermark": (i64, [i64, i64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.fw_abi_version() != abi.FW_ABI_VERSION:
+        raise ImportError("libflinkwin ABI version mismatch")
+    _lib = L
+    return L
+
+
+# every symbol the public header declares (tests check they are exported)
+EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
+            "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_advance",
+            "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_snapshot", "fw_restore",
+            "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_workspace_bytes",
+            "fw_generate", "fw_host_key_group", "fw_host_window_start",
+            "fw_host_next_trigger_watermark"]
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().fw_last_error()
+        raise FlinkWinError(rc, msg.decode() if msg else "")
+    return rc

@@ -93,7 +93,8 @@ class fw_stats(C.Structure):
     _fields_ = [("current_watermark", C.c_int64), ("next_trigger_progress", C.c_int64),
                 ("num_late_records_dropped", C.c_int64), ("live_state_entries", C.c_int64),
                 ("pending_rows", C.c_int64), ("results_available", C.c_int64),
-                ("num_fired_windows", C.c_int64), ("error_flags", C.c_int32),
+                ("num_fired_windows", C.c_int64), ("partials_emitted", C.c_int64),
+                ("error_flags", C.c_int32),
                 ("num_superbuckets", C.c_int32)]
 
 

@@ -1,0 +1,697 @@
+// fw_api.hip -- C-ABI of libflinkwin (include/flinkwin.h): one handle per operator subtask.
+//
+// The handle owns a HIP stream, the device control block, the partial buffer that stands in
+// for RecordsWindowBuffer (TR/operators/aggregate/window/buffers/RecordsWindowBuffer.java), the
+// HBM slice-state table that replaces HeapKeyedStateBackend for this operator
+// (FR/runtime/state/heap/HeapKeyedStateBackend.java:85) together with its timers
+// (InternalTimerServiceImpl), and the result buffer.  Calls are asynchronous on the handle's
+// stream except where a host value is needed (results, stats, snapshot).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fw_internal.h"
+
+using namespace fw;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return fail(FW_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+int64_t next_pow2(int64_t x) {
+    int64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int64_t gcd64(int64_t a, int64_t b) {
+    while (b) {
+        int64_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a < 0 ? -a : a;
+}
+
+int round_nw(int nw) { return nw <= 1 ? 1 : nw <= 2 ? 2 : nw <= 4 ? 4 : 8; }
+
+}  // namespace
+
+struct fw_handle {
+    fw_config cfg;
+    hipStream_t stream = nullptr;
+    WinDesc win{};
+    KeySpace ks{};
+    WordDesc wd{};
+    AggDesc ad{};
+    int nv = 0;
+    int slot_col[MAX_KCOLS] = {0, 0, 0, 0};
+    int nw_t = 1;  // template word count (layout stride)
+    int64_t max_chunks = 0;
+    int cap_e = 1024;
+    bool always_flush = false;
+
+    Ctrl* ctrl = nullptr;
+    uint64_t* parts = nullptr;
+    uint32_t* off = nullptr;
+    int64_t* treq = nullptr;
+    int64_t treq_cap = 0;
+    uint64_t* state = nullptr;
+    int32_t* state_count = nullptr;
+    int64_t* sb_min_timer = nullptr;
+    int64_t* out_key = nullptr;
+    int64_t* out_ws = nullptr;
+    int64_t* out_we = nullptr;
+    uint64_t* out_val[FW_MAX_AGGS] = {};
+    uint32_t* out_null = nullptr;
+    int64_t out_cap = 0;
+
+    // host-staged ingest (double-buffered pinned columns)
+    int64_t stage_cap = 0;
+    int stage_cur = 0;
+    int64_t* h_key[2] = {};
+    int64_t* h_ts[2] = {};
+    int32_t* h_kh[2] = {};
+    int64_t* h_val[2][FW_MAX_COLS] = {};
+    hipEvent_t stage_ev[2] = {};
+    int64_t* d_key = nullptr;
+    int64_t* d_ts = nullptr;
+    int32_t* d_kh = nullptr;
+    int64_t* d_val[FW_MAX_COLS] = {};
+    int64_t reserved = -1;
+
+    // host copies of results
+    std::vector<int64_t> r_key, r_ws, r_we;
+    std::vector<uint64_t> r_val[FW_MAX_AGGS];
+    std::vector<uint32_t> r_null;
+
+    int64_t chunks_ub = 0;  // upper bound of device pending_chunks
+    int64_t host_cur = INT64_MIN;
+};
+
+namespace {
+
+int validate_and_plan(fw_handle* h) {
+    const fw_config& c = h->cfg;
+    if (c.abi_version != FW_ABI_VERSION) return fail(FW_E_INVALID, "abi_version %d != %d", c.abi_version, FW_ABI_VERSION);
+    if (c.api != FW_API_SQL && c.api != FW_API_DATASTREAM) return fail(FW_E_INVALID, "bad api %d", c.api);
+    if (c.n_aggs < 1 || c.n_aggs > FW_MAX_AGGS) return fail(FW_E_INVALID, "n_aggs %d out of range", c.n_aggs);
+    if (c.n_value_cols < 0 || c.n_value_cols > FW_MAX_COLS) return fail(FW_E_INVALID, "n_value_cols out of range");
+    if (c.max_parallelism < 1 || c.max_parallelism > 32768) return fail(FW_E_INVALID, "max_parallelism out of range");
+    if (c.parallelism < 1 || c.parallelism > c.max_parallelism) return fail(FW_E_INVALID, "parallelism out of range");
+    if (c.subtask_index < 0 || c.subtask_index >= c.parallelism) return fail(FW_E_INVALID, "subtask_index out of range");
+    if (c.key_hash < FW_KEYHASH_LONG || c.key_hash > FW_KEYHASH_PRECOMPUTED) return fail(FW_E_INVALID, "bad key_hash");
+    if (c.size_ms <= 0) return fail(FW_E_INVALID, "window size must be > 0");
+    // ---- window (SliceAssigners constructors' argument checks)
+    WinDesc& w = h->win;
+    w.kind = c.window_kind;
+    w.size = c.size_ms;
+    w.offset = c.offset_ms;
+    switch (c.window_kind) {
+        case FW_WIN_TUMBLE:
+            if (!(c.offset_ms > -c.size_ms && c.offset_ms < c.size_ms))
+                return fail(FW_E_INVALID, "Tumbling Window parameters must satisfy abs(offset) < size");
+            w.interval = c.size_ms;
+            w.n_slices = 1;
+            if (c.api == FW_API_DATASTREAM) w.offset = c.offset_ms % c.size_ms;
+            break;
+        case FW_WIN_HOP:
+            if (c.slide_ms <= 0) return fail(FW_E_INVALID, "Hopping Window must satisfy slide > 0 and size > 0");
+            if (c.size_ms % c.slide_ms != 0)
+                return fail(FW_E_INVALID, "Slicing Hopping Window requires size must be an integral multiple of slide");
+            w.interval = gcd64(c.size_ms, c.slide_ms);
+            w.n_slices = (int32_t)(c.size_ms / w.interval);
+            break;
+        case FW_WIN_CUMULATE:
+            if (c.api != FW_API_SQL) return fail(FW_E_INVALID, "CUMULATE is a SQL window");
+            if (c.slide_ms <= 0 || c.size_ms % c.slide_ms != 0)
+                return fail(FW_E_INVALID, "Cumulative Window requires maxSize must be an integral multiple of step");
+            w.interval = c.slide_ms;
+            w.n_slices = (int32_t)(c.size_ms / c.slide_ms);
+            break;
+        default: return fail(FW_E_INVALID, "bad window kind %d", c.window_kind);
+    }
+    w.slice_div = make_udiv((uint64_t)w.interval);
+    w.size_div = make_udiv((uint64_t)w.size);
+    h->always_flush = c.api == FW_API_DATASTREAM;
+
+    // ---- aggregates -> accumulator words
+    WordDesc& wd = h->wd;
+    AggDesc& ad = h->ad;
+    wd.nw = 0;
+    int nslot = 0;
+    auto slot_of = [&](int col) -> int {
+        for (int s = 0; s < nslot; s++)
+            if (h->slot_col[s] == col) return s;
+        if (nslot >= MAX_KCOLS) return -1;
+        h->slot_col[nslot] = col;
+        return nslot++;
+    };
+    auto word_of = [&](int op, int slot) -> int {
+        for (int i = 0; i < wd.nw; i++)
+            if (wd.op[i] == op && (op == W_CNT || wd.col[i] == slot)) return i;
+        if (wd.nw >= MAX_WORDS) return -1;
+        wd.op[wd.nw] = op;
+        wd.col[wd.nw] = op == W_CNT ? 0 : slot;
+        return wd.nw++;
+    };
+    ad.n = c.n_aggs;
+    ad.count_word = -1;
+    ad.count_star_word = -1;
+    for (int g = 0; g < c.n_aggs; g++) {
+        const fw_agg_desc& d = c.aggs[g];
+        ad.kind[g] = d.kind;
+        ad.type[g] = d.type;
+        ad.w1[g] = -1;
+        if (d.type < FW_T_I64 || d.type > FW_T_I32) return fail(FW_E_INVALID, "agg %d: bad type", g);
+        int slot = 0;
+        if (d.kind != FW_AGG_COUNT_STAR) {
+            if (d.input_col < 0 || d.input_col >= c.n_value_cols) return fail(FW_E_INVALID, "agg %d: bad input_col", g);
+            if (c.value_col_types[d.input_col] != d.type)
+                return fail(FW_E_INVALID, "agg %d: type does not match value column type", g);
+            if (d.kind != FW_AGG_COUNT) {
+                slot = slot_of(d.input_col);
+                if (slot < 0) return fail(FW_E_INVALID, "more than %d distinct value columns", MAX_KCOLS);
+            }
+        }
+        const bool f = d.type == FW_T_F64;
+        int w0 = -1;
+        switch (d.kind) {
+            case FW_AGG_COUNT_STAR:
+            case FW_AGG_COUNT: w0 = word_of(W_CNT, 0); break;
+            case FW_AGG_SUM: w0 = word_of(f ? W_SUM_F : W_SUM_I, slot); break;
+            case FW_AGG_MIN: w0 = word_of(f ? W_MIN_D : W_MIN_I, slot); break;
+            case FW_AGG_MAX: w0 = word_of(f ? W_MAX_D : W_MAX_I, slot); break;
+            case FW_AGG_AVG:
+                w0 = word_of(f ? W_SUM_F : W_SUM_I, slot);
+                ad.w1[g] = word_of(W_CNT, 0);
+                break;
+            default: return fail(FW_E_INVALID, "agg %d: unsupported kind %d", g, d.kind);
+        }
+        if (c.api == FW_API_DATASTREAM && (d.kind == FW_AGG_AVG || d.kind == FW_AGG_COUNT))
+            return fail(FW_E_INVALID, "DataStream built-in aggregations are sum/min/max (and COUNT_STAR)");
+        if (w0 < 0 || (d.kind == FW_AGG_AVG && ad.w1[g] < 0)) return fail(FW_E_INVALID, "too many accumulator words");
+        ad.w0[g] = w0;
+    }
+    if (c.count_star_index >= 0) {
+        if (c.count_star_index >= c.n_aggs) return fail(FW_E_INVALID, "count_star_index out of range");
+        const int k = c.aggs[c.count_star_index].kind;
+        if (k != FW_AGG_COUNT_STAR && k != FW_AGG_COUNT) return fail(FW_E_INVALID, "count_star_index is not a COUNT");
+        ad.count_star_word = ad.w0[c.count_star_index];
+    } else if (c.window_kind == FW_WIN_HOP) {
+        if (c.api == FW_API_SQL) return fail(FW_E_INVALID, "Hopping window requires a COUNT(*) in the aggregate functions.");
+        // DataStream sliding windows emit a window iff it received an element: hidden COUNT(*)
+        ad.count_star_word = word_of(W_CNT, 0);
+        if (ad.count_star_word < 0) return fail(FW_E_INVALID, "too many accumulator words");
+    }
+    for (int i = 0; i < wd.nw; i++)
+        if (wd.op[i] == W_CNT) ad.count_word = i;
+    h->nv = nslot;
+    h->nw_t = round_nw(wd.nw);
+    for (int i = wd.nw; i < MAX_WORDS; i++) {
+        wd.op[i] = W_CNT;
+        wd.col[i] = 0;
+    }
+
+    // ---- key space: this subtask's key groups, split into superbuckets
+    KeySpace& ks = h->ks;
+    ks.hash_kind = c.key_hash;
+    ks.max_p = c.max_parallelism;
+    ks.kg_start = (c.subtask_index * c.max_parallelism + c.parallelism - 1) / c.parallelism;
+    const int kg_end = ((c.subtask_index + 1) * c.max_parallelism - 1) / c.parallelism;
+    ks.n_kg = kg_end - ks.kg_start + 1;
+    const int64_t cap_target = std::max<int64_t>(c.state_capacity, 1024);
+    // aim for <= ~60% occupancy of the per-superbucket LDS table
+    h->cap_e = (h->nw_t <= 2 && cap_target / ks.n_kg > 16384 * 600) ? 2048 : 1024;
+    int64_t per_kg = (cap_target + ks.n_kg - 1) / ks.n_kg;
+    int64_t sbk = next_pow2((per_kg + (h->cap_e * 6 / 10) - 1) / (h->cap_e * 6 / 10));
+    while ((int64_t)ks.n_kg * sbk > 16384 && sbk > 1) sbk >>= 1;
+    ks.sb_per_kg_log2 = 0;
+    while ((1ll << ks.sb_per_kg_log2) < sbk) ks.sb_per_kg_log2++;
+    ks.n_sb = ks.n_kg << ks.sb_per_kg_log2;
+    if (c.max_batch_rows <= 0) return fail(FW_E_INVALID, "max_batch_rows must be > 0");
+    if (c.output_capacity <= 0) return fail(FW_E_INVALID, "output_capacity must be > 0");
+    const int64_t rows = (int64_t)BLOCK * ingest_rpt(h->nv);
+    h->max_chunks = 8 * ((c.max_batch_rows + rows - 1) / rows) + 8;
+    h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
+    h->out_cap = c.output_capacity;
+    h->stage_cap = c.max_batch_rows;
+    return FW_OK;
+}
+
+template <typename T>
+int dalloc(T** p, size_t count) {
+    void* v = nullptr;
+    HIP_TRY(hipMalloc(&v, std::max<size_t>(count, 1) * sizeof(T)));
+    *p = (T*)v;
+    return FW_OK;
+}
+
+int allocate(fw_handle* h) {
+    const fw_config& c = h->cfg;
+    HIP_TRY(hipSetDevice(c.device));
+    HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    int rc;
+    const int PW = 2 + h->nw_t, PWE = 3 + h->nw_t;
+    if ((rc = dalloc(&h->ctrl, 1))) return rc;
+    if ((rc = dalloc(&h->parts, (size_t)h->max_chunks * K3_CHUNK * PW))) return rc;
+    if ((rc = dalloc(&h->off, (size_t)(h->ks.n_sb + 1) * h->max_chunks))) return rc;
+    if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
+    if ((rc = dalloc(&h->state, (size_t)h->ks.n_sb * h->cap_e * PWE))) return rc;
+    if ((rc = dalloc(&h->state_count, h->ks.n_sb))) return rc;
+    if ((rc = dalloc(&h->sb_min_timer, h->ks.n_sb))) return rc;
+    if ((rc = dalloc(&h->out_key, h->out_cap))) return rc;
+    if ((rc = dalloc(&h->out_ws, h->out_cap))) return rc;
+    if ((rc = dalloc(&h->out_we, h->out_cap))) return rc;
+    if ((rc = dalloc(&h->out_null, h->out_cap))) return rc;
+    for (int g = 0; g < c.n_aggs; g++)
+        if ((rc = dalloc(&h->out_val[g], h->out_cap))) return rc;
+    HIP_TRY(hipMemsetAsync(h->state_count, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
+    std::vector<int64_t> inf(h->ks.n_sb, INT64_MAX);
+    HIP_TRY(hipMemcpyAsync(h->sb_min_timer, inf.data(), sizeof(int64_t) * h->ks.n_sb, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(launch_init_ctrl(h->ctrl, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return FW_OK;
+}
+
+int alloc_staging(fw_handle* h) {
+    if (h->d_key) return FW_OK;
+    const fw_config& c = h->cfg;
+    const size_t n = (size_t)h->stage_cap;
+    for (int b = 0; b < 2; b++) {
+        HIP_TRY(hipHostMalloc((void**)&h->h_key[b], n * 8, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&h->h_ts[b], n * 8, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&h->h_kh[b], n * 4, hipHostMallocDefault));
+        for (int v = 0; v < c.n_value_cols; v++) HIP_TRY(hipHostMalloc((void**)&h->h_val[b][v], n * 8, hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&h->stage_ev[b], hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(h->stage_ev[b], h->stream));
+    }
+    int rc;
+    if ((rc = dalloc(&h->d_key, n))) return rc;
+    if ((rc = dalloc(&h->d_ts, n))) return rc;
+    if ((rc = dalloc(&h->d_kh, n))) return rc;
+    for (int v = 0; v < c.n_value_cols; v++)
+        if ((rc = dalloc(&h->d_val[v], n))) return rc;
+    return FW_OK;
+}
+
+int read_ctrl(fw_handle* h, Ctrl* out) {
+    HIP_TRY(hipMemcpyAsync(out, h->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (out->error) {
+        return fail(FW_E_CAPACITY, "device capacity exceeded (error bits 0x%x:%s%s%s%s)", out->error,
+                    out->error & ERR_CHUNKS ? " partial-buffer" : "", out->error & ERR_STATE ? " state-table" : "",
+                    out->error & ERR_OUTPUT ? " result-buffer" : "", out->error & ERR_TREQ ? " timer-requests" : "");
+    }
+    return FW_OK;
+}
+
+MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
+    MergeArgs a{};
+    a.ctrl = h->ctrl;
+    a.parts = h->parts;
+    a.off = h->off;
+    a.max_chunks = h->max_chunks;
+    a.treq = h->treq;
+    a.state = h->state;
+    a.state_count = h->state_count;
+    a.sb_min_timer = h->sb_min_timer;
+    a.n_sb = h->ks.n_sb;
+    a.cap_e = h->cap_e;
+    a.win = h->win;
+    a.wd = h->wd;
+    a.ad = h->ad;
+    a.always_flush = h->always_flush;
+    a.out_key = h->out_key;
+    a.out_ws = h->out_ws;
+    a.out_we = h->out_we;
+    for (int g = 0; g < FW_MAX_AGGS; g++) a.out_val[g] = h->out_val[g] ? h->out_val[g] : h->out_val[0];
+    a.out_null = h->out_null;
+    a.out_cap = h->out_cap;
+    a.wm = wm;
+    a.force_flush = force;
+    return a;
+}
+
+int force_flush(fw_handle* h) {
+    HIP_TRY(launch_merge_fire(merge_args(h, INT64_MIN, 1), h->stream));
+    h->chunks_ub = 0;
+    return FW_OK;
+}
+
+int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int32_t* kh, const void* const* vals) {
+    const int64_t per = h->max_chunks / 2 * ((int64_t)BLOCK * ingest_rpt(h->nv));  // split very large pushes
+    for (int64_t o = 0; o < n; o += per) {
+        const int64_t m = std::min(per, n - o);
+        const int64_t rows = (int64_t)BLOCK * ingest_rpt(h->nv);
+        const int64_t chunks = (m + rows - 1) / rows;
+        if (h->chunks_ub + chunks > h->max_chunks) {
+            Ctrl c;
+            int rc = read_ctrl(h, &c);
+            if (rc) return rc;
+            h->chunks_ub = c.pending_chunks;
+            if (h->chunks_ub + chunks > h->max_chunks) {
+                // buffer full: flush into state (RecordsWindowBuffer.addElement EOFException path)
+                if ((rc = force_flush(h))) return rc;
+            }
+        }
+        IngestArgs a{};
+        a.key = key + o;
+        a.ts = ts + o;
+        a.khash = kh ? kh + o : nullptr;
+        for (int s = 0; s < MAX_KCOLS; s++)
+            a.vals[s] = s < h->nv ? (const uint64_t*)vals[h->slot_col[s]] + o : nullptr;
+        a.n = m;
+        a.win = h->win;
+        a.ks = h->ks;
+        a.wd = h->wd;
+        a.nv = h->nv;
+        a.ctrl = h->ctrl;
+        a.parts = h->parts;
+        a.off = h->off;
+        a.max_chunks = h->max_chunks;
+        a.treq = h->treq;
+        a.treq_cap = h->treq_cap;
+        // the kernel template stride must match the handle layout
+        WordDesc wd = h->wd;
+        wd.nw = h->wd.nw;
+        a.wd = wd;
+        HIP_TRY(launch_ingest(a, h->stream));
+        h->chunks_ub += chunks;
+    }
+    return FW_OK;
+}
+
+}  // namespace
+
+// ======================================================================================
+extern "C" {
+
+const char* fw_last_error(void) { return g_err.c_str(); }
+int fw_abi_version(void) { return FW_ABI_VERSION; }
+
+int fw_create(const fw_config* cfg, fw_handle** out) {
+    if (!cfg || !out) return fail(FW_E_INVALID, "null argument");
+    *out = nullptr;
+    fw_handle* h = new fw_handle();
+    h->cfg = *cfg;
+    int rc = validate_and_plan(h);
+    if (!rc) rc = allocate(h);
+    if (rc) {
+        std::string keep = g_err;
+        fw_destroy(h);
+        g_err = keep;
+        return rc;
+    }
+    *out = h;
+    return FW_OK;
+}
+
+int fw_destroy(fw_handle* h) {
+    if (!h) return FW_OK;
+    if (h->stream) hipStreamSynchronize(h->stream);
+    hipFree(h->ctrl);
+    hipFree(h->parts);
+    hipFree(h->off);
+    hipFree(h->treq);
+    hipFree(h->state);
+    hipFree(h->state_count);
+    hipFree(h->sb_min_timer);
+    hipFree(h->out_key);
+    hipFree(h->out_ws);
+    hipFree(h->out_we);
+    hipFree(h->out_null);
+    for (int g = 0; g < FW_MAX_AGGS; g++) hipFree(h->out_val[g]);
+    for (int b = 0; b < 2; b++) {
+        hipHostFree(h->h_key[b]);
+        hipHostFree(h->h_ts[b]);
+        hipHostFree(h->h_kh[b]);
+        for (int v = 0; v < FW_MAX_COLS; v++) hipHostFree(h->h_val[b][v]);
+        if (h->stage_ev[b]) hipEventDestroy(h->stage_ev[b]);
+    }
+    hipFree(h->d_key);
+    hipFree(h->d_ts);
+    hipFree(h->d_kh);
+    for (int v = 0; v < FW_MAX_COLS; v++) hipFree(h->d_val[v]);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return FW_OK;
+}
+
+void* fw_get_stream(fw_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int fw_sync(fw_handle* h) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    Ctrl c;
+    return read_ctrl(h, &c);
+}
+
+int fw_initialize_watermark(fw_handle* h, int64_t watermark) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    HIP_TRY(hipMemcpyAsync(&h->ctrl->cur, &watermark, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->host_cur = watermark;
+    return FW_OK;
+}
+
+int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    if (n < 0 || n > h->stage_cap) return fail(FW_E_INVALID, "reserve %lld rows > max_batch_rows %lld", (long long)n, (long long)h->stage_cap);
+    int rc = alloc_staging(h);
+    if (rc) return rc;
+    const int b = h->stage_cur;
+    HIP_TRY(hipEventSynchronize(h->stage_ev[b]));  // previous H2D from this buffer has finished
+    memset(out, 0, sizeof *out);
+    out->key = h->h_key[b];
+    out->ts = h->h_ts[b];
+    out->key_hash = h->h_kh[b];
+    for (int v = 0; v < h->cfg.n_value_cols; v++) out->values[v] = h->h_val[b][v];
+    h->reserved = n;
+    return FW_OK;
+}
+
+int fw_commit(fw_handle* h, int64_t n) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    if (h->reserved < 0 || n > h->reserved || n < 0) return fail(FW_E_STATE, "commit without matching reserve");
+    h->reserved = -1;
+    const int b = h->stage_cur;
+    h->stage_cur ^= 1;
+    if (n == 0) return FW_OK;
+    // device staging is reused across commits; ingest of the previous commit is ordered before
+    // these copies on the same stream
+    HIP_TRY(hipMemcpyAsync(h->d_key, h->h_key[b], n * 8, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->d_ts, h->h_ts[b], n * 8, hipMemcpyHostToDevice, h->stream));
+    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED)
+        HIP_TRY(hipMemcpyAsync(h->d_kh, h->h_kh[b], n * 4, hipMemcpyHostToDevice, h->stream));
+    for (int s = 0; s < h->nv; s++) {
+        const int v = h->slot_col[s];
+        HIP_TRY(hipMemcpyAsync(h->d_val[v], h->h_val[b][v], n * 8, hipMemcpyHostToDevice, h->stream));
+    }
+    HIP_TRY(hipEventRecord(h->stage_ev[b], h->stream));
+    const void* vals[FW_MAX_COLS];
+    for (int v = 0; v < FW_MAX_COLS; v++) vals[v] = h->d_val[v];
+    return push(h, n, h->d_key, h->d_ts, h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED ? h->d_kh : nullptr, vals);
+}
+
+int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t* d_ts, const int32_t* d_key_hash,
+                   const void* const* d_values) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    if (n < 0) return fail(FW_E_INVALID, "negative n");
+    if (n == 0) return FW_OK;
+    if (!d_key || !d_ts) return fail(FW_E_INVALID, "null key/ts column");
+    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED && !d_key_hash) return fail(FW_E_INVALID, "key_hash column required");
+    if (h->nv > 0 && !d_values) return fail(FW_E_INVALID, "value columns required");
+    for (int s = 0; s < h->nv; s++)
+        if (!d_values[h->slot_col[s]]) return fail(FW_E_INVALID, "value column %d is NULL", h->slot_col[s]);
+    return push(h, n, d_key, d_ts, d_key_hash, d_values);
+}
+
+int fw_advance(fw_handle* h, int64_t watermark) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    HIP_TRY(launch_merge_fire(merge_args(h, watermark, 0), h->stream));
+    if (watermark > h->host_cur) h->host_cur = watermark;
+    return FW_OK;
+}
+
+int fw_flush(fw_handle* h) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    return force_flush(h);
+}
+
+int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    Ctrl c;
+    int rc = read_ctrl(h, &c);
+    if (rc) return rc;
+    const int64_t n = std::min<int64_t>((int64_t)c.out_count, h->out_cap);
+    memset(out, 0, sizeof *out);
+    out->n = n;
+    const int na = h->cfg.n_aggs;
+    if (!copy_to_host) {
+        out->key = h->out_key;
+        out->window_start = h->out_ws;
+        out->window_end = h->out_we;
+        for (int g = 0; g < na; g++) out->values[g] = (int64_t*)h->out_val[g];
+        out->null_mask = h->out_null;
+        return FW_OK;
+    }
+    h->r_key.resize(n);
+    h->r_ws.resize(n);
+    h->r_we.resize(n);
+    h->r_null.resize(n);
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(h->r_key.data(), h->out_key, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->r_ws.data(), h->out_ws, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->r_we.data(), h->out_we, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->r_null.data(), h->out_null, n * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    for (int g = 0; g < na; g++) {
+        h->r_val[g].resize(n);
+        if (n) HIP_TRY(hipMemcpyAsync(h->r_val[g].data(), h->out_val[g], n * 8, hipMemcpyDeviceToHost, h->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    out->key = h->r_key.data();
+    out->window_start = h->r_ws.data();
+    out->window_end = h->r_we.data();
+    for (int g = 0; g < na; g++) out->values[g] = (int64_t*)h->r_val[g].data();
+    out->null_mask = h->r_null.data();
+    return FW_OK;
+}
+
+int fw_results_reset(fw_handle* h) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    HIP_TRY(hipMemsetAsync(&h->ctrl->out_count, 0, sizeof(uint64_t), h->stream));
+    return FW_OK;
+}
+
+int fw_get_stats(fw_handle* h, fw_stats* out) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    Ctrl c;
+    HIP_TRY(hipMemcpyAsync(&c, h->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    memset(out, 0, sizeof *out);
+    out->current_watermark = c.cur;
+    out->next_trigger_progress = c.ntp;
+    out->num_late_records_dropped = (int64_t)c.late_dropped;
+    out->live_state_entries = c.live_entries;
+    out->pending_rows = (int64_t)c.pending_rows;
+    out->results_available = std::min<int64_t>((int64_t)c.out_count, h->out_cap);
+    out->num_fired_windows = (int64_t)c.fired;
+    out->partials_emitted = (int64_t)c.partials;
+    out->error_flags = (int32_t)c.error;
+    out->num_superbuckets = h->ks.n_sb;
+    return FW_OK;
+}
+
+// ---- snapshot: [header][state_count[n_sb]][entries of sb 0][entries of sb 1]...
+struct SnapHeader {
+    uint64_t magic;
+    int32_t version, n_sb, cap_e, pwe;
+    int64_t cur, late_dropped, fired, live;
+};
+static const uint64_t SNAP_MAGIC = 0x464c4b57494e3031ull;  // "FLKWIN01"
+
+int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
+    if (!h || !size) return fail(FW_E_INVALID, "null argument");
+    int rc = force_flush(h);  // prepareSnapshotPreBarrier -> windowBuffer.flush()
+    if (rc) return rc;
+    Ctrl c;
+    if ((rc = read_ctrl(h, &c))) return rc;
+    const int nsb = h->ks.n_sb, pwe = 3 + h->nw_t;
+    std::vector<int32_t> cnt(nsb);
+    HIP_TRY(hipMemcpy(cnt.data(), h->state_count, sizeof(int32_t) * nsb, hipMemcpyDeviceToHost));
+    int64_t total = 0;
+    for (int s = 0; s < nsb; s++) total += cnt[s];
+    const int64_t need = (int64_t)sizeof(SnapHeader) + 4ll * nsb + total * pwe * 8;
+    *size = need;
+    if (!buf) return FW_OK;
+    if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
+    SnapHeader hd{SNAP_MAGIC, 1, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, (int64_t)c.fired, total};
+    char* p = (char*)buf;
+    memcpy(p, &hd, sizeof hd);
+    p += sizeof hd;
+    memcpy(p, cnt.data(), 4ll * nsb);
+    p += 4ll * nsb;
+    for (int s = 0; s < nsb; s++) {
+        if (!cnt[s]) continue;
+        const size_t bytes = (size_t)cnt[s] * pwe * 8;
+        HIP_TRY(hipMemcpy(p, h->state + (size_t)s * h->cap_e * pwe, bytes, hipMemcpyDeviceToHost));
+        p += bytes;
+    }
+    return FW_OK;
+}
+
+int fw_restore(fw_handle* h, const void* buf, int64_t size) {
+    if (!h || !buf) return fail(FW_E_INVALID, "null argument");
+    SnapHeader hd;
+    if (size < (int64_t)sizeof hd) return fail(FW_E_INVALID, "snapshot truncated");
+    memcpy(&hd, buf, sizeof hd);
+    const int nsb = h->ks.n_sb, pwe = 3 + h->nw_t;
+    if (hd.magic != SNAP_MAGIC || hd.n_sb != nsb || hd.pwe != pwe || hd.cap_e != h->cap_e)
+        return fail(FW_E_INVALID, "snapshot layout does not match this operator configuration");
+    const char* p = (const char*)buf + sizeof hd;
+    std::vector<int32_t> cnt(nsb);
+    memcpy(cnt.data(), p, 4ll * nsb);
+    p += 4ll * nsb;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    std::vector<int64_t> mins(nsb, INT64_MAX);
+    for (int s = 0; s < nsb; s++) {
+        if (!cnt[s]) continue;
+        const size_t bytes = (size_t)cnt[s] * pwe * 8;
+        const uint64_t* e = (const uint64_t*)p;
+        for (int i = 0; i < cnt[s]; i++)
+            if (e[(size_t)i * pwe + 2] & F_TIMER) mins[s] = std::min(mins[s], (int64_t)e[(size_t)i * pwe + 1]);
+        HIP_TRY(hipMemcpy(h->state + (size_t)s * h->cap_e * pwe, p, bytes, hipMemcpyHostToDevice));
+        p += bytes;
+    }
+    HIP_TRY(hipMemcpy(h->state_count, cnt.data(), 4ll * nsb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->sb_min_timer, mins.data(), 8ll * nsb, hipMemcpyHostToDevice));
+    HIP_TRY(launch_init_ctrl(h->ctrl, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    Ctrl c;
+    HIP_TRY(hipMemcpy(&c, h->ctrl, sizeof c, hipMemcpyDeviceToHost));
+    c.cur = hd.cur;  // union-list watermark state (WindowAggOperator.initializeState :183-206)
+    c.ntp = INT64_MIN;
+    c.late_dropped = (uint64_t)hd.late_dropped;
+    c.fired = (uint64_t)hd.fired;
+    c.live_entries = hd.live;
+    HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
+    h->chunks_ub = 0;
+    h->host_cur = hd.cur;
+    return FW_OK;
+}
+
+// ---- host-side restatements (the exact code the kernels run), for host partitioners/tests
+int32_t fw_host_key_group(int32_t key_hash_kind, int64_t key, int32_t precomputed_hash, int32_t max_parallelism) {
+    return key_group_for_hash(java_key_hash(key_hash_kind, key, precomputed_hash), max_parallelism);
+}
+int64_t fw_host_window_start(int64_t ts, int64_t offset, int64_t size) {
+    return window_start(ts, offset, make_udiv((uint64_t)size));
+}
+int64_t fw_host_next_trigger_watermark(int64_t wm, int64_t interval) {
+    return next_trigger_watermark(wm, make_udiv((uint64_t)interval));
+}
+
+}  // extern "C"

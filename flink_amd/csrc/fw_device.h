@@ -1,0 +1,175 @@
+// fw_device.h -- arithmetic shared by the gfx950 kernels and the host side of libflinkwin.
+//
+// Everything here is __host__ __device__ so the exact same code that runs in the kernels can
+// be exercised on the CPU (fw_host_* entry points, tests/test_native_host.py).
+//
+// Java semantics: `long`/`int` arithmetic wraps (two's complement), `%` truncates toward zero.
+// The reference functions restated here:
+//   MathUtils.murmurHash / bitMix          flink-core/.../util/MathUtils.java:137-155,194-200
+//   KeyGroupRangeAssignment                 FR/runtime/state/KeyGroupRangeAssignment.java:63-147
+//   BinaryRowData.hashCode                  flink-table-common/.../data/binary/BinaryRowData.java:459
+//     -> MurmurHashUtils.hashBytesByWords   .../MurmurHashUtils.java:70,92-96,131-170 (seed 42)
+//   TimeWindow.getWindowStartWithOffset     FR/streaming/api/windowing/windows/TimeWindow.java:264-272
+//   TimeWindowUtil.isWindowFired / getNextTriggerWatermark
+//                                           TR/util/TimeWindowUtil.java:175-211 (UTC)
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#define FW_HD __host__ __device__ __forceinline__
+
+namespace fw {
+
+// ---------------------------------------------------------------------------------------
+// 32-bit Java int helpers (done in uint32 to get wrap-around without UB)
+// ---------------------------------------------------------------------------------------
+FW_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+FW_HD uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+FW_HD uint32_t murmur_k1(uint32_t k) { return rotl32(k * 0xcc9e2d51u, 15) * 0x1b873593u; }
+FW_HD uint32_t murmur_h1(uint32_t h, uint32_t k1) { return rotl32(h ^ k1, 13) * 5u + 0xe6546b64u; }
+
+// MathUtils.murmurHash(int): one 4-byte Murmur3 block (seed 0), length 4, then |h| with
+// Integer.MIN_VALUE -> 0.
+FW_HD int32_t flink_murmur_hash(int32_t code) {
+    uint32_t h = murmur_h1(0u, murmur_k1((uint32_t)code));
+    h = fmix32(h ^ 4u);
+    const int32_t s = (int32_t)h;
+    if (s >= 0) return s;
+    if (s != INT32_MIN) return -s;
+    return 0;
+}
+
+enum KeyHashKind : int32_t { KH_LONG = 0, KH_INT = 1, KH_BINROW_BIGINT = 2, KH_BINROW_INT = 3, KH_PRE = 4 };
+
+// key.hashCode() as the reference sees it.
+FW_HD int32_t java_key_hash(int32_t kind, int64_t key, int32_t pre) {
+    const uint64_t u = (uint64_t)key;
+    switch (kind) {
+        case KH_LONG: return (int32_t)(uint32_t)(u ^ (u >> 32));
+        case KH_INT: return (int32_t)(uint32_t)u;
+        case KH_BINROW_BIGINT:
+        case KH_BINROW_INT: {
+            // 16-byte key row: 8-byte zero header (BinaryRowWriter.reset), then the field slot.
+            uint32_t h = 42u;
+            h = murmur_h1(h, murmur_k1(0u));
+            h = murmur_h1(h, murmur_k1(0u));
+            h = murmur_h1(h, murmur_k1((uint32_t)u));
+            h = murmur_h1(h, murmur_k1(kind == KH_BINROW_BIGINT ? (uint32_t)(u >> 32) : 0u));
+            return (int32_t)fmix32(h ^ 16u);
+        }
+        default: return pre;
+    }
+}
+
+// KeyGroupRangeAssignment.computeKeyGroupForKeyHash
+FW_HD int32_t key_group_for_hash(int32_t h, int32_t max_p) { return flink_murmur_hash(h) % max_p; }
+// KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup
+FW_HD int32_t operator_for_key_group(int32_t max_p, int32_t p, int32_t kg) { return kg * p / max_p; }
+
+// 64-bit finaliser used for the build's OWN bucketing (not a Flink-visible hash).
+FW_HD uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------------------------------
+// unsigned 64-bit division by an invariant divisor (round-up magic multiplier)
+// ---------------------------------------------------------------------------------------
+struct UDiv {
+    uint64_t d;
+    uint64_t magic;  // 0 => power of two
+    uint32_t shift;
+    uint32_t add;    // 65-bit variant
+};
+
+FW_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+inline UDiv make_udiv(uint64_t d) {  // host only; d > 0
+    UDiv r{};
+    r.d = d;
+    uint32_t l = 63 - (uint32_t)__builtin_clzll(d);
+    if ((d & (d - 1)) == 0) {
+        r.magic = 0;
+        r.shift = l;
+        r.add = 0;
+        return r;
+    }
+    const unsigned __int128 num = (unsigned __int128)1 << (64 + l);
+    uint64_t m = (uint64_t)(num / d);
+    uint64_t rem = (uint64_t)(num - (unsigned __int128)m * d);
+    const uint64_t e = d - rem;
+    if (e < ((uint64_t)1 << l)) {
+        r.shift = l;
+        r.add = 0;
+    } else {
+        m += m;
+        const uint64_t twice = rem + rem;
+        if (twice >= d || twice < rem) m += 1;
+        r.shift = l;
+        r.add = 1;
+    }
+    r.magic = m + 1;
+    return r;
+}
+
+FW_HD uint64_t udiv(uint64_t x, const UDiv& v) {
+    if (v.magic == 0) return x >> v.shift;
+    const uint64_t q = mulhi64(v.magic, x);
+    if (v.add) return (((x - q) >> 1) + q) >> v.shift;
+    return q >> v.shift;
+}
+
+// TimeWindow.getWindowStartWithOffset(ts, offset, size) with Java long semantics.
+FW_HD int64_t window_start(int64_t ts, int64_t offset, const UDiv& size) {
+    const uint64_t x = (uint64_t)ts - (uint64_t)offset;
+    const bool neg = (int64_t)x < 0;
+    const uint64_t ax = neg ? (0ull - x) : x;
+    const uint64_t r = ax - udiv(ax, size) * size.d;  // |x| % size
+    if (neg && r != 0) return (int64_t)((uint64_t)ts - (size.d - r));  // ts - (rem + size)
+    return (int64_t)((uint64_t)ts - r);
+}
+
+FW_HD int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+FW_HD int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+
+// TimeWindowUtil.isWindowFired, UTC shift zone: progress >= windowEnd - 1 (MAX never fires).
+FW_HD bool is_fired(int64_t window_end, int64_t progress) {
+    if (window_end == INT64_MAX) return false;
+    return progress >= wsub(window_end, 1);
+}
+
+// TimeWindowUtil.getNextTriggerWatermark (no daylight saving).
+FW_HD int64_t next_trigger_watermark(int64_t wm, const UDiv& interval) {
+    if (wm == INT64_MAX) return wm;
+    const int64_t start = window_start(wm, 0, interval);
+    const int64_t trig = wsub(wadd(start, (int64_t)interval.d), 1);
+    return trig > wm ? trig : wadd(trig, (int64_t)interval.d);
+}
+
+// Sortable 64-bit key of a double (total order of Double.compare: NaN canonicalised, greatest).
+FW_HD int64_t dkey(uint64_t bits) {
+    if ((bits & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (bits & 0x000FFFFFFFFFFFFFull))
+        bits = 0x7FF8000000000000ull;
+    const int64_t s = (int64_t)bits;
+    return s ^ (int64_t)(((uint64_t)(s >> 63)) >> 1);
+}
+FW_HD uint64_t dkey_inv(int64_t k) { return (uint64_t)(k ^ (int64_t)(((uint64_t)(k >> 63)) >> 1)); }
+
+}  // namespace fw

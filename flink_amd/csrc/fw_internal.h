@@ -1,0 +1,183 @@
+// fw_internal.h -- structures shared by the gfx950 kernels (fw_kernels.hip) and the C-ABI
+// implementation (fw_api.hip).  Not part of the public boundary (include/flinkwin.h is).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/flinkwin.h"
+#include "fw_device.h"
+
+namespace fw {
+
+constexpr int BLOCK = 256;          // threads per workgroup (4 waves of 64)
+constexpr int MAX_WORDS = 8;        // accumulator words per (key, slice)
+constexpr int MAX_KCOLS = 4;        // value columns a kernel loads per record
+constexpr int K3_RPT = 16;          // records per thread in the ingest kernel
+constexpr int K3_CHUNK = BLOCK * K3_RPT;  // records per ingest chunk (one workgroup)
+constexpr int K3_CACHE = 512;       // direct-mapped hot-(key,slice) LDS cache slots
+// records per thread of an ingest instantiation (fewer when many value columns are loaded,
+// to stay within the register file); a chunk holds at most BLOCK * rpt <= K3_CHUNK partials
+constexpr __host__ __device__ int ingest_rpt(int nv) { return nv >= 3 ? 8 : K3_RPT; }
+
+// Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words.
+enum WordOp : int32_t {
+    W_CNT = 0,    // += 1                       COUNT(*), COUNT(col), AVG count
+    W_SUM_I = 1,  // += v (64-bit wrap)         SUM(BIGINT/INT), AVG(BIGINT/INT) sum
+    W_SUM_F = 2,  // += v (IEEE double)         SUM(DOUBLE), AVG(DOUBLE) sum
+    W_MIN_I = 3,  // min (signed)               MIN(BIGINT/INT)
+    W_MAX_I = 4,  // max (signed)               MAX(BIGINT/INT)
+    W_MIN_D = 5,  // min over dkey(v)           MIN(DOUBLE)
+    W_MAX_D = 6   // max over dkey(v)           MAX(DOUBLE)
+};
+
+FW_HD uint64_t word_identity(int32_t op) {
+    switch (op) {
+        case W_MIN_I:
+        case W_MIN_D: return (uint64_t)INT64_MAX;
+        case W_MAX_I:
+        case W_MAX_D: return (uint64_t)INT64_MIN;
+        default: return 0;  // counts, integer sums, and +0.0 for double sums
+    }
+}
+
+// Entry flags of the HBM slice-state table.
+constexpr uint32_t F_ACC = 1u;    // windowState(key, slice) != null
+constexpr uint32_t F_TIMER = 2u;  // event-time timer registered for (key, window = slice)
+
+// Error bits reported through Ctrl::error.
+constexpr uint32_t ERR_CHUNKS = 1u;
+constexpr uint32_t ERR_STATE = 2u;
+constexpr uint32_t ERR_OUTPUT = 4u;
+constexpr uint32_t ERR_TREQ = 8u;
+
+// Device-resident operator control block (one per handle).  Only kernels write it, so a
+// watermark cycle needs no host round trip.
+struct Ctrl {
+    int64_t cur;             // currentProgress == operator / timer-service watermark
+    int64_t ntp;             // nextTriggerProgress
+    int64_t min_pending;     // RecordsWindowBuffer.minSliceEnd of the pending partials
+    int64_t pending_chunks;  // ingest chunks waiting in the partial buffer
+    int64_t n_treq;          // pending timer requests (late records)
+    uint64_t out_count;      // result rows produced since the last reset
+    uint64_t late_dropped;   // numLateRecordsDropped
+    uint64_t fired;          // fired (key, window) timers
+    uint64_t pending_rows;   // rows ingested but not yet flushed
+    int64_t live_entries;    // live (key, slice) entries in the state table
+    uint32_t error;
+    uint32_t k4_done;        // last-workgroup-done ticket of the merge/fire kernel
+    uint64_t partials;       // partials written by the ingest kernel (cumulative)
+    uint64_t pad[3];
+};
+
+// Window / slice description shared by both kernels (SliceAssigners.java).
+struct WinDesc {
+    int32_t kind;         // FW_WIN_*
+    int32_t n_slices;     // HOP slices per window
+    int64_t size;         // window size / cumulate max size
+    int64_t interval;     // slice size (getSliceEndInterval)
+    int64_t offset;
+    UDiv slice_div;       // divisor = interval
+    UDiv size_div;        // divisor = size (CUMULATE getWindowStart)
+};
+
+FW_HD int64_t slice_end_of(const WinDesc& w, int64_t ts) {
+    return wadd(window_start(ts, w.offset, w.slice_div), w.interval);
+}
+// SliceAssigner.getWindowStart(windowEnd)
+FW_HD int64_t window_start_of(const WinDesc& w, int64_t we) {
+    if (w.kind == FW_WIN_CUMULATE) return window_start(wsub(we, 1), w.offset, w.size_div);
+    return wsub(we, w.size);
+}
+// SliceAssigner.getLastWindowEnd(sliceEnd)
+FW_HD int64_t last_window_end_of(const WinDesc& w, int64_t se) {
+    if (w.kind == FW_WIN_TUMBLE) return se;
+    if (w.kind == FW_WIN_HOP) return wadd(wsub(se, w.interval), w.size);
+    return wadd(window_start_of(w, se), w.size);
+}
+// sliceStateMergeTarget (SliceSharedSyncStateWindowAggProcessor.java:120-132)
+FW_HD int64_t merge_target_of(const WinDesc& w, int64_t se) {
+    if (w.kind == FW_WIN_CUMULATE) return wadd(window_start_of(w, se), w.interval);
+    return se;
+}
+
+struct KeySpace {
+    int32_t hash_kind;
+    int32_t max_p;
+    int32_t kg_start;      // first key group owned by this subtask
+    int32_t n_kg;          // key groups owned
+    int32_t sb_per_kg_log2;
+    int32_t n_sb;          // superbuckets = n_kg << sb_per_kg_log2
+};
+
+FW_HD int32_t superbucket_of(const KeySpace& ks, int64_t key, int32_t pre) {
+    const int32_t kg = key_group_for_hash(java_key_hash(ks.hash_kind, key, pre), ks.max_p);
+    const uint32_t sub = ks.sb_per_kg_log2 ? (uint32_t)(mix64((uint64_t)key) >> (64 - ks.sb_per_kg_log2)) : 0u;
+    return ((kg - ks.kg_start) << ks.sb_per_kg_log2) + (int32_t)sub;
+}
+
+struct WordDesc {
+    int32_t nw;
+    int32_t op[MAX_WORDS];
+    int32_t col[MAX_WORDS];
+};
+
+struct AggDesc {
+    int32_t n;
+    int32_t kind[FW_MAX_AGGS];
+    int32_t type[FW_MAX_AGGS];
+    int32_t w0[FW_MAX_AGGS];
+    int32_t w1[FW_MAX_AGGS];
+    int32_t count_word;  // word holding COUNT(*) for emptiness / null rules, -1 if none
+    int32_t count_star_word;  // word of the SQL indexOfCountStar aggregate, -1 if none
+};
+
+struct IngestArgs {
+    const int64_t* key;
+    const int64_t* ts;
+    const int32_t* khash;
+    const uint64_t* vals[MAX_KCOLS];
+    int64_t n;
+    WinDesc win;
+    KeySpace ks;
+    WordDesc wd;
+    int32_t nv;            // value columns loaded
+    int32_t col_map[MAX_KCOLS];  // kernel column slot -> value column index (for the host)
+    Ctrl* ctrl;
+    uint64_t* parts;       // partial buffer: max_chunks * K3_CHUNK * (2 + nw) words
+    uint32_t* off;         // [n_sb + 1][max_chunks] run starts
+    int64_t max_chunks;
+    int64_t* treq;         // timer requests: (key, window, sb) triples
+    int64_t treq_cap;
+};
+
+struct MergeArgs {
+    Ctrl* ctrl;
+    const uint64_t* parts;
+    const uint32_t* off;
+    int64_t max_chunks;
+    const int64_t* treq;
+    uint64_t* state;         // [n_sb][cap_e][3 + nw] words: key, slice, flags, acc...
+    int32_t* state_count;    // live entries per superbucket
+    int64_t* sb_min_timer;   // min windowEnd with a timer per superbucket (INT64_MAX: none)
+    int32_t n_sb;
+    int32_t cap_e;
+    WinDesc win;
+    WordDesc wd;
+    AggDesc ad;
+    int32_t always_flush;    // DataStream: state is updated per record, flush every advance
+    int64_t* out_key;
+    int64_t* out_ws;
+    int64_t* out_we;
+    uint64_t* out_val[FW_MAX_AGGS];
+    uint32_t* out_null;
+    int64_t out_cap;
+    int64_t wm;              // watermark of this advance
+    int32_t force_flush;     // prepareCheckpoint: flush, no timers
+    int32_t pad;
+};
+
+// launchers (fw_kernels.hip)
+hipError_t launch_ingest(const IngestArgs& a, hipStream_t s);
+hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s);
+hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s);
+
+}  // namespace fw

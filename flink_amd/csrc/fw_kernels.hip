@@ -1,0 +1,907 @@
+// fw_kernels.hip -- gfx950 kernels of libflinkwin (MI355X, CDNA4, wave64).
+//
+// Data path per watermark interval (SURVEY.md 2.2 kernel list):
+//   k_ingest      (K1+K2+K3)  key-group + slice assignment + late classification, then a
+//                 coalesced-load, LDS-staged segmented reduce: a direct-mapped LDS cache folds
+//                 repeated (key, slice) pairs (hot keys), the rest pass through; the chunk's
+//                 partials are counting-sorted by superbucket in LDS and written contiguously.
+//                 Restates AbstractSliceSyncStateWindowAggProcessor.processElement (:96-126),
+//                 RecordsWindowBuffer.addElement (:81) and the per-group fold of AggCombiner (:76-99).
+//   k_merge_fire  (K4+K5)  one workgroup per superbucket: loads its slice-state entries from HBM
+//                 into an LDS hash table, merges the pending partials (flush), registers timers,
+//                 then fires every due (key, window) timer in timestamp rounds (fireWindow / merge /
+//                 clearWindow / nextTriggerWindow) and writes the live entries back.
+//                 Restates RecordsWindowBuffer.flush (:115), AggCombiner.combine (:76-115),
+//                 InternalTimerServiceImpl.tryAdvanceWatermark (:328-348), WindowAggOperator.onTimer
+//                 (:258), Slice{Unshared,Shared}SyncStateWindowAggProcessor.fireWindow and
+//                 AbstractSliceSyncStateWindowAggProcessor.clearWindow (:161-167).
+// All control decisions (flush? fire? next trigger progress) are made on the device from the
+// Ctrl block, so a watermark cycle is two launches and no host synchronisation.
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "fw_internal.h"
+
+namespace fw {
+
+// compile-time loop: f(std::integral_constant<int, J>) for J in [0, N).  Keeps per-record
+// register arrays indexed by constants regardless of the unroller's size heuristics.
+template <typename F, int... Js>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Js...>) {
+    (f(std::integral_constant<int, Js>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+#define LDS_SCOPE __HIP_MEMORY_SCOPE_WORKGROUP
+#define DEV_SCOPE __HIP_MEMORY_SCOPE_AGENT
+
+__device__ __forceinline__ double as_f64(uint64_t b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ uint64_t f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }
+
+// select value column `col` from a per-record register array without dynamic indexing
+template <int N>
+__device__ __forceinline__ uint64_t pick_col(const uint64_t (&v)[N], int32_t col) {
+    uint64_t r = v[0];
+#pragma unroll
+    for (int c = 1; c < N; c++)
+        if (col == c) r = v[c];
+    return r;
+}
+
+// value of one accumulator word for a single record (accumulate on the identity)
+__device__ __forceinline__ uint64_t record_word(int32_t op, uint64_t v) {
+    switch (op) {
+        case W_CNT: return 1;
+        case W_MIN_D:
+        case W_MAX_D: return (uint64_t)dkey(v);
+        default: return v;  // SUM_I, SUM_F (bits), MIN_I, MAX_I
+    }
+}
+
+// atomically fold `v` into an LDS accumulator word
+__device__ __forceinline__ void lds_fold(int32_t op, uint64_t* slot, uint64_t v) {
+    switch (op) {
+        case W_CNT:
+        case W_SUM_I: __hip_atomic_fetch_add(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+        case W_SUM_F: __hip_atomic_fetch_add((double*)slot, as_f64(v), __ATOMIC_RELAXED, LDS_SCOPE); break;
+        case W_MIN_I:
+        case W_MIN_D: __hip_atomic_fetch_min((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+        default: __hip_atomic_fetch_max((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+    }
+}
+
+// fold in registers (used when merging slices at fire time, in the reference's order)
+__device__ __forceinline__ uint64_t reg_fold(int32_t op, uint64_t a, uint64_t b) {
+    switch (op) {
+        case W_CNT:
+        case W_SUM_I: return a + b;
+        case W_SUM_F: return f64_bits(as_f64(a) + as_f64(b));
+        case W_MIN_I:
+        case W_MIN_D: return (int64_t)a < (int64_t)b ? a : b;
+        default: return (int64_t)a > (int64_t)b ? a : b;
+    }
+}
+
+__device__ __forceinline__ uint32_t cache_hash(int64_t k, int64_t s) {
+    return (uint32_t)mix64((uint64_t)k ^ ((uint64_t)s * 0x9E3779B97F4A7C15ull));
+}
+__device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
+    return (uint32_t)(mix64((uint64_t)k * 0xD6E8FEB86659FD93ull + (uint64_t)s) >> 17);
+}
+
+// exclusive scan of n u32 in LDS by one 256-thread block; returns total in buf[n]
+__device__ void block_exclusive_scan(uint32_t* buf, int n, uint32_t* tmp) {
+    const int tid = threadIdx.x;
+    const int per = (n + BLOCK - 1) / BLOCK;
+    const int b = tid * per;
+    const int e = min(b + per, n);
+    uint32_t s = 0;
+    for (int i = b; i < e; i++) s += buf[i];
+    tmp[tid] = s;
+    __syncthreads();
+    // Hillis-Steele over 256 partial sums
+    for (int d = 1; d < BLOCK; d <<= 1) {
+        uint32_t x = tid >= d ? tmp[tid - d] : 0;
+        __syncthreads();
+        tmp[tid] += x;
+        __syncthreads();
+    }
+    uint32_t run = tmp[tid] - s;  // exclusive prefix of this thread's segment
+    for (int i = b; i < e; i++) {
+        uint32_t v = buf[i];
+        buf[i] = run;
+        run += v;
+    }
+    if (tid == BLOCK - 1) buf[n] = tmp[BLOCK - 1];
+    __syncthreads();
+}
+
+// ======================================================================================
+// K1+K2+K3: ingest (slice assignment + LDS-staged segmented reduce + superbucket partition)
+// ======================================================================================
+template <int NV, int NW, int RPT>
+__global__ __launch_bounds__(BLOCK) void k_ingest(IngestArgs a) {
+    constexpr int NVR = NV > 0 ? NV : 1;
+    constexpr int PW = 2 + NW;
+    constexpr int CHUNK = BLOCK * RPT;
+    __shared__ int64_t c_key[K3_CACHE];
+    __shared__ int64_t c_slice[K3_CACHE];
+    __shared__ uint32_t c_state[K3_CACHE];
+    __shared__ uint32_t c_sb[K3_CACHE];
+    __shared__ uint32_t c_rank[K3_CACHE];
+    __shared__ uint64_t c_acc[NW][K3_CACHE];
+    __shared__ uint32_t s_tmp[BLOCK];
+    __shared__ int64_t s_min;
+    __shared__ uint64_t s_drop;
+    __shared__ uint64_t s_rows;
+    __shared__ int64_t s_chunk;
+    extern __shared__ uint32_t hist[];  // n_sb + 1
+
+    const int tid = threadIdx.x;
+    Ctrl* ctrl = a.ctrl;
+    const int n_sb = a.ks.n_sb;
+    if (tid == 0) {
+        s_chunk = __hip_atomic_fetch_add(&ctrl->pending_chunks, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
+        s_min = INT64_MAX;
+        s_drop = 0;
+        s_rows = 0;
+    }
+    for (int i = tid; i < K3_CACHE; i += BLOCK) c_state[i] = 0;
+    for (int i = tid; i <= n_sb; i += BLOCK) hist[i] = 0;
+    __syncthreads();
+    const int64_t chunk = s_chunk;
+    if (chunk >= a.max_chunks) {
+        if (tid == 0) __hip_atomic_fetch_or(&ctrl->error, ERR_CHUNKS, __ATOMIC_RELAXED, DEV_SCOPE);
+        return;
+    }
+    const int64_t cur = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t base = (int64_t)blockIdx.x * CHUNK;
+
+    int64_t rk[RPT], rs[RPT];
+    uint64_t rv[RPT][NVR];
+    int32_t rsb[RPT];
+    uint32_t rrank[RPT];
+    uint32_t valid = 0, pass = 0;
+    int64_t lmin = INT64_MAX;
+    uint32_t ldrop = 0, lrows = 0;
+
+    // ---- coalesced column loads: lane i of a wave reads element base + j*256 + i
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int64_t i = base + (int64_t)j * BLOCK + tid;
+        rk[j] = 0;
+        rs[j] = 0;
+#pragma unroll
+        for (int c = 0; c < NVR; c++) rv[j][c] = 0;
+        if (i < a.n) {
+            rk[j] = a.key[i];
+            rs[j] = a.ts[i];
+#pragma unroll
+            for (int c = 0; c < NV; c++) rv[j][c] = a.vals[c][i];
+            valid |= 1u << j;
+        }
+    });
+    // ---- K1/K2: key group -> superbucket, slice end, late classification
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        rsb[j] = 0;
+        if (!(valid & (1u << j))) return;
+        const int64_t i = base + (int64_t)j * BLOCK + tid;
+        const int32_t pre = a.khash ? a.khash[i] : 0;
+        const int64_t se = slice_end_of(a.win, rs[j]);
+        int64_t target = se;
+        rsb[j] = superbucket_of(a.ks, rk[j], pre);
+        if (is_fired(se, cur)) {
+            if (is_fired(last_window_end_of(a.win, se), cur)) {  // late for every window: drop
+                valid &= ~(1u << j);
+                ldrop++;
+                return;
+            }
+            target = merge_target_of(a.win, se);
+            // timer for the first unfired window (processElement :111-117)
+            const int64_t steps = (int64_t)((uint64_t)wsub(wadd(cur, 1), se) / (uint64_t)a.win.interval) + 1;
+            const int64_t unfired = wadd(se, steps * a.win.interval);
+            const int64_t r = __hip_atomic_fetch_add(&ctrl->n_treq, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
+            if (r < a.treq_cap) {
+                a.treq[3 * r] = rk[j];
+                a.treq[3 * r + 1] = unfired;
+                a.treq[3 * r + 2] = rsb[j];
+            } else {
+                __hip_atomic_fetch_or(&ctrl->error, ERR_TREQ, __ATOMIC_RELAXED, DEV_SCOPE);
+            }
+        }
+        rs[j] = target;
+        lmin = min(lmin, target);
+        lrows++;
+    });
+    // ---- K3: fold into the hot (key, slice) cache, or pass through
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if (!(valid & (1u << j))) return;
+        const uint32_t h = cache_hash(rk[j], rs[j]) & (K3_CACHE - 1);
+        bool absorbed = false;
+        uint32_t st = __hip_atomic_load(&c_state[h], __ATOMIC_ACQUIRE, LDS_SCOPE);
+        if (st == 0) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(&c_state[h], &expect, 1u, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, LDS_SCOPE)) {
+                c_key[h] = rk[j];
+                c_slice[h] = rs[j];
+                c_sb[h] = (uint32_t)rsb[j];
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    c_acc[w][h] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
+                __hip_atomic_store(&c_state[h], 2u, __ATOMIC_RELEASE, LDS_SCOPE);
+                absorbed = true;
+            }
+        } else if (st == 2 && c_key[h] == rk[j] && c_slice[h] == rs[j]) {
+#pragma unroll
+            for (int w = 0; w < NW; w++)
+                if (w < a.wd.nw)
+                    lds_fold(a.wd.op[w], &c_acc[w][h], record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])));
+            absorbed = true;
+        }
+        if (!absorbed) pass |= 1u << j;
+    });
+    __syncthreads();
+    // ---- ranks within superbucket runs
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if (pass & (1u << j)) rrank[j] = atomicAdd(&hist[rsb[j]], 1u);
+    });
+    for (int h = tid; h < K3_CACHE; h += BLOCK)
+        if (c_state[h] == 2) c_rank[h] = atomicAdd(&hist[c_sb[h]], 1u);
+    __syncthreads();
+    block_exclusive_scan(hist, n_sb, s_tmp);
+    // ---- write the chunk's partials, sorted by superbucket
+    uint64_t* out = a.parts + (size_t)chunk * K3_CHUNK * PW;  // chunk stride is K3_CHUNK for every RPT
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if (!(pass & (1u << j))) return;
+        uint64_t* p = out + (size_t)(hist[rsb[j]] + rrank[j]) * PW;
+        p[0] = (uint64_t)rk[j];
+        p[1] = (uint64_t)rs[j];
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            p[2 + w] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
+    });
+    for (int h = tid; h < K3_CACHE; h += BLOCK) {
+        if (c_state[h] != 2) continue;
+        uint64_t* p = out + (size_t)(hist[c_sb[h]] + c_rank[h]) * PW;
+        p[0] = (uint64_t)c_key[h];
+        p[1] = (uint64_t)c_slice[h];
+#pragma unroll
+        for (int w = 0; w < NW; w++) p[2 + w] = c_acc[w][h];
+    }
+    for (int s = tid; s <= n_sb; s += BLOCK) a.off[(size_t)s * a.max_chunks + chunk] = hist[s];
+    // ---- block reductions -> control block
+    if (lmin != INT64_MAX) __hip_atomic_fetch_min(&s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
+    if (ldrop) atomicAdd((unsigned long long*)&s_drop, (unsigned long long)ldrop);
+    if (lrows) atomicAdd((unsigned long long*)&s_rows, (unsigned long long)lrows);
+    __syncthreads();
+    if (tid == 0) {
+        if (s_min != INT64_MAX) __hip_atomic_fetch_min(&ctrl->min_pending, s_min, __ATOMIC_RELAXED, DEV_SCOPE);
+        if (s_drop) __hip_atomic_fetch_add(&ctrl->late_dropped, s_drop, __ATOMIC_RELAXED, DEV_SCOPE);
+        if (s_rows) __hip_atomic_fetch_add(&ctrl->pending_rows, s_rows, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_fetch_add(&ctrl->partials, (uint64_t)hist[n_sb], __ATOMIC_RELAXED, DEV_SCOPE);
+    }
+}
+
+// ======================================================================================
+// K4+K5: merge pending partials into the HBM slice-state table, fire due timers
+// ======================================================================================
+template <int NW, int E>
+struct StateLds {
+    uint32_t idx[2 * E];   // open-addressing index: 0 empty, 1 claiming, 2+e entry e
+    int64_t key[E];
+    int64_t slice[E];
+    uint32_t flag[E];
+    uint64_t acc[NW][E];
+    int32_t n;             // entries in use
+    uint32_t overflow;
+};
+
+constexpr uint32_t IDX_DEAD = 0xFFFFFFFFu;
+
+template <int NW, int E>
+__device__ __forceinline__ void init_entry_acc(StateLds<NW, E>& S, int e, const WordDesc& wd) {
+#pragma unroll
+    for (int w = 0; w < NW; w++) S.acc[w][e] = w < wd.nw ? word_identity(wd.op[w]) : 0;
+}
+
+template <int NW, int E>
+__device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
+    constexpr uint32_t MASK = 2 * E - 1;
+    uint32_t h = index_hash(k, s) & MASK;
+    for (int probes = 0; probes < 2 * E;) {
+        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_ACQUIRE, LDS_SCOPE);
+        if (st == 0) return -1;
+        if (st == 1) continue;  // being inserted by another lane: re-read
+        const uint32_t e = st - 2;
+        if (e < (uint32_t)E && S.key[e] == k && S.slice[e] == s) return (int)e;
+        h = (h + 1) & MASK;
+        probes++;
+    }
+    return -1;
+}
+
+template <int NW, int E>
+__device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd) {
+    constexpr uint32_t MASK = 2 * E - 1;
+    uint32_t h = index_hash(k, s) & MASK;
+    for (int probes = 0; probes < 2 * E;) {
+        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_ACQUIRE, LDS_SCOPE);
+        if (st == 1) continue;
+        if (st == 0) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 1u, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, LDS_SCOPE)) {
+                const int e = atomicAdd(&S.n, 1);
+                if (e >= E) {
+                    S.overflow = 1;
+                    __hip_atomic_store(&S.idx[h], IDX_DEAD, __ATOMIC_RELEASE, LDS_SCOPE);
+                    return -1;
+                }
+                S.key[e] = k;
+                S.slice[e] = s;
+                S.flag[e] = 0;
+                init_entry_acc(S, e, wd);
+                __hip_atomic_store(&S.idx[h], 2u + (uint32_t)e, __ATOMIC_RELEASE, LDS_SCOPE);
+                return e;
+            }
+            continue;  // lost the race: re-read this slot
+        }
+        const uint32_t e = st - 2;
+        if (e < (uint32_t)E && S.key[e] == k && S.slice[e] == s) return (int)e;
+        h = (h + 1) & MASK;
+        probes++;
+    }
+    S.overflow = 1;
+    return -1;
+}
+
+template <int NW>
+__device__ void emit_row(const MergeArgs& a, int64_t key, int64_t we, const uint64_t* acc) {
+    Ctrl* c = a.ctrl;
+    const uint64_t i = atomicAdd((unsigned long long*)&c->out_count, 1ull);
+    if ((int64_t)i >= a.out_cap) {
+        __hip_atomic_fetch_or(&c->error, ERR_OUTPUT, __ATOMIC_RELAXED, DEV_SCOPE);
+        return;
+    }
+    a.out_key[i] = key;
+    a.out_ws[i] = window_start_of(a.win, we);
+    a.out_we[i] = we;
+    const bool no_rows = a.ad.count_word >= 0 && acc[a.ad.count_word] == 0;
+    uint32_t nm = 0;
+    for (int g = 0; g < a.ad.n; g++) {
+        const int32_t kind = a.ad.kind[g], type = a.ad.type[g];
+        const uint64_t w0 = acc[a.ad.w0[g]];
+        uint64_t v = 0;
+        switch (kind) {
+            case FW_AGG_COUNT_STAR:
+            case FW_AGG_COUNT: v = w0; break;
+            case FW_AGG_SUM:
+                v = type == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)w0 : w0;
+                if (no_rows) nm |= 1u << g;
+                break;
+            case FW_AGG_MIN:
+            case FW_AGG_MAX:
+                v = type == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
+                if (no_rows) nm |= 1u << g;
+                break;
+            case FW_AGG_AVG: {
+                const uint64_t cnt = acc[a.ad.w1[g]];
+                if (cnt == 0) { nm |= 1u << g; break; }
+                if (type == FW_T_F64) v = f64_bits(as_f64(w0) / (double)(int64_t)cnt);
+                else {
+                    int64_t q = (int64_t)w0 / (int64_t)cnt;
+                    if (type == FW_T_I32) q = (int32_t)q;
+                    v = (uint64_t)q;
+                }
+                break;
+            }
+        }
+        a.out_val[g][i] = v;
+    }
+    a.out_null[i] = nm;
+}
+
+template <int NW, int E>
+__device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t we, uint32_t* fired) {
+    const WinDesc& w = a.win;
+    const WordDesc& wd = a.wd;
+    const int64_t k = S.key[e];
+    uint64_t acc[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) acc[i] = i < wd.nw ? word_identity(wd.op[i]) : 0;
+    atomicAdd(fired, 1u);
+    bool nonempty;
+    if (w.kind == FW_WIN_TUMBLE) {
+        // SliceUnsharedSyncStateWindowAggProcessor.fireWindow (:54-66)
+        if (S.flag[e] & F_ACC) {
+#pragma unroll
+            for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
+        }
+        nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
+        if (nonempty) emit_row<NW>(a, k, we, acc);
+        atomicAnd(&S.flag[e], ~F_ACC);  // clearWindow: expiredSlices(we) = [we]
+        return;
+    }
+    if (w.kind == FW_WIN_HOP) {
+        // mergeSlices with a null target: fold the n slices ending at we, newest first
+        int64_t s = we;
+        for (int j = 0; j < w.n_slices; j++) {
+            const int e2 = find_entry(S, k, s);
+            if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
+#pragma unroll
+                for (int i = 0; i < NW; i++)
+                    if (i < wd.nw) acc[i] = reg_fold(wd.op[i], acc[i], S.acc[i][e2]);
+            }
+            s = wsub(s, w.interval);
+        }
+        nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
+        if (nonempty) {
+            emit_row<NW>(a, k, we, acc);
+            // nextTriggerWindow: register windowEnd + sliceSize while the window is non-empty
+            const int e3 = find_or_insert(S, k, wadd(we, w.interval), wd);
+            if (e3 >= 0) atomicOr(&S.flag[e3], F_TIMER);
+        }
+        // clearWindow: expiredSlices = [windowStart + sliceSize]
+        const int e2 = find_entry(S, k, wadd(wsub(we, w.size), w.interval));
+        if (e2 >= 0) atomicAnd(&S.flag[e2], ~F_ACC);
+        return;
+    }
+    // CUMULATE: merge the window's slice into the first-slice state (mergeSlices -> merge)
+    const int64_t ws = window_start_of(w, we);
+    const int64_t first = wadd(ws, w.interval);
+    const int ef = find_or_insert(S, k, first, wd);
+    if (ef >= 0 && (S.flag[ef] & F_ACC)) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) acc[i] = S.acc[i][ef];
+    }
+    if (we != first) {
+        const int e2 = find_entry(S, k, we);
+        if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
+#pragma unroll
+            for (int i = 0; i < NW; i++)
+                if (i < wd.nw) acc[i] = reg_fold(wd.op[i], acc[i], S.acc[i][e2]);
+        }
+    }
+    if (ef >= 0) {  // windowState.update(firstSlice, acc)
+#pragma unroll
+        for (int i = 0; i < NW; i++) S.acc[i][ef] = acc[i];
+        atomicOr(&S.flag[ef], F_ACC);
+    }
+    nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
+    if (nonempty) emit_row<NW>(a, k, we, acc);
+    const int64_t next = wadd(we, w.interval);
+    const int64_t last = wadd(ws, w.size);
+    if (!(next > last)) {
+        const int e3 = find_or_insert(S, k, next, wd);
+        if (e3 >= 0) atomicOr(&S.flag[e3], F_TIMER);
+    }
+    // clearWindow (CumulativeSliceAssigner.expiredSlices)
+    if (we == first) {
+    } else {
+        const int e2 = find_entry(S, k, we);
+        if (e2 >= 0) atomicAnd(&S.flag[e2], ~F_ACC);
+        if (we == last && ef >= 0) atomicAnd(&S.flag[ef], ~F_ACC);
+    }
+}
+
+template <int NW, int E>
+__global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
+    constexpr int PW = 2 + NW;
+    constexpr int PWE = 3 + NW;
+    __shared__ StateLds<NW, E> S;
+    __shared__ int32_t s_work;
+    __shared__ int64_t s_vmin;
+    __shared__ int32_t s_nlive;
+    __shared__ int64_t s_newmin;
+    __shared__ uint32_t s_fired;
+
+    const int tid = threadIdx.x;
+    const int sb = blockIdx.x;
+    Ctrl* c = a.ctrl;
+    const int64_t W = a.wm;
+    // read the control block once (the last workgroup rewrites it after every block has read it)
+    const int64_t cur = __hip_atomic_load(&c->cur, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t pend = __hip_atomic_load(&c->pending_chunks, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t ntreq = min(__hip_atomic_load(&c->n_treq, __ATOMIC_RELAXED, DEV_SCOPE), (int64_t)0x7fffffff);
+    const int64_t ntp = __hip_atomic_load(&c->ntp, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t minp = __hip_atomic_load(&c->min_pending, __ATOMIC_RELAXED, DEV_SCOPE);
+    const bool adv = !a.force_flush && W > cur;
+    const bool do_flush = pend > 0 &&
+                          (a.force_flush || (adv && (a.always_flush || (W >= ntp && is_fired(minp, W)))));
+    const bool do_fire = adv;
+    const int64_t w_old = cur;
+    const int32_t n0 = a.state_count[sb];
+
+    if (tid == 0) {
+        s_work = (ntreq > 0) || (do_fire && is_fired(a.sb_min_timer[sb], W));
+        s_fired = 0;
+    }
+    __syncthreads();
+    const bool work0 = s_work != 0;
+    __syncthreads();
+    if (!work0 && do_flush) {  // any pending run for this superbucket?
+        for (int64_t ci = tid; ci < pend; ci += BLOCK)
+            if (a.off[(size_t)(sb + 1) * a.max_chunks + ci] > a.off[(size_t)sb * a.max_chunks + ci]) s_work = 1;
+    }
+    __syncthreads();
+    if (s_work) {
+        // ---- load this superbucket's entries into LDS
+        for (int i = tid; i < 2 * E; i += BLOCK) S.idx[i] = 0;
+        if (tid == 0) {
+            S.n = n0;
+            S.overflow = 0;
+        }
+        __syncthreads();
+        const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
+        for (int e = tid; e < n0; e += BLOCK) {
+            const uint64_t* p = st + (size_t)e * PWE;
+            const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
+            S.key[e] = k;
+            S.slice[e] = s;
+            S.flag[e] = (uint32_t)p[2];
+#pragma unroll
+            for (int w = 0; w < NW; w++) S.acc[w][e] = p[3 + w];
+            uint32_t h = index_hash(k, s) & (2 * E - 1);
+            for (;;) {
+                uint32_t expect = 0;
+                if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 2u + (uint32_t)e, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, LDS_SCOPE))
+                    break;
+                h = (h + 1) & (2 * E - 1);
+            }
+        }
+        __syncthreads();
+        // ---- timers registered by late records in processElement
+        for (int64_t r = tid; r < ntreq; r += BLOCK) {
+            if (a.treq[3 * r + 2] != sb) continue;
+            const int e = find_or_insert(S, a.treq[3 * r], a.treq[3 * r + 1], a.wd);
+            if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
+        }
+        // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket
+        if (do_flush) {
+            for (int64_t ci = tid; ci < pend; ci += BLOCK) {
+                const uint32_t s0 = a.off[(size_t)sb * a.max_chunks + ci];
+                const uint32_t s1 = a.off[(size_t)(sb + 1) * a.max_chunks + ci];
+                const uint64_t* p = a.parts + ((size_t)ci * K3_CHUNK + s0) * PW;
+                for (uint32_t q = s0; q < s1; q++, p += PW) {
+                    const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
+                    const int e = find_or_insert(S, k, s, a.wd);
+                    if (e < 0) continue;
+#pragma unroll
+                    for (int w = 0; w < NW; w++)
+                        if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], p[2 + w]);
+                    // register the window timer unless already fired (AggCombiner.java:103-110)
+                    atomicOr(&S.flag[e], is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER));
+                }
+            }
+        }
+        __syncthreads();
+        // ---- fire: InternalTimerServiceImpl.tryAdvanceWatermark, timestamp order
+        if (do_fire) {
+            for (;;) {
+                if (tid == 0) s_vmin = INT64_MAX;
+                __syncthreads();
+                const int n = min(S.n, E);
+                for (int e = tid; e < n; e += BLOCK)
+                    if ((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W))
+                        __hip_atomic_fetch_min(&s_vmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
+                __syncthreads();
+                const int64_t v = s_vmin;
+                if (v == INT64_MAX) break;
+                for (int e = tid; e < n; e += BLOCK) {
+                    if ((S.flag[e] & F_TIMER) && S.slice[e] == v) {
+                        atomicAnd(&S.flag[e], ~F_TIMER);
+                        fire_one(a, S, e, v, &s_fired);
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // ---- write back live entries
+        if (tid == 0) {
+            s_nlive = 0;
+            s_newmin = INT64_MAX;
+        }
+        __syncthreads();
+        const int n = min(S.n, E);
+        uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
+        for (int e = tid; e < n; e += BLOCK) {
+            const uint32_t f = S.flag[e];
+            if (!(f & (F_ACC | F_TIMER))) continue;
+            const int pos = atomicAdd(&s_nlive, 1);
+            uint64_t* p = so + (size_t)pos * PWE;
+            p[0] = (uint64_t)S.key[e];
+            p[1] = (uint64_t)S.slice[e];
+            p[2] = f;
+#pragma unroll
+            for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];
+            if (f & F_TIMER) __hip_atomic_fetch_min(&s_newmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            a.state_count[sb] = s_nlive;
+            a.sb_min_timer[sb] = s_newmin;
+            __hip_atomic_fetch_add(&c->live_entries, (int64_t)(s_nlive - n0), __ATOMIC_RELAXED, DEV_SCOPE);
+            if (s_fired) __hip_atomic_fetch_add(&c->fired, (uint64_t)s_fired, __ATOMIC_RELAXED, DEV_SCOPE);
+            if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
+        }
+    }
+    // ---- last workgroup publishes the new progress (all workgroups read the old one above)
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        const uint32_t t = atomicAdd(&c->k4_done, 1u);
+        if (t == gridDim.x - 1) {
+            __threadfence();
+            if (adv) {
+                c->cur = W;
+                if (W >= ntp) c->ntp = next_trigger_watermark(W, a.win.slice_div);
+            }
+            if (do_flush) {
+                c->pending_chunks = 0;
+                c->min_pending = INT64_MAX;
+                c->pending_rows = 0;
+            }
+            c->n_treq = 0;
+            c->k4_done = 0;
+            __threadfence();
+        }
+    }
+}
+
+__global__ void k_init_ctrl(Ctrl* c) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        c->cur = INT64_MIN;
+        c->ntp = INT64_MIN;
+        c->min_pending = INT64_MAX;
+        c->pending_chunks = 0;
+        c->n_treq = 0;
+        c->out_count = 0;
+        c->late_dropped = 0;
+        c->fired = 0;
+        c->pending_rows = 0;
+        c->live_entries = 0;
+        c->error = 0;
+        c->k4_done = 0;
+        c->partials = 0;
+    }
+}
+
+hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
+    hipLaunchKernelGGL(k_init_ctrl, dim3(1), dim3(64), 0, s, c);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// template dispatch
+// ---------------------------------------------------------------------------------------
+template <int NV, int NW>
+static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s) {
+    constexpr int RPT = ingest_rpt(NV);
+    const int64_t grid = (a.n + BLOCK * RPT - 1) / (BLOCK * RPT);
+    if (grid == 0) return hipSuccess;
+    const size_t dyn = (size_t)(a.ks.n_sb + 1) * sizeof(uint32_t);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            64 * 1024);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_ingest<NV, NW, RPT>), dim3((unsigned)grid), dim3(BLOCK), dyn, s, a);
+    return hipGetLastError();
+}
+
+template <int NV>
+static hipError_t ingest_nv(const IngestArgs& a, hipStream_t s) {
+    const int nw = a.wd.nw;
+    if (nw <= 1) return ingest_nw<NV, 1>(a, s);
+    if (nw <= 2) return ingest_nw<NV, 2>(a, s);
+    if (nw <= 4) return ingest_nw<NV, 4>(a, s);
+    return ingest_nw<NV, 8>(a, s);
+}
+
+hipError_t launch_ingest(const IngestArgs& a, hipStream_t s) {
+    switch (a.nv) {
+        case 0: return ingest_nv<0>(a, s);
+        case 1: return ingest_nv<1>(a, s);
+        case 2: return ingest_nv<2>(a, s);
+        default: return ingest_nv<4>(a, s);
+    }
+}
+
+// LDS per merge workgroup: 2E*4 (index) + E*(20 + 8*NW) bytes; E = 2048 only for NW <= 2.
+template <int NW>
+static hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
+    if (NW <= 2 && a.cap_e == 2048)
+        hipLaunchKernelGGL((k_merge_fire<NW, (NW <= 2 ? 2048 : 1024)>), dim3(a.n_sb), dim3(BLOCK), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_merge_fire<NW, 1024>), dim3(a.n_sb), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s) {
+    const int nw = a.wd.nw;
+    if (nw <= 1) return merge_nw<1>(a, s);
+    if (nw <= 2) return merge_nw<2>(a, s);
+    if (nw <= 4) return merge_nw<4>(a, s);
+    return merge_nw<8>(a, s);
+}
+
+// ======================================================================================
+// stand-alone kernels: key groups, exchange partitioning, synthetic generator
+// ======================================================================================
+__global__ void k_key_groups(const int64_t* key, const int32_t* kh, int64_t n, int32_t kind, int32_t max_p,
+                             int32_t p, int32_t* kg, int32_t* dest) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t g = key_group_for_hash(java_key_hash(kind, key[i], kh ? kh[i] : 0), max_p);
+    if (kg) kg[i] = g;
+    if (dest) dest[i] = operator_for_key_group(max_p, p, g);
+}
+
+constexpr int PART_TILE = 4096;
+constexpr int PART_MAXP = 64;
+
+__global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, int64_t n, int32_t kind, int32_t max_p,
+                                                     int32_t p, uint32_t* counts) {
+    __shared__ uint32_t h[PART_MAXP];
+    const int tid = threadIdx.x;
+    if (tid < PART_MAXP) h[tid] = 0;
+    __syncthreads();
+    const int64_t b = (int64_t)blockIdx.x * PART_TILE;
+    for (int j = tid; j < PART_TILE; j += BLOCK) {
+        const int64_t i = b + j;
+        if (i >= n) break;
+        const int32_t g = key_group_for_hash(java_key_hash(kind, key[i], 0), max_p);
+        atomicAdd(&h[operator_for_key_group(max_p, p, g)], 1u);
+    }
+    __syncthreads();
+    if (tid < p) counts[(size_t)blockIdx.x * p + tid] = h[tid];
+}
+
+// one block: offsets[blk][d] = sum_{d'<d} total(d') + sum_{b'<blk} counts[b'][d]
+__global__ __launch_bounds__(BLOCK) void k_part_scan(uint32_t* counts, int64_t nblk, int32_t p, int64_t* totals) {
+    __shared__ uint64_t tot[PART_MAXP];
+    const int tid = threadIdx.x;
+    if (tid < p) {
+        uint64_t s = 0;
+        for (int64_t b = 0; b < nblk; b++) s += counts[b * p + tid];
+        tot[tid] = s;
+    }
+    __syncthreads();
+    if (tid < p) {
+        uint64_t base = 0;
+        for (int d = 0; d < tid; d++) base += tot[d];
+        uint64_t run = base;
+        for (int64_t b = 0; b < nblk; b++) {
+            const uint32_t v = counts[b * p + tid];
+            counts[b * p + tid] = (uint32_t)run;  // fits: n < 2^32 per call
+            run += v;
+        }
+        totals[tid] = (int64_t)tot[tid];
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, const int64_t* ts, const uint64_t* const* vals,
+                                                        int32_t ncols, int64_t n, int32_t kind, int32_t max_p,
+                                                        int32_t p, const uint32_t* offsets, int64_t* okey, int64_t* ots,
+                                                        uint64_t* const* ovals) {
+    __shared__ uint32_t h[PART_MAXP];
+    const int tid = threadIdx.x;
+    if (tid < p) h[tid] = offsets[(size_t)blockIdx.x * p + tid];
+    __syncthreads();
+    const int64_t b = (int64_t)blockIdx.x * PART_TILE;
+    for (int j = tid; j < PART_TILE; j += BLOCK) {
+        const int64_t i = b + j;
+        if (i >= n) break;
+        const int64_t k = key[i];
+        const int32_t g = key_group_for_hash(java_key_hash(kind, k, 0), max_p);
+        const uint32_t pos = atomicAdd(&h[operator_for_key_group(max_p, p, g)], 1u);
+        okey[pos] = k;
+        ots[pos] = ts[i];
+        for (int c = 0; c < ncols; c++) ovals[c][pos] = vals[c][i];
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) { return mix64(x + 0x9E3779B97F4A7C15ull); }
+
+__global__ void k_generate(fw_gen_params gp, int64_t i0, int64_t n, int64_t* key, int64_t* ts, int64_t* val) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t i = (uint64_t)(i0 + j);
+    const uint64_t u = splitmix64(gp.seed ^ (i * 0x9E3779B97F4A7C15ull));
+    const int64_t t = gp.t0_ms + (int64_t)i * 1000 / gp.rate_per_s - (int64_t)(u % (uint64_t)gp.ooo_ms);
+    int64_t k;
+    if (gp.key_dist == 0) {
+        k = gp.key_base + (int64_t)((u >> 20) % (uint64_t)gp.key_count);
+    } else {
+        const double x = (double)(u >> 11) * (1.0 / 9007199254740992.0);
+        int64_t lo = 0, hi = gp.key_count - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (gp.zipf_cdf[mid] > x) hi = mid; else lo = mid + 1;
+        }
+        k = gp.key_base + lo;
+    }
+    uint64_t v;
+    if (gp.value_kind == 0) v = 1 + u % 1000000000ull;
+    else if (gp.value_kind == 1) v = f64_bits(1000.0 * (double)(u >> 11) * (1.0 / 9007199254740992.0));
+    else v = u % 1000000ull;
+    if (key) key[j] = k;
+    if (ts) ts[j] = t;
+    if (val) val[j] = (int64_t)v;
+}
+
+}  // namespace fw
+
+// ======================================================================================
+// C-ABI wrappers for the stand-alone kernels
+// ======================================================================================
+using namespace fw;
+
+extern "C" int fw_assign_key_groups(const int64_t* d_key, const int32_t* d_key_hash, int64_t n, int32_t key_hash_kind,
+                                    int32_t max_parallelism, int32_t parallelism, int32_t* d_kg, int32_t* d_dest,
+                                    void* stream) {
+    if (n <= 0) return FW_OK;
+    if (!d_key || max_parallelism <= 0 || parallelism <= 0) return FW_E_INVALID;
+    hipLaunchKernelGGL(k_key_groups, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d_key,
+                       d_key_hash, n, key_hash_kind, max_parallelism, parallelism, d_kg, d_dest);
+    return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
+}
+
+extern "C" int64_t fw_partition_workspace_bytes(int64_t n, int32_t parallelism) {
+    const int64_t nblk = (n + PART_TILE - 1) / PART_TILE;
+    return (nblk * parallelism * 4 + 2 * FW_MAX_COLS * 8 + 255) & ~255ll;
+}
+
+extern "C" int fw_partition_by_dest(const int64_t* d_key, const int64_t* d_ts, const void* const* d_values,
+                                    int32_t n_cols, int64_t n, int32_t key_hash_kind, int32_t max_parallelism,
+                                    int32_t parallelism, int64_t* d_out_key, int64_t* d_out_ts,
+                                    void* const* d_out_values, int64_t* d_counts, void* d_workspace,
+                                    int64_t workspace_bytes, void* stream) {
+    if (parallelism <= 0 || parallelism > PART_MAXP || n_cols < 0 || n_cols > FW_MAX_COLS) return FW_E_INVALID;
+    if (key_hash_kind == FW_KEYHASH_PRECOMPUTED) return FW_E_INVALID;
+    if (workspace_bytes < fw_partition_workspace_bytes(n, parallelism)) return FW_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (n <= 0) {
+        return hipMemsetAsync(d_counts, 0, sizeof(int64_t) * parallelism, s) == hipSuccess ? FW_OK : FW_E_DEVICE;
+    }
+    const int64_t nblk = (n + PART_TILE - 1) / PART_TILE;
+    uint32_t* counts = (uint32_t*)d_workspace;
+    // value-column pointer arrays live in the workspace tail (device-visible)
+    const uint64_t** dv = (const uint64_t**)((char*)d_workspace + nblk * parallelism * 4);
+    dv = (const uint64_t**)(((uintptr_t)dv + 15) & ~(uintptr_t)15);
+    uint64_t** dov = (uint64_t**)(dv + FW_MAX_COLS);
+    const void* hv[2 * FW_MAX_COLS] = {nullptr};
+    for (int c = 0; c < n_cols; c++) {
+        hv[c] = d_values[c];
+        hv[FW_MAX_COLS + c] = d_out_values[c];
+    }
+    if (hipMemcpyAsync(dv, hv, sizeof(hv), hipMemcpyHostToDevice, s) != hipSuccess) return FW_E_DEVICE;
+    hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, n, key_hash_kind, max_parallelism,
+                       parallelism, counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(BLOCK), 0, s, counts, nblk, parallelism, d_counts);
+    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_ts,
+                       (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
+                       d_out_key, d_out_ts, (uint64_t* const*)dov);
+    return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
+}
+
+extern "C" int fw_generate(const fw_gen_params* gp, int64_t i0, int64_t n, int64_t* d_key, int64_t* d_ts,
+                           int64_t* d_value, void* stream) {
+    if (!gp || gp->rate_per_s <= 0 || gp->ooo_ms <= 0 || gp->key_count <= 0) return FW_E_INVALID;
+    if (gp->key_dist == 1 && !gp->zipf_cdf) return FW_E_INVALID;
+    if (n <= 0) return FW_OK;
+    hipLaunchKernelGGL(k_generate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *gp, i0, n,
+                       d_key, d_ts, d_value);
+    return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
+}

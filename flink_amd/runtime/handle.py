@@ -1,0 +1,135 @@
+"""Python wrapper of one libflinkwin operator handle (one Flink operator subtask).
+
+The handle is single-threaded like Flink's mailbox thread (MailboxProcessor.java:58-91).
+"""
+import ctypes as C
+
+import numpy as np
+
+from .. import abi
+from .._native import check, lib
+
+
+def _np_view(ptr, n, dtype):
+    if n == 0:
+        return np.empty(0, dtype)
+    ct = {np.int64: C.c_int64, np.int32: C.c_int32, np.uint32: C.c_uint32, np.uint64: C.c_uint64}[dtype]
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,))
+
+
+class WindowAggHandle:
+    def __init__(self, cfg: abi.fw_config):
+        self.cfg = cfg
+        self._h = C.c_void_p()
+        check(lib().fw_create(C.byref(cfg), C.byref(self._h)))
+        self.n_aggs = cfg.n_aggs
+
+    # ---- lifecycle
+    def close(self):
+        if self._h:
+            lib().fw_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream_ptr(self):
+        return lib().fw_get_stream(self._h)
+
+    def sync(self):
+        check(lib().fw_sync(self._h))
+
+    def initialize_watermark(self, wm):
+        check(lib().fw_initialize_watermark(self._h, int(wm)))
+
+    # ---- ingest
+    def push_host(self, keys, ts, values=(), key_hashes=None):
+        """Host columns -> pinned staging -> device (fw_reserve / fw_commit)."""
+        keys = np.asarray(keys, dtype=np.int64)
+        n = len(keys)
+        cap = self.cfg.max_batch_rows
+        for o in range(0, n, cap):
+            m = min(cap, n - o)
+            cols = abi.fw_host_cols()
+            check(lib().fw_reserve(self._h, m, C.byref(cols)))
+            if m:
+                _np_view(cols.key, m, np.int64)[:] = keys[o:o + m]
+                _np_view(cols.ts, m, np.int64)[:] = np.asarray(ts, dtype=np.int64)[o:o + m]
+                if key_hashes is not None:
+                    _np_view(cols.key_hash, m, np.int32)[:] = np.asarray(key_hashes, dtype=np.int32)[o:o + m]
+                for c, v in enumerate(values):
+                    v = np.asarray(v)
+                    if v.dtype == np.float64:
+                        v = v.view(np.int64)
+                    _np_view(cols.values[c], m, np.int64)[:] = v.astype(np.int64, copy=False)[o:o + m]
+            check(lib().fw_commit(self._h, m))
+
+    def push_device(self, keys, ts, values=(), key_hashes=None):
+        """Device-resident columns (torch cuda tensors, int64 / float64).  The handle's stream
+        waits for the producer's current stream before reading them."""
+        import torch
+        n = keys.numel()
+        if n == 0:
+            return
+        ext = torch.cuda.ExternalStream(self.stream_ptr, device=keys.device)
+        ext.wait_stream(torch.cuda.current_stream(keys.device))
+        arr = (C.c_void_p * abi.FW_MAX_COLS)()
+        for c, v in enumerate(values):
+            arr[c] = v.data_ptr()
+        check(lib().fw_push_device(self._h, n, keys.data_ptr(), ts.data_ptr(),
+                                   key_hashes.data_ptr() if key_hashes is not None else None, arr))
+        # keep the inputs alive until the stream has consumed them
+        for t in (keys, ts, *values):
+            t.record_stream(ext)
+
+    # ---- progress / output
+    def advance(self, wm):
+        check(lib().fw_advance(self._h, int(wm)))
+
+    def flush(self):
+        check(lib().fw_flush(self._h))
+
+    def results(self, reset=True):
+        r = abi.fw_result()
+        check(lib().fw_results(self._h, C.byref(r), 1))
+        n = r.n
+        out = {
+            "key": _np_view(r.key, n, np.int64).copy(),
+            "window_start": _np_view(r.window_start, n, np.int64).copy(),
+            "window_end": _np_view(r.window_end, n, np.int64).copy(),
+            "values": [_np_view(r.values[a], n, np.int64).copy() for a in range(self.n_aggs)],
+            "null_mask": _np_view(r.null_mask, n, np.uint32).copy(),
+        }
+        if reset:
+            self.reset_results()
+        return out
+
+    def device_results(self):
+        """(n, fw_result with device pointers) -- for device-side sinks."""
+        r = abi.fw_result()
+        check(lib().fw_results(self._h, C.byref(r), 0))
+        return r.n, r
+
+    def reset_results(self):
+        check(lib().fw_results_reset(self._h))
+
+    def stats(self):
+        s = abi.fw_stats()
+        check(lib().fw_get_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in abi.fw_stats._fields_}
+
+    # ---- checkpoint
+    def snapshot(self) -> bytes:
+        size = C.c_int64()
+        check(lib().fw_snapshot(self._h, None, 0, C.byref(size)))
+        buf = C.create_string_buffer(size.value)
+        check(lib().fw_snapshot(self._h, buf, size.value, C.byref(size)))
+        return buf.raw[:size.value]
+
+    def restore(self, blob: bytes):
+        buf = C.create_string_buffer(blob, len(blob))
+        check(lib().fw_restore(self._h, buf, len(blob)))

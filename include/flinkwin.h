@@ -169,6 +169,7 @@ typedef struct {
     int64_t pending_rows;              /* rows buffered (not yet flushed into state)    */
     int64_t results_available;
     int64_t num_fired_windows;         /* numFiredTimers analogue                       */
+    int64_t partials_emitted;          /* partial (key, slice) aggregates written by ingest */
     int32_t error_flags;
     int32_t num_superbuckets;
 } fw_stats;
@@ -238,6 +239,14 @@ typedef struct {
 } fw_gen_params;
 int fw_generate(const fw_gen_params* gp, int64_t i0, int64_t n, int64_t* d_key, int64_t* d_ts,
                 int64_t* d_value, void* stream);
+
+/* ---- host-side restatements (no device use): the same code the kernels run -------------- */
+/* KeyGroupRangeAssignment.assignToKeyGroup on key.hashCode() as fw_key_hash_kind defines it. */
+int32_t fw_host_key_group(int32_t key_hash_kind, int64_t key, int32_t precomputed_hash, int32_t max_parallelism);
+/* TimeWindow.getWindowStartWithOffset (FR/streaming/api/windowing/windows/TimeWindow.java:264). */
+int64_t fw_host_window_start(int64_t ts, int64_t offset, int64_t size);
+/* TimeWindowUtil.getNextTriggerWatermark, UTC (TR/util/TimeWindowUtil.java:186). */
+int64_t fw_host_next_trigger_watermark(int64_t watermark, int64_t interval);
 
 #ifdef __cplusplus
 }

@@ -112,3 +112,31 @@ class OracleAdapter:
     @property
     def late_dropped(self):
         return self.op.late_dropped
+
+
+class GpuAdapter:
+    """Drives the HIP operator (libflinkwin via flink_amd) through a fixture."""
+
+    def __init__(self, fx, **overrides):
+        from flink_amd.runtime.handle import WindowAggHandle
+        self._cls = WindowAggHandle
+        self.cfg = fixture_config(fx, **overrides)
+        self.h = WindowAggHandle(self.cfg)
+        self.dropped_before = 0
+
+    def process_batch(self, k, t, h, vals):
+        self.h.push_host(k, t, vals, key_hashes=h)
+
+    def process_watermark(self, w):
+        self.h.advance(w)
+        return self.h.results(reset=True)
+
+    def snapshot_restore(self):
+        blob = self.h.snapshot()
+        self.h.close()
+        self.h = self._cls(self.cfg)
+        self.h.restore(blob)
+
+    @property
+    def late_dropped(self):
+        return self.h.stats()["num_late_records_dropped"]

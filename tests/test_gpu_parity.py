@@ -1,0 +1,231 @@
+"""GPU parity: the HIP operator (libflinkwin) against the CPU oracle and the reference's golden
+fixtures.  Integer aggregates and window boundaries must be bit-exact; DOUBLE SUM/AVG within
+1e-9 relative (north_star), DOUBLE MIN/MAX equal as values.  Run on an MI355X via gpurun."""
+import zlib
+
+import numpy as np
+import pytest
+
+from fixture_runner import GpuAdapter, load_fixtures, replay
+from flink_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = load_fixtures()
+REL_TOL = 1e-9
+
+
+def _torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    _torch_cuda()
+
+
+@pytest.mark.parametrize("fx", FIXTURES, ids=[f["name"] for f in FIXTURES])
+def test_gpu_reproduces_reference_golden(fx):
+    replay(fx, GpuAdapter(fx))
+
+
+# ------------------------------------------------------------------------------------------
+# randomized streams with late records, compared watermark by watermark against the oracle
+# ------------------------------------------------------------------------------------------
+def _rows(res, cfg, double_cols):
+    n_aggs = cfg.n_aggs
+    rows = []
+    for i in range(len(res["key"])):
+        rows.append((int(res["key"][i]), int(res["window_start"][i]), int(res["window_end"][i]),
+                     tuple(int(res["values"][a][i]) for a in range(n_aggs)), int(res["null_mask"][i])))
+    rows.sort()
+    return rows
+
+
+def _compare(got, want, double_cols, ctx):
+    assert len(got) == len(want), f"{ctx}: {len(got)} rows vs oracle {len(want)}"
+    for g, w in zip(got, want):
+        assert g[:3] == w[:3], f"{ctx}: key/window {g[:3]} != {w[:3]}"
+        assert g[4] == w[4], f"{ctx}: null mask {g} != {w}"
+        for a, (x, y) in enumerate(zip(g[3], w[3])):
+            if a in double_cols and not (g[4] >> a & 1):
+                xd = float(np.int64(x).view(np.float64))
+                yd = float(np.int64(y).view(np.float64))
+                assert xd == pytest.approx(yd, rel=REL_TOL, abs=0.0), f"{ctx}: agg {a} {xd} vs {yd}"
+            else:
+                assert x == y, f"{ctx}: agg {a} {x} != {y} (row {g} vs {w})"
+
+
+def _stream(seed, n, n_keys, ooo, step_ms, n_wm, dup_wm=False):
+    """Events spread over time with out-of-orderness `ooo`; watermarks lag less than `ooo`, so
+    a share of the records is late (some dropped, some merged into unfired windows)."""
+    rng = np.random.default_rng(seed)
+    per = n // n_wm
+    batches = []
+    t0 = 1_600_000_000_000
+    for b in range(n_wm):
+        base = t0 + b * step_ms
+        ts = base + rng.integers(0, step_ms, per) - rng.integers(0, ooo, per)
+        keys = rng.integers(0, n_keys, per).astype(np.int64) * 7919 - 50000
+        iv = rng.integers(-1000, 1000, per).astype(np.int64)
+        dv = rng.random(per) * 1000.0
+        wm = base + step_ms - ooo // 3
+        batches.append((keys, ts.astype(np.int64), iv, dv, wm))
+        if dup_wm and b % 3 == 0:
+            batches.append((keys[:0], ts[:0], iv[:0], dv[:0], wm - 5))  # non-advancing watermark
+    return batches
+
+
+def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None):
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    o = OracleOperator(cfg)
+    g = WindowAggHandle(cfg)
+    for bi, (k, t, iv, dv, wm) in enumerate(batches):
+        vals = [iv, dv.view(np.int64)]
+        o.process_batch(k, t, vals)
+        for part in np.array_split(np.arange(len(k)), split):
+            g.push_host(k[part], t[part], [v[part] for v in vals])
+        o.process_watermark(wm)
+        g.advance(wm)
+        want = _rows(o.results(clear=True), cfg, double_cols)
+        got = _rows(g.results(reset=True), cfg, double_cols)
+        _compare(got, want, double_cols, f"batch {bi} wm {wm}")
+        if snapshot_at is not None and bi == snapshot_at:
+            o.snapshot_restore()
+            blob = g.snapshot()
+            g.close()
+            g = WindowAggHandle(cfg)
+            g.restore(blob)
+    assert g.stats()["num_late_records_dropped"] == o.late_dropped
+    assert g.stats()["error_flags"] == 0
+    return o.late_dropped
+
+
+I64, F64, I32 = abi.T_I64, abi.T_F64, abi.T_I32
+VT = [I64, F64]
+CASES = {
+    "sql_tumble_int_aggs": dict(window_kind=abi.WIN_TUMBLE, size_ms=10000,
+                                aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MIN, 0, I64), (abi.AGG_MAX, 0, I64)]),
+    "sql_tumble_offset": dict(window_kind=abi.WIN_TUMBLE, size_ms=7000, offset_ms=-2500,
+                              aggs=[(abi.AGG_MAX, 0, I64), (abi.AGG_COUNT_STAR, 0, I64)]),
+    "sql_tumble_double": dict(window_kind=abi.WIN_TUMBLE, size_ms=5000,
+                              aggs=[(abi.AGG_SUM, 1, F64), (abi.AGG_AVG, 1, F64), (abi.AGG_MIN, 1, F64), (abi.AGG_MAX, 1, F64)]),
+    "sql_hop": dict(window_kind=abi.WIN_HOP, size_ms=10000, slide_ms=2000, count_star_index=0,
+                    aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MAX, 1, F64)]),
+    "sql_hop_offset": dict(window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=3000, offset_ms=1000, count_star_index=1,
+                           aggs=[(abi.AGG_SUM, 0, I64), (abi.AGG_COUNT_STAR, 0, I64)]),
+    "sql_cumulate_countstar": dict(window_kind=abi.WIN_CUMULATE, size_ms=12000, slide_ms=2000, count_star_index=0,
+                                   aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MIN, 0, I64), (abi.AGG_MAX, 0, I64)]),
+    "sql_cumulate_nocount": dict(window_kind=abi.WIN_CUMULATE, size_ms=9000, slide_ms=3000,
+                                 aggs=[(abi.AGG_SUM, 0, I64), (abi.AGG_AVG, 0, I64)]),
+    "ds_tumble_sum": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_TUMBLE, size_ms=4000,
+                          aggs=[(abi.AGG_SUM, 0, I64)]),
+    "ds_sliding_max": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000,
+                           aggs=[(abi.AGG_MAX, 0, I64)]),
+    "ds_sliding_min_double": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=4000, slide_ms=1000,
+                                  aggs=[(abi.AGG_MIN, 1, F64)]),
+}
+
+
+def _cfg(kw, **extra):
+    kw = dict(kw)
+    kw.update(extra)
+    kw.setdefault("value_col_types", VT)
+    kw.setdefault("key_hash", abi.KEYHASH_LONG)
+    kw.setdefault("state_capacity", 1 << 16)
+    kw.setdefault("max_batch_rows", 1 << 16)
+    kw.setdefault("output_capacity", 1 << 18)
+    return abi.make_config(**kw)
+
+
+def _double_cols(kw):
+    return {a for a, (k, c, t) in enumerate(kw["aggs"]) if t == F64 and k in (abi.AGG_SUM, abi.AGG_AVG, abi.AGG_MIN, abi.AGG_MAX)}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_random_stream_matches_oracle(name):
+    kw = CASES[name]
+    late = _run_both(_cfg(kw), _stream(zlib.crc32(name.encode()) % 1000, 60000, 700, ooo=2 * kw["size_ms"] + 1500,
+                                       step_ms=1500, n_wm=30), _double_cols(kw))
+    assert late > 0  # the stream exercises the late-record paths
+
+
+@pytest.mark.parametrize("name", ["sql_hop", "sql_cumulate_countstar", "ds_sliding_max"])
+def test_split_pushes_snapshot_and_stale_watermarks(name):
+    kw = CASES[name]
+    _run_both(_cfg(kw), _stream(5, 40000, 300, ooo=2500, step_ms=1000, n_wm=24, dup_wm=True),
+              _double_cols(kw), split=3, snapshot_at=11)
+
+
+def test_hot_keys_fold_in_lds_cache():
+    # Zipf-skewed keys: most records of a chunk fold into a handful of cache slots
+    rng = np.random.default_rng(3)
+    kw = CASES["sql_cumulate_countstar"]
+    batches = []
+    for b in range(10):
+        n = 50000
+        keys = np.minimum(rng.zipf(1.3, n), 5000).astype(np.int64)
+        ts = 1_600_000_000_000 + b * 2000 + rng.integers(0, 2000, n)
+        batches.append((keys, ts.astype(np.int64), rng.integers(0, 100, n), rng.random(n), 1_600_000_000_000 + b * 2000 + 1000))
+    _run_both(_cfg(kw), batches, set())
+
+
+def test_int_sum_wraps_like_java():
+    cfg = _cfg(dict(window_kind=abi.WIN_TUMBLE, size_ms=1000, aggs=[(abi.AGG_SUM, 0, I32), (abi.AGG_SUM, 1, I64)]),
+               value_col_types=[I32, I64])
+    k = np.zeros(8, np.int64)
+    t = np.arange(8, dtype=np.int64)
+    big = np.full(8, 2**31 - 7, np.int64)
+    huge = np.full(8, 2**62, np.int64)
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    g, o = WindowAggHandle(cfg), OracleOperator(cfg)
+    g.push_host(k, t, [big, huge])
+    o.process_batch(k, t, [big, huge])
+    g.advance(5000)
+    o.process_watermark(5000)
+    rg, ro = g.results(), o.results()
+    w32 = (8 * (2**31 - 7)) & 0xFFFFFFFF
+    w32 = w32 - 2**32 if w32 >= 2**31 else w32
+    assert list(rg["values"][0]) == list(ro["values"][0]) == [w32]
+    assert list(rg["values"][1]) == list(ro["values"][1]) == [0]  # 8 * 2^62 wraps to 0
+
+
+def test_device_generator_matches_host_generator():
+    torch = _torch_cuda()
+    from flink_amd import _native
+    from oracle import oracle as O
+    import ctypes as C
+    cdf = O.zipf_cdf(1000, 1.1)
+    dcdf = torch.tensor(cdf, device="cuda")
+    for dist, vk in ((0, 0), (0, 1), (1, 2)):
+        gp = abi.fw_gen_params(seed=42, t0_ms=1599998400000, rate_per_s=1000000, ooo_ms=4000, key_base=1000,
+                               key_count=1000 if dist else 1000000, key_dist=dist, value_kind=vk,
+                               zipf_cdf=dcdf.data_ptr() if dist else None)
+        n, i0 = 100000, 123456789
+        k = torch.empty(n, dtype=torch.int64, device="cuda")
+        t = torch.empty_like(k)
+        v = torch.empty_like(k)
+        s = torch.cuda.current_stream().cuda_stream
+        _native.check(_native.lib().fw_generate(C.byref(gp), i0, n, k.data_ptr(), t.data_ptr(), v.data_ptr(), s))
+        hk, ht, hv = O.generate(gp, i0, n, cdf if dist else None)
+        assert np.array_equal(k.cpu().numpy(), hk)
+        assert np.array_equal(t.cpu().numpy(), ht)
+        assert np.array_equal(v.cpu().numpy(), hv)
+
+
+def test_device_key_groups_match_oracle():
+    torch = _torch_cuda()
+    from flink_amd.runtime.keygroups import assign_key_groups_device
+    from oracle import oracle as O
+    rng = np.random.default_rng(11)
+    keys = rng.integers(-(1 << 63), (1 << 63) - 1, 5000, dtype=np.int64)
+    for kind in (abi.KEYHASH_LONG, abi.KEYHASH_BINROW_BIGINT):
+        kg, dest = assign_key_groups_device(torch.tensor(keys, device="cuda"), 128, 8, kind)
+        want = np.array([O.key_group(kind, int(x), 128) for x in keys])
+        assert np.array_equal(kg.cpu().numpy(), want)
+        assert np.array_equal(dest.cpu().numpy(), want * 8 // 128)

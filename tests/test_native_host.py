@@ -1,0 +1,68 @@
+"""CPU-side checks of the native library: it loads, exports every symbol include/flinkwin.h
+declares, and its host-side restatements (the code the kernels run) agree with the oracle.
+No device call is made here."""
+import re
+
+import numpy as np
+import pytest
+
+from flink_amd import _native, abi
+from oracle import oracle as O
+
+HEADER = __import__("os").path.join(__import__("os").path.dirname(__file__), "..", "include", "flinkwin.h")
+
+
+def test_library_loads_and_exports_header_symbols():
+    L = _native.lib()
+    text = open(HEADER).read()
+    declared = set(re.findall(r"^\s*(?:int|int32_t|int64_t|void\s*\*|const char\s*\*)\s+(fw_\w+)\s*\(", text, re.M))
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(_native.EXPORTED) == declared
+    assert L.fw_abi_version() == abi.FW_ABI_VERSION
+
+
+def test_config_struct_layout_matches_header():
+    import ctypes as C
+    # fw_config: 4 ints, 3 int64, 2 ints, 8 agg descs (16 B), int, 8 ints, 4 ints, 3 int64
+    assert C.sizeof(abi.fw_config) == 16 + 24 + 8 + 128 + 4 + 32 + 16 + 4 + 24
+
+
+def test_window_start_matches_oracle():
+    L = _native.lib()
+    rng = np.random.default_rng(7)
+    for _ in range(20000):
+        size = int(rng.choice([1, 2, 3, 7, 1000, 3600000, 86400000, int(rng.integers(1, 1 << 40))]))
+        off = int(rng.integers(-size + 1, size)) if size > 1 else 0
+        ts = int(rng.integers(-(1 << 62), 1 << 62))
+        assert L.fw_host_window_start(ts, off, size) == O.window_start_with_offset(ts, off, size)
+    for ts in (-(1 << 63), (1 << 63) - 1, 0, -1):
+        assert L.fw_host_window_start(ts, 0, 1000) == O.window_start_with_offset(ts, 0, 1000)
+
+
+def test_next_trigger_watermark_matches_oracle():
+    L = _native.lib()
+    for wm in (-(1 << 63), -1, 0, 999, 1000, 1999, (1 << 63) - 1, 1599998400000):
+        for iv in (1, 1000, 2000, 60000):
+            assert L.fw_host_next_trigger_watermark(wm, iv) == O.next_trigger_watermark(wm, iv)
+
+
+@pytest.mark.parametrize("kind", [abi.KEYHASH_LONG, abi.KEYHASH_INT, abi.KEYHASH_BINROW_BIGINT, abi.KEYHASH_BINROW_INT])
+def test_key_group_matches_oracle(kind):
+    L = _native.lib()
+    rng = np.random.default_rng(kind)
+    for k in list(rng.integers(-(1 << 63), (1 << 63) - 1, 3000)) + [0, 1, -1]:
+        for mp in (128, 1000):
+            assert L.fw_host_key_group(kind, int(k), 0, mp) == O.key_group(kind, int(k), mp)
+
+
+def test_invalid_configs_fail_without_device():
+    # argument validation happens before any device call
+    from flink_amd.runtime.handle import WindowAggHandle
+    with pytest.raises(_native.FlinkWinError, match="Hopping window requires a COUNT"):
+        WindowAggHandle(abi.make_config(window_kind=abi.WIN_HOP, size_ms=3000, slide_ms=1000,
+                                        aggs=[(abi.AGG_SUM, 0, abi.T_I64)], value_col_types=[abi.T_I64]))
+    with pytest.raises(_native.FlinkWinError, match="integral multiple"):
+        WindowAggHandle(abi.make_config(window_kind=abi.WIN_CUMULATE, size_ms=3000, slide_ms=700,
+                                        aggs=[(abi.AGG_SUM, 0, abi.T_I64)], value_col_types=[abi.T_I64]))

@@ -129,7 +129,7 @@ class OracleOperator:
         if clear:
             L.or_clear_results(self.h)
         return {"key": key, "window_start": ws, "window_end": we,
-                "values": [vals[a] for a in range(na)], "null_mask": nm, "epoch": ep}
+                "values": [vals[a].view(np.int64) for a in range(na)], "null_mask": nm, "epoch": ep}
 
 
 def murmur_hash(code):

@@ -181,11 +181,12 @@ def main():
         return rk, rt, rv
 
     def global_watermark(b):
-        w = torch.tensor([watermark(b, wl["rate"])], dtype=torch.int64, device=dev)
+        w = watermark(b, wl["rate"])
         if world > 1:  # StatusWatermarkValve: min over input channels
-            dist.all_reduce(w, op=dist.ReduceOp.MIN)
-            return int(w.item())
-        return int(w[0])
+            t = torch.tensor([w], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return int(t.item())
+        return w
 
     out_cap = 2 * keys_total // world + (1 << 20)
     if wl["window"][0] == "CUMULATE":

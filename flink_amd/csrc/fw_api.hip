@@ -69,13 +69,16 @@ struct fw_handle {
     int nv = 0;
     int slot_col[MAX_KCOLS] = {0, 0, 0, 0};
     int nw_t = 1;  // template word count (layout stride)
-    int64_t max_chunks = 0;
+    int64_t cap_rows = 0;     // rows per partial-buffer slot (= max rows per push piece)
+    int64_t max_nch = 0;      // ingest chunks per push piece
     int cap_e = 1024;
     bool always_flush = false;
 
     Ctrl* ctrl = nullptr;
     uint64_t* parts = nullptr;
-    uint32_t* off = nullptr;
+    uint32_t* cnt = nullptr;
+    uint32_t* tile_sum = nullptr;
+    uint32_t* starts = nullptr;
     int64_t* treq = nullptr;
     int64_t treq_cap = 0;
     uint64_t* state = nullptr;
@@ -86,7 +89,17 @@ struct fw_handle {
     int64_t* out_we = nullptr;
     uint64_t* out_val[FW_MAX_AGGS] = {};
     uint32_t* out_null = nullptr;
-    int64_t out_cap = 0;
+    int64_t out_cap = 0;       // result rows between resets (= overflow region rows)
+    int64_t slab_cap = 0;      // output slab rows per superbucket
+    int32_t* sb_out = nullptr;
+    uint32_t* sb_fired = nullptr;
+    int64_t* chunk_stats = nullptr;
+    int64_t* coff = nullptr;   // compaction offsets [n_sb + 2]
+    int64_t* res_key = nullptr;
+    int64_t* res_ws = nullptr;
+    int64_t* res_we = nullptr;
+    uint64_t* res_val[FW_MAX_AGGS] = {};
+    uint32_t* res_null = nullptr;
 
     // host-staged ingest (double-buffered pinned columns)
     int64_t stage_cap = 0;
@@ -107,7 +120,7 @@ struct fw_handle {
     std::vector<uint64_t> r_val[FW_MAX_AGGS];
     std::vector<uint32_t> r_null;
 
-    int64_t chunks_ub = 0;  // upper bound of device pending_chunks
+    int64_t pushes_ub = 0;  // upper bound of device pending_pushes
     int64_t host_cur = INT64_MIN;
 };
 
@@ -253,10 +266,11 @@ int validate_and_plan(fw_handle* h) {
     ks.n_sb = ks.n_kg << ks.sb_per_kg_log2;
     if (c.max_batch_rows <= 0) return fail(FW_E_INVALID, "max_batch_rows must be > 0");
     if (c.output_capacity <= 0) return fail(FW_E_INVALID, "output_capacity must be > 0");
-    const int64_t rows = (int64_t)BLOCK * ingest_rpt(h->nv);
-    h->max_chunks = 8 * ((c.max_batch_rows + rows - 1) / rows) + 8;
+    h->cap_rows = ((c.max_batch_rows + K3_CH - 1) / K3_CH) * K3_CH;
+    h->max_nch = h->cap_rows / K3_CH;
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     h->out_cap = c.output_capacity;
+    h->slab_cap = std::max<int64_t>(64, (2 * c.output_capacity + ks.n_sb - 1) / ks.n_sb);
     h->stage_cap = c.max_batch_rows;
     return FW_OK;
 }
@@ -276,18 +290,33 @@ int allocate(fw_handle* h) {
     int rc;
     const int PW = 2 + h->nw_t, PWE = 3 + h->nw_t;
     if ((rc = dalloc(&h->ctrl, 1))) return rc;
-    if ((rc = dalloc(&h->parts, (size_t)h->max_chunks * K3_CHUNK * PW))) return rc;
-    if ((rc = dalloc(&h->off, (size_t)(h->ks.n_sb + 1) * h->max_chunks))) return rc;
+    if ((rc = dalloc(&h->parts, (size_t)FW_MAX_PENDING * h->cap_rows * PW))) return rc;
+    if ((rc = dalloc(&h->cnt, (size_t)h->ks.n_sb * h->max_nch))) return rc;
+    if ((rc = dalloc(&h->tile_sum, (size_t)h->ks.n_sb * h->max_nch / 2048 + 2))) return rc;
+    if ((rc = dalloc(&h->starts, (size_t)FW_MAX_PENDING * (h->ks.n_sb + 1)))) return rc;
     if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
     if ((rc = dalloc(&h->state, (size_t)h->ks.n_sb * h->cap_e * PWE))) return rc;
     if ((rc = dalloc(&h->state_count, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->sb_min_timer, h->ks.n_sb))) return rc;
-    if ((rc = dalloc(&h->out_key, h->out_cap))) return rc;
-    if ((rc = dalloc(&h->out_ws, h->out_cap))) return rc;
-    if ((rc = dalloc(&h->out_we, h->out_cap))) return rc;
-    if ((rc = dalloc(&h->out_null, h->out_cap))) return rc;
+    const size_t orows = (size_t)h->ks.n_sb * h->slab_cap + h->out_cap;
+    if ((rc = dalloc(&h->out_key, orows))) return rc;
+    if ((rc = dalloc(&h->out_ws, orows))) return rc;
+    if ((rc = dalloc(&h->out_we, orows))) return rc;
+    if ((rc = dalloc(&h->out_null, orows))) return rc;
     for (int g = 0; g < c.n_aggs; g++)
-        if ((rc = dalloc(&h->out_val[g], h->out_cap))) return rc;
+        if ((rc = dalloc(&h->out_val[g], orows))) return rc;
+    if ((rc = dalloc(&h->res_key, h->out_cap))) return rc;
+    if ((rc = dalloc(&h->res_ws, h->out_cap))) return rc;
+    if ((rc = dalloc(&h->res_we, h->out_cap))) return rc;
+    if ((rc = dalloc(&h->res_null, h->out_cap))) return rc;
+    for (int g = 0; g < c.n_aggs; g++)
+        if ((rc = dalloc(&h->res_val[g], h->out_cap))) return rc;
+    if ((rc = dalloc(&h->sb_out, h->ks.n_sb))) return rc;
+    if ((rc = dalloc(&h->sb_fired, h->ks.n_sb))) return rc;
+    if ((rc = dalloc(&h->coff, h->ks.n_sb + 2))) return rc;
+    if ((rc = dalloc(&h->chunk_stats, 3 * h->max_nch + 3))) return rc;
+    HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
+    HIP_TRY(hipMemsetAsync(h->sb_fired, 0, sizeof(uint32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->state_count, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
     std::vector<int64_t> inf(h->ks.n_sb, INT64_MAX);
     HIP_TRY(hipMemcpyAsync(h->sb_min_timer, inf.data(), sizeof(int64_t) * h->ks.n_sb, hipMemcpyHostToDevice, h->stream));
@@ -332,8 +361,8 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     MergeArgs a{};
     a.ctrl = h->ctrl;
     a.parts = h->parts;
-    a.off = h->off;
-    a.max_chunks = h->max_chunks;
+    a.starts = h->starts;
+    a.cap_rows = h->cap_rows;
     a.treq = h->treq;
     a.state = h->state;
     a.state_count = h->state_count;
@@ -350,6 +379,9 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     for (int g = 0; g < FW_MAX_AGGS; g++) a.out_val[g] = h->out_val[g] ? h->out_val[g] : h->out_val[0];
     a.out_null = h->out_null;
     a.out_cap = h->out_cap;
+    a.slab_cap = h->slab_cap;
+    a.sb_out = h->sb_out;
+    a.sb_fired = h->sb_fired;
     a.wm = wm;
     a.force_flush = force;
     return a;
@@ -357,22 +389,19 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
 
 int force_flush(fw_handle* h) {
     HIP_TRY(launch_merge_fire(merge_args(h, INT64_MIN, 1), h->stream));
-    h->chunks_ub = 0;
+    h->pushes_ub = 0;
     return FW_OK;
 }
 
 int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int32_t* kh, const void* const* vals) {
-    const int64_t per = h->max_chunks / 2 * ((int64_t)BLOCK * ingest_rpt(h->nv));  // split very large pushes
-    for (int64_t o = 0; o < n; o += per) {
-        const int64_t m = std::min(per, n - o);
-        const int64_t rows = (int64_t)BLOCK * ingest_rpt(h->nv);
-        const int64_t chunks = (m + rows - 1) / rows;
-        if (h->chunks_ub + chunks > h->max_chunks) {
+    for (int64_t o = 0; o < n; o += h->cap_rows) {
+        const int64_t m = std::min(h->cap_rows, n - o);
+        if (h->pushes_ub >= FW_MAX_PENDING) {
             Ctrl c;
             int rc = read_ctrl(h, &c);
             if (rc) return rc;
-            h->chunks_ub = c.pending_chunks;
-            if (h->chunks_ub + chunks > h->max_chunks) {
+            h->pushes_ub = c.pending_pushes;
+            if (h->pushes_ub >= FW_MAX_PENDING) {
                 // buffer full: flush into state (RecordsWindowBuffer.addElement EOFException path)
                 if ((rc = force_flush(h))) return rc;
             }
@@ -390,16 +419,16 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.nv = h->nv;
         a.ctrl = h->ctrl;
         a.parts = h->parts;
-        a.off = h->off;
-        a.max_chunks = h->max_chunks;
+        a.cap_rows = h->cap_rows;
+        a.cnt = h->cnt;
+        a.tile_sum = h->tile_sum;
+        a.starts = h->starts;
+        a.chunk_stats = h->chunk_stats;
+        a.n_chunks = (m + K3_CH - 1) / K3_CH;
         a.treq = h->treq;
         a.treq_cap = h->treq_cap;
-        // the kernel template stride must match the handle layout
-        WordDesc wd = h->wd;
-        wd.nw = h->wd.nw;
-        a.wd = wd;
         HIP_TRY(launch_ingest(a, h->stream));
-        h->chunks_ub += chunks;
+        h->pushes_ub++;
     }
     return FW_OK;
 }
@@ -434,7 +463,9 @@ int fw_destroy(fw_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     hipFree(h->ctrl);
     hipFree(h->parts);
-    hipFree(h->off);
+    hipFree(h->cnt);
+    hipFree(h->tile_sum);
+    hipFree(h->starts);
     hipFree(h->treq);
     hipFree(h->state);
     hipFree(h->state_count);
@@ -444,6 +475,15 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->out_we);
     hipFree(h->out_null);
     for (int g = 0; g < FW_MAX_AGGS; g++) hipFree(h->out_val[g]);
+    for (int g = 0; g < FW_MAX_AGGS; g++) hipFree(h->res_val[g]);
+    hipFree(h->res_key);
+    hipFree(h->res_ws);
+    hipFree(h->res_we);
+    hipFree(h->res_null);
+    hipFree(h->sb_out);
+    hipFree(h->sb_fired);
+    hipFree(h->coff);
+    hipFree(h->chunk_stats);
     for (int b = 0; b < 2; b++) {
         hipHostFree(h->h_key[b]);
         hipHostFree(h->h_ts[b]);
@@ -542,19 +582,45 @@ int fw_flush(fw_handle* h) {
 
 int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    CompactArgs ca{};
+    ca.ctrl = h->ctrl;
+    ca.sb_out = h->sb_out;
+    ca.off = h->coff;
+    ca.n_sb = h->ks.n_sb;
+    ca.n_aggs = h->cfg.n_aggs;
+    ca.slab_cap = h->slab_cap;
+    ca.out_key = h->out_key;
+    ca.out_ws = h->out_ws;
+    ca.out_we = h->out_we;
+    ca.out_null = h->out_null;
+    for (int g = 0; g < h->cfg.n_aggs; g++) {
+        ca.out_val[g] = h->out_val[g];
+        ca.res_val[g] = h->res_val[g];
+    }
+    ca.res_key = h->res_key;
+    ca.res_ws = h->res_ws;
+    ca.res_we = h->res_we;
+    ca.res_null = h->res_null;
+    ca.res_cap = h->out_cap;
+    HIP_TRY(launch_compact(ca, h->stream));
     Ctrl c;
     int rc = read_ctrl(h, &c);
     if (rc) return rc;
-    const int64_t n = std::min<int64_t>((int64_t)c.out_count, h->out_cap);
+    int64_t total = 0;
+    HIP_TRY(hipMemcpy(&total, h->coff + h->ks.n_sb + 1, sizeof total, hipMemcpyDeviceToHost));
+    if (total > h->out_cap)
+        return fail(FW_E_CAPACITY, "%lld result rows exceed output_capacity %lld (read results more often)",
+                    (long long)total, (long long)h->out_cap);
+    const int64_t n = total;
     memset(out, 0, sizeof *out);
     out->n = n;
     const int na = h->cfg.n_aggs;
     if (!copy_to_host) {
-        out->key = h->out_key;
-        out->window_start = h->out_ws;
-        out->window_end = h->out_we;
-        for (int g = 0; g < na; g++) out->values[g] = (int64_t*)h->out_val[g];
-        out->null_mask = h->out_null;
+        out->key = h->res_key;
+        out->window_start = h->res_ws;
+        out->window_end = h->res_we;
+        for (int g = 0; g < na; g++) out->values[g] = (int64_t*)h->res_val[g];
+        out->null_mask = h->res_null;
         return FW_OK;
     }
     h->r_key.resize(n);
@@ -562,14 +628,14 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     h->r_we.resize(n);
     h->r_null.resize(n);
     if (n) {
-        HIP_TRY(hipMemcpyAsync(h->r_key.data(), h->out_key, n * 8, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipMemcpyAsync(h->r_ws.data(), h->out_ws, n * 8, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipMemcpyAsync(h->r_we.data(), h->out_we, n * 8, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipMemcpyAsync(h->r_null.data(), h->out_null, n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->r_key.data(), h->res_key, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->r_ws.data(), h->res_ws, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->r_we.data(), h->res_we, n * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->r_null.data(), h->res_null, n * 4, hipMemcpyDeviceToHost, h->stream));
     }
     for (int g = 0; g < na; g++) {
         h->r_val[g].resize(n);
-        if (n) HIP_TRY(hipMemcpyAsync(h->r_val[g].data(), h->out_val[g], n * 8, hipMemcpyDeviceToHost, h->stream));
+        if (n) HIP_TRY(hipMemcpyAsync(h->r_val[g].data(), h->res_val[g], n * 8, hipMemcpyDeviceToHost, h->stream));
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
     out->key = h->r_key.data();
@@ -583,22 +649,35 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
 int fw_results_reset(fw_handle* h) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     HIP_TRY(hipMemsetAsync(&h->ctrl->out_count, 0, sizeof(uint64_t), h->stream));
+    HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
     return FW_OK;
 }
 
 int fw_get_stats(fw_handle* h, fw_stats* out) {
     if (!h || !out) return fail(FW_E_INVALID, "null argument");
     Ctrl c;
+    const int nsb = h->ks.n_sb;
+    std::vector<int32_t> cnt(nsb), sbo(nsb);
+    std::vector<uint32_t> fired(nsb);
     HIP_TRY(hipMemcpyAsync(&c, h->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(cnt.data(), h->state_count, 4ll * nsb, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(sbo.data(), h->sb_out, 4ll * nsb, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(fired.data(), h->sb_fired, 4ll * nsb, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
+    int64_t live = 0, avail = std::min<int64_t>((int64_t)c.out_count, h->out_cap), nf = (int64_t)c.fired;
+    for (int s = 0; s < nsb; s++) {
+        live += cnt[s];
+        avail += sbo[s];
+        nf += fired[s];
+    }
     memset(out, 0, sizeof *out);
     out->current_watermark = c.cur;
     out->next_trigger_progress = c.ntp;
     out->num_late_records_dropped = (int64_t)c.late_dropped;
-    out->live_state_entries = c.live_entries;
+    out->live_state_entries = live;
     out->pending_rows = (int64_t)c.pending_rows;
-    out->results_available = std::min<int64_t>((int64_t)c.out_count, h->out_cap);
-    out->num_fired_windows = (int64_t)c.fired;
+    out->results_available = avail;
+    out->num_fired_windows = nf;
     out->partials_emitted = (int64_t)c.partials;
     out->error_flags = (int32_t)c.error;
     out->num_superbuckets = h->ks.n_sb;
@@ -628,7 +707,7 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    SnapHeader hd{SNAP_MAGIC, 1, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, (int64_t)c.fired, total};
+    SnapHeader hd{SNAP_MAGIC, 1, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, 0, total};
     char* p = (char*)buf;
     memcpy(p, &hd, sizeof hd);
     p += sizeof hd;
@@ -678,7 +757,7 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     c.fired = (uint64_t)hd.fired;
     c.live_entries = hd.live;
     HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
-    h->chunks_ub = 0;
+    h->pushes_ub = 0;
     h->host_cur = hd.cur;
     return FW_OK;
 }

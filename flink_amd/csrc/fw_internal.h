@@ -11,12 +11,12 @@ namespace fw {
 constexpr int BLOCK = 256;          // threads per workgroup (4 waves of 64)
 constexpr int MAX_WORDS = 8;        // accumulator words per (key, slice)
 constexpr int MAX_KCOLS = 4;        // value columns a kernel loads per record
-constexpr int K3_RPT = 16;          // records per thread in the ingest kernel
-constexpr int K3_CHUNK = BLOCK * K3_RPT;  // records per ingest chunk (one workgroup)
-constexpr int K3_CACHE = 512;       // direct-mapped hot-(key,slice) LDS cache slots
-// records per thread of an ingest instantiation (fewer when many value columns are loaded,
-// to stay within the register file); a chunk holds at most BLOCK * rpt <= K3_CHUNK partials
-constexpr __host__ __device__ int ingest_rpt(int nv) { return nv >= 3 ? 8 : K3_RPT; }
+constexpr int K3_SRPT = 8;                  // rows per thread per sub-tile (registers)
+constexpr int K3_SUB = BLOCK * K3_SRPT;     // rows per sub-tile (2048)
+constexpr int K3_NSUB = 4;                  // sub-tiles per chunk
+constexpr int K3_CH = K3_SUB * K3_NSUB;     // rows per ingest chunk = one workgroup (8192)
+constexpr int K3_SLOTS = 1024;              // LDS (key, slice) fold slots per sub-tile
+constexpr int FW_MAX_PENDING = 8;           // pushes buffered between two flushes
 
 // Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words.
 enum WordOp : int32_t {
@@ -55,7 +55,7 @@ struct Ctrl {
     int64_t cur;             // currentProgress == operator / timer-service watermark
     int64_t ntp;             // nextTriggerProgress
     int64_t min_pending;     // RecordsWindowBuffer.minSliceEnd of the pending partials
-    int64_t pending_chunks;  // ingest chunks waiting in the partial buffer
+    int64_t pending_pushes;  // pushes waiting in the partial buffer (flushed by k_merge_fire)
     int64_t n_treq;          // pending timer requests (late records)
     uint64_t out_count;      // result rows produced since the last reset
     uint64_t late_dropped;   // numLateRecordsDropped
@@ -63,8 +63,8 @@ struct Ctrl {
     uint64_t pending_rows;   // rows ingested but not yet flushed
     int64_t live_entries;    // live (key, slice) entries in the state table
     uint32_t error;
-    uint32_t k4_done;        // last-workgroup-done ticket of the merge/fire kernel
-    uint64_t partials;       // partials written by the ingest kernel (cumulative)
+    int32_t push_slot;       // partial-buffer slot of the push being ingested
+    uint64_t partials;       // partials written by the ingest kernels (cumulative)
     uint64_t pad[3];
 };
 
@@ -140,11 +140,14 @@ struct IngestArgs {
     KeySpace ks;
     WordDesc wd;
     int32_t nv;            // value columns loaded
-    int32_t col_map[MAX_KCOLS];  // kernel column slot -> value column index (for the host)
     Ctrl* ctrl;
-    uint64_t* parts;       // partial buffer: max_chunks * K3_CHUNK * (2 + nw) words
-    uint32_t* off;         // [n_sb + 1][max_chunks] run starts
-    int64_t max_chunks;
+    uint64_t* parts;       // partial buffer: FW_MAX_PENDING slots of cap_rows * (2 + nw) words
+    int64_t cap_rows;      // rows per slot (>= rows of one push)
+    uint32_t* cnt;         // [n_sb][n_chunks] partial counts, scanned in place into cursors
+    uint32_t* tile_sum;    // scan workspace
+    uint32_t* starts;      // [FW_MAX_PENDING][n_sb + 1] superbucket segment starts per slot
+    int64_t* chunk_stats;  // [n_chunks][3]: min target slice, dropped rows, accepted rows
+    int64_t n_chunks;
     int64_t* treq;         // timer requests: (key, window, sb) triples
     int64_t treq_cap;
 };
@@ -152,8 +155,8 @@ struct IngestArgs {
 struct MergeArgs {
     Ctrl* ctrl;
     const uint64_t* parts;
-    const uint32_t* off;
-    int64_t max_chunks;
+    const uint32_t* starts;
+    int64_t cap_rows;
     const int64_t* treq;
     uint64_t* state;         // [n_sb][cap_e][3 + nw] words: key, slice, flags, acc...
     int32_t* state_count;    // live entries per superbucket
@@ -164,18 +167,42 @@ struct MergeArgs {
     WordDesc wd;
     AggDesc ad;
     int32_t always_flush;    // DataStream: state is updated per record, flush every advance
-    int64_t* out_key;
+    int64_t* out_key;        // output slabs: [n_sb][slab_cap] rows, then out_cap overflow rows
     int64_t* out_ws;
     int64_t* out_we;
     uint64_t* out_val[FW_MAX_AGGS];
     uint32_t* out_null;
-    int64_t out_cap;
+    int32_t* sb_out;         // rows in each superbucket's slab
+    uint32_t* sb_fired;      // fired timers per superbucket (cumulative)
+    int64_t slab_cap;
+    int64_t out_cap;         // overflow rows
     int64_t wm;              // watermark of this advance
     int32_t force_flush;     // prepareCheckpoint: flush, no timers
     int32_t pad;
 };
 
+struct CompactArgs {
+    Ctrl* ctrl;
+    const int32_t* sb_out;
+    int64_t* off;            // [n_sb + 2]
+    int32_t n_sb;
+    int32_t n_aggs;
+    int64_t slab_cap;
+    const int64_t* out_key;
+    const int64_t* out_ws;
+    const int64_t* out_we;
+    const uint64_t* out_val[FW_MAX_AGGS];
+    const uint32_t* out_null;
+    int64_t* res_key;
+    int64_t* res_ws;
+    int64_t* res_we;
+    uint64_t* res_val[FW_MAX_AGGS];
+    uint32_t* res_null;
+    int64_t res_cap;
+};
+
 // launchers (fw_kernels.hip)
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 hipError_t launch_ingest(const IngestArgs& a, hipStream_t s);
 hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s);
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s);

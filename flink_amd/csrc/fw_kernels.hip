@@ -121,173 +121,365 @@ __device__ void block_exclusive_scan(uint32_t* buf, int n, uint32_t* tmp) {
 }
 
 // ======================================================================================
-// K1+K2+K3: ingest (slice assignment + LDS-staged segmented reduce + superbucket partition)
+// K1+K2+K3: ingest = count -> flat scan -> scatter (a radix-style partition by superbucket)
+//
+// Both passes walk the same chunk (CH rows, one workgroup) in sub-tiles of SUB rows held in
+// registers.  Inside a sub-tile, rows with equal (key, slice) are folded into one partial through
+// an LDS slot table whose owner is the lowest row index hashing to the slot (deterministic, so the
+// count pass and the scatter pass agree on how many partials each superbucket gets).  The counts
+// are laid out superbucket-major ([sb][chunk]) so one flat exclusive scan yields every chunk's
+// write cursor and each superbucket's partials end up contiguous for the merge kernel.
 // ======================================================================================
-template <int NV, int NW, int RPT>
-__global__ __launch_bounds__(BLOCK) void k_ingest(IngestArgs a) {
+__device__ __forceinline__ int64_t chunk_of_block(int64_t b, int64_t nch) {
+    // XCD-aware: blocks b, b+8, b+16, ... share an XCD (round-robin dispatch, speed only), so
+    // give them adjacent chunks -> adjacent [sb][chunk] cells and partial runs merge in that L2.
+    if (nch % 8 != 0) return b;
+    return (b % 8) * (nch / 8) + b / 8;
+}
+
+template <bool SCATTER, int NV, int NW>
+__global__ __launch_bounds__(BLOCK) void k_chunk(IngestArgs a) {
     constexpr int NVR = NV > 0 ? NV : 1;
     constexpr int PW = 2 + NW;
-    constexpr int CHUNK = BLOCK * RPT;
-    __shared__ int64_t c_key[K3_CACHE];
-    __shared__ int64_t c_slice[K3_CACHE];
-    __shared__ uint32_t c_state[K3_CACHE];
-    __shared__ uint32_t c_sb[K3_CACHE];
-    __shared__ uint32_t c_rank[K3_CACHE];
-    __shared__ uint64_t c_acc[NW][K3_CACHE];
-    __shared__ uint32_t s_tmp[BLOCK];
+    constexpr int NWS = SCATTER ? NW : 1;
+    __shared__ uint32_t claim[K3_SLOTS];
+    __shared__ int64_t ckey[K3_SLOTS];
+    __shared__ int64_t cslice[K3_SLOTS];
+    __shared__ uint32_t csb[SCATTER ? K3_SLOTS : 1];
+    __shared__ uint64_t cacc[NWS][SCATTER ? K3_SLOTS : 1];
     __shared__ int64_t s_min;
     __shared__ uint64_t s_drop;
     __shared__ uint64_t s_rows;
-    __shared__ int64_t s_chunk;
-    extern __shared__ uint32_t hist[];  // n_sb + 1
+    __shared__ int32_t s_slot;
+    extern __shared__ uint32_t cur[];  // per-superbucket count (pass 1) / write cursor (pass 2)
 
     const int tid = threadIdx.x;
     Ctrl* ctrl = a.ctrl;
     const int n_sb = a.ks.n_sb;
+    const int64_t nch = a.n_chunks;
+    const int64_t c = chunk_of_block(blockIdx.x, nch);
+    const int64_t cur_wm = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
     if (tid == 0) {
-        s_chunk = __hip_atomic_fetch_add(&ctrl->pending_chunks, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
         s_min = INT64_MAX;
         s_drop = 0;
         s_rows = 0;
+        s_slot = SCATTER ? __hip_atomic_load(&ctrl->push_slot, __ATOMIC_RELAXED, DEV_SCOPE) : 0;
     }
-    for (int i = tid; i < K3_CACHE; i += BLOCK) c_state[i] = 0;
-    for (int i = tid; i <= n_sb; i += BLOCK) hist[i] = 0;
+    if (SCATTER) {
+        for (int s = tid; s < n_sb; s += BLOCK) cur[s] = a.cnt[(size_t)s * nch + c];
+    } else {
+        for (int s = tid; s < n_sb; s += BLOCK) cur[s] = 0;
+    }
     __syncthreads();
-    const int64_t chunk = s_chunk;
-    if (chunk >= a.max_chunks) {
-        if (tid == 0) __hip_atomic_fetch_or(&ctrl->error, ERR_CHUNKS, __ATOMIC_RELAXED, DEV_SCOPE);
-        return;
-    }
-    const int64_t cur = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
-    const int64_t base = (int64_t)blockIdx.x * CHUNK;
-
-    int64_t rk[RPT], rs[RPT];
-    uint64_t rv[RPT][NVR];
-    int32_t rsb[RPT];
-    uint32_t rrank[RPT];
-    uint32_t valid = 0, pass = 0;
+    const int32_t slot = s_slot;
+    if (SCATTER && slot >= FW_MAX_PENDING) return;  // error flagged by k_scan_top
+    uint64_t* out = a.parts + (size_t)slot * a.cap_rows * PW;
     int64_t lmin = INT64_MAX;
     uint32_t ldrop = 0, lrows = 0;
 
-    // ---- coalesced column loads: lane i of a wave reads element base + j*256 + i
-    static_for<RPT>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const int64_t i = base + (int64_t)j * BLOCK + tid;
-        rk[j] = 0;
-        rs[j] = 0;
+    for (int sub = 0; sub < K3_NSUB; sub++) {
+        for (int h = tid; h < K3_SLOTS; h += BLOCK) claim[h] = 0xFFFFFFFFu;
+        __syncthreads();
+        int64_t rk[K3_SRPT], rs[K3_SRPT];
+        uint64_t rv[K3_SRPT][NVR];
+        int32_t rsb[K3_SRPT];
+        uint32_t rh[K3_SRPT];
+        uint32_t valid = 0;
+        const int64_t base = c * K3_CH + (int64_t)sub * K3_SUB;
+        // ---- coalesced column loads: lane i reads row base + j*256 + i
+        static_for<K3_SRPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const int64_t i = base + (int64_t)j * BLOCK + tid;
+            rk[j] = 0;
+            rs[j] = 0;
 #pragma unroll
-        for (int c = 0; c < NVR; c++) rv[j][c] = 0;
-        if (i < a.n) {
-            rk[j] = a.key[i];
-            rs[j] = a.ts[i];
+            for (int q = 0; q < NVR; q++) rv[j][q] = 0;
+            if (i < a.n) {
+                rk[j] = a.key[i];
+                rs[j] = a.ts[i];
+                if (SCATTER) {
 #pragma unroll
-            for (int c = 0; c < NV; c++) rv[j][c] = a.vals[c][i];
-            valid |= 1u << j;
-        }
-    });
-    // ---- K1/K2: key group -> superbucket, slice end, late classification
-    static_for<RPT>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        rsb[j] = 0;
-        if (!(valid & (1u << j))) return;
-        const int64_t i = base + (int64_t)j * BLOCK + tid;
-        const int32_t pre = a.khash ? a.khash[i] : 0;
-        const int64_t se = slice_end_of(a.win, rs[j]);
-        int64_t target = se;
-        rsb[j] = superbucket_of(a.ks, rk[j], pre);
-        if (is_fired(se, cur)) {
-            if (is_fired(last_window_end_of(a.win, se), cur)) {  // late for every window: drop
-                valid &= ~(1u << j);
-                ldrop++;
-                return;
+                    for (int q = 0; q < NV; q++) rv[j][q] = a.vals[q][i];
+                }
+                valid |= 1u << j;
             }
-            target = merge_target_of(a.win, se);
-            // timer for the first unfired window (processElement :111-117)
-            const int64_t steps = (int64_t)((uint64_t)wsub(wadd(cur, 1), se) / (uint64_t)a.win.interval) + 1;
-            const int64_t unfired = wadd(se, steps * a.win.interval);
-            const int64_t r = __hip_atomic_fetch_add(&ctrl->n_treq, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
-            if (r < a.treq_cap) {
-                a.treq[3 * r] = rk[j];
-                a.treq[3 * r + 1] = unfired;
-                a.treq[3 * r + 2] = rsb[j];
-            } else {
-                __hip_atomic_fetch_or(&ctrl->error, ERR_TREQ, __ATOMIC_RELAXED, DEV_SCOPE);
+        });
+        // ---- K1/K2: slice end, late classification, key group -> superbucket, slot claim
+        static_for<K3_SRPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            rsb[j] = 0;
+            rh[j] = 0;
+            if (!(valid & (1u << j))) return;
+            const int64_t i = base + (int64_t)j * BLOCK + tid;
+            const int32_t pre = a.khash ? a.khash[i] : 0;
+            const int64_t se = slice_end_of(a.win, rs[j]);
+            int64_t target = se;
+            rsb[j] = superbucket_of(a.ks, rk[j], pre);
+            if (is_fired(se, cur_wm)) {
+                if (is_fired(last_window_end_of(a.win, se), cur_wm)) {  // late for every window: drop
+                    valid &= ~(1u << j);
+                    ldrop++;
+                    return;
+                }
+                target = merge_target_of(a.win, se);
+                if (SCATTER) {  // timer for the first unfired window (processElement :111-117)
+                    const int64_t steps = (int64_t)((uint64_t)wsub(wadd(cur_wm, 1), se) / (uint64_t)a.win.interval) + 1;
+                    const int64_t unfired = wadd(se, steps * a.win.interval);
+                    const int64_t r = __hip_atomic_fetch_add(&ctrl->n_treq, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
+                    if (r < a.treq_cap) {
+                        a.treq[3 * r] = rk[j];
+                        a.treq[3 * r + 1] = unfired;
+                        a.treq[3 * r + 2] = rsb[j];
+                    } else {
+                        __hip_atomic_fetch_or(&ctrl->error, ERR_TREQ, __ATOMIC_RELAXED, DEV_SCOPE);
+                    }
+                }
             }
-        }
-        rs[j] = target;
-        lmin = min(lmin, target);
-        lrows++;
-    });
-    // ---- K3: fold into the hot (key, slice) cache, or pass through
-    static_for<RPT>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if (!(valid & (1u << j))) return;
-        const uint32_t h = cache_hash(rk[j], rs[j]) & (K3_CACHE - 1);
-        bool absorbed = false;
-        uint32_t st = __hip_atomic_load(&c_state[h], __ATOMIC_ACQUIRE, LDS_SCOPE);
-        if (st == 0) {
-            uint32_t expect = 0;
-            if (__hip_atomic_compare_exchange_strong(&c_state[h], &expect, 1u, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, LDS_SCOPE)) {
-                c_key[h] = rk[j];
-                c_slice[h] = rs[j];
-                c_sb[h] = (uint32_t)rsb[j];
+            rs[j] = target;
+            lmin = min(lmin, target);
+            lrows++;
+            rh[j] = cache_hash(rk[j], target) & (K3_SLOTS - 1);
+            atomicMin(&claim[rh[j]], (uint32_t)(j * BLOCK + tid));
+        });
+        __syncthreads();
+        // ---- slot owners publish their (key, slice) and seed the slot accumulator
+        static_for<K3_SRPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if (!(valid & (1u << j)) || claim[rh[j]] != (uint32_t)(j * BLOCK + tid)) return;
+            ckey[rh[j]] = rk[j];
+            cslice[rh[j]] = rs[j];
+            if (SCATTER) {
+                csb[rh[j]] = (uint32_t)rsb[j];
 #pragma unroll
                 for (int w = 0; w < NW; w++)
-                    c_acc[w][h] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
-                __hip_atomic_store(&c_state[h], 2u, __ATOMIC_RELEASE, LDS_SCOPE);
-                absorbed = true;
+                    cacc[w][rh[j]] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
+            } else {
+                atomicAdd(&cur[rsb[j]], 1u);  // the slot owner emits one partial
             }
-        } else if (st == 2 && c_key[h] == rk[j] && c_slice[h] == rs[j]) {
+        });
+        __syncthreads();
+        // ---- everyone else: fold into the owner's slot, or pass through as a partial
+        static_for<K3_SRPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if (!(valid & (1u << j))) return;
+            const uint32_t h = rh[j];
+            if (claim[h] == (uint32_t)(j * BLOCK + tid)) return;
+            if (ckey[h] == rk[j] && cslice[h] == rs[j]) {
+                if (SCATTER) {
 #pragma unroll
-            for (int w = 0; w < NW; w++)
-                if (w < a.wd.nw)
-                    lds_fold(a.wd.op[w], &c_acc[w][h], record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])));
-            absorbed = true;
+                    for (int w = 0; w < NW; w++)
+                        if (w < a.wd.nw)
+                            lds_fold(a.wd.op[w], &cacc[w][h], record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])));
+                }
+                return;
+            }
+            const uint32_t pos = atomicAdd(&cur[rsb[j]], 1u);
+            if (SCATTER) {
+                uint64_t* p = out + (size_t)pos * PW;
+                p[0] = (uint64_t)rk[j];
+                p[1] = (uint64_t)rs[j];
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    p[2 + w] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
+            }
+        });
+        __syncthreads();
+        if (SCATTER) {  // slot owners write the folded partial
+            static_for<K3_SRPT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                if (!(valid & (1u << j))) return;
+                const uint32_t h = rh[j];
+                if (claim[h] != (uint32_t)(j * BLOCK + tid)) return;
+                const uint32_t pos = atomicAdd(&cur[csb[h]], 1u);
+                uint64_t* p = out + (size_t)pos * PW;
+                p[0] = (uint64_t)ckey[h];
+                p[1] = (uint64_t)cslice[h];
+#pragma unroll
+                for (int w = 0; w < NW; w++) p[2 + w] = cacc[w][h];
+            });
+            __syncthreads();
         }
-        if (!absorbed) pass |= 1u << j;
-    });
-    __syncthreads();
-    // ---- ranks within superbucket runs
-    static_for<RPT>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if (pass & (1u << j)) rrank[j] = atomicAdd(&hist[rsb[j]], 1u);
-    });
-    for (int h = tid; h < K3_CACHE; h += BLOCK)
-        if (c_state[h] == 2) c_rank[h] = atomicAdd(&hist[c_sb[h]], 1u);
-    __syncthreads();
-    block_exclusive_scan(hist, n_sb, s_tmp);
-    // ---- write the chunk's partials, sorted by superbucket
-    uint64_t* out = a.parts + (size_t)chunk * K3_CHUNK * PW;  // chunk stride is K3_CHUNK for every RPT
-    static_for<RPT>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if (!(pass & (1u << j))) return;
-        uint64_t* p = out + (size_t)(hist[rsb[j]] + rrank[j]) * PW;
-        p[0] = (uint64_t)rk[j];
-        p[1] = (uint64_t)rs[j];
-#pragma unroll
-        for (int w = 0; w < NW; w++)
-            p[2 + w] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
-    });
-    for (int h = tid; h < K3_CACHE; h += BLOCK) {
-        if (c_state[h] != 2) continue;
-        uint64_t* p = out + (size_t)(hist[c_sb[h]] + c_rank[h]) * PW;
-        p[0] = (uint64_t)c_key[h];
-        p[1] = (uint64_t)c_slice[h];
-#pragma unroll
-        for (int w = 0; w < NW; w++) p[2 + w] = c_acc[w][h];
     }
-    for (int s = tid; s <= n_sb; s += BLOCK) a.off[(size_t)s * a.max_chunks + chunk] = hist[s];
-    // ---- block reductions -> control block
+    if (!SCATTER) {
+        for (int s = tid; s < n_sb; s += BLOCK) a.cnt[(size_t)s * nch + c] = cur[s];
+        return;
+    }
+    // ---- per-push superbucket starts (chunk 0 of every superbucket) and control counters
+    if (c == 0)
+        for (int s = tid; s < n_sb; s += BLOCK) a.starts[(size_t)slot * (n_sb + 1) + s] = a.cnt[(size_t)s * nch];
     if (lmin != INT64_MAX) __hip_atomic_fetch_min(&s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
     if (ldrop) atomicAdd((unsigned long long*)&s_drop, (unsigned long long)ldrop);
     if (lrows) atomicAdd((unsigned long long*)&s_rows, (unsigned long long)lrows);
     __syncthreads();
-    if (tid == 0) {
-        if (s_min != INT64_MAX) __hip_atomic_fetch_min(&ctrl->min_pending, s_min, __ATOMIC_RELAXED, DEV_SCOPE);
-        if (s_drop) __hip_atomic_fetch_add(&ctrl->late_dropped, s_drop, __ATOMIC_RELAXED, DEV_SCOPE);
-        if (s_rows) __hip_atomic_fetch_add(&ctrl->pending_rows, s_rows, __ATOMIC_RELAXED, DEV_SCOPE);
-        __hip_atomic_fetch_add(&ctrl->partials, (uint64_t)hist[n_sb], __ATOMIC_RELAXED, DEV_SCOPE);
+    if (tid == 0) {  // reduced into the control block by k_push_stats (no contended atomics)
+        a.chunk_stats[3 * c] = s_min;
+        a.chunk_stats[3 * c + 1] = (int64_t)s_drop;
+        a.chunk_stats[3 * c + 2] = (int64_t)s_rows;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_push_stats(const int64_t* st, int64_t nch, Ctrl* ctrl) {
+    __shared__ int64_t mn[BLOCK];
+    __shared__ int64_t dr[BLOCK];
+    __shared__ int64_t rw[BLOCK];
+    int64_t m = INT64_MAX, d = 0, r = 0;
+    for (int64_t i = threadIdx.x; i < nch; i += BLOCK) {
+        m = min(m, st[3 * i]);
+        d += st[3 * i + 1];
+        r += st[3 * i + 2];
+    }
+    mn[threadIdx.x] = m;
+    dr[threadIdx.x] = d;
+    rw[threadIdx.x] = r;
+    __syncthreads();
+    for (int k = BLOCK / 2; k > 0; k >>= 1) {
+        if (threadIdx.x < k) {
+            mn[threadIdx.x] = min(mn[threadIdx.x], mn[threadIdx.x + k]);
+            dr[threadIdx.x] += dr[threadIdx.x + k];
+            rw[threadIdx.x] += rw[threadIdx.x + k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        ctrl->min_pending = min(ctrl->min_pending, mn[0]);
+        ctrl->late_dropped += (uint64_t)dr[0];
+        ctrl->pending_rows += (uint64_t)rw[0];
+    }
+}
+
+// ---- result compaction: slabs (+ overflow) -> one contiguous result set ----------------------
+__global__ __launch_bounds__(BLOCK) void k_compact_scan(const int32_t* sb_out, int32_t n_sb, int64_t* off, Ctrl* ctrl,
+                                                        int64_t out_cap) {
+    __shared__ int64_t tmp[BLOCK];
+    __shared__ int64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < n_sb; base += BLOCK) {
+        const int i = base + threadIdx.x;
+        const int64_t v = i < n_sb ? sb_out[i] : 0;
+        tmp[threadIdx.x] = v;
+        __syncthreads();
+        for (int d = 1; d < BLOCK; d <<= 1) {
+            const int64_t x = threadIdx.x >= d ? tmp[threadIdx.x - d] : 0;
+            __syncthreads();
+            tmp[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (i < n_sb) off[i] = carry + tmp[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == BLOCK - 1) carry += tmp[BLOCK - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int64_t ovf = (int64_t)min(ctrl->out_count, (uint64_t)out_cap);
+        off[n_sb] = carry;          // slab rows
+        off[n_sb + 1] = carry + ovf;  // total rows
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_compact_copy(CompactArgs a) {
+    const int sb = blockIdx.x;
+    int64_t src0, dst0, n;
+    if (sb < a.n_sb) {
+        src0 = (int64_t)sb * a.slab_cap;
+        dst0 = a.off[sb];
+        n = a.sb_out[sb];
+    } else {  // overflow region
+        src0 = (int64_t)a.n_sb * a.slab_cap;
+        dst0 = a.off[a.n_sb];
+        n = a.off[a.n_sb + 1] - a.off[a.n_sb];
+    }
+    for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
+        const int64_t d = dst0 + i, sidx = src0 + i;
+        if (d >= a.res_cap) break;
+        a.res_key[d] = a.out_key[sidx];
+        a.res_ws[d] = a.out_ws[sidx];
+        a.res_we[d] = a.out_we[sidx];
+        a.res_null[d] = a.out_null[sidx];
+        for (int g = 0; g < a.n_aggs; g++) a.res_val[g][d] = a.out_val[g][sidx];
+    }
+}
+
+// ---- flat exclusive scan of the [sb][chunk] counts (u32), three launches --------------------
+constexpr int SCAN_TILE = BLOCK * 8;
+
+__global__ __launch_bounds__(BLOCK) void k_scan_tiles(const uint32_t* v, int64_t n, uint32_t* tile_sum) {
+    __shared__ uint32_t red[BLOCK];
+    const int64_t b = (int64_t)blockIdx.x * SCAN_TILE;
+    uint32_t s = 0;
+    for (int j = 0; j < 8; j++) {
+        const int64_t i = b + (int64_t)j * BLOCK + threadIdx.x;
+        if (i < n) s += v[i];
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int d = BLOCK / 2; d > 0; d >>= 1) {
+        if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = red[0];
+}
+
+// one block: exclusive scan of the tile sums; takes this push's slot in the partial buffer
+__global__ __launch_bounds__(BLOCK) void k_scan_top(uint32_t* tile_sum, int64_t ntiles, Ctrl* ctrl, uint32_t* starts,
+                                                   int32_t n_sb, uint64_t rows) {
+    __shared__ uint32_t tmp[BLOCK];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < ntiles; base += BLOCK) {
+        const int64_t i = base + threadIdx.x;
+        const uint32_t v = i < ntiles ? tile_sum[i] : 0;
+        tmp[threadIdx.x] = v;
+        __syncthreads();
+        for (int d = 1; d < BLOCK; d <<= 1) {
+            const uint32_t x = threadIdx.x >= d ? tmp[threadIdx.x - d] : 0;
+            __syncthreads();
+            tmp[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if (i < ntiles) tile_sum[i] = carry + tmp[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == BLOCK - 1) carry += tmp[BLOCK - 1];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int64_t slot = ctrl->pending_pushes;
+        if (slot >= FW_MAX_PENDING) {
+            ctrl->error |= ERR_CHUNKS;
+            ctrl->push_slot = FW_MAX_PENDING;
+        } else {
+            ctrl->push_slot = (int32_t)slot;
+            ctrl->pending_pushes = slot + 1;
+            starts[(size_t)slot * (n_sb + 1) + n_sb] = carry;  // total partials of this push
+            ctrl->partials += carry;
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_scan_apply(uint32_t* v, int64_t n, const uint32_t* tile_off) {
+    __shared__ uint32_t tmp[BLOCK];
+    const int64_t b = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * 8;
+    uint32_t x[8];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        x[j] = b + j < n ? v[b + j] : 0;
+        s += x[j];
+    }
+    tmp[threadIdx.x] = s;
+    __syncthreads();
+    for (int d = 1; d < BLOCK; d <<= 1) {
+        const uint32_t y = threadIdx.x >= d ? tmp[threadIdx.x - d] : 0;
+        __syncthreads();
+        tmp[threadIdx.x] += y;
+        __syncthreads();
+    }
+    uint32_t run = tile_off[blockIdx.x] + tmp[threadIdx.x] - s;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        if (b + j < n) v[b + j] = run;
+        run += x[j];
     }
 }
 
@@ -364,13 +556,23 @@ __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const Wo
     return -1;
 }
 
+// Emission is atomic-free at device scope: each superbucket appends to its own output slab
+// (LDS cursor); only slab overflow falls back to a shared overflow region.  fw_results compacts
+// slabs + overflow into one contiguous result set on demand (k_compact_*).
 template <int NW>
-__device__ void emit_row(const MergeArgs& a, int64_t key, int64_t we, const uint64_t* acc) {
+__device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
     Ctrl* c = a.ctrl;
-    const uint64_t i = atomicAdd((unsigned long long*)&c->out_count, 1ull);
-    if ((int64_t)i >= a.out_cap) {
-        __hip_atomic_fetch_or(&c->error, ERR_OUTPUT, __ATOMIC_RELAXED, DEV_SCOPE);
-        return;
+    const int32_t pos = atomicAdd(s_emit, 1);
+    int64_t i;
+    if (pos < a.slab_cap) {
+        i = (int64_t)sb * a.slab_cap + pos;
+    } else {
+        const uint64_t o = atomicAdd((unsigned long long*)&c->out_count, 1ull);
+        if ((int64_t)o >= a.out_cap) {
+            __hip_atomic_fetch_or(&c->error, ERR_OUTPUT, __ATOMIC_RELAXED, DEV_SCOPE);
+            return;
+        }
+        i = (int64_t)a.n_sb * a.slab_cap + (int64_t)o;
     }
     a.out_key[i] = key;
     a.out_ws[i] = window_start_of(a.win, we);
@@ -411,7 +613,8 @@ __device__ void emit_row(const MergeArgs& a, int64_t key, int64_t we, const uint
 }
 
 template <int NW, int E>
-__device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t we, uint32_t* fired) {
+__device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t we, uint32_t* fired, int sb,
+                         int32_t* s_emit) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
     const int64_t k = S.key[e];
@@ -427,7 +630,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
             for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
         }
         nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
-        if (nonempty) emit_row<NW>(a, k, we, acc);
+        if (nonempty) emit_row<NW>(a, sb, s_emit, k, we, acc);
         atomicAnd(&S.flag[e], ~F_ACC);  // clearWindow: expiredSlices(we) = [we]
         return;
     }
@@ -445,7 +648,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
         }
         nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
         if (nonempty) {
-            emit_row<NW>(a, k, we, acc);
+            emit_row<NW>(a, sb, s_emit, k, we, acc);
             // nextTriggerWindow: register windowEnd + sliceSize while the window is non-empty
             const int e3 = find_or_insert(S, k, wadd(we, w.interval), wd);
             if (e3 >= 0) atomicOr(&S.flag[e3], F_TIMER);
@@ -477,7 +680,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
         atomicOr(&S.flag[ef], F_ACC);
     }
     nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
-    if (nonempty) emit_row<NW>(a, k, we, acc);
+    if (nonempty) emit_row<NW>(a, sb, s_emit, k, we, acc);
     const int64_t next = wadd(we, w.interval);
     const int64_t last = wadd(ws, w.size);
     if (!(next > last)) {
@@ -503,14 +706,15 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
     __shared__ int32_t s_nlive;
     __shared__ int64_t s_newmin;
     __shared__ uint32_t s_fired;
+    __shared__ int32_t s_emit;
 
     const int tid = threadIdx.x;
     const int sb = blockIdx.x;
     Ctrl* c = a.ctrl;
     const int64_t W = a.wm;
-    // read the control block once (the last workgroup rewrites it after every block has read it)
+    // control decisions; k_finalize applies the same decisions to the control block afterwards
     const int64_t cur = __hip_atomic_load(&c->cur, __ATOMIC_RELAXED, DEV_SCOPE);
-    const int64_t pend = __hip_atomic_load(&c->pending_chunks, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t pend = __hip_atomic_load(&c->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
     const int64_t ntreq = min(__hip_atomic_load(&c->n_treq, __ATOMIC_RELAXED, DEV_SCOPE), (int64_t)0x7fffffff);
     const int64_t ntp = __hip_atomic_load(&c->ntp, __ATOMIC_RELAXED, DEV_SCOPE);
     const int64_t minp = __hip_atomic_load(&c->min_pending, __ATOMIC_RELAXED, DEV_SCOPE);
@@ -524,13 +728,14 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
     if (tid == 0) {
         s_work = (ntreq > 0) || (do_fire && is_fired(a.sb_min_timer[sb], W));
         s_fired = 0;
+        s_emit = a.sb_out[sb];
     }
     __syncthreads();
     const bool work0 = s_work != 0;
     __syncthreads();
-    if (!work0 && do_flush) {  // any pending run for this superbucket?
-        for (int64_t ci = tid; ci < pend; ci += BLOCK)
-            if (a.off[(size_t)(sb + 1) * a.max_chunks + ci] > a.off[(size_t)sb * a.max_chunks + ci]) s_work = 1;
+    if (!work0 && do_flush && tid < pend) {  // any pending partial for this superbucket?
+        const uint32_t* st = a.starts + (size_t)tid * (a.n_sb + 1);
+        if (st[sb + 1] > st[sb]) s_work = 1;
     }
     __syncthreads();
     if (s_work) {
@@ -568,11 +773,12 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
         }
         // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket
         if (do_flush) {
-            for (int64_t ci = tid; ci < pend; ci += BLOCK) {
-                const uint32_t s0 = a.off[(size_t)sb * a.max_chunks + ci];
-                const uint32_t s1 = a.off[(size_t)(sb + 1) * a.max_chunks + ci];
-                const uint64_t* p = a.parts + ((size_t)ci * K3_CHUNK + s0) * PW;
-                for (uint32_t q = s0; q < s1; q++, p += PW) {
+            for (int64_t pi = 0; pi < pend; pi++) {  // contiguous, coalesced segment per push
+                const uint32_t* st = a.starts + (size_t)pi * (a.n_sb + 1);
+                const uint32_t s0 = st[sb], s1 = st[sb + 1];
+                const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
+                for (uint32_t q = s0 + tid; q < s1; q += BLOCK) {
+                    const uint64_t* p = seg + (size_t)q * PW;
                     const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
                     const int e = find_or_insert(S, k, s, a.wd);
                     if (e < 0) continue;
@@ -600,7 +806,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
                 for (int e = tid; e < n; e += BLOCK) {
                     if ((S.flag[e] & F_TIMER) && S.slice[e] == v) {
                         atomicAnd(&S.flag[e], ~F_TIMER);
-                        fire_one(a, S, e, v, &s_fired);
+                        fire_one(a, S, e, v, &s_fired, sb, &s_emit);
                     }
                 }
                 __syncthreads();
@@ -630,32 +836,30 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
         if (tid == 0) {
             a.state_count[sb] = s_nlive;
             a.sb_min_timer[sb] = s_newmin;
-            __hip_atomic_fetch_add(&c->live_entries, (int64_t)(s_nlive - n0), __ATOMIC_RELAXED, DEV_SCOPE);
-            if (s_fired) __hip_atomic_fetch_add(&c->fired, (uint64_t)s_fired, __ATOMIC_RELAXED, DEV_SCOPE);
+            a.sb_out[sb] = min(s_emit, a.slab_cap);
+            if (s_fired) a.sb_fired[sb] += s_fired;
             if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
         }
     }
-    // ---- last workgroup publishes the new progress (all workgroups read the old one above)
-    __syncthreads();
-    if (tid == 0) {
-        __threadfence();
-        const uint32_t t = atomicAdd(&c->k4_done, 1u);
-        if (t == gridDim.x - 1) {
-            __threadfence();
-            if (adv) {
-                c->cur = W;
-                if (W >= ntp) c->ntp = next_trigger_watermark(W, a.win.slice_div);
-            }
-            if (do_flush) {
-                c->pending_chunks = 0;
-                c->min_pending = INT64_MAX;
-                c->pending_rows = 0;
-            }
-            c->n_treq = 0;
-            c->k4_done = 0;
-            __threadfence();
-        }
+}
+
+// applies the control decisions of the preceding k_merge_fire (one thread; the kernel boundary
+// orders it after every merge workgroup has read the old values)
+__global__ void k_finalize(Ctrl* c, int64_t W, int32_t force_flush, int32_t always_flush, UDiv slice_div) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t cur = c->cur, pend = c->pending_pushes, ntp = c->ntp;
+    const bool adv = !force_flush && W > cur;
+    const bool do_flush = pend > 0 && (force_flush || (adv && (always_flush || (W >= ntp && is_fired(c->min_pending, W)))));
+    if (adv) {
+        c->cur = W;
+        if (W >= ntp) c->ntp = next_trigger_watermark(W, slice_div);
     }
+    if (do_flush) {
+        c->pending_pushes = 0;
+        c->min_pending = INT64_MAX;
+        c->pending_rows = 0;
+    }
+    c->n_treq = 0;
 }
 
 __global__ void k_init_ctrl(Ctrl* c) {
@@ -663,7 +867,8 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->cur = INT64_MIN;
         c->ntp = INT64_MIN;
         c->min_pending = INT64_MAX;
-        c->pending_chunks = 0;
+        c->pending_pushes = 0;
+        c->push_slot = 0;
         c->n_treq = 0;
         c->out_count = 0;
         c->late_dropped = 0;
@@ -671,9 +876,14 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->pending_rows = 0;
         c->live_entries = 0;
         c->error = 0;
-        c->k4_done = 0;
         c->partials = 0;
     }
+}
+
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(BLOCK), 0, s, a.sb_out, a.n_sb, a.off, a.ctrl, a.res_cap);
+    hipLaunchKernelGGL(k_compact_copy, dim3(a.n_sb + 1), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
@@ -686,17 +896,24 @@ hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
 // ---------------------------------------------------------------------------------------
 template <int NV, int NW>
 static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s) {
-    constexpr int RPT = ingest_rpt(NV);
-    const int64_t grid = (a.n + BLOCK * RPT - 1) / (BLOCK * RPT);
-    if (grid == 0) return hipSuccess;
-    const size_t dyn = (size_t)(a.ks.n_sb + 1) * sizeof(uint32_t);
+    const int64_t nch = a.n_chunks;
+    if (nch == 0) return hipSuccess;
+    const size_t dyn = (size_t)a.ks.n_sb * sizeof(uint32_t);
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            64 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_chunk<false, NV, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_chunk<true, NV, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_ingest<NV, NW, RPT>), dim3((unsigned)grid), dim3(BLOCK), dyn, s, a);
+    const int64_t L = (int64_t)a.ks.n_sb * nch;
+    const int64_t ntiles = (L + SCAN_TILE - 1) / SCAN_TILE;
+    hipLaunchKernelGGL((k_chunk<false, NV, NW>), dim3((unsigned)nch), dim3(BLOCK), dyn, s, a);
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(BLOCK), 0, s, a.cnt, L, a.tile_sum);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(BLOCK), 0, s, a.tile_sum, ntiles, a.ctrl, a.starts, a.ks.n_sb,
+                       (uint64_t)a.n);
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(BLOCK), 0, s, a.cnt, L, a.tile_sum);
+    hipLaunchKernelGGL((k_chunk<true, NV, NW>), dim3((unsigned)nch), dim3(BLOCK), dyn, s, a);
+    hipLaunchKernelGGL(k_push_stats, dim3(1), dim3(BLOCK), 0, s, a.chunk_stats, nch, a.ctrl);
     return hipGetLastError();
 }
 
@@ -718,7 +935,6 @@ hipError_t launch_ingest(const IngestArgs& a, hipStream_t s) {
     }
 }
 
-// LDS per merge workgroup: 2E*4 (index) + E*(20 + 8*NW) bytes; E = 2048 only for NW <= 2.
 template <int NW>
 static hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
     if (NW <= 2 && a.cap_e == 2048)
@@ -728,12 +944,20 @@ static hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s) {
+static hipError_t merge_any(const MergeArgs& a, hipStream_t s) {
     const int nw = a.wd.nw;
     if (nw <= 1) return merge_nw<1>(a, s);
     if (nw <= 2) return merge_nw<2>(a, s);
     if (nw <= 4) return merge_nw<4>(a, s);
     return merge_nw<8>(a, s);
+}
+
+hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s) {
+    hipError_t e = merge_any(a, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, a.ctrl, a.wm, a.force_flush, a.always_flush,
+                       a.win.slice_div);
+    return hipGetLastError();
 }
 
 // ======================================================================================

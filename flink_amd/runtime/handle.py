@@ -82,9 +82,10 @@ class WindowAggHandle:
             arr[c] = v.data_ptr()
         check(lib().fw_push_device(self._h, n, keys.data_ptr(), ts.data_ptr(),
                                    key_hashes.data_ptr() if key_hashes is not None else None, arr))
-        # keep the inputs alive until the stream has consumed them
-        for t in (keys, ts, *values):
-            t.record_stream(ext)
+        # the producer stream must not reuse the input memory before the ingest kernel has read
+        # it: order the producer's later work after this push (no record_stream: the handle's
+        # stream dies with the handle, before torch frees the tensors)
+        torch.cuda.current_stream(keys.device).wait_stream(ext)
 
     # ---- progress / output
     def advance(self, wm):

@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-sample", type=int, default=4 * B, help="events for the CPU baseline leg")
+    ap.add_argument("--cpu-sample", type=int, default=B, help="events for the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     ap.add_argument("--verbose", action="store_true")
@@ -192,33 +192,19 @@ def main():
     if wl["window"][0] == "CUMULATE":
         out_cap = keys_total + (1 << 20)
 
-    def run(first, nsteps, handle, timed):
-        ext = torch.cuda.ExternalStream(handle.stream_ptr, device=dev)
-        ev = []
+    def run(first, nsteps, handle):
         for b in range(first, first + nsteps):
             k, t, v = exchange(b)
             wm = global_watermark(b)
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e2 = torch.cuda.Event(enable_timing=True)
-                ext.wait_stream(torch.cuda.current_stream(dev))
-                e0.record(ext)
             handle.push_device(k, t, [v] if nv else [])
-            if timed:
-                e1.record(ext)
             handle.reset_results()       # blackhole sink: results of the previous watermark consumed
             handle.advance(wm)
-            if timed:
-                e2.record(ext)
-                ev.append((e0, e1, e2))
-        return ev
 
     cfg = build_config(wl, world, rank, keys_total, out_cap)
     # warmup on its own operator instance (first batches of the same stream)
     if args.warmup:
         hw = WindowAggHandle(cfg)
-        run(0, args.warmup, hw, False)
+        run(0, args.warmup, hw)
         hw.sync()
         hw.close()
     h = WindowAggHandle(cfg)
@@ -226,8 +212,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    h.set_profiling(True)          # hipEvents around every launch on the operator's stream
     t0 = time.perf_counter()
-    events = run(args.warmup, args.steps, h, True)
+    run(args.warmup, args.steps, h)
     h.sync()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -239,20 +226,22 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     st = h.stats()
-    ingest_ms = [a.elapsed_time(b_) for a, b_, _ in events]
-    fire_ms = [b_.elapsed_time(c) for _, b_, c in events]
+    kt = h.kernel_times()
     if st["error_flags"]:
         raise SystemExit(f"device error flags {st['error_flags']}")
 
     n_total = args.steps * B * world
     value = n_total / elapsed
     # ---------------- roofline of the segmented-reduce (ingest) kernel ----------------------
-    w_partial = 8 * (2 + wl["nw"])   # partial = key, slice, accumulator words (8 B each)
-    g_per = st["partials_emitted"] / args.steps
-    n_per = st["rows_ingested"] / args.steps if "rows_ingested" in st else B
-    bytes_per_launch = n_per * wl["w_in"] + g_per * w_partial
-    avg_ingest_s = float(np.mean(ingest_ms)) / 1e3
-    achieved = bytes_per_launch / avg_ingest_s / 1e9
+    # algorithmic bytes per launch: N_b * sum(w_in) + G_b * w_partial, with
+    # w_partial = key + slice + accumulator words (8 B each) and G_b the partials it wrote
+    red_ms, red_n = kt["reduce"]
+    w_partial = 8 * (2 + wl["nw"])
+    rows_per_launch = n_total / world / red_n
+    g_per_launch = st["partials_emitted"] / red_n
+    bytes_per_launch = rows_per_launch * wl["w_in"] + g_per_launch * w_partial
+    avg_reduce_s = red_ms / red_n / 1e3
+    achieved = bytes_per_launch / avg_reduce_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -282,10 +271,12 @@ def main():
                        "max_parallelism": 128, "superbuckets": st["num_superbuckets"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "kernel": "k_ingest (slice assign + LDS segmented reduce + partition)",
-                         "algorithmic_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ingest_s * 1e6},
+                         "kernel": "fw::k_ingest (K1 key group + K2 slice assign + K3 LDS segmented reduce, "
+                                   "chunk-local superbucket sort)",
+                         "algorithmic_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_reduce_s * 1e6,
+                         "launches": red_n, "partials_per_launch": g_per_launch},
             "cpu_baseline": cpu,
-            "breakdown_ms_per_step": {"ingest": float(np.mean(ingest_ms)), "watermark_fire": float(np.mean(fire_ms))},
+            "device_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         }
         print(json.dumps(line), flush=True)
     h.close()

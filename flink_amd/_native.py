@@ -49,6 +49,8 @@ def lib():
         "fw_results": (i32, [vp, P(abi.fw_result), i32]),
         "fw_results_reset": (i32, [vp]),
         "fw_get_stats": (i32, [vp, P(abi.fw_stats)]),
+        "fw_set_profiling": (i32, [vp, i32]),
+        "fw_get_kernel_times": (i32, [vp, P(abi.fw_kernel_times)]),
         "fw_snapshot": (i32, [vp, vp, i64, P(i64)]),
         "fw_restore": (i32, [vp, vp, i64]),
         "fw_assign_key_groups": (i32, [vp, vp, i64, i32, i32, i32, vp, vp, vp]),
@@ -72,7 +74,8 @@ def lib():
 # every symbol the public header declares (tests check they are exported)
 EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
             "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_advance",
-            "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_snapshot", "fw_restore",
+            "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_set_profiling",
+            "fw_get_kernel_times", "fw_snapshot", "fw_restore",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_window_start",
             "fw_host_next_trigger_watermark"]

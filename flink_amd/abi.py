@@ -98,6 +98,14 @@ class fw_stats(C.Structure):
                 ("num_superbuckets", C.c_int32)]
 
 
+KT_PARTITION, KT_SCAN, KT_REDUCE, KT_MERGE, KT_OTHER = 0, 1, 2, 3, 4
+FW_KT_N = 8
+
+
+class fw_kernel_times(C.Structure):
+    _fields_ = [("ms", C.c_double * FW_KT_N), ("launches", C.c_int64 * FW_KT_N)]
+
+
 class fw_gen_params(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("t0_ms", C.c_int64), ("rate_per_s", C.c_int64),
                 ("ooo_ms", C.c_int64), ("key_base", C.c_int64), ("key_count", C.c_int64),

@@ -57,6 +57,61 @@ int64_t gcd64(int64_t a, int64_t b) {
 
 int round_nw(int nw) { return nw <= 1 ? 1 : nw <= 2 ? 2 : nw <= 4 ? 4 : 8; }
 
+// hipEvent pairs recorded around launches on the handle stream; resolved by fw_get_kernel_times
+struct EvTimer final : KTimer {
+    struct Rec {
+        int kind;
+        hipEvent_t b, e;
+    };
+    std::vector<hipEvent_t> pool;
+    std::vector<Rec> recs;
+    hipEvent_t open[FW_KT_N] = {};
+    double ms[FW_KT_N] = {};
+    int64_t n[FW_KT_N] = {};
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void mark(int kind, bool end, hipStream_t s) override {
+        hipEvent_t ev = get();
+        (void)hipEventRecord(ev, s);
+        if (!end) {
+            open[kind] = ev;
+        } else {
+            recs.push_back({kind, open[kind], ev});
+            open[kind] = nullptr;
+        }
+    }
+    hipError_t resolve() {
+        for (const Rec& r : recs) {
+            hipError_t e = hipEventSynchronize(r.e);
+            if (e != hipSuccess) return e;
+            float t = 0.f;
+            e = hipEventElapsedTime(&t, r.b, r.e);
+            if (e != hipSuccess) return e;
+            ms[r.kind] += t;
+            n[r.kind]++;
+            pool.push_back(r.b);
+            pool.push_back(r.e);
+        }
+        recs.clear();
+        return hipSuccess;
+    }
+    ~EvTimer() override {
+        for (const Rec& r : recs) {
+            hipEventDestroy(r.b);
+            hipEventDestroy(r.e);
+        }
+        for (hipEvent_t e : pool) hipEventDestroy(e);
+    }
+};
+
 }  // namespace
 
 struct fw_handle {
@@ -70,15 +125,15 @@ struct fw_handle {
     int slot_col[MAX_KCOLS] = {0, 0, 0, 0};
     int nw_t = 1;  // template word count (layout stride)
     int64_t cap_rows = 0;     // rows per partial-buffer slot (= max rows per push piece)
+    int64_t chunk_rows = 0;   // rows per ingest chunk (IG_BLOCK * ig_rpt(nw_t))
     int64_t max_nch = 0;      // ingest chunks per push piece
     int cap_e = 1024;
     bool always_flush = false;
 
     Ctrl* ctrl = nullptr;
     uint64_t* parts = nullptr;
-    uint32_t* cnt = nullptr;
-    uint32_t* tile_sum = nullptr;
-    uint32_t* starts = nullptr;
+    uint32_t* cells = nullptr;   // [FW_MAX_PENDING][n_sb][max_nch]
+    int32_t* slot_nch = nullptr;  // [FW_MAX_PENDING]
     int64_t* treq = nullptr;
     int64_t treq_cap = 0;
     uint64_t* state = nullptr;
@@ -122,6 +177,7 @@ struct fw_handle {
 
     int64_t pushes_ub = 0;  // upper bound of device pending_pushes
     int64_t host_cur = INT64_MIN;
+    KTimer* timer = nullptr;  // non-null while fw_set_profiling is on
 };
 
 namespace {
@@ -256,18 +312,23 @@ int validate_and_plan(fw_handle* h) {
     const int kg_end = ((c.subtask_index + 1) * c.max_parallelism - 1) / c.parallelism;
     ks.n_kg = kg_end - ks.kg_start + 1;
     const int64_t cap_target = std::max<int64_t>(c.state_capacity, 1024);
-    // aim for <= ~60% occupancy of the per-superbucket LDS table
-    h->cap_e = (h->nw_t <= 2 && cap_target / ks.n_kg > 16384 * 600) ? 2048 : 1024;
+    // aim for <= ~55% occupancy of the per-superbucket LDS table (hash skew headroom)
+    h->cap_e = mg_entries(h->nw_t);
+    const int64_t fill = h->cap_e * 55 / 100;
     int64_t per_kg = (cap_target + ks.n_kg - 1) / ks.n_kg;
-    int64_t sbk = next_pow2((per_kg + (h->cap_e * 6 / 10) - 1) / (h->cap_e * 6 / 10));
-    while ((int64_t)ks.n_kg * sbk > 16384 && sbk > 1) sbk >>= 1;
+    int64_t sbk = next_pow2((per_kg + fill - 1) / fill);
+    const int64_t max_sb = std::min<int64_t>(16384, ig_max_sb(h->nw_t));
+    while ((int64_t)ks.n_kg * sbk > max_sb && sbk > 1) sbk >>= 1;
+    if ((int64_t)ks.n_kg * sbk > max_sb) return fail(FW_E_INVALID, "too many key groups per subtask for the ingest histogram");
     ks.sb_per_kg_log2 = 0;
     while ((1ll << ks.sb_per_kg_log2) < sbk) ks.sb_per_kg_log2++;
     ks.n_sb = ks.n_kg << ks.sb_per_kg_log2;
     if (c.max_batch_rows <= 0) return fail(FW_E_INVALID, "max_batch_rows must be > 0");
     if (c.output_capacity <= 0) return fail(FW_E_INVALID, "output_capacity must be > 0");
-    h->cap_rows = ((c.max_batch_rows + K3_CH - 1) / K3_CH) * K3_CH;
-    h->max_nch = h->cap_rows / K3_CH;
+    h->chunk_rows = (int64_t)IG_BLOCK * ig_rpt(h->nw_t);
+    h->cap_rows = ((c.max_batch_rows + h->chunk_rows - 1) / h->chunk_rows) * h->chunk_rows;
+    h->cap_rows = std::min<int64_t>(h->cap_rows, (int64_t)MG_MAX_CELLS * h->chunk_rows);  // longer pushes are split
+    h->max_nch = h->cap_rows / h->chunk_rows;
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     h->out_cap = c.output_capacity;
     h->slab_cap = std::max<int64_t>(64, (2 * c.output_capacity + ks.n_sb - 1) / ks.n_sb);
@@ -291,9 +352,8 @@ int allocate(fw_handle* h) {
     const int PW = 2 + h->nw_t, PWE = 3 + h->nw_t;
     if ((rc = dalloc(&h->ctrl, 1))) return rc;
     if ((rc = dalloc(&h->parts, (size_t)FW_MAX_PENDING * h->cap_rows * PW))) return rc;
-    if ((rc = dalloc(&h->cnt, (size_t)h->ks.n_sb * h->max_nch))) return rc;
-    if ((rc = dalloc(&h->tile_sum, (size_t)h->ks.n_sb * h->max_nch / 2048 + 2))) return rc;
-    if ((rc = dalloc(&h->starts, (size_t)FW_MAX_PENDING * (h->ks.n_sb + 1)))) return rc;
+    if ((rc = dalloc(&h->cells, (size_t)FW_MAX_PENDING * h->ks.n_sb * h->max_nch))) return rc;
+    if ((rc = dalloc(&h->slot_nch, FW_MAX_PENDING))) return rc;
     if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
     if ((rc = dalloc(&h->state, (size_t)h->ks.n_sb * h->cap_e * PWE))) return rc;
     if ((rc = dalloc(&h->state_count, h->ks.n_sb))) return rc;
@@ -314,7 +374,7 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->sb_out, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->sb_fired, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->coff, h->ks.n_sb + 2))) return rc;
-    if ((rc = dalloc(&h->chunk_stats, 3 * h->max_nch + 3))) return rc;
+    if ((rc = dalloc(&h->chunk_stats, 4 * h->max_nch + 4))) return rc;
     HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_fired, 0, sizeof(uint32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->state_count, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
@@ -361,7 +421,9 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     MergeArgs a{};
     a.ctrl = h->ctrl;
     a.parts = h->parts;
-    a.starts = h->starts;
+    a.cells = h->cells;
+    a.slot_nch = h->slot_nch;
+    a.max_nch = h->max_nch;
     a.cap_rows = h->cap_rows;
     a.treq = h->treq;
     a.state = h->state;
@@ -388,7 +450,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
 }
 
 int force_flush(fw_handle* h) {
-    HIP_TRY(launch_merge_fire(merge_args(h, INT64_MIN, 1), h->stream));
+    HIP_TRY(launch_merge_fire(merge_args(h, INT64_MIN, 1), h->stream, h->timer));
     h->pushes_ub = 0;
     return FW_OK;
 }
@@ -420,14 +482,14 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.ctrl = h->ctrl;
         a.parts = h->parts;
         a.cap_rows = h->cap_rows;
-        a.cnt = h->cnt;
-        a.tile_sum = h->tile_sum;
-        a.starts = h->starts;
+        a.cells = h->cells;
+        a.slot_nch = h->slot_nch;
+        a.max_nch = h->max_nch;
         a.chunk_stats = h->chunk_stats;
-        a.n_chunks = (m + K3_CH - 1) / K3_CH;
+        a.n_chunks = (m + h->chunk_rows - 1) / h->chunk_rows;
         a.treq = h->treq;
         a.treq_cap = h->treq_cap;
-        HIP_TRY(launch_ingest(a, h->stream));
+        HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
     }
     return FW_OK;
@@ -463,9 +525,8 @@ int fw_destroy(fw_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     hipFree(h->ctrl);
     hipFree(h->parts);
-    hipFree(h->cnt);
-    hipFree(h->tile_sum);
-    hipFree(h->starts);
+    hipFree(h->cells);
+    hipFree(h->slot_nch);
     hipFree(h->treq);
     hipFree(h->state);
     hipFree(h->state_count);
@@ -495,6 +556,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->d_ts);
     hipFree(h->d_kh);
     for (int v = 0; v < FW_MAX_COLS; v++) hipFree(h->d_val[v]);
+    delete h->timer;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return FW_OK;
@@ -570,7 +632,7 @@ int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t*
 
 int fw_advance(fw_handle* h, int64_t watermark) {
     if (!h) return fail(FW_E_INVALID, "null handle");
-    HIP_TRY(launch_merge_fire(merge_args(h, watermark, 0), h->stream));
+    HIP_TRY(launch_merge_fire(merge_args(h, watermark, 0), h->stream, h->timer));
     if (watermark > h->host_cur) h->host_cur = watermark;
     return FW_OK;
 }
@@ -602,7 +664,7 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     ca.res_we = h->res_we;
     ca.res_null = h->res_null;
     ca.res_cap = h->out_cap;
-    HIP_TRY(launch_compact(ca, h->stream));
+    HIP_TRY(launch_compact(ca, h->stream, h->timer));
     Ctrl c;
     int rc = read_ctrl(h, &c);
     if (rc) return rc;
@@ -681,6 +743,27 @@ int fw_get_stats(fw_handle* h, fw_stats* out) {
     out->partials_emitted = (int64_t)c.partials;
     out->error_flags = (int32_t)c.error;
     out->num_superbuckets = h->ks.n_sb;
+    return FW_OK;
+}
+
+int fw_set_profiling(fw_handle* h, int enable) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    delete h->timer;
+    h->timer = enable ? new EvTimer() : nullptr;
+    return FW_OK;
+}
+
+int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    memset(out, 0, sizeof *out);
+    if (!h->timer) return FW_OK;
+    EvTimer* t = static_cast<EvTimer*>(h->timer);
+    HIP_TRY(t->resolve());
+    for (int k = 0; k < FW_KT_N; k++) {
+        out->ms[k] = t->ms[k];
+        out->launches[k] = t->n[k];
+    }
     return FW_OK;
 }
 

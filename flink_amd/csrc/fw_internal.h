@@ -8,15 +8,29 @@
 
 namespace fw {
 
-constexpr int BLOCK = 256;          // threads per workgroup (4 waves of 64)
+constexpr int BLOCK = 256;          // threads per workgroup of the small helper kernels
 constexpr int MAX_WORDS = 8;        // accumulator words per (key, slice)
 constexpr int MAX_KCOLS = 4;        // value columns a kernel loads per record
-constexpr int K3_SRPT = 8;                  // rows per thread per sub-tile (registers)
-constexpr int K3_SUB = BLOCK * K3_SRPT;     // rows per sub-tile (2048)
-constexpr int K3_NSUB = 4;                  // sub-tiles per chunk
-constexpr int K3_CH = K3_SUB * K3_NSUB;     // rows per ingest chunk = one workgroup (8192)
-constexpr int K3_SLOTS = 1024;              // LDS (key, slice) fold slots per sub-tile
-constexpr int FW_MAX_PENDING = 8;           // pushes buffered between two flushes
+constexpr int FW_MAX_PENDING = 8;   // pushes buffered between two flushes
+
+// ---- ingest (K1+K2+K3): one 1024-thread workgroup per chunk of IG_BLOCK * RPT rows
+constexpr int IG_BLOCK = 1024;
+constexpr int IG_SRPT = 2;                      // rows per thread per fold sub-tile
+constexpr int IG_SUB = IG_BLOCK * IG_SRPT;      // rows per fold sub-tile (2048)
+// LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)
+constexpr int ig_slots(int nw) { return nw <= 4 ? 2048 : 1024; }
+// static LDS of k_ingest (fold table) and the superbucket limit its dynamic histogram allows
+constexpr int ig_static_lds(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw) + 512; }
+constexpr int ig_max_sb(int nw) { return (160 * 1024 - ig_static_lds(nw)) / 4; }
+constexpr int IG_MAX_CH = IG_BLOCK * 8;         // largest chunk (rows)
+// rows per thread by accumulator words: keeps the chunk's partials in registers
+constexpr int ig_rpt(int nw) { return nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
+
+// ---- merge/fire (K4+K5): one 1024-thread workgroup per superbucket
+constexpr int MG_BLOCK = 1024;
+constexpr int MG_MAX_CELLS = 1024;              // chunks per pending push a merge workgroup reads
+// LDS slice-state capacity (entries) per superbucket by accumulator words
+constexpr int mg_entries(int nw) { return nw <= 1 ? 4096 : nw <= 4 ? 2048 : 1024; }
 
 // Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words.
 enum WordOp : int32_t {
@@ -141,11 +155,13 @@ struct IngestArgs {
     WordDesc wd;
     int32_t nv;            // value columns loaded
     Ctrl* ctrl;
-    uint64_t* parts;       // partial buffer: FW_MAX_PENDING slots of cap_rows * (2 + nw) words
+    uint64_t* parts;       // partial buffer: FW_MAX_PENDING slots of cap_rows * (2 + nw) words;
+                           // chunk c owns rows [c*CH, (c+1)*CH) of its slot, sorted by superbucket
     int64_t cap_rows;      // rows per slot (>= rows of one push)
-    uint32_t* cnt;         // [n_sb][n_chunks] partial counts, scanned in place into cursors
-    uint32_t* tile_sum;    // scan workspace
-    uint32_t* starts;      // [FW_MAX_PENDING][n_sb + 1] superbucket segment starts per slot
+    uint32_t* cells;       // [FW_MAX_PENDING][n_sb][max_nch]: start | count << 16 of each
+                           // (superbucket, chunk) cell inside the chunk's region
+    int32_t* slot_nch;     // [FW_MAX_PENDING] chunks of each pending push
+    int64_t max_nch;
     int64_t* chunk_stats;  // [n_chunks][3]: min target slice, dropped rows, accepted rows
     int64_t n_chunks;
     int64_t* treq;         // timer requests: (key, window, sb) triples
@@ -155,7 +171,9 @@ struct IngestArgs {
 struct MergeArgs {
     Ctrl* ctrl;
     const uint64_t* parts;
-    const uint32_t* starts;
+    const uint32_t* cells;   // see IngestArgs
+    const int32_t* slot_nch;
+    int64_t max_nch;
     int64_t cap_rows;
     const int64_t* treq;
     uint64_t* state;         // [n_sb][cap_e][3 + nw] words: key, slice, flags, acc...
@@ -201,10 +219,19 @@ struct CompactArgs {
     int64_t res_cap;
 };
 
+// Optional per-launch timing hook (fw_set_profiling): records hipEvents around launches.
+struct KTimer {
+    virtual void mark(int kind, bool end, hipStream_t s) = 0;
+    virtual ~KTimer() = default;
+};
+inline void kt_mark(KTimer* t, int kind, bool end, hipStream_t s) {
+    if (t) t->mark(kind, end, s);
+}
+
 // launchers (fw_kernels.hip)
-hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
-hipError_t launch_ingest(const IngestArgs& a, hipStream_t s);
-hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s);
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t);
+hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t);
+hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s);
 
 }  // namespace fw

@@ -93,257 +93,276 @@ __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
     return (uint32_t)(mix64((uint64_t)k * 0xD6E8FEB86659FD93ull + (uint64_t)s) >> 17);
 }
 
-// exclusive scan of n u32 in LDS by one 256-thread block; returns total in buf[n]
-__device__ void block_exclusive_scan(uint32_t* buf, int n, uint32_t* tmp) {
-    const int tid = threadIdx.x;
-    const int per = (n + BLOCK - 1) / BLOCK;
-    const int b = tid * per;
-    const int e = min(b + per, n);
-    uint32_t s = 0;
-    for (int i = b; i < e; i++) s += buf[i];
-    tmp[tid] = s;
-    __syncthreads();
-    // Hillis-Steele over 256 partial sums
-    for (int d = 1; d < BLOCK; d <<= 1) {
-        uint32_t x = tid >= d ? tmp[tid - d] : 0;
-        __syncthreads();
-        tmp[tid] += x;
-        __syncthreads();
-    }
-    uint32_t run = tmp[tid] - s;  // exclusive prefix of this thread's segment
-    for (int i = b; i < e; i++) {
-        uint32_t v = buf[i];
-        buf[i] = run;
-        run += v;
-    }
-    if (tid == BLOCK - 1) buf[n] = tmp[BLOCK - 1];
-    __syncthreads();
-}
-
 // ======================================================================================
-// K1+K2+K3: ingest = count -> flat scan -> scatter (a radix-style partition by superbucket)
+// K1+K2+K3: single-pass ingest = slice/key-group assignment + LDS segmented reduce + a
+// chunk-local counting sort of the partials by superbucket.
 //
-// Both passes walk the same chunk (CH rows, one workgroup) in sub-tiles of SUB rows held in
-// registers.  Inside a sub-tile, rows with equal (key, slice) are folded into one partial through
-// an LDS slot table whose owner is the lowest row index hashing to the slot (deterministic, so the
-// count pass and the scatter pass agree on how many partials each superbucket gets).  The counts
-// are laid out superbucket-major ([sb][chunk]) so one flat exclusive scan yields every chunk's
-// write cursor and each superbucket's partials end up contiguous for the merge kernel.
+// One 1024-thread workgroup owns a chunk of CH = 1024*RPT rows and keeps all of them in
+// registers (row j*1024 + tid, coalesced column loads, every load of the chunk in flight at
+// once).  The chunk is folded in fold sub-tiles of 2048 rows: rows with equal (key, slice) meet
+// in an LDS slot table whose owner is the lowest row index hashing to the slot (so a hot key,
+// which occurs early, keeps its slot); the owner ends up holding the folded partial in its
+// registers.  The surviving partials are then ranked per superbucket with LDS atomics, the
+// per-superbucket counts are scanned, and every partial is stored at
+//     parts[slot][c*CH + start(sb) + rank]
+// so each (superbucket, chunk) cell is contiguous.  The cell table cells[slot][sb][chunk]
+// (start | count << 16) tells the merge kernel where its rows are: no count pass, no global
+// scan, one launch per push (+ a one-block stats reduce).
+// Restates AbstractSliceSyncStateWindowAggProcessor.processElement (:96-126: slice assignment,
+// late drop / late merge + timer), RecordsWindowBuffer.addElement (:81, grouping by
+// (key, sliceEnd)) and the per-group fold of AggCombiner.combine (:76-99).
 // ======================================================================================
-__device__ __forceinline__ int64_t chunk_of_block(int64_t b, int64_t nch) {
-    // XCD-aware: blocks b, b+8, b+16, ... share an XCD (round-robin dispatch, speed only), so
-    // give them adjacent chunks -> adjacent [sb][chunk] cells and partial runs merge in that L2.
-    if (nch % 8 != 0) return b;
-    return (b % 8) * (nch / 8) + b / 8;
+
+// inclusive scan of one value per thread over a 1024-thread block (wave shuffles + LDS)
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int NWV = 1024 / 64;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    if (tid < 64) {
+        uint32_t x = tid < NWV ? wsum[tid] : 0u;
+#pragma unroll
+        for (int d = 1; d < NWV; d <<= 1) {
+            const uint32_t t = __shfl_up(x, d, 64);
+            if (lane >= d) x += t;
+        }
+        if (tid < NWV) wsum[tid] = x;
+    }
+    __syncthreads();
+    if (w > 0) v += wsum[w - 1];
+    *total = wsum[NWV - 1];
+    return v;
 }
 
-template <bool SCATTER, int NV, int NW>
-__global__ __launch_bounds__(BLOCK) void k_chunk(IngestArgs a) {
+template <int NV, int NW, int RPT>
+__global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
+    constexpr int CH = IG_BLOCK * RPT;
+    constexpr int NSUB = RPT / IG_SRPT;
     constexpr int NVR = NV > 0 ? NV : 1;
     constexpr int PW = 2 + NW;
-    constexpr int NWS = SCATTER ? NW : 1;
-    __shared__ uint32_t claim[K3_SLOTS];
-    __shared__ int64_t ckey[K3_SLOTS];
-    __shared__ int64_t cslice[K3_SLOTS];
-    __shared__ uint32_t csb[SCATTER ? K3_SLOTS : 1];
-    __shared__ uint64_t cacc[NWS][SCATTER ? K3_SLOTS : 1];
+    constexpr int IG_SLOTS = ig_slots(NW);
+    static_assert(RPT % IG_SRPT == 0, "fold sub-tiles must tile the chunk");
+    __shared__ uint32_t claim[IG_SLOTS];
+    __shared__ int64_t ckey[IG_SLOTS];
+    __shared__ int64_t cslice[IG_SLOTS];
+    __shared__ uint64_t cacc[NW][IG_SLOTS];
+    __shared__ uint32_t wsum[IG_BLOCK / 64];
     __shared__ int64_t s_min;
     __shared__ uint64_t s_drop;
     __shared__ uint64_t s_rows;
-    __shared__ int32_t s_slot;
-    extern __shared__ uint32_t cur[];  // per-superbucket count (pass 1) / write cursor (pass 2)
+    extern __shared__ uint32_t hist[];  // [n_sb]: partials per superbucket -> cell start
 
     const int tid = threadIdx.x;
     Ctrl* ctrl = a.ctrl;
     const int n_sb = a.ks.n_sb;
-    const int64_t nch = a.n_chunks;
-    const int64_t c = chunk_of_block(blockIdx.x, nch);
+    const int64_t c = blockIdx.x;
+    // the push's slot in the partial buffer; k_push_stats (next launch) advances pending_pushes
+    const int64_t slot = __hip_atomic_load(&ctrl->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
+    if (slot >= FW_MAX_PENDING) {
+        if (tid == 0) __hip_atomic_fetch_or(&ctrl->error, ERR_CHUNKS, __ATOMIC_RELAXED, DEV_SCOPE);
+        return;
+    }
     const int64_t cur_wm = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
     if (tid == 0) {
         s_min = INT64_MAX;
         s_drop = 0;
         s_rows = 0;
-        s_slot = SCATTER ? __hip_atomic_load(&ctrl->push_slot, __ATOMIC_RELAXED, DEV_SCOPE) : 0;
     }
-    if (SCATTER) {
-        for (int s = tid; s < n_sb; s += BLOCK) cur[s] = a.cnt[(size_t)s * nch + c];
-    } else {
-        for (int s = tid; s < n_sb; s += BLOCK) cur[s] = 0;
-    }
-    __syncthreads();
-    const int32_t slot = s_slot;
-    if (SCATTER && slot >= FW_MAX_PENDING) return;  // error flagged by k_scan_top
-    uint64_t* out = a.parts + (size_t)slot * a.cap_rows * PW;
+    for (int s = tid; s < n_sb; s += IG_BLOCK) hist[s] = 0;
+
+    // ---- coalesced column loads of the whole chunk (all in flight before the first use)
+    const int64_t base = c * CH;
+    int64_t rk[RPT], rs[RPT];
+    uint64_t rv[RPT][NVR];
+    int32_t pre[RPT];
+    uint32_t valid = 0;
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int64_t i = base + (int64_t)j * IG_BLOCK + tid;
+        rk[j] = 0;
+        rs[j] = 0;
+        pre[j] = 0;
+#pragma unroll
+        for (int q = 0; q < NVR; q++) rv[j][q] = 0;
+        if (i < a.n) {
+            rk[j] = a.key[i];
+            rs[j] = a.ts[i];
+            if (a.khash) pre[j] = a.khash[i];
+#pragma unroll
+            for (int q = 0; q < NV; q++) rv[j][q] = a.vals[q][i];
+            valid |= 1u << j;
+        }
+    });
+    // ---- K1/K2: key group -> superbucket, slice end, late classification, record words
+    int32_t rsb[RPT];
+    uint64_t racc[RPT][NW];
     int64_t lmin = INT64_MAX;
     uint32_t ldrop = 0, lrows = 0;
-
-    for (int sub = 0; sub < K3_NSUB; sub++) {
-        for (int h = tid; h < K3_SLOTS; h += BLOCK) claim[h] = 0xFFFFFFFFu;
-        __syncthreads();
-        int64_t rk[K3_SRPT], rs[K3_SRPT];
-        uint64_t rv[K3_SRPT][NVR];
-        int32_t rsb[K3_SRPT];
-        uint32_t rh[K3_SRPT];
-        uint32_t valid = 0;
-        const int64_t base = c * K3_CH + (int64_t)sub * K3_SUB;
-        // ---- coalesced column loads: lane i reads row base + j*256 + i
-        static_for<K3_SRPT>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            const int64_t i = base + (int64_t)j * BLOCK + tid;
-            rk[j] = 0;
-            rs[j] = 0;
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        rsb[j] = 0;
 #pragma unroll
-            for (int q = 0; q < NVR; q++) rv[j][q] = 0;
-            if (i < a.n) {
-                rk[j] = a.key[i];
-                rs[j] = a.ts[i];
-                if (SCATTER) {
-#pragma unroll
-                    for (int q = 0; q < NV; q++) rv[j][q] = a.vals[q][i];
-                }
-                valid |= 1u << j;
-            }
-        });
-        // ---- K1/K2: slice end, late classification, key group -> superbucket, slot claim
-        static_for<K3_SRPT>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            rsb[j] = 0;
-            rh[j] = 0;
-            if (!(valid & (1u << j))) return;
-            const int64_t i = base + (int64_t)j * BLOCK + tid;
-            const int32_t pre = a.khash ? a.khash[i] : 0;
-            const int64_t se = slice_end_of(a.win, rs[j]);
-            int64_t target = se;
-            rsb[j] = superbucket_of(a.ks, rk[j], pre);
-            if (is_fired(se, cur_wm)) {
-                if (is_fired(last_window_end_of(a.win, se), cur_wm)) {  // late for every window: drop
-                    valid &= ~(1u << j);
-                    ldrop++;
-                    return;
-                }
-                target = merge_target_of(a.win, se);
-                if (SCATTER) {  // timer for the first unfired window (processElement :111-117)
-                    const int64_t steps = (int64_t)((uint64_t)wsub(wadd(cur_wm, 1), se) / (uint64_t)a.win.interval) + 1;
-                    const int64_t unfired = wadd(se, steps * a.win.interval);
-                    const int64_t r = __hip_atomic_fetch_add(&ctrl->n_treq, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
-                    if (r < a.treq_cap) {
-                        a.treq[3 * r] = rk[j];
-                        a.treq[3 * r + 1] = unfired;
-                        a.treq[3 * r + 2] = rsb[j];
-                    } else {
-                        __hip_atomic_fetch_or(&ctrl->error, ERR_TREQ, __ATOMIC_RELAXED, DEV_SCOPE);
-                    }
-                }
-            }
-            rs[j] = target;
-            lmin = min(lmin, target);
-            lrows++;
-            rh[j] = cache_hash(rk[j], target) & (K3_SLOTS - 1);
-            atomicMin(&claim[rh[j]], (uint32_t)(j * BLOCK + tid));
-        });
-        __syncthreads();
-        // ---- slot owners publish their (key, slice) and seed the slot accumulator
-        static_for<K3_SRPT>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            if (!(valid & (1u << j)) || claim[rh[j]] != (uint32_t)(j * BLOCK + tid)) return;
-            ckey[rh[j]] = rk[j];
-            cslice[rh[j]] = rs[j];
-            if (SCATTER) {
-                csb[rh[j]] = (uint32_t)rsb[j];
-#pragma unroll
-                for (int w = 0; w < NW; w++)
-                    cacc[w][rh[j]] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
-            } else {
-                atomicAdd(&cur[rsb[j]], 1u);  // the slot owner emits one partial
-            }
-        });
-        __syncthreads();
-        // ---- everyone else: fold into the owner's slot, or pass through as a partial
-        static_for<K3_SRPT>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            if (!(valid & (1u << j))) return;
-            const uint32_t h = rh[j];
-            if (claim[h] == (uint32_t)(j * BLOCK + tid)) return;
-            if (ckey[h] == rk[j] && cslice[h] == rs[j]) {
-                if (SCATTER) {
-#pragma unroll
-                    for (int w = 0; w < NW; w++)
-                        if (w < a.wd.nw)
-                            lds_fold(a.wd.op[w], &cacc[w][h], record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])));
-                }
+        for (int w = 0; w < NW; w++) racc[j][w] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
+        if (!(valid & (1u << j))) return;
+        rsb[j] = superbucket_of(a.ks, rk[j], pre[j]);
+        const int64_t se = slice_end_of(a.win, rs[j]);
+        int64_t target = se;
+        if (is_fired(se, cur_wm)) {
+            if (is_fired(last_window_end_of(a.win, se), cur_wm)) {  // late for every window: drop
+                valid &= ~(1u << j);
+                ldrop++;
                 return;
             }
-            const uint32_t pos = atomicAdd(&cur[rsb[j]], 1u);
-            if (SCATTER) {
-                uint64_t* p = out + (size_t)pos * PW;
-                p[0] = (uint64_t)rk[j];
-                p[1] = (uint64_t)rs[j];
+            target = merge_target_of(a.win, se);
+            // timer for the first unfired window (processElement :111-117)
+            const int64_t steps = (int64_t)((uint64_t)wsub(wadd(cur_wm, 1), se) / (uint64_t)a.win.interval) + 1;
+            const int64_t unfired = wadd(se, steps * a.win.interval);
+            const int64_t r = __hip_atomic_fetch_add(&ctrl->n_treq, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
+            if (r < a.treq_cap) {
+                a.treq[3 * r] = rk[j];
+                a.treq[3 * r + 1] = unfired;
+                a.treq[3 * r + 2] = rsb[j];
+            } else {
+                __hip_atomic_fetch_or(&ctrl->error, ERR_TREQ, __ATOMIC_RELAXED, DEV_SCOPE);
+            }
+        }
+        rs[j] = target;
+        lmin = min(lmin, target);
+        lrows++;
+    });
+    // ---- K3: fold equal (key, slice) rows, one 2048-row sub-tile at a time
+    static_for<NSUB>([&](auto S) {
+        constexpr int s = decltype(S)::value;
+        uint32_t rh[IG_SRPT];
+        __syncthreads();  // previous sub-tile's owners are done with claim/cacc
+        for (int h = tid; h < IG_SLOTS; h += IG_BLOCK) claim[h] = 0xFFFFFFFFu;
+        __syncthreads();
+        static_for<IG_SRPT>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            rh[q] = cache_hash(rk[j], rs[j]) & (IG_SLOTS - 1);
+            if (valid & (1u << j)) atomicMin(&claim[rh[q]], (uint32_t)(j * IG_BLOCK + tid));
+        });
+        __syncthreads();
+        static_for<IG_SRPT>([&](auto Q) {  // slot owners publish their (key, slice) and partial
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
+            ckey[rh[q]] = rk[j];
+            cslice[rh[q]] = rs[j];
+#pragma unroll
+            for (int w = 0; w < NW; w++) cacc[w][rh[q]] = racc[j][w];
+        });
+        __syncthreads();
+        static_for<IG_SRPT>([&](auto Q) {  // everyone else folds into a matching owner
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            const uint32_t h = rh[q];
+            if (!(valid & (1u << j)) || claim[h] == (uint32_t)(j * IG_BLOCK + tid)) return;
+            if (ckey[h] == rk[j] && cslice[h] == rs[j]) {
 #pragma unroll
                 for (int w = 0; w < NW; w++)
-                    p[2 + w] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
+                    if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w][h], racc[j][w]);
+                valid &= ~(1u << j);
             }
         });
         __syncthreads();
-        if (SCATTER) {  // slot owners write the folded partial
-            static_for<K3_SRPT>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                if (!(valid & (1u << j))) return;
-                const uint32_t h = rh[j];
-                if (claim[h] != (uint32_t)(j * BLOCK + tid)) return;
-                const uint32_t pos = atomicAdd(&cur[csb[h]], 1u);
-                uint64_t* p = out + (size_t)pos * PW;
-                p[0] = (uint64_t)ckey[h];
-                p[1] = (uint64_t)cslice[h];
+        static_for<IG_SRPT>([&](auto Q) {  // owners take the folded partial back
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
 #pragma unroll
-                for (int w = 0; w < NW; w++) p[2 + w] = cacc[w][h];
-            });
-            __syncthreads();
-        }
+            for (int w = 0; w < NW; w++) racc[j][w] = cacc[w][rh[q]];
+        });
+    });
+    // ---- rank the partials per superbucket, scan, publish the cells
+    uint32_t rrank[RPT];
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        rrank[j] = (valid & (1u << j)) ? atomicAdd(&hist[rsb[j]], 1u) : 0u;
+    });
+    __syncthreads();
+    uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch + c;
+    const int per = (n_sb + IG_BLOCK - 1) / IG_BLOCK;
+    const int sb0 = min(tid * per, n_sb), sb1 = min(sb0 + per, n_sb);
+    uint32_t seg = 0;
+    for (int i = sb0; i < sb1; i++) seg += hist[i];
+    uint32_t total;
+    const uint32_t incl = block_incl_scan(seg, wsum, &total);
+    uint32_t run = incl - seg;
+    for (int i = sb0; i < sb1; i++) {
+        const uint32_t v = hist[i];
+        hist[i] = run;
+        cells[(size_t)i * a.max_nch] = run | (v << 16);
+        run += v;
     }
-    if (!SCATTER) {
-        for (int s = tid; s < n_sb; s += BLOCK) a.cnt[(size_t)s * nch + c] = cur[s];
-        return;
-    }
-    // ---- per-push superbucket starts (chunk 0 of every superbucket) and control counters
-    if (c == 0)
-        for (int s = tid; s < n_sb; s += BLOCK) a.starts[(size_t)slot * (n_sb + 1) + s] = a.cnt[(size_t)s * nch];
+    __syncthreads();
+    // ---- store the partials: contiguous cells, one chunk region per workgroup
+    uint64_t* out = a.parts + ((size_t)slot * a.cap_rows + (size_t)base) * PW;
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if (!(valid & (1u << j))) return;
+        uint64_t* p = out + (size_t)(hist[rsb[j]] + rrank[j]) * PW;
+        p[0] = (uint64_t)rk[j];
+        p[1] = (uint64_t)rs[j];
+#pragma unroll
+        for (int w = 0; w < NW; w++) p[2 + w] = racc[j][w];
+    });
+    // ---- control counters (reduced into the control block by k_push_stats)
     if (lmin != INT64_MAX) __hip_atomic_fetch_min(&s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
     if (ldrop) atomicAdd((unsigned long long*)&s_drop, (unsigned long long)ldrop);
     if (lrows) atomicAdd((unsigned long long*)&s_rows, (unsigned long long)lrows);
     __syncthreads();
-    if (tid == 0) {  // reduced into the control block by k_push_stats (no contended atomics)
-        a.chunk_stats[3 * c] = s_min;
-        a.chunk_stats[3 * c + 1] = (int64_t)s_drop;
-        a.chunk_stats[3 * c + 2] = (int64_t)s_rows;
+    if (tid == 0) {
+        a.chunk_stats[4 * c] = s_min;
+        a.chunk_stats[4 * c + 1] = (int64_t)s_drop;
+        a.chunk_stats[4 * c + 2] = (int64_t)s_rows;
+        a.chunk_stats[4 * c + 3] = (int64_t)total;
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_push_stats(const int64_t* st, int64_t nch, Ctrl* ctrl) {
+// one block: reduce the chunk stats into the control block and commit the push's slot
+__global__ __launch_bounds__(BLOCK) void k_push_stats(const int64_t* st, int64_t nch, Ctrl* ctrl, int32_t* slot_nch) {
     __shared__ int64_t mn[BLOCK];
     __shared__ int64_t dr[BLOCK];
     __shared__ int64_t rw[BLOCK];
-    int64_t m = INT64_MAX, d = 0, r = 0;
+    __shared__ int64_t pt[BLOCK];
+    int64_t m = INT64_MAX, d = 0, r = 0, q = 0;
     for (int64_t i = threadIdx.x; i < nch; i += BLOCK) {
-        m = min(m, st[3 * i]);
-        d += st[3 * i + 1];
-        r += st[3 * i + 2];
+        m = min(m, st[4 * i]);
+        d += st[4 * i + 1];
+        r += st[4 * i + 2];
+        q += st[4 * i + 3];
     }
     mn[threadIdx.x] = m;
     dr[threadIdx.x] = d;
     rw[threadIdx.x] = r;
+    pt[threadIdx.x] = q;
     __syncthreads();
     for (int k = BLOCK / 2; k > 0; k >>= 1) {
         if (threadIdx.x < k) {
             mn[threadIdx.x] = min(mn[threadIdx.x], mn[threadIdx.x + k]);
             dr[threadIdx.x] += dr[threadIdx.x + k];
             rw[threadIdx.x] += rw[threadIdx.x + k];
+            pt[threadIdx.x] += pt[threadIdx.x + k];
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        ctrl->min_pending = min(ctrl->min_pending, mn[0]);
+        const int64_t slot = ctrl->pending_pushes;
+        if (slot < FW_MAX_PENDING) {
+            slot_nch[slot] = (int32_t)nch;
+            ctrl->pending_pushes = slot + 1;
+            ctrl->min_pending = min(ctrl->min_pending, mn[0]);
+            ctrl->pending_rows += (uint64_t)rw[0];
+            ctrl->partials += (uint64_t)pt[0];
+        }
         ctrl->late_dropped += (uint64_t)dr[0];
-        ctrl->pending_rows += (uint64_t)rw[0];
     }
 }
 
@@ -397,89 +416,6 @@ __global__ __launch_bounds__(BLOCK) void k_compact_copy(CompactArgs a) {
         a.res_we[d] = a.out_we[sidx];
         a.res_null[d] = a.out_null[sidx];
         for (int g = 0; g < a.n_aggs; g++) a.res_val[g][d] = a.out_val[g][sidx];
-    }
-}
-
-// ---- flat exclusive scan of the [sb][chunk] counts (u32), three launches --------------------
-constexpr int SCAN_TILE = BLOCK * 8;
-
-__global__ __launch_bounds__(BLOCK) void k_scan_tiles(const uint32_t* v, int64_t n, uint32_t* tile_sum) {
-    __shared__ uint32_t red[BLOCK];
-    const int64_t b = (int64_t)blockIdx.x * SCAN_TILE;
-    uint32_t s = 0;
-    for (int j = 0; j < 8; j++) {
-        const int64_t i = b + (int64_t)j * BLOCK + threadIdx.x;
-        if (i < n) s += v[i];
-    }
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int d = BLOCK / 2; d > 0; d >>= 1) {
-        if (threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) tile_sum[blockIdx.x] = red[0];
-}
-
-// one block: exclusive scan of the tile sums; takes this push's slot in the partial buffer
-__global__ __launch_bounds__(BLOCK) void k_scan_top(uint32_t* tile_sum, int64_t ntiles, Ctrl* ctrl, uint32_t* starts,
-                                                   int32_t n_sb, uint64_t rows) {
-    __shared__ uint32_t tmp[BLOCK];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int64_t base = 0; base < ntiles; base += BLOCK) {
-        const int64_t i = base + threadIdx.x;
-        const uint32_t v = i < ntiles ? tile_sum[i] : 0;
-        tmp[threadIdx.x] = v;
-        __syncthreads();
-        for (int d = 1; d < BLOCK; d <<= 1) {
-            const uint32_t x = threadIdx.x >= d ? tmp[threadIdx.x - d] : 0;
-            __syncthreads();
-            tmp[threadIdx.x] += x;
-            __syncthreads();
-        }
-        if (i < ntiles) tile_sum[i] = carry + tmp[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == BLOCK - 1) carry += tmp[BLOCK - 1];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const int64_t slot = ctrl->pending_pushes;
-        if (slot >= FW_MAX_PENDING) {
-            ctrl->error |= ERR_CHUNKS;
-            ctrl->push_slot = FW_MAX_PENDING;
-        } else {
-            ctrl->push_slot = (int32_t)slot;
-            ctrl->pending_pushes = slot + 1;
-            starts[(size_t)slot * (n_sb + 1) + n_sb] = carry;  // total partials of this push
-            ctrl->partials += carry;
-        }
-    }
-}
-
-__global__ __launch_bounds__(BLOCK) void k_scan_apply(uint32_t* v, int64_t n, const uint32_t* tile_off) {
-    __shared__ uint32_t tmp[BLOCK];
-    const int64_t b = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * 8;
-    uint32_t x[8];
-    uint32_t s = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        x[j] = b + j < n ? v[b + j] : 0;
-        s += x[j];
-    }
-    tmp[threadIdx.x] = s;
-    __syncthreads();
-    for (int d = 1; d < BLOCK; d <<= 1) {
-        const uint32_t y = threadIdx.x >= d ? tmp[threadIdx.x - d] : 0;
-        __syncthreads();
-        tmp[threadIdx.x] += y;
-        __syncthreads();
-    }
-    uint32_t run = tile_off[blockIdx.x] + tmp[threadIdx.x] - s;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        if (b + j < n) v[b + j] = run;
-        run += x[j];
     }
 }
 
@@ -696,11 +632,23 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
     }
 }
 
+// XCD-aware superbucket order: blocks b, b+8, b+16, ... are dealt to one XCD (round robin,
+// speed only), so they get consecutive superbuckets, whose cells sit next to each other in
+// every chunk region -> the boundary lines two cells share are read from the same L2.
+__device__ __forceinline__ int sb_of_block(int b, int n_sb) {
+    if (n_sb % 8 != 0) return b;
+    return (b % 8) * (n_sb / 8) + b / 8;
+}
+
 template <int NW, int E>
-__global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
+__global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
+    constexpr int CH = IG_BLOCK * ig_rpt(NW);  // chunk rows of the ingest kernel that wrote the cells
     __shared__ StateLds<NW, E> S;
+    __shared__ uint32_t s_cb[MG_MAX_CELLS + 1];  // flat prefix of the cell counts of one push
+    __shared__ uint32_t s_src[MG_MAX_CELLS];     // first row of each cell inside the push's slot
+    __shared__ uint32_t wsum[MG_BLOCK / 64];
     __shared__ int32_t s_work;
     __shared__ int64_t s_vmin;
     __shared__ int32_t s_nlive;
@@ -709,7 +657,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
     __shared__ int32_t s_emit;
 
     const int tid = threadIdx.x;
-    const int sb = blockIdx.x;
+    const int sb = sb_of_block(blockIdx.x, a.n_sb);
     Ctrl* c = a.ctrl;
     const int64_t W = a.wm;
     // control decisions; k_finalize applies the same decisions to the control block afterwards
@@ -726,28 +674,21 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
     const int32_t n0 = a.state_count[sb];
 
     if (tid == 0) {
-        s_work = (ntreq > 0) || (do_fire && is_fired(a.sb_min_timer[sb], W));
+        s_work = (ntreq > 0) || do_flush || (do_fire && is_fired(a.sb_min_timer[sb], W));
         s_fired = 0;
         s_emit = a.sb_out[sb];
     }
     __syncthreads();
-    const bool work0 = s_work != 0;
-    __syncthreads();
-    if (!work0 && do_flush && tid < pend) {  // any pending partial for this superbucket?
-        const uint32_t* st = a.starts + (size_t)tid * (a.n_sb + 1);
-        if (st[sb + 1] > st[sb]) s_work = 1;
-    }
-    __syncthreads();
     if (s_work) {
         // ---- load this superbucket's entries into LDS
-        for (int i = tid; i < 2 * E; i += BLOCK) S.idx[i] = 0;
+        for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
         if (tid == 0) {
             S.n = n0;
             S.overflow = 0;
         }
         __syncthreads();
         const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
-        for (int e = tid; e < n0; e += BLOCK) {
+        for (int e = tid; e < n0; e += MG_BLOCK) {
             const uint64_t* p = st + (size_t)e * PWE;
             const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
             S.key[e] = k;
@@ -766,19 +707,31 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
         }
         __syncthreads();
         // ---- timers registered by late records in processElement
-        for (int64_t r = tid; r < ntreq; r += BLOCK) {
+        for (int64_t r = tid; r < ntreq; r += MG_BLOCK) {
             if (a.treq[3 * r + 2] != sb) continue;
             const int e = find_or_insert(S, a.treq[3 * r], a.treq[3 * r + 1], a.wd);
             if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
         }
         // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket
         if (do_flush) {
-            for (int64_t pi = 0; pi < pend; pi++) {  // contiguous, coalesced segment per push
-                const uint32_t* st = a.starts + (size_t)pi * (a.n_sb + 1);
-                const uint32_t s0 = st[sb], s1 = st[sb + 1];
+            for (int64_t pi = 0; pi < pend; pi++) {
+                const int nch = a.slot_nch[pi];
+                const uint32_t* cl = a.cells + ((size_t)pi * a.n_sb + sb) * a.max_nch;
+                const uint32_t v = tid < nch ? cl[tid] : 0u;  // nch <= MG_MAX_CELLS == MG_BLOCK
+                uint32_t total;
+                const uint32_t incl = block_incl_scan(v >> 16, wsum, &total);
+                s_cb[tid + 1] = incl;
+                s_src[tid] = (uint32_t)tid * CH + (v & 0xFFFFu);
+                if (tid == 0) s_cb[0] = 0;
+                __syncthreads();
                 const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
-                for (uint32_t q = s0 + tid; q < s1; q += BLOCK) {
-                    const uint64_t* p = seg + (size_t)q * PW;
+                for (uint32_t r = tid; r < total; r += MG_BLOCK) {
+                    int lo = 0, hi = nch;  // s_cb[lo] <= r < s_cb[hi]
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_cb[mid] <= r) lo = mid; else hi = mid;
+                    }
+                    const uint64_t* p = seg + (size_t)(s_src[lo] + (r - s_cb[lo])) * PW;
                     const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
                     const int e = find_or_insert(S, k, s, a.wd);
                     if (e < 0) continue;
@@ -788,6 +741,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
                     // register the window timer unless already fired (AggCombiner.java:103-110)
                     atomicOr(&S.flag[e], is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER));
                 }
+                __syncthreads();
             }
         }
         __syncthreads();
@@ -797,13 +751,13 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
                 if (tid == 0) s_vmin = INT64_MAX;
                 __syncthreads();
                 const int n = min(S.n, E);
-                for (int e = tid; e < n; e += BLOCK)
+                for (int e = tid; e < n; e += MG_BLOCK)
                     if ((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W))
                         __hip_atomic_fetch_min(&s_vmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
                 __syncthreads();
                 const int64_t v = s_vmin;
                 if (v == INT64_MAX) break;
-                for (int e = tid; e < n; e += BLOCK) {
+                for (int e = tid; e < n; e += MG_BLOCK) {
                     if ((S.flag[e] & F_TIMER) && S.slice[e] == v) {
                         atomicAnd(&S.flag[e], ~F_TIMER);
                         fire_one(a, S, e, v, &s_fired, sb, &s_emit);
@@ -820,7 +774,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_fire(MergeArgs a) {
         __syncthreads();
         const int n = min(S.n, E);
         uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
-        for (int e = tid; e < n; e += BLOCK) {
+        for (int e = tid; e < n; e += MG_BLOCK) {
             const uint32_t f = S.flag[e];
             if (!(f & (F_ACC | F_TIMER))) continue;
             const int pos = atomicAdd(&s_nlive, 1);
@@ -880,9 +834,11 @@ __global__ void k_init_ctrl(Ctrl* c) {
     }
 }
 
-hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t) {
+    kt_mark(t, FW_KT_OTHER, false, s);
     hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(BLOCK), 0, s, a.sb_out, a.n_sb, a.off, a.ctrl, a.res_cap);
     hipLaunchKernelGGL(k_compact_copy, dim3(a.n_sb + 1), dim3(BLOCK), 0, s, a);
+    kt_mark(t, FW_KT_OTHER, true, s);
     return hipGetLastError();
 }
 
@@ -895,52 +851,51 @@ hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
 // template dispatch
 // ---------------------------------------------------------------------------------------
 template <int NV, int NW>
-static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s) {
+static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
+    constexpr int RPT = ig_rpt(NW);
     const int64_t nch = a.n_chunks;
     if (nch == 0) return hipSuccess;
     const size_t dyn = (size_t)a.ks.n_sb * sizeof(uint32_t);
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void*)k_chunk<false, NV, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_chunk<true, NV, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-        attr_set = true;
+    static int dyn_max = -1;
+    if (dyn_max < 0) {  // allow the histogram up to the CU's 160 KiB beside the static fold table
+        hipFuncAttributes fa{};
+        hipError_t e = hipFuncGetAttributes(&fa, (const void*)k_ingest<NV, NW, RPT>);
+        if (e != hipSuccess) return e;
+        dyn_max = 160 * 1024 - (int)fa.sharedSizeBytes;
+        e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn_max);
+        if (e != hipSuccess) return e;
     }
-    const int64_t L = (int64_t)a.ks.n_sb * nch;
-    const int64_t ntiles = (L + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL((k_chunk<false, NV, NW>), dim3((unsigned)nch), dim3(BLOCK), dyn, s, a);
-    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)ntiles), dim3(BLOCK), 0, s, a.cnt, L, a.tile_sum);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(BLOCK), 0, s, a.tile_sum, ntiles, a.ctrl, a.starts, a.ks.n_sb,
-                       (uint64_t)a.n);
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)ntiles), dim3(BLOCK), 0, s, a.cnt, L, a.tile_sum);
-    hipLaunchKernelGGL((k_chunk<true, NV, NW>), dim3((unsigned)nch), dim3(BLOCK), dyn, s, a);
-    hipLaunchKernelGGL(k_push_stats, dim3(1), dim3(BLOCK), 0, s, a.chunk_stats, nch, a.ctrl);
+    if ((int64_t)dyn > dyn_max) return hipErrorInvalidValue;
+    kt_mark(t, FW_KT_REDUCE, false, s);
+    hipLaunchKernelGGL((k_ingest<NV, NW, RPT>), dim3((unsigned)nch), dim3(IG_BLOCK), dyn, s, a);
+    kt_mark(t, FW_KT_REDUCE, true, s);
+    kt_mark(t, FW_KT_OTHER, false, s);
+    hipLaunchKernelGGL(k_push_stats, dim3(1), dim3(BLOCK), 0, s, a.chunk_stats, nch, a.ctrl, a.slot_nch);
+    kt_mark(t, FW_KT_OTHER, true, s);
     return hipGetLastError();
 }
 
 template <int NV>
-static hipError_t ingest_nv(const IngestArgs& a, hipStream_t s) {
+static hipError_t ingest_nv(const IngestArgs& a, hipStream_t s, KTimer* t) {
     const int nw = a.wd.nw;
-    if (nw <= 1) return ingest_nw<NV, 1>(a, s);
-    if (nw <= 2) return ingest_nw<NV, 2>(a, s);
-    if (nw <= 4) return ingest_nw<NV, 4>(a, s);
-    return ingest_nw<NV, 8>(a, s);
+    if (nw <= 1) return ingest_nw<NV, 1>(a, s, t);
+    if (nw <= 2) return ingest_nw<NV, 2>(a, s, t);
+    if (nw <= 4) return ingest_nw<NV, 4>(a, s, t);
+    return ingest_nw<NV, 8>(a, s, t);
 }
 
-hipError_t launch_ingest(const IngestArgs& a, hipStream_t s) {
+hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t) {
     switch (a.nv) {
-        case 0: return ingest_nv<0>(a, s);
-        case 1: return ingest_nv<1>(a, s);
-        case 2: return ingest_nv<2>(a, s);
-        default: return ingest_nv<4>(a, s);
+        case 0: return ingest_nv<0>(a, s, t);
+        case 1: return ingest_nv<1>(a, s, t);
+        case 2: return ingest_nv<2>(a, s, t);
+        default: return ingest_nv<4>(a, s, t);
     }
 }
 
 template <int NW>
 static hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
-    if (NW <= 2 && a.cap_e == 2048)
-        hipLaunchKernelGGL((k_merge_fire<NW, (NW <= 2 ? 2048 : 1024)>), dim3(a.n_sb), dim3(BLOCK), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_merge_fire<NW, 1024>), dim3(a.n_sb), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL((k_merge_fire<NW, mg_entries(NW)>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
     return hipGetLastError();
 }
 
@@ -952,11 +907,15 @@ static hipError_t merge_any(const MergeArgs& a, hipStream_t s) {
     return merge_nw<8>(a, s);
 }
 
-hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s) {
+hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s, KTimer* t) {
+    kt_mark(t, FW_KT_MERGE, false, s);
     hipError_t e = merge_any(a, s);
+    kt_mark(t, FW_KT_MERGE, true, s);
     if (e != hipSuccess) return e;
+    kt_mark(t, FW_KT_OTHER, false, s);
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, a.ctrl, a.wm, a.force_flush, a.always_flush,
                        a.win.slice_div);
+    kt_mark(t, FW_KT_OTHER, true, s);
     return hipGetLastError();
 }
 

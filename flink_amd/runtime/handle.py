@@ -123,6 +123,18 @@ class WindowAggHandle:
         check(lib().fw_get_stats(self._h, C.byref(s)))
         return {f: getattr(s, f) for f, _ in abi.fw_stats._fields_}
 
+    # ---- device timing (hipEvents around each launch on the handle stream)
+    def set_profiling(self, enable=True):
+        check(lib().fw_set_profiling(self._h, 1 if enable else 0))
+
+    def kernel_times(self):
+        """{kind: (ms, launches)} accumulated since set_profiling(True)."""
+        t = abi.fw_kernel_times()
+        check(lib().fw_get_kernel_times(self._h, C.byref(t)))
+        names = {abi.KT_PARTITION: "partition", abi.KT_SCAN: "scan", abi.KT_REDUCE: "reduce",
+                 abi.KT_MERGE: "merge", abi.KT_OTHER: "other"}
+        return {n: (t.ms[k], t.launches[k]) for k, n in names.items()}
+
     # ---- checkpoint
     def snapshot(self) -> bytes:
         size = C.c_int64()

@@ -203,6 +203,24 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host);
 int fw_results_reset(fw_handle* h);
 int fw_get_stats(fw_handle* h, fw_stats* out);
 
+/* ---- per-kernel device timing (hipEvents on the handle stream, around each launch) ------- */
+/* The reference has no per-kernel profiler for this path (flame graphs and latency
+   markers only); this is the MI355X-side equivalent used by bench.py for the roofline figure. */
+#define FW_KT_PARTITION 0   /* K1: key group -> superbucket row histogram per chunk            */
+#define FW_KT_SCAN 1        /* exclusive scan of the [superbucket][chunk] histogram             */
+#define FW_KT_REDUCE 2      /* K2+K3: slice assign + LDS segmented reduce + scatter of partials */
+#define FW_KT_MERGE 3       /* K4+K5: merge partials into the HBM slice table + fire windows    */
+#define FW_KT_OTHER 4       /* control-block / stats / compaction launches                      */
+#define FW_KT_N 8
+typedef struct {
+    double ms[FW_KT_N];          /* accumulated device time per kernel class                 */
+    int64_t launches[FW_KT_N];   /* timed launches per kernel class                          */
+} fw_kernel_times;
+/* enable != 0 starts timing (and resets the accumulators); 0 stops it. */
+int fw_set_profiling(fw_handle* h, int enable);
+/* synchronises the handle stream, then returns the accumulated times */
+int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out);
+
 /* ---- checkpoint -------------------------------------------------------------------- */
 /* Flushes, then serialises watermark + state + timers.  *size receives the byte count;
    call with buf == NULL to query it. */

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -178,6 +179,7 @@ struct fw_handle {
     int64_t pushes_ub = 0;  // upper bound of device pending_pushes
     int64_t host_cur = INT64_MIN;
     KTimer* timer = nullptr;  // non-null while fw_set_profiling is on
+    int ablate = 0;           // FW_ABLATE (development timing builds only; results are wrong)
 };
 
 namespace {
@@ -224,6 +226,8 @@ int validate_and_plan(fw_handle* h) {
     }
     w.slice_div = make_udiv((uint64_t)w.interval);
     w.size_div = make_udiv((uint64_t)w.size);
+    w.fast32 = w.interval < (1ll << 30) && w.offset < (1ll << 61) && w.offset > -(1ll << 61);
+    w.slice_div32 = make_udiv32(w.fast32 ? (uint32_t)w.interval : 1u);
     h->always_flush = c.api == FW_API_DATASTREAM;
 
     // ---- aggregates -> accumulator words
@@ -308,6 +312,7 @@ int validate_and_plan(fw_handle* h) {
     KeySpace& ks = h->ks;
     ks.hash_kind = c.key_hash;
     ks.max_p = c.max_parallelism;
+    ks.maxp_div = make_udiv32((uint32_t)c.max_parallelism);
     ks.kg_start = (c.subtask_index * c.max_parallelism + c.parallelism - 1) / c.parallelism;
     const int kg_end = ((c.subtask_index + 1) * c.max_parallelism - 1) / c.parallelism;
     ks.n_kg = kg_end - ks.kg_start + 1;
@@ -317,7 +322,7 @@ int validate_and_plan(fw_handle* h) {
     const int64_t fill = h->cap_e * 55 / 100;
     int64_t per_kg = (cap_target + ks.n_kg - 1) / ks.n_kg;
     int64_t sbk = next_pow2((per_kg + fill - 1) / fill);
-    const int64_t max_sb = std::min<int64_t>(16384, ig_max_sb(h->nw_t));
+    const int64_t max_sb = IG_MAX_SB;
     while ((int64_t)ks.n_kg * sbk > max_sb && sbk > 1) sbk >>= 1;
     if ((int64_t)ks.n_kg * sbk > max_sb) return fail(FW_E_INVALID, "too many key groups per subtask for the ingest histogram");
     ks.sb_per_kg_log2 = 0;
@@ -327,7 +332,6 @@ int validate_and_plan(fw_handle* h) {
     if (c.output_capacity <= 0) return fail(FW_E_INVALID, "output_capacity must be > 0");
     h->chunk_rows = (int64_t)IG_BLOCK * ig_rpt(h->nw_t);
     h->cap_rows = ((c.max_batch_rows + h->chunk_rows - 1) / h->chunk_rows) * h->chunk_rows;
-    h->cap_rows = std::min<int64_t>(h->cap_rows, (int64_t)MG_MAX_CELLS * h->chunk_rows);  // longer pushes are split
     h->max_nch = h->cap_rows / h->chunk_rows;
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     h->out_cap = c.output_capacity;
@@ -410,9 +414,10 @@ int read_ctrl(fw_handle* h, Ctrl* out) {
     HIP_TRY(hipMemcpyAsync(out, h->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (out->error) {
-        return fail(FW_E_CAPACITY, "device capacity exceeded (error bits 0x%x:%s%s%s%s)", out->error,
+        return fail(FW_E_CAPACITY, "device error (bits 0x%x:%s%s%s%s%s)", out->error,
                     out->error & ERR_CHUNKS ? " partial-buffer" : "", out->error & ERR_STATE ? " state-table" : "",
-                    out->error & ERR_OUTPUT ? " result-buffer" : "", out->error & ERR_TREQ ? " timer-requests" : "");
+                    out->error & ERR_OUTPUT ? " result-buffer" : "", out->error & ERR_TREQ ? " timer-requests" : "",
+                    out->error & ERR_KEYGROUP ? " key-group-not-owned" : "");
     }
     return FW_OK;
 }
@@ -489,6 +494,8 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.n_chunks = (m + h->chunk_rows - 1) / h->chunk_rows;
         a.treq = h->treq;
         a.treq_cap = h->treq_cap;
+        a.lds_bytes = IG_LDS;
+        a.ablate = h->ablate;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
     }
@@ -508,6 +515,7 @@ int fw_create(const fw_config* cfg, fw_handle** out) {
     *out = nullptr;
     fw_handle* h = new fw_handle();
     h->cfg = *cfg;
+    if (const char* ab = getenv("FW_ABLATE")) h->ablate = atoi(ab);
     int rc = validate_and_plan(h);
     if (!rc) rc = allocate(h);
     if (rc) {

@@ -136,6 +136,33 @@ FW_HD uint64_t udiv(uint64_t x, const UDiv& v) {
     return q >> v.shift;
 }
 
+// unsigned 32-bit division by an invariant divisor (Granlund-Montgomery round-up multiplier)
+struct UDiv32 {
+    uint32_t d;
+    uint32_t magic;
+    uint32_t sh1, sh2;
+};
+
+inline UDiv32 make_udiv32(uint32_t d) {  // host only; d > 0
+    UDiv32 r{};
+    r.d = d;
+    uint32_t l = 0;
+    while ((1ull << l) < d) l++;  // ceil(log2 d)
+    r.magic = (uint32_t)((((uint64_t)1 << 32) * ((1ull << l) - d)) / d + 1);
+    r.sh1 = l < 1 ? l : 1;
+    r.sh2 = l - r.sh1;
+    return r;
+}
+
+FW_HD uint32_t udiv32(uint32_t n, const UDiv32& v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t t = __umulhi(v.magic, n);
+#else
+    const uint32_t t = (uint32_t)(((uint64_t)v.magic * n) >> 32);
+#endif
+    return (t + ((n - t) >> v.sh1)) >> v.sh2;
+}
+
 // TimeWindow.getWindowStartWithOffset(ts, offset, size) with Java long semantics.
 FW_HD int64_t window_start(int64_t ts, int64_t offset, const UDiv& size) {
     const uint64_t x = (uint64_t)ts - (uint64_t)offset;

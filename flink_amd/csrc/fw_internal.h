@@ -13,22 +13,22 @@ constexpr int MAX_WORDS = 8;        // accumulator words per (key, slice)
 constexpr int MAX_KCOLS = 4;        // value columns a kernel loads per record
 constexpr int FW_MAX_PENDING = 8;   // pushes buffered between two flushes
 
-// ---- ingest (K1+K2+K3): one 1024-thread workgroup per chunk of IG_BLOCK * RPT rows
-constexpr int IG_BLOCK = 1024;
+// ---- ingest (K1+K2+K3): one 512-thread workgroup per chunk of IG_BLOCK * RPT rows, two
+// workgroups per CU (one loads while the other folds / sorts / stores)
+constexpr int IG_BLOCK = 512;
 constexpr int IG_SRPT = 2;                      // rows per thread per fold sub-tile
-constexpr int IG_SUB = IG_BLOCK * IG_SRPT;      // rows per fold sub-tile (2048)
-// LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)
-constexpr int ig_slots(int nw) { return nw <= 4 ? 2048 : 1024; }
-// static LDS of k_ingest (fold table) and the superbucket limit its dynamic histogram allows
-constexpr int ig_static_lds(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw) + 512; }
-constexpr int ig_max_sb(int nw) { return (160 * 1024 - ig_static_lds(nw)) / 4; }
-constexpr int IG_MAX_CH = IG_BLOCK * 8;         // largest chunk (rows)
-// rows per thread by accumulator words: keeps the chunk's partials in registers
+constexpr int IG_SUB = IG_BLOCK * IG_SRPT;      // rows per fold sub-tile (1024)
+constexpr int IG_LDS = 78 * 1024;               // dynamic LDS per workgroup: histogram + fold/stage area
+constexpr int IG_MAX_SB = 8192;                 // superbuckets the ingest histogram holds (32 KiB)
+// rows per thread by accumulator words: the chunk's partials stay in registers (<= 128 VGPRs)
 constexpr int ig_rpt(int nw) { return nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
+// LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)
+constexpr int ig_slots(int nw) { return nw <= 2 ? 1024 : nw <= 4 ? 512 : 256; }
+constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw); }
 
 // ---- merge/fire (K4+K5): one 1024-thread workgroup per superbucket
 constexpr int MG_BLOCK = 1024;
-constexpr int MG_MAX_CELLS = 1024;              // chunks per pending push a merge workgroup reads
+constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a time per pending push
 // LDS slice-state capacity (entries) per superbucket by accumulator words
 constexpr int mg_entries(int nw) { return nw <= 1 ? 4096 : nw <= 4 ? 2048 : 1024; }
 
@@ -62,6 +62,7 @@ constexpr uint32_t ERR_CHUNKS = 1u;
 constexpr uint32_t ERR_STATE = 2u;
 constexpr uint32_t ERR_OUTPUT = 4u;
 constexpr uint32_t ERR_TREQ = 8u;
+constexpr uint32_t ERR_KEYGROUP = 16u;  // a record's key group is outside this subtask's range
 
 // Device-resident operator control block (one per handle).  Only kernels write it, so a
 // watermark cycle needs no host round trip.
@@ -91,6 +92,9 @@ struct WinDesc {
     int64_t offset;
     UDiv slice_div;       // divisor = interval
     UDiv size_div;        // divisor = size (CUMULATE getWindowStart)
+    UDiv32 slice_div32;   // divisor = interval, for the 32-bit fast path
+    int32_t fast32;       // interval < 2^30 and |offset| < 2^61: rows near a chunk base use 32-bit math
+    int32_t pad;
 };
 
 FW_HD int64_t slice_end_of(const WinDesc& w, int64_t ts) {
@@ -120,12 +124,23 @@ struct KeySpace {
     int32_t n_kg;          // key groups owned
     int32_t sb_per_kg_log2;
     int32_t n_sb;          // superbuckets = n_kg << sb_per_kg_log2
+    UDiv32 maxp_div;       // divisor max_p
 };
 
-FW_HD int32_t superbucket_of(const KeySpace& ks, int64_t key, int32_t pre) {
-    const int32_t kg = key_group_for_hash(java_key_hash(ks.hash_kind, key, pre), ks.max_p);
-    const uint32_t sub = ks.sb_per_kg_log2 ? (uint32_t)(mix64((uint64_t)key) >> (64 - ks.sb_per_kg_log2)) : 0u;
+// Routing of one key: m = MathUtils.murmurHash(key.hashCode()) (>= 0), key group = m % maxP
+// (KeyGroupRangeAssignment.computeKeyGroupForKeyHash), and the build's own sub-bucket inside
+// the key group from the quotient bits m / maxP (uniform, since m is a murmur hash).
+FW_HD int32_t route_key(const KeySpace& ks, int64_t key, int32_t pre, uint32_t* m_out) {
+    const uint32_t m = (uint32_t)flink_murmur_hash(java_key_hash(ks.hash_kind, key, pre));
+    const uint32_t q = udiv32(m, ks.maxp_div);
+    const int32_t kg = (int32_t)(m - q * (uint32_t)ks.max_p);
+    const uint32_t sub = q & ((1u << ks.sb_per_kg_log2) - 1u);
+    *m_out = m;
     return ((kg - ks.kg_start) << ks.sb_per_kg_log2) + (int32_t)sub;
+}
+FW_HD int32_t superbucket_of(const KeySpace& ks, int64_t key, int32_t pre) {
+    uint32_t m;
+    return route_key(ks, key, pre, &m);
 }
 
 struct WordDesc {
@@ -166,7 +181,12 @@ struct IngestArgs {
     int64_t n_chunks;
     int64_t* treq;         // timer requests: (key, window, sb) triples
     int64_t treq_cap;
+    int32_t lds_bytes;     // dynamic LDS of the launch (IG_LDS)
+    int32_t ablate;        // development only (FW_ABLATE env): skip phases to time the others
 };
+constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
+constexpr int AB_NO_SORT = 2;    // skip rank/scan/cells; store partials at their row position
+constexpr int AB_NO_STORE = 4;   // skip the partial stores
 
 struct MergeArgs {
     Ctrl* ctrl;

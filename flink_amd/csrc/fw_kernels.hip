@@ -86,8 +86,10 @@ __device__ __forceinline__ uint64_t reg_fold(int32_t op, uint64_t a, uint64_t b)
     }
 }
 
-__device__ __forceinline__ uint32_t cache_hash(int64_t k, int64_t s) {
-    return (uint32_t)mix64((uint64_t)k ^ ((uint64_t)s * 0x9E3779B97F4A7C15ull));
+// fold slot of a (key, slice): from the key's murmur (already computed for routing) and the slice
+__device__ __forceinline__ uint32_t fold_slot(uint32_t m, int64_t s, int slots) {
+    const uint32_t h = (m ^ ((uint32_t)s * 0x9E3779B1u) ^ (uint32_t)((uint64_t)s >> 32)) * 0x85EBCA6Bu;
+    return (h ^ (h >> 15)) & (uint32_t)(slots - 1);
 }
 __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
     return (uint32_t)(mix64((uint64_t)k * 0xD6E8FEB86659FD93ull + (uint64_t)s) >> 17);
@@ -113,10 +115,11 @@ __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
 // (key, sliceEnd)) and the per-group fold of AggCombiner.combine (:76-99).
 // ======================================================================================
 
-// inclusive scan of one value per thread over a 1024-thread block (wave shuffles + LDS)
+// inclusive scan of one value per thread over an NT-thread block (wave shuffles + LDS)
+template <int NT>
 __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    constexpr int NWV = 1024 / 64;
+    constexpr int NWV = NT / 64;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t t = __shfl_up(v, d, 64);
@@ -140,26 +143,30 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, 
 }
 
 template <int NV, int NW, int RPT>
-__global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
+__global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int CH = IG_BLOCK * RPT;
     constexpr int NSUB = RPT / IG_SRPT;
     constexpr int NVR = NV > 0 ? NV : 1;
     constexpr int PW = 2 + NW;
-    constexpr int IG_SLOTS = ig_slots(NW);
+    constexpr int SL = ig_slots(NW);
     static_assert(RPT % IG_SRPT == 0, "fold sub-tiles must tile the chunk");
-    __shared__ uint32_t claim[IG_SLOTS];
-    __shared__ int64_t ckey[IG_SLOTS];
-    __shared__ int64_t cslice[IG_SLOTS];
-    __shared__ uint64_t cacc[NW][IG_SLOTS];
     __shared__ uint32_t wsum[IG_BLOCK / 64];
     __shared__ int64_t s_min;
     __shared__ uint64_t s_drop;
     __shared__ uint64_t s_rows;
-    extern __shared__ uint32_t hist[];  // [n_sb]: partials per superbucket -> cell start
+    // dynamic LDS: [hist: n_sb u32 (8-B aligned)][area: fold table, later the store stage]
+    extern __shared__ uint64_t lds[];
+    const int n_sb = a.ks.n_sb;
+    uint32_t* hist = (uint32_t*)lds;  // partials per superbucket -> cell start
+    uint64_t* area = lds + ((n_sb + 1) >> 1);
+    const int area_words = (a.lds_bytes >> 3) - ((n_sb + 1) >> 1);
+    uint32_t* claim = (uint32_t*)area;                   // [SL]
+    int64_t* ckey = (int64_t*)(area + (SL >> 1));       // [SL]
+    int64_t* cslice = ckey + SL;                         // [SL]
+    uint64_t* cacc = (uint64_t*)(cslice + SL);           // [NW][SL]
 
     const int tid = threadIdx.x;
     Ctrl* ctrl = a.ctrl;
-    const int n_sb = a.ks.n_sb;
     const int64_t c = blockIdx.x;
     // the push's slot in the partial buffer; k_push_stats (next launch) advances pending_pushes
     const int64_t slot = __hip_atomic_load(&ctrl->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
@@ -177,6 +184,7 @@ __global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
 
     // ---- coalesced column loads of the whole chunk (all in flight before the first use)
     const int64_t base = c * CH;
+    const int64_t ts0 = a.ts[base];  // chunk base for the 32-bit slice arithmetic
     int64_t rk[RPT], rs[RPT];
     uint64_t rv[RPT][NVR];
     int32_t pre[RPT];
@@ -198,19 +206,40 @@ __global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
             valid |= 1u << j;
         }
     });
+    // slice-aligned base 2^30 ms below the chunk's first row: rows within 2^31 ms of it take
+    // the 32-bit path (one mul_hi instead of a 64-bit magic division)
+    const bool fast = a.win.fast32 && ts0 > -(1ll << 61) && ts0 < (1ll << 61);
+    const int64_t tbase = fast ? window_start(ts0, a.win.offset, a.win.slice_div) -
+                                     (int64_t)((1u << 30) / (uint32_t)a.win.interval) * a.win.interval
+                               : 0;
     // ---- K1/K2: key group -> superbucket, slice end, late classification, record words
     int32_t rsb[RPT];
+    uint32_t rm[RPT];
     uint64_t racc[RPT][NW];
     int64_t lmin = INT64_MAX;
     uint32_t ldrop = 0, lrows = 0;
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
         rsb[j] = 0;
+        rm[j] = 0;
 #pragma unroll
         for (int w = 0; w < NW; w++) racc[j][w] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
         if (!(valid & (1u << j))) return;
-        rsb[j] = superbucket_of(a.ks, rk[j], pre[j]);
-        const int64_t se = slice_end_of(a.win, rs[j]);
+        rsb[j] = route_key(a.ks, rk[j], pre[j], &rm[j]);
+        if ((uint32_t)rsb[j] >= (uint32_t)n_sb) {  // key group not owned by this subtask
+            __hip_atomic_fetch_or(&ctrl->error, ERR_KEYGROUP, __ATOMIC_RELAXED, DEV_SCOPE);
+            valid &= ~(1u << j);
+            return;
+        }
+        int64_t se;
+        const uint64_t d = (uint64_t)rs[j] - (uint64_t)tbase;
+        if (fast && d < (1ull << 31)) {
+            const uint32_t d32 = (uint32_t)d;
+            const uint32_t r = d32 - udiv32(d32, a.win.slice_div32) * (uint32_t)a.win.interval;
+            se = rs[j] - (int64_t)r + a.win.interval;
+        } else {
+            se = slice_end_of(a.win, rs[j]);
+        }
         int64_t target = se;
         if (is_fired(se, cur_wm)) {
             if (is_fired(last_window_end_of(a.win, se), cur_wm)) {  // late for every window: drop
@@ -235,17 +264,17 @@ __global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
         lmin = min(lmin, target);
         lrows++;
     });
-    // ---- K3: fold equal (key, slice) rows, one 2048-row sub-tile at a time
-    static_for<NSUB>([&](auto S) {
+    // ---- K3: fold equal (key, slice) rows, one 1024-row sub-tile at a time
+    if (!(a.ablate & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
         constexpr int s = decltype(S)::value;
         uint32_t rh[IG_SRPT];
         __syncthreads();  // previous sub-tile's owners are done with claim/cacc
-        for (int h = tid; h < IG_SLOTS; h += IG_BLOCK) claim[h] = 0xFFFFFFFFu;
+        for (int h = tid; h < SL; h += IG_BLOCK) claim[h] = 0xFFFFFFFFu;
         __syncthreads();
         static_for<IG_SRPT>([&](auto Q) {
             constexpr int q = decltype(Q)::value;
             constexpr int j = s * IG_SRPT + q;
-            rh[q] = cache_hash(rk[j], rs[j]) & (IG_SLOTS - 1);
+            rh[q] = fold_slot(rm[j], rs[j], SL);
             if (valid & (1u << j)) atomicMin(&claim[rh[q]], (uint32_t)(j * IG_BLOCK + tid));
         });
         __syncthreads();
@@ -256,7 +285,7 @@ __global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
             ckey[rh[q]] = rk[j];
             cslice[rh[q]] = rs[j];
 #pragma unroll
-            for (int w = 0; w < NW; w++) cacc[w][rh[q]] = racc[j][w];
+            for (int w = 0; w < NW; w++) cacc[w * SL + rh[q]] = racc[j][w];
         });
         __syncthreads();
         static_for<IG_SRPT>([&](auto Q) {  // everyone else folds into a matching owner
@@ -267,7 +296,7 @@ __global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
             if (ckey[h] == rk[j] && cslice[h] == rs[j]) {
 #pragma unroll
                 for (int w = 0; w < NW; w++)
-                    if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w][h], racc[j][w]);
+                    if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w * SL + h], racc[j][w]);
                 valid &= ~(1u << j);
             }
         });
@@ -277,14 +306,15 @@ __global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
             constexpr int j = s * IG_SRPT + q;
             if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
 #pragma unroll
-            for (int w = 0; w < NW; w++) racc[j][w] = cacc[w][rh[q]];
+            for (int w = 0; w < NW; w++) racc[j][w] = cacc[w * SL + rh[q]];
         });
     });
     // ---- rank the partials per superbucket, scan, publish the cells
-    uint32_t rrank[RPT];
+    uint32_t rdst[RPT];
+    const bool sort = !(a.ablate & AB_NO_SORT);
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        rrank[j] = (valid & (1u << j)) ? atomicAdd(&hist[rsb[j]], 1u) : 0u;
+        rdst[j] = (sort && (valid & (1u << j))) ? atomicAdd(&hist[rsb[j]], 1u) : (uint32_t)(j * IG_BLOCK + tid);
     });
     __syncthreads();
     uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch + c;
@@ -293,26 +323,50 @@ __global__ __launch_bounds__(IG_BLOCK) void k_ingest(IngestArgs a) {
     uint32_t seg = 0;
     for (int i = sb0; i < sb1; i++) seg += hist[i];
     uint32_t total;
-    const uint32_t incl = block_incl_scan(seg, wsum, &total);
+    const uint32_t incl = block_incl_scan<IG_BLOCK>(seg, wsum, &total);
     uint32_t run = incl - seg;
-    for (int i = sb0; i < sb1; i++) {
-        const uint32_t v = hist[i];
-        hist[i] = run;
-        cells[(size_t)i * a.max_nch] = run | (v << 16);
-        run += v;
-    }
+    if (sort)
+        for (int i = sb0; i < sb1; i++) {
+            const uint32_t v = hist[i];
+            hist[i] = run;
+            cells[(size_t)i * a.max_nch] = run | (v << 16);
+            run += v;
+        }
     __syncthreads();
-    // ---- store the partials: contiguous cells, one chunk region per workgroup
+    if (sort)
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if (valid & (1u << j)) rdst[j] += hist[rsb[j]];
+        });
+    else
+        total = CH;
+    // ---- store the partials through an LDS stage so every global store is a full line
     uint64_t* out = a.parts + ((size_t)slot * a.cap_rows + (size_t)base) * PW;
-    static_for<RPT>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        if (!(valid & (1u << j))) return;
-        uint64_t* p = out + (size_t)(hist[rsb[j]] + rrank[j]) * PW;
-        p[0] = (uint64_t)rk[j];
-        p[1] = (uint64_t)rs[j];
+    const uint32_t wrows = (uint32_t)(area_words / PW) & ~1u;
+    if (!(a.ablate & AB_NO_STORE))
+        for (uint32_t w0 = 0; w0 < total; w0 += wrows) {
+            __syncthreads();  // fold table / previous window no longer read
+            static_for<RPT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                const uint32_t d = rdst[j] - w0;
+                if (!(valid & (1u << j)) || d >= wrows) return;
+                uint64_t* p = area + (size_t)d * PW;
+                p[0] = (uint64_t)rk[j];
+                p[1] = (uint64_t)rs[j];
 #pragma unroll
-        for (int w = 0; w < NW; w++) p[2 + w] = racc[j][w];
-    });
+                for (int w = 0; w < NW; w++) p[2 + w] = racc[j][w];
+            });
+            __syncthreads();
+            const uint32_t nwords = min(wrows, total - w0) * PW;
+            uint64_t* dst = out + (size_t)w0 * PW;  // 16-B aligned: slot, chunk and window bases are even rows
+            for (uint32_t q = 2 * tid; q < nwords; q += 2 * IG_BLOCK) {
+                if (q + 1 < nwords) {
+                    *(ulonglong2*)(dst + q) = *(const ulonglong2*)(area + q);
+                } else {
+                    dst[q] = area[q];
+                }
+            }
+        }
     // ---- control counters (reduced into the control block by k_push_stats)
     if (lmin != INT64_MAX) __hip_atomic_fetch_min(&s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
     if (ldrop) atomicAdd((unsigned long long*)&s_drop, (unsigned long long)ldrop);
@@ -646,8 +700,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int PWE = 3 + NW;
     constexpr int CH = IG_BLOCK * ig_rpt(NW);  // chunk rows of the ingest kernel that wrote the cells
     __shared__ StateLds<NW, E> S;
-    __shared__ uint32_t s_cb[MG_MAX_CELLS + 1];  // flat prefix of the cell counts of one push
-    __shared__ uint32_t s_src[MG_MAX_CELLS];     // first row of each cell inside the push's slot
+    __shared__ uint32_t s_cb[MG_CELL_GROUP + 1];  // flat prefix of the cell counts of a cell group
+    __shared__ uint32_t s_src[MG_CELL_GROUP];     // first row of each cell inside the push's slot
     __shared__ uint32_t wsum[MG_BLOCK / 64];
     __shared__ int32_t s_work;
     __shared__ int64_t s_vmin;
@@ -716,32 +770,35 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         if (do_flush) {
             for (int64_t pi = 0; pi < pend; pi++) {
                 const int nch = a.slot_nch[pi];
-                const uint32_t* cl = a.cells + ((size_t)pi * a.n_sb + sb) * a.max_nch;
-                const uint32_t v = tid < nch ? cl[tid] : 0u;  // nch <= MG_MAX_CELLS == MG_BLOCK
-                uint32_t total;
-                const uint32_t incl = block_incl_scan(v >> 16, wsum, &total);
-                s_cb[tid + 1] = incl;
-                s_src[tid] = (uint32_t)tid * CH + (v & 0xFFFFu);
-                if (tid == 0) s_cb[0] = 0;
-                __syncthreads();
                 const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
-                for (uint32_t r = tid; r < total; r += MG_BLOCK) {
-                    int lo = 0, hi = nch;  // s_cb[lo] <= r < s_cb[hi]
-                    while (hi - lo > 1) {
-                        const int mid = (lo + hi) >> 1;
-                        if (s_cb[mid] <= r) lo = mid; else hi = mid;
-                    }
-                    const uint64_t* p = seg + (size_t)(s_src[lo] + (r - s_cb[lo])) * PW;
-                    const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
-                    const int e = find_or_insert(S, k, s, a.wd);
-                    if (e < 0) continue;
+                const uint32_t* cl = a.cells + ((size_t)pi * a.n_sb + sb) * a.max_nch;
+                for (int g0 = 0; g0 < nch; g0 += MG_CELL_GROUP) {
+                    const int ng = min(MG_CELL_GROUP, nch - g0);
+                    const uint32_t v = tid < ng ? cl[g0 + tid] : 0u;
+                    uint32_t total;
+                    const uint32_t incl = block_incl_scan<MG_BLOCK>(v >> 16, wsum, &total);
+                    s_cb[tid + 1] = incl;
+                    s_src[tid] = (uint32_t)(g0 + tid) * CH + (v & 0xFFFFu);
+                    if (tid == 0) s_cb[0] = 0;
+                    __syncthreads();
+                    for (uint32_t r = tid; r < total; r += MG_BLOCK) {
+                        int lo = 0, hi = ng;  // s_cb[lo] <= r < s_cb[hi]
+                        while (hi - lo > 1) {
+                            const int mid = (lo + hi) >> 1;
+                            if (s_cb[mid] <= r) lo = mid; else hi = mid;
+                        }
+                        const uint64_t* p = seg + (size_t)(s_src[lo] + (r - s_cb[lo])) * PW;
+                        const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
+                        const int e = find_or_insert(S, k, s, a.wd);
+                        if (e < 0) continue;
 #pragma unroll
-                    for (int w = 0; w < NW; w++)
-                        if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], p[2 + w]);
-                    // register the window timer unless already fired (AggCombiner.java:103-110)
-                    atomicOr(&S.flag[e], is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER));
+                        for (int w = 0; w < NW; w++)
+                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], p[2 + w]);
+                        // register the window timer unless already fired (AggCombiner.java:103-110)
+                        atomicOr(&S.flag[e], is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER));
+                    }
+                    __syncthreads();
                 }
-                __syncthreads();
             }
         }
         __syncthreads();
@@ -855,19 +912,17 @@ static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
     constexpr int RPT = ig_rpt(NW);
     const int64_t nch = a.n_chunks;
     if (nch == 0) return hipSuccess;
-    const size_t dyn = (size_t)a.ks.n_sb * sizeof(uint32_t);
-    static int dyn_max = -1;
-    if (dyn_max < 0) {  // allow the histogram up to the CU's 160 KiB beside the static fold table
-        hipFuncAttributes fa{};
-        hipError_t e = hipFuncGetAttributes(&fa, (const void*)k_ingest<NV, NW, RPT>);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, IG_LDS);
         if (e != hipSuccess) return e;
-        dyn_max = 160 * 1024 - (int)fa.sharedSizeBytes;
-        e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn_max);
-        if (e != hipSuccess) return e;
+        attr_set = true;
     }
-    if ((int64_t)dyn > dyn_max) return hipErrorInvalidValue;
+    // the fold table and the histogram must fit the dynamic LDS
+    if ((int64_t)((a.ks.n_sb + 1) / 2) * 8 + ig_fold_bytes(NW) > a.lds_bytes) return hipErrorInvalidValue;
     kt_mark(t, FW_KT_REDUCE, false, s);
-    hipLaunchKernelGGL((k_ingest<NV, NW, RPT>), dim3((unsigned)nch), dim3(IG_BLOCK), dyn, s, a);
+    hipLaunchKernelGGL((k_ingest<NV, NW, RPT>), dim3((unsigned)nch), dim3(IG_BLOCK), a.lds_bytes, s, a);
     kt_mark(t, FW_KT_REDUCE, true, s);
     kt_mark(t, FW_KT_OTHER, false, s);
     hipLaunchKernelGGL(k_push_stats, dim3(1), dim3(BLOCK), 0, s, a.chunk_stats, nch, a.ctrl, a.slot_nch);

@@ -103,7 +103,8 @@ FW_KT_N = 8
 
 
 class fw_kernel_times(C.Structure):
-    _fields_ = [("ms", C.c_double * FW_KT_N), ("launches", C.c_int64 * FW_KT_N)]
+    _fields_ = [("ms", C.c_double * FW_KT_N), ("launches", C.c_int64 * FW_KT_N),
+                ("merge_phase_cycles", C.c_int64 * FW_KT_N)]
 
 
 class fw_gen_params(C.Structure):

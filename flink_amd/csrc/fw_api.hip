@@ -180,6 +180,7 @@ struct fw_handle {
     int64_t host_cur = INT64_MIN;
     KTimer* timer = nullptr;  // non-null while fw_set_profiling is on
     int ablate = 0;           // FW_ABLATE (development timing builds only; results are wrong)
+    unsigned long long* stamps = nullptr;  // [N_STAMPS] merge phase cycles (FW_ABLATE & AB_STAMPS)
 };
 
 namespace {
@@ -379,6 +380,8 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->sb_fired, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->coff, h->ks.n_sb + 2))) return rc;
     if ((rc = dalloc(&h->chunk_stats, 4 * h->max_nch + 4))) return rc;
+    if ((rc = dalloc(&h->stamps, N_STAMPS))) return rc;
+    HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(unsigned long long) * N_STAMPS, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_fired, 0, sizeof(uint32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->state_count, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
@@ -451,6 +454,8 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.sb_fired = h->sb_fired;
     a.wm = wm;
     a.force_flush = force;
+    a.ablate = h->ablate;
+    a.stamps = h->stamps;
     return a;
 }
 
@@ -553,6 +558,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->sb_fired);
     hipFree(h->coff);
     hipFree(h->chunk_stats);
+    hipFree(h->stamps);
     for (int b = 0; b < 2; b++) {
         hipHostFree(h->h_key[b]);
         hipHostFree(h->h_ts[b]);
@@ -765,6 +771,10 @@ int fw_set_profiling(fw_handle* h, int enable) {
 int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
     if (!h || !out) return fail(FW_E_INVALID, "null argument");
     memset(out, 0, sizeof *out);
+    unsigned long long st[N_STAMPS];
+    HIP_TRY(hipMemcpyAsync(st, h->stamps, sizeof st, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    for (int k = 0; k < N_STAMPS && k < FW_KT_N; k++) out->merge_phase_cycles[k] = (int64_t)st[k];
     if (!h->timer) return FW_OK;
     EvTimer* t = static_cast<EvTimer*>(h->timer);
     HIP_TRY(t->resolve());

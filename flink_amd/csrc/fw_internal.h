@@ -28,7 +28,7 @@ constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw)
 
 // ---- merge/fire (K4+K5): one 1024-thread workgroup per superbucket
 constexpr int MG_BLOCK = 1024;
-constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a time per pending push
+constexpr int MG_CELL_GROUP = 512;              // cells (chunks) scanned at a time per pending push
 // LDS slice-state capacity (entries) per superbucket by accumulator words
 constexpr int mg_entries(int nw) { return nw <= 1 ? 4096 : nw <= 4 ? 2048 : 1024; }
 
@@ -187,6 +187,12 @@ struct IngestArgs {
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
 constexpr int AB_NO_SORT = 2;    // skip rank/scan/cells; store partials at their row position
 constexpr int AB_NO_STORE = 4;   // skip the partial stores
+constexpr int AB_M_NO_GATHER = 8;    // merge: skip reading/merging the pending partials
+constexpr int AB_M_NO_FIRE = 16;     // merge: skip the fire rounds
+constexpr int AB_M_NO_WB = 32;       // merge: skip the state write-back
+constexpr int AB_M_NO_LOAD = 64;     // merge: skip loading the state into LDS
+constexpr int AB_STAMPS = 128;       // merge: accumulate per-phase s_memtime cycles (diagnostic)
+constexpr int N_STAMPS = 8;
 
 struct MergeArgs {
     Ctrl* ctrl;
@@ -216,7 +222,8 @@ struct MergeArgs {
     int64_t out_cap;         // overflow rows
     int64_t wm;              // watermark of this advance
     int32_t force_flush;     // prepareCheckpoint: flush, no timers
-    int32_t pad;
+    int32_t ablate;          // development only (FW_ABLATE)
+    unsigned long long* stamps;  // [N_STAMPS] phase cycles summed over workgroups (AB_STAMPS)
 };
 
 struct CompactArgs {

@@ -91,8 +91,13 @@ __device__ __forceinline__ uint32_t fold_slot(uint32_t m, int64_t s, int slots) 
     const uint32_t h = (m ^ ((uint32_t)s * 0x9E3779B1u) ^ (uint32_t)((uint64_t)s >> 32)) * 0x85EBCA6Bu;
     return (h ^ (h >> 15)) & (uint32_t)(slots - 1);
 }
+// LDS state-table index hash of a (key, slice): 32-bit multiply-xorshift (build-internal)
 __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
-    return (uint32_t)(mix64((uint64_t)k * 0xD6E8FEB86659FD93ull + (uint64_t)s) >> 17);
+    uint32_t h = (uint32_t)k * 0x9E3779B1u ^ (uint32_t)((uint64_t)k >> 32) * 0x85EBCA77u;
+    h ^= ((uint32_t)s * 0xC2B2AE3Du) ^ (uint32_t)((uint64_t)s >> 32);
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    return h ^ (h >> 13);
 }
 
 // ======================================================================================
@@ -483,6 +488,8 @@ struct StateLds {
     int64_t slice[E];
     uint32_t flag[E];
     uint64_t acc[NW][E];
+    uint16_t due[E];       // entries whose timer is due at this watermark (each fires once)
+    int32_t ndue;
     int32_t n;             // entries in use
     uint32_t overflow;
 };
@@ -544,6 +551,17 @@ __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const Wo
     }
     S.overflow = 1;
     return -1;
+}
+
+// register an event-time timer on entry e; a timer that is already due at this watermark joins
+// the due list (an entry's timer fires at most once per advance: its timestamp is its slice end)
+template <int NW, int E>
+__device__ __forceinline__ void set_timer(StateLds<NW, E>& S, int e, int64_t W) {
+    const uint32_t old = atomicOr(&S.flag[e], F_TIMER);
+    if (!(old & F_TIMER) && is_fired(S.slice[e], W)) {
+        const int q = atomicAdd(&S.ndue, 1);
+        if (q < E) S.due[q] = (uint16_t)e;
+    }
 }
 
 // Emission is atomic-free at device scope: each superbucket appends to its own output slab
@@ -641,7 +659,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
             emit_row<NW>(a, sb, s_emit, k, we, acc);
             // nextTriggerWindow: register windowEnd + sliceSize while the window is non-empty
             const int e3 = find_or_insert(S, k, wadd(we, w.interval), wd);
-            if (e3 >= 0) atomicOr(&S.flag[e3], F_TIMER);
+            if (e3 >= 0) set_timer(S, e3, a.wm);
         }
         // clearWindow: expiredSlices = [windowStart + sliceSize]
         const int e2 = find_entry(S, k, wadd(wsub(we, w.size), w.interval));
@@ -675,7 +693,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
     const int64_t last = wadd(ws, w.size);
     if (!(next > last)) {
         const int e3 = find_or_insert(S, k, next, wd);
-        if (e3 >= 0) atomicOr(&S.flag[e3], F_TIMER);
+        if (e3 >= 0) set_timer(S, e3, a.wm);
     }
     // clearWindow (CumulativeSliceAssigner.expiredSlices)
     if (we == first) {
@@ -685,6 +703,29 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
         if (we == last && ef >= 0) atomicAnd(&S.flag[ef], ~F_ACC);
     }
 }
+
+// diagnostic phase stamps (FW_ABLATE & AB_STAMPS): lane 0 sums cycles per phase
+struct Stamps {
+    bool on;
+    uint64_t t;
+    uint64_t acc[N_STAMPS];
+    __device__ void init(bool enable) {
+        on = enable;
+        for (int i = 0; i < N_STAMPS; i++) acc[i] = 0;
+        if (on) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void mark(int phase) {  // call right after a __syncthreads()
+        if (!on) return;
+        const uint64_t n = __builtin_amdgcn_s_memtime();
+        acc[phase] += n - t;
+        t = n;
+    }
+    __device__ void flush(unsigned long long* dst) {
+        if (!on || threadIdx.x != 0 || !dst) return;
+        for (int i = 0; i < N_STAMPS; i++)
+            if (acc[i]) atomicAdd(&dst[i], (unsigned long long)acc[i]);
+    }
+};
 
 // XCD-aware superbucket order: blocks b, b+8, b+16, ... are dealt to one XCD (round robin,
 // speed only), so they get consecutive superbuckets, whose cells sit next to each other in
@@ -727,6 +768,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     const int64_t w_old = cur;
     const int32_t n0 = a.state_count[sb];
 
+    Stamps stm;
+    stm.init((a.ablate & AB_STAMPS) != 0);
     if (tid == 0) {
         s_work = (ntreq > 0) || do_flush || (do_fire && is_fired(a.sb_min_timer[sb], W));
         s_fired = 0;
@@ -737,12 +780,12 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         // ---- load this superbucket's entries into LDS
         for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
         if (tid == 0) {
-            S.n = n0;
+            S.n = (a.ablate & AB_M_NO_LOAD) ? 0 : n0;
             S.overflow = 0;
         }
         __syncthreads();
         const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
-        for (int e = tid; e < n0; e += MG_BLOCK) {
+        if (!(a.ablate & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
             const uint64_t* p = st + (size_t)e * PWE;
             const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
             S.key[e] = k;
@@ -760,6 +803,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             }
         }
         __syncthreads();
+        stm.mark(0);
         // ---- timers registered by late records in processElement
         for (int64_t r = tid; r < ntreq; r += MG_BLOCK) {
             if (a.treq[3 * r + 2] != sb) continue;
@@ -767,7 +811,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
         }
         // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket
-        if (do_flush) {
+        if (do_flush && !(a.ablate & AB_M_NO_GATHER)) {
             for (int64_t pi = 0; pi < pend; pi++) {
                 const int nch = a.slot_nch[pi];
                 const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
@@ -777,51 +821,86 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     const uint32_t v = tid < ng ? cl[g0 + tid] : 0u;
                     uint32_t total;
                     const uint32_t incl = block_incl_scan<MG_BLOCK>(v >> 16, wsum, &total);
-                    s_cb[tid + 1] = incl;
-                    s_src[tid] = (uint32_t)(g0 + tid) * CH + (v & 0xFFFFu);
+                    if (tid < MG_CELL_GROUP) {
+                        s_cb[tid + 1] = incl;
+                        s_src[tid] = (uint32_t)(g0 + tid) * CH + (v & 0xFFFFu);
+                    }
                     if (tid == 0) s_cb[0] = 0;
                     __syncthreads();
-                    for (uint32_t r = tid; r < total; r += MG_BLOCK) {
-                        int lo = 0, hi = ng;  // s_cb[lo] <= r < s_cb[hi]
-                        while (hi - lo > 1) {
-                            const int mid = (lo + hi) >> 1;
-                            if (s_cb[mid] <= r) lo = mid; else hi = mid;
-                        }
-                        const uint64_t* p = seg + (size_t)(s_src[lo] + (r - s_cb[lo])) * PW;
-                        const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
-                        const int e = find_or_insert(S, k, s, a.wd);
-                        if (e < 0) continue;
+                    constexpr int U = 4;  // rows in flight per thread
+                    for (uint32_t r0 = tid; r0 < total; r0 += U * MG_BLOCK) {
+                        uint64_t row[U][PW];
+                        static_for<U>([&](auto UU) {
+                            constexpr int u = decltype(UU)::value;
+                            const uint32_t r = r0 + u * MG_BLOCK;
+                            if (r >= total) return;
+                            int lo = 0, hi = ng;  // s_cb[lo] <= r < s_cb[hi]
+                            while (hi - lo > 1) {
+                                const int mid = (lo + hi) >> 1;
+                                if (s_cb[mid] <= r) lo = mid; else hi = mid;
+                            }
+                            const uint64_t* p = seg + (size_t)(s_src[lo] + (r - s_cb[lo])) * PW;
 #pragma unroll
-                        for (int w = 0; w < NW; w++)
-                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], p[2 + w]);
-                        // register the window timer unless already fired (AggCombiner.java:103-110)
-                        atomicOr(&S.flag[e], is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER));
+                            for (int w = 0; w < PW; w++) row[u][w] = p[w];
+                        });
+                        static_for<U>([&](auto UU) {
+                            constexpr int u = decltype(UU)::value;
+                            if (r0 + u * MG_BLOCK >= total) return;
+                            const int64_t k = (int64_t)row[u][0], s = (int64_t)row[u][1];
+                            const int e = find_or_insert(S, k, s, a.wd);
+                            if (e < 0) return;
+#pragma unroll
+                            for (int w = 0; w < NW; w++)
+                                if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
+                            // register the window timer unless already fired (AggCombiner.java:103-110)
+                            atomicOr(&S.flag[e], is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER));
+                        });
                     }
                     __syncthreads();
                 }
             }
         }
         __syncthreads();
+        stm.mark(1);
         // ---- fire: InternalTimerServiceImpl.tryAdvanceWatermark, timestamp order
-        if (do_fire) {
+        if (do_fire && !(a.ablate & AB_M_NO_FIRE)) {
+            // due list: entries whose timer fires at W (dense work for the rounds below)
+            if (tid == 0) S.ndue = 0;
+            __syncthreads();
+            const int n = min(S.n, E);
+            for (int e = tid; e < n; e += MG_BLOCK)
+                if ((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W)) {
+                    const int q = atomicAdd(&S.ndue, 1);
+                    S.due[q] = (uint16_t)e;
+                }
+            __syncthreads();
+            stm.mark(6);
+            // rounds in timestamp order (per key the reference fires windows in order, and a
+            // fired HOP/CUMULATE window can register the next one); keys are independent
             for (;;) {
                 if (tid == 0) s_vmin = INT64_MAX;
                 __syncthreads();
-                const int n = min(S.n, E);
-                for (int e = tid; e < n; e += MG_BLOCK)
-                    if ((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W))
-                        __hip_atomic_fetch_min(&s_vmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
+                const int nd = min(S.ndue, E);
+                for (int q = tid; q < nd; q += MG_BLOCK) {
+                    const int e = S.due[q];
+                    if (S.flag[e] & F_TIMER) __hip_atomic_fetch_min(&s_vmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
+                }
                 __syncthreads();
+                stm.mark(4);
                 const int64_t v = s_vmin;
                 if (v == INT64_MAX) break;
-                for (int e = tid; e < n; e += MG_BLOCK) {
+                stm.acc[7]++;
+                for (int q = tid; q < nd; q += MG_BLOCK) {
+                    const int e = S.due[q];
                     if ((S.flag[e] & F_TIMER) && S.slice[e] == v) {
                         atomicAnd(&S.flag[e], ~F_TIMER);
                         fire_one(a, S, e, v, &s_fired, sb, &s_emit);
                     }
                 }
                 __syncthreads();
+                stm.mark(5);
             }
+            if (S.ndue > E && tid == 0) S.overflow = 1;
         }
         // ---- write back live entries
         if (tid == 0) {
@@ -829,9 +908,10 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             s_newmin = INT64_MAX;
         }
         __syncthreads();
+        stm.mark(2);
         const int n = min(S.n, E);
         uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
-        for (int e = tid; e < n; e += MG_BLOCK) {
+        if (!(a.ablate & AB_M_NO_WB)) for (int e = tid; e < n; e += MG_BLOCK) {
             const uint32_t f = S.flag[e];
             if (!(f & (F_ACC | F_TIMER))) continue;
             const int pos = atomicAdd(&s_nlive, 1);
@@ -851,6 +931,9 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             if (s_fired) a.sb_fired[sb] += s_fired;
             if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
         }
+        __syncthreads();
+        stm.mark(3);
+        stm.flush(a.stamps);
     }
 }
 

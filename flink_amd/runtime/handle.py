@@ -133,7 +133,9 @@ class WindowAggHandle:
         check(lib().fw_get_kernel_times(self._h, C.byref(t)))
         names = {abi.KT_PARTITION: "partition", abi.KT_SCAN: "scan", abi.KT_REDUCE: "reduce",
                  abi.KT_MERGE: "merge", abi.KT_OTHER: "other"}
-        return {n: (t.ms[k], t.launches[k]) for k, n in names.items()}
+        out = {n: (t.ms[k], t.launches[k]) for k, n in names.items()}
+        out["merge_phase_cycles"] = list(t.merge_phase_cycles)
+        return out
 
     # ---- checkpoint
     def snapshot(self) -> bytes:

@@ -215,6 +215,8 @@ int fw_get_stats(fw_handle* h, fw_stats* out);
 typedef struct {
     double ms[FW_KT_N];          /* accumulated device time per kernel class                 */
     int64_t launches[FW_KT_N];   /* timed launches per kernel class                          */
+    int64_t merge_phase_cycles[FW_KT_N];  /* diagnostic builds only (FW_ABLATE stamps): shader
+                                             cycles per merge phase, summed over workgroups     */
 } fw_kernel_times;
 /* enable != 0 starts timing (and resets the accumulators); 0 stops it. */
 int fw_set_profiling(fw_handle* h, int enable);

@@ -57,5 +57,57 @@ def main():
     os.environ.pop("FW_ABLATE", None)
 
 
+
+
+def merge_main(wl_name, variants, steps=12):
+    """Full push + advance loop; reports the merge kernel's average time per step."""
+    wl = bench.WORKLOADS[wl_name]
+    dev = torch.device("cuda", 0)
+    L = _native.lib()
+    zipf_t = None
+    if wl["dist"] == 1:
+        import numpy as np
+        w = 1.0 / np.power(np.arange(1, wl["keys"] + 1, dtype=np.float64), wl["zipf_s"])
+        cdf = np.cumsum(w)
+        zipf_t = torch.tensor(cdf / cdf[-1], device=dev)
+    gp, keys_total = bench.gen_params(wl, 1, zipf_t.data_ptr() if zipf_t is not None else None)
+    gk = torch.empty((steps, bench.B), dtype=torch.int64, device=dev)
+    gt, gv = torch.empty_like(gk), torch.empty_like(gk)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for b in range(steps):
+        _native.check(L.fw_generate(C.byref(gp), b * bench.B, bench.B, gk[b].data_ptr(), gt[b].data_ptr(),
+                                    gv[b].data_ptr(), s))
+    torch.cuda.synchronize()
+    out_cap = 2 * keys_total + (1 << 20)
+    cfg = bench.build_config(wl, 1, 0, keys_total, out_cap)
+    for ab in variants:
+        os.environ["FW_ABLATE"] = str(ab)
+        h = WindowAggHandle(cfg)
+        try:
+            for b in range(steps):
+                if b == 3:
+                    h.sync()
+                    h.set_profiling(True)
+                h.push_device(gk[b], gt[b], [gv[b]] if wl["value_cols"] else [])
+                h.reset_results()
+                h.advance(bench.watermark(b, wl["rate"]))
+        except _native.FlinkWinError as e:  # ablated runs may overflow the state table
+            print(json.dumps({"workload": wl_name, "ablate": ab, "error": str(e)}), flush=True)
+            h.close()
+            continue
+        kt = h.kernel_times()
+        ms, n = kt["merge"]
+        print(json.dumps({"workload": wl_name, "ablate": ab, "merge_ms_per_step": round(ms / (steps - 3), 4),
+                          "reduce_us": round(kt["reduce"][0] / kt["reduce"][1] * 1e3, 2),
+                          "phase_Mcycles": [round(x / 1e6, 1) for x in kt["merge_phase_cycles"][:7]],
+                          "rounds": kt["merge_phase_cycles"][7], "fired": h.stats()["num_fired_windows"],
+                          "errors": h.stats()["error_flags"]}), flush=True)
+        h.close()
+    os.environ.pop("FW_ABLATE", None)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "merge":
+        merge_main(sys.argv[2], [int(x) for x in sys.argv[3].split(",")])
+    else:
+        main()

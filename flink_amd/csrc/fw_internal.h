@@ -20,6 +20,8 @@ constexpr int IG_SRPT = 2;                      // rows per thread per fold sub-
 constexpr int IG_SUB = IG_BLOCK * IG_SRPT;      // rows per fold sub-tile (1024)
 constexpr int IG_LDS = 78 * 1024;               // dynamic LDS per workgroup: histogram + fold/stage area
 constexpr int IG_MAX_SB = 8192;                 // superbuckets the ingest histogram holds (32 KiB)
+constexpr int IG_HDR_WORDS = 16;                // 8-B words of per-chunk counters at the LDS base
+constexpr int ig_hist_words(int n_sb) { return ((n_sb + 3) >> 2) << 1; }  // 16-B multiple
 // rows per thread by accumulator words: the chunk's partials stay in registers (<= 128 VGPRs)
 constexpr int ig_rpt(int nw) { return nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
 // LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)
@@ -192,6 +194,9 @@ constexpr int AB_M_NO_FIRE = 16;     // merge: skip the fire rounds
 constexpr int AB_M_NO_WB = 32;       // merge: skip the state write-back
 constexpr int AB_M_NO_LOAD = 64;     // merge: skip loading the state into LDS
 constexpr int AB_STAMPS = 128;       // merge: accumulate per-phase s_memtime cycles (diagnostic)
+constexpr int AB_M_NO_HASH = 512;    // merge: gather loads the partials but does not insert them
+constexpr int AB_M_NO_FOLDOP = 1024; // merge: insert the partials but skip the accumulator/flag atomics
+constexpr int AB_GSTAMPS = 256;      // merge: with AB_STAMPS, phases 4/5/6 time the gather's scan/load/fold
 constexpr int N_STAMPS = 8;
 
 struct MergeArgs {

@@ -155,16 +155,17 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int PW = 2 + NW;
     constexpr int SL = ig_slots(NW);
     static_assert(RPT % IG_SRPT == 0, "fold sub-tiles must tile the chunk");
-    __shared__ uint32_t wsum[IG_BLOCK / 64];
-    __shared__ int64_t s_min;
-    __shared__ uint64_t s_drop;
-    __shared__ uint64_t s_rows;
-    // dynamic LDS: [hist: n_sb u32 (8-B aligned)][area: fold table, later the store stage]
-    extern __shared__ uint64_t lds[];
+    // dynamic LDS only (16-B aligned base, G17): [header 16 words][hist: n_sb u32, padded to
+    // 16 B][area: fold table, later the store stage]
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    int64_t* s_min = (int64_t*)&lds[0];
+    unsigned long long* s_drop = (unsigned long long*)&lds[1];
+    unsigned long long* s_rows = (unsigned long long*)&lds[2];
+    uint32_t* wsum = (uint32_t*)&lds[4];  // IG_BLOCK / 64 words
     const int n_sb = a.ks.n_sb;
-    uint32_t* hist = (uint32_t*)lds;  // partials per superbucket -> cell start
-    uint64_t* area = lds + ((n_sb + 1) >> 1);
-    const int area_words = (a.lds_bytes >> 3) - ((n_sb + 1) >> 1);
+    uint32_t* hist = (uint32_t*)(lds + IG_HDR_WORDS);  // partials per superbucket -> cell start
+    uint64_t* area = lds + IG_HDR_WORDS + ig_hist_words(n_sb);
+    const int area_words = (a.lds_bytes >> 3) - IG_HDR_WORDS - ig_hist_words(n_sb);
     uint32_t* claim = (uint32_t*)area;                   // [SL]
     int64_t* ckey = (int64_t*)(area + (SL >> 1));       // [SL]
     int64_t* cslice = ckey + SL;                         // [SL]
@@ -181,9 +182,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     }
     const int64_t cur_wm = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
     if (tid == 0) {
-        s_min = INT64_MAX;
-        s_drop = 0;
-        s_rows = 0;
+        *s_min = INT64_MAX;
+        *s_drop = 0;
+        *s_rows = 0;
     }
     for (int s = tid; s < n_sb; s += IG_BLOCK) hist[s] = 0;
 
@@ -373,14 +374,14 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             }
         }
     // ---- control counters (reduced into the control block by k_push_stats)
-    if (lmin != INT64_MAX) __hip_atomic_fetch_min(&s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
-    if (ldrop) atomicAdd((unsigned long long*)&s_drop, (unsigned long long)ldrop);
-    if (lrows) atomicAdd((unsigned long long*)&s_rows, (unsigned long long)lrows);
+    if (lmin != INT64_MAX) __hip_atomic_fetch_min(s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
+    if (ldrop) atomicAdd(s_drop, (unsigned long long)ldrop);
+    if (lrows) atomicAdd(s_rows, (unsigned long long)lrows);
     __syncthreads();
     if (tid == 0) {
-        a.chunk_stats[4 * c] = s_min;
-        a.chunk_stats[4 * c + 1] = (int64_t)s_drop;
-        a.chunk_stats[4 * c + 2] = (int64_t)s_rows;
+        a.chunk_stats[4 * c] = *s_min;
+        a.chunk_stats[4 * c + 1] = (int64_t)*s_drop;
+        a.chunk_stats[4 * c + 2] = (int64_t)*s_rows;
         a.chunk_stats[4 * c + 3] = (int64_t)total;
     }
 }
@@ -502,12 +503,19 @@ __device__ __forceinline__ void init_entry_acc(StateLds<NW, E>& S, int e, const 
     for (int w = 0; w < NW; w++) S.acc[w][e] = w < wd.nw ? word_identity(wd.op[w]) : 0;
 }
 
+// LDS publication protocol of the index: the inserting lane writes the entry's fields, then
+// (after a compiler barrier) the index word with a relaxed store.  LDS executes one wave's
+// requests in issue order and a reader's field loads depend on the index value it read, so a
+// reader that sees 2+e sees the fields.  Acquire/release orderings are not used: at workgroup
+// scope they also order global memory, making every publish wait for earlier result stores.
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
 template <int NW, int E>
 __device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
     constexpr uint32_t MASK = 2 * E - 1;
     uint32_t h = index_hash(k, s) & MASK;
     for (int probes = 0; probes < 2 * E;) {
-        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_ACQUIRE, LDS_SCOPE);
+        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_RELAXED, LDS_SCOPE);
         if (st == 0) return -1;
         if (st == 1) continue;  // being inserted by another lane: re-read
         const uint32_t e = st - 2;
@@ -518,12 +526,15 @@ __device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
     return -1;
 }
 
+// Finds (k, s) or inserts it.  A new entry starts from `v` folded into the identity (or the
+// identity when v is null) with flags `flag0`; *inserted tells the caller it must not fold v again.
 template <int NW, int E>
-__device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd) {
+__device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd,
+                              const uint64_t* v = nullptr, uint32_t flag0 = 0, bool* inserted = nullptr) {
     constexpr uint32_t MASK = 2 * E - 1;
     uint32_t h = index_hash(k, s) & MASK;
     for (int probes = 0; probes < 2 * E;) {
-        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_ACQUIRE, LDS_SCOPE);
+        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_RELAXED, LDS_SCOPE);
         if (st == 1) continue;
         if (st == 0) {
             uint32_t expect = 0;
@@ -532,14 +543,20 @@ __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const Wo
                 const int e = atomicAdd(&S.n, 1);
                 if (e >= E) {
                     S.overflow = 1;
-                    __hip_atomic_store(&S.idx[h], IDX_DEAD, __ATOMIC_RELEASE, LDS_SCOPE);
+                    __hip_atomic_store(&S.idx[h], IDX_DEAD, __ATOMIC_RELAXED, LDS_SCOPE);
                     return -1;
                 }
                 S.key[e] = k;
                 S.slice[e] = s;
-                S.flag[e] = 0;
-                init_entry_acc(S, e, wd);
-                __hip_atomic_store(&S.idx[h], 2u + (uint32_t)e, __ATOMIC_RELEASE, LDS_SCOPE);
+                S.flag[e] = flag0;
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    S.acc[w][e] = w < wd.nw ? (v ? reg_fold(wd.op[w], word_identity(wd.op[w]), v[w])
+                                                 : word_identity(wd.op[w]))
+                                            : 0;
+                compiler_fence();
+                __hip_atomic_store(&S.idx[h], 2u + (uint32_t)e, __ATOMIC_RELAXED, LDS_SCOPE);
+                if (inserted) *inserted = true;
                 return e;
             }
             continue;  // lost the race: re-read this slot
@@ -551,6 +568,30 @@ __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const Wo
     }
     S.overflow = 1;
     return -1;
+}
+
+// First-probe lookups of M (key, slice) pairs with their LDS loads issued together (the lookups
+// of one lane are independent; issuing them back to back overlaps their latencies).  e[j] is the
+// entry, -1 when the home slot is empty, -2 when the first probe does not decide (collision or
+// an insertion in flight): the caller then takes the probing path.
+template <int NW, int E, int M>
+__device__ __forceinline__ void probe_batch(StateLds<NW, E>& S, const int64_t* k, const int64_t* s, int* e) {
+    constexpr uint32_t MASK = 2 * E - 1;
+    uint32_t st[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) st[j] = __hip_atomic_load(&S.idx[index_hash(k[j], s[j]) & MASK], __ATOMIC_RELAXED, LDS_SCOPE);
+    int64_t kk[M], ss[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        const uint32_t ei = min(st[j] - 2u, (uint32_t)(E - 1));
+        kk[j] = S.key[ei];
+        ss[j] = S.slice[ei];
+    }
+#pragma unroll
+    for (int j = 0; j < M; j++)
+        e[j] = st[j] == 0 ? -1
+               : (st[j] >= 2 && st[j] - 2 < (uint32_t)E && kk[j] == k[j] && ss[j] == s[j]) ? (int)(st[j] - 2)
+                                                                                          : -2;
 }
 
 // register an event-time timer on entry e; a timer that is already due at this watermark joins
@@ -643,16 +684,35 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
         return;
     }
     if (w.kind == FW_WIN_HOP) {
-        // mergeSlices with a null target: fold the n slices ending at we, newest first
+        // mergeSlices with a null target: fold the n slices ending at we, newest first; the
+        // lookups go in batches of HB with their first probes issued together
+        constexpr int HB = NW <= 2 ? 8 : NW <= 4 ? 4 : 2;
+        const int n = w.n_slices;
+        const int64_t s_exp = wadd(wsub(we, w.size), w.interval);  // clearWindow's expired slice
+        int e_exp = -3;
         int64_t s = we;
-        for (int j = 0; j < w.n_slices; j++) {
-            const int e2 = find_entry(S, k, s);
-            if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
+        for (int j0 = 0; j0 < n; j0 += HB) {
+            int64_t kk[HB], ss[HB];
+            int eb[HB];
 #pragma unroll
-                for (int i = 0; i < NW; i++)
-                    if (i < wd.nw) acc[i] = reg_fold(wd.op[i], acc[i], S.acc[i][e2]);
+            for (int j = 0; j < HB; j++) {
+                kk[j] = k;
+                ss[j] = s;
+                s = wsub(s, w.interval);  // wrapping, like the reference's long arithmetic
             }
-            s = wsub(s, w.interval);
+            probe_batch<NW, E, HB>(S, kk, ss, eb);
+#pragma unroll
+            for (int j = 0; j < HB; j++) {
+                if (j0 + j >= n) break;
+                int e2 = eb[j];
+                if (e2 == -2) e2 = find_entry(S, k, ss[j]);
+                if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
+#pragma unroll
+                    for (int i = 0; i < NW; i++)
+                        if (i < wd.nw) acc[i] = reg_fold(wd.op[i], acc[i], S.acc[i][e2]);
+                }
+                if (ss[j] == s_exp) e_exp = e2;
+            }
         }
         nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
         if (nonempty) {
@@ -662,7 +722,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
             if (e3 >= 0) set_timer(S, e3, a.wm);
         }
         // clearWindow: expiredSlices = [windowStart + sliceSize]
-        const int e2 = find_entry(S, k, wadd(wsub(we, w.size), w.interval));
+        const int e2 = e_exp != -3 ? e_exp : find_entry(S, k, s_exp);
         if (e2 >= 0) atomicAnd(&S.flag[e2], ~F_ACC);
         return;
     }
@@ -742,7 +802,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int CH = IG_BLOCK * ig_rpt(NW);  // chunk rows of the ingest kernel that wrote the cells
     __shared__ StateLds<NW, E> S;
     __shared__ uint32_t s_cb[MG_CELL_GROUP + 1];  // flat prefix of the cell counts of a cell group
-    __shared__ uint32_t s_src[MG_CELL_GROUP];     // first row of each cell inside the push's slot
+    __shared__ uint16_t s_start[MG_CELL_GROUP];   // first row of each cell inside its chunk region
     __shared__ uint32_t wsum[MG_BLOCK / 64];
     __shared__ int32_t s_work;
     __shared__ int64_t s_vmin;
@@ -770,6 +830,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
 
     Stamps stm;
     stm.init((a.ablate & AB_STAMPS) != 0);
+    const bool gdet = (a.ablate & AB_GSTAMPS) != 0;
     if (tid == 0) {
         s_work = (ntreq > 0) || do_flush || (do_fire && is_fired(a.sb_min_timer[sb], W));
         s_fired = 0;
@@ -812,52 +873,102 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         }
         // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket
         if (do_flush && !(a.ablate & AB_M_NO_GATHER)) {
-            for (int64_t pi = 0; pi < pend; pi++) {
-                const int nch = a.slot_nch[pi];
-                const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
-                const uint32_t* cl = a.cells + ((size_t)pi * a.n_sb + sb) * a.max_nch;
-                for (int g0 = 0; g0 < nch; g0 += MG_CELL_GROUP) {
-                    const int ng = min(MG_CELL_GROUP, nch - g0);
-                    const uint32_t v = tid < ng ? cl[g0 + tid] : 0u;
-                    uint32_t total;
-                    const uint32_t incl = block_incl_scan<MG_BLOCK>(v >> 16, wsum, &total);
-                    if (tid < MG_CELL_GROUP) {
-                        s_cb[tid + 1] = incl;
-                        s_src[tid] = (uint32_t)(g0 + tid) * CH + (v & 0xFFFFu);
-                    }
-                    if (tid == 0) s_cb[0] = 0;
-                    __syncthreads();
-                    constexpr int U = 4;  // rows in flight per thread
-                    for (uint32_t r0 = tid; r0 < total; r0 += U * MG_BLOCK) {
-                        uint64_t row[U][PW];
-                        static_for<U>([&](auto UU) {
-                            constexpr int u = decltype(UU)::value;
-                            const uint32_t r = r0 + u * MG_BLOCK;
-                            if (r >= total) return;
-                            int lo = 0, hi = ng;  // s_cb[lo] <= r < s_cb[hi]
-                            while (hi - lo > 1) {
-                                const int mid = (lo + hi) >> 1;
-                                if (s_cb[mid] <= r) lo = mid; else hi = mid;
-                            }
-                            const uint64_t* p = seg + (size_t)(s_src[lo] + (r - s_cb[lo])) * PW;
-#pragma unroll
-                            for (int w = 0; w < PW; w++) row[u][w] = p[w];
-                        });
-                        static_for<U>([&](auto UU) {
-                            constexpr int u = decltype(UU)::value;
-                            if (r0 + u * MG_BLOCK >= total) return;
-                            const int64_t k = (int64_t)row[u][0], s = (int64_t)row[u][1];
-                            const int e = find_or_insert(S, k, s, a.wd);
-                            if (e < 0) return;
-#pragma unroll
-                            for (int w = 0; w < NW; w++)
-                                if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
-                            // register the window timer unless already fired (AggCombiner.java:103-110)
-                            atomicOr(&S.flag[e], is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER));
-                        });
-                    }
-                    __syncthreads();
+            // cell groups of all pending pushes as one flat sequence; the next group's cell words
+            // are loaded while the current group is folded
+            int n_groups = 0;
+            for (int64_t pi = 0; pi < pend; pi++) n_groups += (a.slot_nch[pi] + MG_CELL_GROUP - 1) / MG_CELL_GROUP;
+            auto cell_word = [&](int k, int& pi_out, int& g0_out, int& ng_out) -> uint32_t {
+                int pi = 0;
+                for (;;) {
+                    const int ngp = (a.slot_nch[pi] + MG_CELL_GROUP - 1) / MG_CELL_GROUP;
+                    if (k < ngp) break;
+                    k -= ngp;
+                    pi++;
                 }
+                pi_out = pi;
+                g0_out = k * MG_CELL_GROUP;
+                ng_out = min(MG_CELL_GROUP, a.slot_nch[pi] - g0_out);
+                const uint32_t* cl = a.cells + ((size_t)pi * a.n_sb + sb) * a.max_nch;
+                return tid < ng_out ? cl[g0_out + tid] : 0u;
+            };
+            int pi_n = 0, g0_n = 0, ng_n = 0;
+            uint32_t v_n = n_groups > 0 ? cell_word(0, pi_n, g0_n, ng_n) : 0u;
+            for (int k = 0; k < n_groups; k++) {
+                const int pi = pi_n, g0 = g0_n, ng = ng_n;
+                const uint32_t v = v_n;
+                if (k + 1 < n_groups) v_n = cell_word(k + 1, pi_n, g0_n, ng_n);
+                const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
+                uint32_t total;
+                const uint32_t incl = block_incl_scan<MG_BLOCK>(v >> 16, wsum, &total);
+                if (tid < MG_CELL_GROUP) {
+                    s_cb[tid + 1] = incl;
+                    s_start[tid] = (uint16_t)(v & 0xFFFFu);
+                }
+                if (tid == 0) s_cb[0] = 0;
+                __syncthreads();
+                if (gdet) stm.mark(4);
+                const int top = 1 << (31 - __builtin_clz((unsigned)ng));  // highest power of two <= ng
+                constexpr int U = NW <= 2 ? 4 : NW <= 4 ? 2 : 1;  // rows in flight per thread (VGPR budget)
+                for (uint32_t r0 = tid; r0 < total; r0 += U * MG_BLOCK) {
+                    // cell of each row: s_cb[lo] <= r < s_cb[lo + 1], the U searches advance together
+                    int lo[U];
+                    uint32_t rr[U];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        lo[u] = 0;
+                        rr[u] = min(r0 + u * MG_BLOCK, total - 1);
+                    }
+                    for (int step = top; step > 0; step >>= 1) {
+#pragma unroll
+                        for (int u = 0; u < U; u++) {
+                            const int c = lo[u] + step;
+                            if (c < ng && s_cb[c] <= rr[u]) lo[u] = c;
+                        }
+                    }
+                    uint64_t row[U][PW];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const uint64_t* p =
+                            seg + ((size_t)(g0 + lo[u]) * CH + s_start[lo[u]] + (rr[u] - s_cb[lo[u]])) * PW;
+#pragma unroll
+                        for (int w = 0; w < PW; w++) row[u][w] = p[w];
+                    }
+                    if (gdet) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        stm.mark(5);
+                    }
+                    int ge[U];
+                    if (!(a.ablate & AB_M_NO_HASH)) {
+                        int64_t gk[U], gs[U];
+#pragma unroll
+                        for (int u = 0; u < U; u++) {
+                            gk[u] = (int64_t)row[u][0];
+                            gs[u] = (int64_t)row[u][1];
+                        }
+                        probe_batch<NW, E, U>(S, gk, gs, ge);
+                    }
+                    static_for<U>([&](auto UU) {
+                        constexpr int u = decltype(UU)::value;
+                        if (r0 + u * MG_BLOCK >= total) return;
+                        const int64_t k = (int64_t)row[u][0], s = (int64_t)row[u][1];
+                        if (a.ablate & AB_M_NO_HASH) {
+                            if (k == -7 && s == -7) S.overflow = 1;  // keeps the loads live
+                            return;
+                        }
+                        // register the window timer unless already fired (AggCombiner.java:103-110)
+                        const uint32_t fl = is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER);
+                        int e = ge[u];
+                        bool ins = false;
+                        if (e < 0) e = find_or_insert(S, k, s, a.wd, &row[u][2], fl, &ins);
+                        if (e < 0 || ins || (a.ablate & AB_M_NO_FOLDOP)) return;
+#pragma unroll
+                        for (int w = 0; w < NW; w++)
+                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
+                        atomicOr(&S.flag[e], fl);
+                    });
+                }
+                __syncthreads();
+                if (gdet) stm.mark(6);
             }
         }
         __syncthreads();
@@ -874,7 +985,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     S.due[q] = (uint16_t)e;
                 }
             __syncthreads();
-            stm.mark(6);
+            if (!gdet) stm.mark(6);
             // rounds in timestamp order (per key the reference fires windows in order, and a
             // fired HOP/CUMULATE window can register the next one); keys are independent
             for (;;) {
@@ -886,7 +997,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     if (S.flag[e] & F_TIMER) __hip_atomic_fetch_min(&s_vmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
                 }
                 __syncthreads();
-                stm.mark(4);
+                if (!gdet) stm.mark(4);
                 const int64_t v = s_vmin;
                 if (v == INT64_MAX) break;
                 stm.acc[7]++;
@@ -898,7 +1009,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     }
                 }
                 __syncthreads();
-                stm.mark(5);
+                if (!gdet) stm.mark(5);
             }
             if (S.ndue > E && tid == 0) S.overflow = 1;
         }
@@ -1003,7 +1114,7 @@ static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
         attr_set = true;
     }
     // the fold table and the histogram must fit the dynamic LDS
-    if ((int64_t)((a.ks.n_sb + 1) / 2) * 8 + ig_fold_bytes(NW) > a.lds_bytes) return hipErrorInvalidValue;
+    if ((int64_t)(IG_HDR_WORDS + ig_hist_words(a.ks.n_sb)) * 8 + ig_fold_bytes(NW) > a.lds_bytes) return hipErrorInvalidValue;
     kt_mark(t, FW_KT_REDUCE, false, s);
     hipLaunchKernelGGL((k_ingest<NV, NW, RPT>), dim3((unsigned)nch), dim3(IG_BLOCK), a.lds_bytes, s, a);
     kt_mark(t, FW_KT_REDUCE, true, s);

@@ -66,7 +66,9 @@ def build_config(wl, world, rank, keys_total, out_cap):
         count_star_index=wl["count_star"],
         value_col_types=[abi.TYPE_NAMES[t] for t in wl["value_cols"]],
         key_hash=abi.KEYHASH_BINROW_BIGINT, max_parallelism=128, parallelism=world,
-        subtask_index=rank, state_capacity=int(keys_total * wl["state_per_key"]),
+        subtask_index=rank,
+        # this subtask's share of the keys (key-group range), with headroom for shard imbalance
+        state_capacity=int(keys_total * wl["state_per_key"] / world * (1.0 if world == 1 else 1.25)),
         max_batch_rows=2 * B, output_capacity=out_cap)
 
 
@@ -109,7 +111,11 @@ def main():
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-sample", type=int, default=B, help="events for the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary (tools/traffic.py); default: newest profiles/r*/traffic_<workload>.json")
+    ap.add_argument("--calibrate-traffic", action="store_true",
+                    help="launch fw_assign_key_groups over 2^28 keys before timing: a known-byte "
+                         "8-B/lane read (2 GiB) + 4-B/lane write (1 GiB) that calibrates FETCH_SIZE/WRITE_SIZE")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -150,43 +156,18 @@ def main():
         _native.check(L.fw_generate(C.byref(gp), i0, B, gk[b].data_ptr(), gt[b].data_ptr(), gv[b].data_ptr(), s))
     torch.cuda.synchronize(dev)
 
-    # ---------------- keyBy exchange (N > 1) ----------------------------------------------
-    ws_bytes = L.fw_partition_workspace_bytes(B, world)
-    workspace = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
-    pk = torch.empty(B, dtype=torch.int64, device=dev)
-    pt = torch.empty_like(pk)
-    pv = torch.empty_like(pk)
-    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    # ---------------- keyBy exchange (N > 1): device partition + RCCL all-to-all ------------
+    from flink_amd.runtime.exchange import KeyByExchange
+    ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
 
     def exchange(b):
         if world == 1:
             return gk[b], gt[b], gv[b]
-        vin = (C.c_void_p * abi.FW_MAX_COLS)(gv[b].data_ptr())
-        vout = (C.c_void_p * abi.FW_MAX_COLS)(pv.data_ptr())
-        _native.check(L.fw_partition_by_dest(gk[b].data_ptr(), gt[b].data_ptr(), vin, 1, B, abi.KEYHASH_BINROW_BIGINT,
-                                             128, world, pk.data_ptr(), pt.data_ptr(), vout, counts.data_ptr(),
-                                             workspace.data_ptr(), workspace.numel(), torch.cuda.current_stream(dev).cuda_stream))
-        rc = torch.empty_like(counts)
-        dist.all_to_all_single(rc, counts)
-        send = counts.tolist()
-        recv = rc.tolist()
-        n = sum(recv)
-        rk = torch.empty(n, dtype=torch.int64, device=dev)
-        rt = torch.empty_like(rk)
-        rv = torch.empty_like(rk)
-        dist.all_to_all_single(rk, pk, recv, send)
-        dist.all_to_all_single(rt, pt, recv, send)
-        if nv:
-            dist.all_to_all_single(rv, pv, recv, send)
-        return rk, rt, rv
+        k, t, v = ex.exchange(gk[b], gt[b], [gv[b]] if nv else [])
+        return k, t, (v[0] if nv else None)
 
     def global_watermark(b):
-        w = watermark(b, wl["rate"])
-        if world > 1:  # StatusWatermarkValve: min over input channels
-            t = torch.tensor([w], dtype=torch.int64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            return int(t.item())
-        return w
+        return ex.global_watermark(watermark(b, wl["rate"]))
 
     out_cap = 2 * keys_total // world + (1 << 20)
     if wl["window"][0] == "CUMULATE":
@@ -199,6 +180,17 @@ def main():
             handle.push_device(k, t, [v] if nv else [])
             handle.reset_results()       # blackhole sink: results of the previous watermark consumed
             handle.advance(wm)
+
+    if args.calibrate_traffic:
+        # same access width as k_ingest's column loads (global_load_dwordx2 per lane), sized far
+        # past the 256 MiB Infinity Cache so every byte comes from HBM
+        nc = 1 << 28
+        ck = torch.zeros(nc, dtype=torch.int64, device=dev)
+        cd = torch.empty(nc, dtype=torch.int32, device=dev)
+        _native.check(L.fw_assign_key_groups(ck.data_ptr(), None, nc, abi.KEYHASH_LONG, 128, 8,
+                                             None, cd.data_ptr(), s))
+        torch.cuda.synchronize(dev)
+        del ck, cd
 
     cfg = build_config(wl, world, rank, keys_total, out_cap)
     # warmup on its own operator instance (first batches of the same stream)
@@ -243,13 +235,15 @@ def main():
     avg_reduce_s = red_ms / red_n / 1e3
     achieved = bytes_per_launch / avg_reduce_s / 1e9
     traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("workload") == args.workload:
-                traffic = tj.get("k_ingest_bytes_per_launch")
-        except Exception:
-            traffic = None
+    tpath = args.traffic_json
+    if tpath is None:
+        import glob
+        found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{args.workload}.json")))
+        tpath = found[-1] if found else ""
+    if tpath and os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if tj.get("workload") == args.workload:
+            traffic = tj.get("k_ingest_hbm_bytes_per_launch")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -58,6 +58,7 @@ def lib():
         "fw_partition_workspace_bytes": (i64, [i64, i32]),
         "fw_generate": (i32, [P(abi.fw_gen_params), i64, i64, vp, vp, vp, vp]),
         "fw_host_key_group": (i32, [i32, i64, i32, i32]),
+        "fw_host_assign_key_groups": (i32, [vp, vp, i64, i32, i32, i32, vp, vp]),
         "fw_host_window_start": (i64, [i64, i64, i64]),
         "fw_host_next_trigger_watermark": (i64, [i64, i64]),
     }
@@ -77,7 +78,7 @@ EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_ge
             "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_workspace_bytes",
-            "fw_generate", "fw_host_key_group", "fw_host_window_start",
+            "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
             "fw_host_next_trigger_watermark"]
 
 

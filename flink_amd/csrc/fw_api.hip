@@ -867,6 +867,17 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
 int32_t fw_host_key_group(int32_t key_hash_kind, int64_t key, int32_t precomputed_hash, int32_t max_parallelism) {
     return key_group_for_hash(java_key_hash(key_hash_kind, key, precomputed_hash), max_parallelism);
 }
+int fw_host_assign_key_groups(const int64_t* key, const int32_t* key_hash, int64_t n, int32_t key_hash_kind,
+                              int32_t max_parallelism, int32_t parallelism, int32_t* kg, int32_t* dest) {
+    if (n < 0 || (n > 0 && !key) || max_parallelism <= 0 || parallelism <= 0 || parallelism > max_parallelism)
+        return fail(FW_E_INVALID, "fw_host_assign_key_groups: bad arguments");
+    for (int64_t i = 0; i < n; i++) {
+        const int32_t g = key_group_for_hash(java_key_hash(key_hash_kind, key[i], key_hash ? key_hash[i] : 0), max_parallelism);
+        if (kg) kg[i] = g;
+        if (dest) dest[i] = operator_for_key_group(max_parallelism, parallelism, g);
+    }
+    return FW_OK;
+}
 int64_t fw_host_window_start(int64_t ts, int64_t offset, int64_t size) {
     return window_start(ts, offset, make_udiv((uint64_t)size));
 }

@@ -1,0 +1,94 @@
+"""keyBy exchange between operator subtasks, one rank per GPU.
+
+Replaces the reference's record routing + network shuffle for a keyed window operator:
+KeyGroupStreamPartitioner.selectChannel (flink-runtime/.../streaming/runtime/partitioner/
+KeyGroupStreamPartitioner.java:55-65, destination = computeOperatorIndexForKeyGroup(maxP, p,
+assignToKeyGroup(key)), KeyGroupRangeAssignment.java:63-127) followed by
+ChannelSelectorRecordWriter.emit (flink-runtime/.../io/network/api/writer/
+ChannelSelectorRecordWriter.java:54) over Netty, and the receiving side's
+StatusWatermarkValve.inputWatermark (min over input channels, StatusWatermarkValve.java:153).
+
+Here a columnar batch is counting-sorted by destination subtask, then moved with one
+all-to-all per column (RCCL over xGMI for device batches; gloo for host batches).  Partitioning
+runs where the batch lives: device batches on the GPU (fw_partition_by_dest), host-staged
+batches with the library's host routine (fw_host_assign_key_groups) - the reference routes
+records on the sending task's CPU too.  Both use the same key-group code the kernels run.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import abi
+from .._native import check, lib
+
+
+class KeyByExchange:
+    def __init__(self, key_hash_kind, max_parallelism=128, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.kind = key_hash_kind
+        self.max_p = max_parallelism
+        self._ws = None
+
+    # ---- routing ------------------------------------------------------------------------
+    def partition(self, key, ts, values):
+        """Rows grouped by destination subtask (ascending).  Returns (key, ts, values, counts)
+        with counts[d] = rows for subtask d; stable within a destination."""
+        p = self.world
+        if key.is_cuda:
+            return self._partition_device(key, ts, values)
+        n = key.numel()
+        dest = np.empty(n, dtype=np.int32)
+        kn = np.ascontiguousarray(key.numpy())
+        check(lib().fw_host_assign_key_groups(kn.ctypes.data, None, n, self.kind, self.max_p, p,
+                                              None, dest.ctypes.data))
+        order = torch.from_numpy(np.argsort(dest, kind="stable"))
+        counts = torch.from_numpy(np.bincount(dest, minlength=p).astype(np.int64))
+        return key[order], ts[order], [v[order] for v in values], counts
+
+    def _partition_device(self, key, ts, values):
+        p, n, dev = self.world, key.numel(), key.device
+        L = lib()
+        ws = L.fw_partition_workspace_bytes(n, p)
+        if self._ws is None or self._ws.numel() < ws or self._ws.device != dev:
+            self._ws = torch.empty(max(ws, 256), dtype=torch.uint8, device=dev)
+        pk, pt = torch.empty_like(key), torch.empty_like(ts)
+        pv = [torch.empty_like(v) for v in values]
+        counts = torch.empty(p, dtype=torch.int64, device=dev)
+        vin = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in values])
+        vout = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in pv])
+        check(L.fw_partition_by_dest(key.data_ptr(), ts.data_ptr(), vin, len(values), n, self.kind,
+                                     self.max_p, p, pk.data_ptr(), pt.data_ptr(), vout, counts.data_ptr(),
+                                     self._ws.data_ptr(), self._ws.numel(),
+                                     torch.cuda.current_stream(dev).cuda_stream))
+        return pk, pt, pv, counts
+
+    # ---- exchange -----------------------------------------------------------------------
+    def exchange(self, key, ts, values):
+        """Send every row to the subtask owning its key group; returns this subtask's rows
+        (grouped by source rank, each source's rows in their partitioned order)."""
+        if self.world == 1:
+            return key, ts, list(values)
+        pk, pt, pv, counts = self.partition(key, ts, values)
+        rc = torch.empty_like(counts)
+        dist.all_to_all_single(rc, counts, group=self.group)
+        send, recv = counts.tolist(), rc.tolist()
+        n = sum(recv)
+        out = []
+        for col in [pk, pt] + pv:
+            r = torch.empty(n, dtype=col.dtype, device=col.device)
+            dist.all_to_all_single(r, col, recv, send, group=self.group)
+            out.append(r)
+        return out[0], out[1], out[2:]
+
+    def global_watermark(self, w):
+        """StatusWatermarkValve: the combined watermark is the min over all input channels."""
+        if self.world == 1:
+            return int(w)
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([int(w)], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())

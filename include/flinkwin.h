@@ -263,6 +263,10 @@ int fw_generate(const fw_gen_params* gp, int64_t i0, int64_t n, int64_t* d_key, 
 /* ---- host-side restatements (no device use): the same code the kernels run -------------- */
 /* KeyGroupRangeAssignment.assignToKeyGroup on key.hashCode() as fw_key_hash_kind defines it. */
 int32_t fw_host_key_group(int32_t key_hash_kind, int64_t key, int32_t precomputed_hash, int32_t max_parallelism);
+/* Vector form for host-resident batches (the Java-side partitioner of host-staged records):
+   kg[i] / dest[i] as fw_assign_key_groups computes them on the device. Either output may be NULL. */
+int fw_host_assign_key_groups(const int64_t* key, const int32_t* key_hash, int64_t n, int32_t key_hash_kind,
+                              int32_t max_parallelism, int32_t parallelism, int32_t* kg, int32_t* dest);
 /* TimeWindow.getWindowStartWithOffset (FR/streaming/api/windowing/windows/TimeWindow.java:264). */
 int64_t fw_host_window_start(int64_t ts, int64_t offset, int64_t size);
 /* TimeWindowUtil.getNextTriggerWatermark, UTC (TR/util/TimeWindowUtil.java:186). */

@@ -1,0 +1,118 @@
+"""N > 1 path on CPU: world-size-2 `gloo` run of the keyBy exchange (flink_amd/runtime/exchange.py).
+
+Each rank is one operator subtask (parallelism 2, maxParallelism 128).  It generates its slice
+of every global batch (the bench's layout), routes rows to the owner of their key group through
+KeyByExchange (host partitioner + all_to_all_single), min-reduces the watermark
+(StatusWatermarkValve), and feeds a per-subtask operator.  Every batch is routed through the
+exchange, so the test checks three things:
+  * every received row belongs to this subtask's key-group range
+    (KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex, :93-106);
+  * no row is lost or duplicated;
+  * the union of the two subtasks' window results equals one unsharded operator's results.
+The per-subtask operator here is the CPU oracle: this test covers the exchange and the
+key-group sharding on CPU.  The GPU operator behind the same sharding is covered by
+test_gpu_parity.py::test_sharded_subtasks_match_unsharded_oracle.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from flink_amd import abi
+
+WORLD = 2
+T0 = 1_600_000_000_000
+
+
+def _stream(rank, batch, n):
+    rng = np.random.default_rng(1000 * batch + rank)
+    k = rng.integers(0, 4000, n).astype(np.int64)
+    t = (T0 + batch * 3000 + rng.integers(-2500, 3000, n)).astype(np.int64)
+    v = rng.integers(-10**6, 10**6, n).astype(np.int64)
+    return k, t, v
+
+
+def _cfg(parallelism, subtask):
+    return abi.make_config(window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000, count_star_index=0,
+                           aggs=[(abi.AGG_COUNT_STAR, 0, abi.T_I64), (abi.AGG_SUM, 0, abi.T_I64),
+                                 (abi.AGG_MAX, 0, abi.T_I64)],
+                           value_col_types=[abi.T_I64], key_hash=abi.KEYHASH_BINROW_BIGINT,
+                           max_parallelism=128, parallelism=parallelism, subtask_index=subtask)
+
+
+def _rows(r):
+    return sorted(zip(r["key"].tolist(), r["window_end"].tolist(), *[v.tolist() for v in r["values"]]))
+
+
+def _worker(rank, port, n_batches, n, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from flink_amd.runtime.exchange import KeyByExchange
+        from oracle.oracle import OracleOperator, key_group, key_group_range
+
+        ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+        lo, hi = key_group_range(128, WORLD, rank)
+        op = OracleOperator(_cfg(WORLD, rank))
+        rows, received = [], 0
+        for b in range(n_batches):
+            k, t, v = _stream(rank, b, n)
+            rk, rt, rv = ex.exchange(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)])
+            received += rk.numel()
+            kgs = {key_group(abi.KEYHASH_BINROW_BIGINT, int(x), 128) for x in np.unique(rk.numpy())}
+            assert all(lo <= g <= hi for g in kgs), f"rank {rank}: foreign key group"
+            op.process_batch(rk.numpy(), rt.numpy(), [rv[0].numpy()])
+            # ranks propose different watermarks; the valve takes the min
+            wm = ex.global_watermark(T0 + b * 3000 - 3000 + 500 * rank)
+            assert wm == T0 + b * 3000 - 3000
+            op.process_watermark(wm)
+            rows += _rows(op.results())
+        op.process_watermark(T0 + n_batches * 3000 + 60000)
+        rows += _rows(op.results())
+        out_q.put((rank, received, rows, op.late_dropped))
+        op.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_gloo_two_subtasks_union_equals_unsharded():
+    from oracle.oracle import OracleOperator
+
+    n_batches, n = 8, 3000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, n_batches, n, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert sum(r[1] for r in res) == WORLD * n_batches * n  # nothing lost or duplicated
+    got = sorted(row for r in res for row in r[2])
+
+    # one unsharded subtask over the same global stream and watermarks
+    op = OracleOperator(_cfg(1, 0))
+    want = []
+    for b in range(n_batches):
+        cols = [_stream(r, b, n) for r in range(WORLD)]
+        op.process_batch(*[np.concatenate([c[i] for c in cols]) for i in (0, 1)], [np.concatenate([c[2] for c in cols])])
+        op.process_watermark(T0 + b * 3000 - 3000)
+        want += _rows(op.results())
+    op.process_watermark(T0 + n_batches * 3000 + 60000)
+    want += _rows(op.results())
+    assert sum(r[3] for r in res) == op.late_dropped
+    assert len(got) > 1000 and got == sorted(want)
+    op.close()

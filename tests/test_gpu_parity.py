@@ -229,3 +229,140 @@ def test_device_key_groups_match_oracle():
         want = np.array([O.key_group(kind, int(x), 128) for x in keys])
         assert np.array_equal(kg.cpu().numpy(), want)
         assert np.array_equal(dest.cpu().numpy(), want * 8 // 128)
+
+
+# ------------------------------------------------------------------------------------------
+# key-group sharding: p subtasks on one device behind the device partitioner
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("p", [2, 4])
+def test_sharded_subtasks_match_unsharded_oracle(p):
+    """The N > 1 data path minus the collective: fw_partition_by_dest routes every batch to p
+    subtask handles (parallelism p, subtask i owns computeKeyGroupRangeForOperatorIndex(128, p, i));
+    the union of their window results equals one unsharded oracle operator, and no handle sees a
+    foreign key group (ERR_KEYGROUP would be raised)."""
+    torch = _torch_cuda()
+    from flink_amd.runtime.exchange import KeyByExchange
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = dict(window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000, count_star_index=0,
+              aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MIN, 1, F64)])
+    cfgs = [_cfg(kw, key_hash=abi.KEYHASH_BINROW_BIGINT, parallelism=p, subtask_index=i) for i in range(p)]
+    o = OracleOperator(_cfg(kw, key_hash=abi.KEYHASH_BINROW_BIGINT))
+    hs = [WindowAggHandle(c) for c in cfgs]
+    ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+    ex.world = p  # route for p subtasks; the all-to-all is replaced by slicing on one device
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(21, 60000, 2000, ooo=3000, step_ms=1500, n_wm=20)):
+        vals = [iv, dv.view(np.int64)]
+        o.process_batch(k, t, vals)
+        dk, dt = torch.tensor(k, device="cuda"), torch.tensor(t, device="cuda")
+        dvs = [torch.tensor(v, device="cuda") for v in vals]
+        pk, pt, pv, counts = ex.partition(dk, dt, dvs)
+        off = 0
+        for i, c in enumerate(counts.tolist()):
+            if c:
+                hs[i].push_device(pk[off:off + c], pt[off:off + c], [v[off:off + c] for v in pv])
+            off += c
+        o.process_watermark(wm)
+        got = []
+        for h in hs:
+            h.advance(wm)
+            got += _rows(h.results(reset=True), cfgs[0], {2})
+        _compare(sorted(got), _rows(o.results(clear=True), cfgs[0], {2}), {2}, f"p={p} batch {bi}")
+    assert sum(h.stats()["num_late_records_dropped"] for h in hs) == o.late_dropped
+    assert all(h.stats()["error_flags"] == 0 for h in hs)
+    for h in hs:
+        h.close()
+
+
+# ------------------------------------------------------------------------------------------
+# BASELINE-sized streams: the bench workloads at full batch size (2^22 events per watermark),
+# checked on a key subset against the oracle (window results of a key depend only on that
+# key's records, so the oracle replays only the subset) plus size-independent properties
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("wl_name", ["cfg2", "cfg3", "cfg4", "cfg5"])
+def test_bench_workload_full_size_key_subset(wl_name):
+    torch = _torch_cuda()
+    import ctypes as C
+    import bench
+    from flink_amd import _native
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    wl = bench.WORKLOADS[wl_name]
+    steps, B, MOD, PICK = 6, bench.B, 97, 13
+    L = _native.lib()
+    zipf_t = None
+    if wl["dist"] == 1:
+        w = 1.0 / np.power(np.arange(1, wl["keys"] + 1, dtype=np.float64), wl["zipf_s"])
+        cdf = np.cumsum(w)
+        zipf_t = torch.tensor(cdf / cdf[-1], device="cuda")
+    gp, keys_total = bench.gen_params(wl, 1, zipf_t.data_ptr() if zipf_t is not None else None)
+    cfg = bench.build_config(wl, 1, 0, keys_total, 8 * keys_total + (1 << 20))
+    g, o = WindowAggHandle(cfg), OracleOperator(cfg)
+    k = torch.empty(B, dtype=torch.int64, device="cuda")
+    t, v = torch.empty_like(k), torch.empty_like(k)
+    s = torch.cuda.current_stream().cuda_stream
+    got, want, n_sub = [], [], 0
+    total_rows = 0
+    count_sum = 0
+    cs = wl["count_star"]
+    for b in range(steps + 1):
+        wm = bench.watermark(b, wl["rate"])
+        if b == steps:  # last: fire every window (CUMULATE: a few more steps; its 1 h windows
+            wm = bench.T0 + 10**9 if wl["window"][0] != "CUMULATE" else wm + 120_000  # emit every step)
+        if b < steps:
+            _native.check(L.fw_generate(C.byref(gp), b * B, B, k.data_ptr(), t.data_ptr(), v.data_ptr(), s))
+            g.push_device(k, t, [v] if cfg.n_value_cols else [])
+            m = (k % MOD) == PICK
+            hk, ht, hv = k[m].cpu().numpy(), t[m].cpu().numpy(), v[m].cpu().numpy()
+            n_sub += len(hk)
+            o.process_batch(hk, ht, [hv] if cfg.n_value_cols else [])
+        g.advance(wm)
+        o.process_watermark(wm)
+        r = g.results(reset=True)
+        total_rows += len(r["key"])
+        if cs >= 0:
+            count_sum += int(r["values"][cs].sum())
+        sel = (r["key"] % MOD) == PICK
+        sub = {"key": r["key"][sel], "window_start": r["window_start"][sel], "window_end": r["window_end"][sel],
+               "values": [x[sel] for x in r["values"]], "null_mask": r["null_mask"][sel]}
+        dcols = {a for a, (kk, c, ty) in enumerate(wl["aggs"]) if ty == "DOUBLE"}
+        got_b, want_b = _rows(sub, cfg, dcols), _rows(o.results(clear=True), cfg, dcols)
+        _compare(got_b, want_b, dcols, f"{wl_name} step {b}")
+        got += got_b
+    st = g.stats()
+    assert st["error_flags"] == 0 and st["num_late_records_dropped"] == 0 == o.late_dropped
+    assert n_sub > 1000 and len(got) > 100 and total_rows > len(got)
+    kind = wl["window"][0]
+    if kind == "HOP" and cs >= 0:       # every event is counted in size/slide windows
+        assert count_sum == steps * B * (wl["window"][1] // wl["window"][2])
+    g.close()
+
+
+# ------------------------------------------------------------------------------------------
+# edge cases of the reference's tests: empty batches and watermarks with nothing to fire,
+# a single record, and a batch larger than max_batch_rows (split into pushes)
+# ------------------------------------------------------------------------------------------
+def test_empty_and_tiny_batches_and_oversized_push():
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = CASES["sql_cumulate_countstar"]
+    cfg = _cfg(kw, max_batch_rows=4096)
+    g, o = WindowAggHandle(cfg), OracleOperator(cfg)
+    rng = np.random.default_rng(9)
+    t0 = 1_600_000_000_000
+    plan = [0, 1, 0, 10000, 3, 0, 25000]
+    for bi, n in enumerate(plan):
+        k = rng.integers(0, 50, n).astype(np.int64)
+        t = (t0 + bi * 2000 + rng.integers(-1000, 2000, n)).astype(np.int64)
+        vals = [rng.integers(-5, 5, n).astype(np.int64), rng.random(n).view(np.int64)]
+        g.push_host(k, t, vals)
+        o.process_batch(k, t, vals)
+        wm = t0 + bi * 2000 - 1
+        g.advance(wm)
+        o.process_watermark(wm)
+        _compare(_rows(g.results(reset=True), cfg, set()), _rows(o.results(clear=True), cfg, set()), set(), f"batch {bi}")
+    g.advance(t0 + 10**7)
+    o.process_watermark(t0 + 10**7)
+    _compare(_rows(g.results(reset=True), cfg, set()), _rows(o.results(clear=True), cfg, set()), set(), "final")
+    assert g.stats()["num_late_records_dropped"] == o.late_dropped
+    g.close()

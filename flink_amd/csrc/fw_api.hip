@@ -133,7 +133,8 @@ struct fw_handle {
 
     Ctrl* ctrl = nullptr;
     uint64_t* parts = nullptr;
-    uint32_t* cells = nullptr;   // [FW_MAX_PENDING][n_sb][max_nch]
+    int64_t cell_cols = 0;       // cell_pad(max_nch): cells per superbucket per slot
+    uint32_t* cells = nullptr;   // [FW_MAX_PENDING][cell_cols / 16][n_sb][16] (cell_index)
     int32_t* slot_nch = nullptr;  // [FW_MAX_PENDING]
     int64_t* treq = nullptr;
     int64_t treq_cap = 0;
@@ -334,6 +335,7 @@ int validate_and_plan(fw_handle* h) {
     h->chunk_rows = (int64_t)IG_BLOCK * ig_rpt(h->nw_t);
     h->cap_rows = ((c.max_batch_rows + h->chunk_rows - 1) / h->chunk_rows) * h->chunk_rows;
     h->max_nch = h->cap_rows / h->chunk_rows;
+    h->cell_cols = cell_pad(h->max_nch);
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     h->out_cap = c.output_capacity;
     h->slab_cap = std::max<int64_t>(64, (2 * c.output_capacity + ks.n_sb - 1) / ks.n_sb);
@@ -357,7 +359,7 @@ int allocate(fw_handle* h) {
     const int PW = 2 + h->nw_t, PWE = 3 + h->nw_t;
     if ((rc = dalloc(&h->ctrl, 1))) return rc;
     if ((rc = dalloc(&h->parts, (size_t)FW_MAX_PENDING * h->cap_rows * PW))) return rc;
-    if ((rc = dalloc(&h->cells, (size_t)FW_MAX_PENDING * h->ks.n_sb * h->max_nch))) return rc;
+    if ((rc = dalloc(&h->cells, (size_t)FW_MAX_PENDING * h->ks.n_sb * h->cell_cols))) return rc;
     if ((rc = dalloc(&h->slot_nch, FW_MAX_PENDING))) return rc;
     if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
     if ((rc = dalloc(&h->state, (size_t)h->ks.n_sb * h->cap_e * PWE))) return rc;
@@ -431,7 +433,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.parts = h->parts;
     a.cells = h->cells;
     a.slot_nch = h->slot_nch;
-    a.max_nch = h->max_nch;
+    a.max_nch = h->cell_cols;
     a.cap_rows = h->cap_rows;
     a.treq = h->treq;
     a.state = h->state;
@@ -494,7 +496,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.cap_rows = h->cap_rows;
         a.cells = h->cells;
         a.slot_nch = h->slot_nch;
-        a.max_nch = h->max_nch;
+        a.max_nch = h->cell_cols;
         a.chunk_stats = h->chunk_stats;
         a.n_chunks = (m + h->chunk_rows - 1) / h->chunk_rows;
         a.treq = h->treq;

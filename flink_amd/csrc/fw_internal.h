@@ -34,6 +34,24 @@ constexpr int MG_CELL_GROUP = 512;              // cells (chunks) scanned at a t
 // LDS slice-state capacity (entries) per superbucket by accumulator words
 constexpr int mg_entries(int nw) { return nw <= 1 ? 4096 : nw <= 4 ? 2048 : 1024; }
 
+// ---- cell table tiling.  A cell word (start | count << 16) is written once per (chunk,
+// superbucket) by the ingest workgroup of that chunk.  16 cells share one 64-B line, and the 16
+// chunks of a line are ones the dispatcher deals to the same XCD at about the same time
+// (blocks c, c+8, ..., c+120 of a 128-block group), so their 4-B stores merge in that XCD's L2
+// into one full-line write instead of 16 partial-sector writes.  Per slot the table is
+// [tile][n_sb][16]; the merge kernel reads a superbucket's cells as whole lines.
+constexpr int CELL_LANES = 16;
+__host__ __device__ constexpr int64_t cell_pad(int64_t nch) { return (nch + 127) / 128 * 128; }
+__host__ __device__ inline size_t cell_index(int64_t c, int64_t n_sb, int64_t sb) {
+    const int64_t tile = (c >> 7) * 8 + (c & 7);
+    return ((size_t)tile * n_sb + sb) * CELL_LANES + ((c >> 3) & 15);
+}
+// flat cell position f (= tile * 16 + lane) -> chunk; inverse of cell_index's (tile, lane)
+__host__ __device__ inline int64_t cell_chunk(int64_t f) {
+    const int64_t tile = f >> 4;
+    return (tile >> 3) * 128 + (tile & 7) + 8 * (f & 15);
+}
+
 // Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words.
 enum WordOp : int32_t {
     W_CNT = 0,    // += 1                       COUNT(*), COUNT(col), AVG count
@@ -175,10 +193,10 @@ struct IngestArgs {
     uint64_t* parts;       // partial buffer: FW_MAX_PENDING slots of cap_rows * (2 + nw) words;
                            // chunk c owns rows [c*CH, (c+1)*CH) of its slot, sorted by superbucket
     int64_t cap_rows;      // rows per slot (>= rows of one push)
-    uint32_t* cells;       // [FW_MAX_PENDING][n_sb][max_nch]: start | count << 16 of each
-                           // (superbucket, chunk) cell inside the chunk's region
+    uint32_t* cells;       // [FW_MAX_PENDING][max_nch / 16][n_sb][16] (cell_index): start | count << 16
+                           // of each (superbucket, chunk) cell inside the chunk's region
     int32_t* slot_nch;     // [FW_MAX_PENDING] chunks of each pending push
-    int64_t max_nch;
+    int64_t max_nch;       // cell_pad(chunks per slot): cells per superbucket per slot
     int64_t* chunk_stats;  // [n_chunks][3]: min target slice, dropped rows, accepted rows
     int64_t n_chunks;
     int64_t* treq;         // timer requests: (key, window, sb) triples

@@ -112,8 +112,8 @@ __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
 // registers.  The surviving partials are then ranked per superbucket with LDS atomics, the
 // per-superbucket counts are scanned, and every partial is stored at
 //     parts[slot][c*CH + start(sb) + rank]
-// so each (superbucket, chunk) cell is contiguous.  The cell table cells[slot][sb][chunk]
-// (start | count << 16) tells the merge kernel where its rows are: no count pass, no global
+// so each (superbucket, chunk) cell is contiguous.  The cell table (cell_index: XCD-tiled
+// [slot][chunk/16][sb][16], start | count << 16) tells the merge kernel where its rows are: no count pass, no global
 // scan, one launch per push (+ a one-block stats reduce).
 // Restates AbstractSliceSyncStateWindowAggProcessor.processElement (:96-126: slice assignment,
 // late drop / late merge + timer), RecordsWindowBuffer.addElement (:81, grouping by
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         rdst[j] = (sort && (valid & (1u << j))) ? atomicAdd(&hist[rsb[j]], 1u) : (uint32_t)(j * IG_BLOCK + tid);
     });
     __syncthreads();
-    uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch + c;
+    uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch;
     const int per = (n_sb + IG_BLOCK - 1) / IG_BLOCK;
     const int sb0 = min(tid * per, n_sb), sb1 = min(sb0 + per, n_sb);
     uint32_t seg = 0;
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         for (int i = sb0; i < sb1; i++) {
             const uint32_t v = hist[i];
             hist[i] = run;
-            cells[(size_t)i * a.max_nch] = run | (v << 16);
+            cells[cell_index(c, n_sb, i)] = run | (v << 16);
             run += v;
         }
     __syncthreads();
@@ -876,20 +876,25 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             // cell groups of all pending pushes as one flat sequence; the next group's cell words
             // are loaded while the current group is folded
             int n_groups = 0;
-            for (int64_t pi = 0; pi < pend; pi++) n_groups += (a.slot_nch[pi] + MG_CELL_GROUP - 1) / MG_CELL_GROUP;
+            // cells are enumerated in flat tile order f (cell_chunk(f) is the chunk); padding
+            // positions past the push's last chunk count as empty
+            for (int64_t pi = 0; pi < pend; pi++)
+                n_groups += (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
             auto cell_word = [&](int k, int& pi_out, int& g0_out, int& ng_out) -> uint32_t {
                 int pi = 0;
                 for (;;) {
-                    const int ngp = (a.slot_nch[pi] + MG_CELL_GROUP - 1) / MG_CELL_GROUP;
+                    const int ngp = (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
                     if (k < ngp) break;
                     k -= ngp;
                     pi++;
                 }
                 pi_out = pi;
                 g0_out = k * MG_CELL_GROUP;
-                ng_out = min(MG_CELL_GROUP, a.slot_nch[pi] - g0_out);
-                const uint32_t* cl = a.cells + ((size_t)pi * a.n_sb + sb) * a.max_nch;
-                return tid < ng_out ? cl[g0_out + tid] : 0u;
+                ng_out = min(MG_CELL_GROUP, (int)cell_pad(a.slot_nch[pi]) - g0_out);
+                const int64_t f = g0_out + tid;
+                if (tid >= ng_out || cell_chunk(f) >= a.slot_nch[pi]) return 0u;
+                const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
+                return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
             };
             int pi_n = 0, g0_n = 0, ng_n = 0;
             uint32_t v_n = n_groups > 0 ? cell_word(0, pi_n, g0_n, ng_n) : 0u;
@@ -929,7 +934,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         const uint64_t* p =
-                            seg + ((size_t)(g0 + lo[u]) * CH + s_start[lo[u]] + (rr[u] - s_cb[lo[u]])) * PW;
+                            seg + ((size_t)cell_chunk(g0 + lo[u]) * CH + s_start[lo[u]] + (rr[u] - s_cb[lo[u]])) * PW;
 #pragma unroll
                         for (int w = 0; w < PW; w++) row[u][w] = p[w];
                     }

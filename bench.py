@@ -117,6 +117,10 @@ def main():
                     help="launch fw_assign_key_groups over 2^28 keys before timing: a known-byte "
                          "8-B/lane read (2 GiB) + 4-B/lane write (1 GiB) that calibrates FETCH_SIZE/WRITE_SIZE")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
+                         "one-GPU box: ranks share the GPUs round robin and the exchange is staged "
+                         "through host memory; never used for reported numbers")
     args = ap.parse_args()
 
     import torch
@@ -127,10 +131,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.dist_backend == "nccl":
+        gpu = local
+    else:  # rehearsal only: several ranks may share one GPU
+        gpu = local % torch.cuda.device_count()
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from flink_amd import _native, abi
     from flink_amd.runtime.handle import WindowAggHandle
@@ -214,7 +225,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     st = h.stats()
@@ -261,7 +272,9 @@ def main():
             "data": "synthetic (SplitMix64 Nexmark-shaped generator, seed 42, device-resident)",
             "config": {"workload": f"{args.workload}: {wl['desc']}", "events_per_gpu_per_step": B,
                        "keys_total": keys_total, "rate_per_gpu_ev_s": wl["rate"],
-                       "parallelism": f"key-group sharded x{world}" + (" + RCCL all-to-all" if world > 1 else ""),
+                       "parallelism": f"key-group sharded x{world}" + (
+                           "" if world == 1 else " + RCCL all-to-all" if args.dist_backend == "nccl"
+                           else " + gloo all-to-all (rehearsal, shared GPU)"),
                        "max_parallelism": 128, "superbuckets": st["num_superbuckets"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,

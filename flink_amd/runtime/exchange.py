@@ -73,15 +73,21 @@ class KeyByExchange:
         if self.world == 1:
             return key, ts, list(values)
         pk, pt, pv, counts = self.partition(key, ts, values)
+        # gloo moves host tensors only: device batches are staged through host memory (used to
+        # rehearse the N > 1 path on one GPU; RCCL moves device memory directly over xGMI)
+        stage = key.is_cuda and dist.get_backend(self.group) != "nccl"
+        cols = [pk, pt] + pv
+        if stage:
+            counts, cols = counts.cpu(), [c.cpu() for c in cols]
         rc = torch.empty_like(counts)
         dist.all_to_all_single(rc, counts, group=self.group)
         send, recv = counts.tolist(), rc.tolist()
         n = sum(recv)
         out = []
-        for col in [pk, pt] + pv:
+        for col in cols:
             r = torch.empty(n, dtype=col.dtype, device=col.device)
             dist.all_to_all_single(r, col, recv, send, group=self.group)
-            out.append(r)
+            out.append(r.to(key.device) if stage else r)
         return out[0], out[1], out[2:]
 
     def global_watermark(self, w):

@@ -53,6 +53,8 @@ def lib():
         "fw_get_kernel_times": (i32, [vp, P(abi.fw_kernel_times)]),
         "fw_snapshot": (i32, [vp, vp, i64, P(i64)]),
         "fw_restore": (i32, [vp, vp, i64]),
+        "fw_snapshot_key_group": (i32, [vp, i32, vp, i64, P(i64)]),
+        "fw_restore_key_group": (i32, [vp, vp, i64]),
         "fw_assign_key_groups": (i32, [vp, vp, i64, i32, i32, i32, vp, vp, vp]),
         "fw_partition_by_dest": (i32, [vp, vp, vp, i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp]),
         "fw_partition_workspace_bytes": (i64, [i64, i32]),
@@ -76,7 +78,7 @@ def lib():
 EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
             "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_advance",
             "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_set_profiling",
-            "fw_get_kernel_times", "fw_snapshot", "fw_restore",
+            "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
             "fw_host_next_trigger_watermark"]

@@ -865,6 +865,118 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     return FW_OK;
 }
 
+// ---- key-group-partitioned checkpoint (rescaling) --------------------------------------
+// The heap backend writes keyed state per key group (HeapSnapshotStrategy.java:97 ->
+// AbstractStateTableSnapshot.writeStateInKeyGroup :112) and a rescaled job hands every new
+// subtask the key groups of its computeKeyGroupRangeForOperatorIndex range.  The blob of one key
+// group is therefore independent of this build's superbucket split: entries carry the sub-bucket
+// they came from, and a restoring handle re-routes every key with the same route_key the
+// ingest kernel runs (only a precomputed-hash key cannot be re-hashed; it keeps its sub-bucket
+// bits, which works for any target split not finer than the source's).
+struct KgHeader {
+    uint64_t magic;
+    int32_t version, key_group, pwe, nw, sb_log2, hash_kind;
+    int64_t win_size, win_interval, cur, n;
+};
+static const uint64_t KG_MAGIC = 0x464c4b574b473031ull;  // "FLKWKG01"
+
+int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t capacity, int64_t* size) {
+    if (!h || !size) return fail(FW_E_INVALID, "null argument");
+    const KeySpace& ks = h->ks;
+    const int li = key_group - ks.kg_start;
+    if (li < 0 || li >= ks.n_kg) return fail(FW_E_INVALID, "key group %d is not owned by this subtask", key_group);
+    int rc = force_flush(h);  // prepareSnapshotPreBarrier -> windowBuffer.flush()
+    if (rc) return rc;
+    Ctrl c;
+    if ((rc = read_ctrl(h, &c))) return rc;
+    const int L = ks.sb_per_kg_log2, nsub = 1 << L, pwe = 3 + h->nw_t;
+    std::vector<int32_t> cnt(nsub);
+    HIP_TRY(hipMemcpy(cnt.data(), h->state_count + ((size_t)li << L), sizeof(int32_t) * nsub, hipMemcpyDeviceToHost));
+    int64_t total = 0;
+    for (int q = 0; q < nsub; q++) total += cnt[q];
+    const int64_t need = (int64_t)sizeof(KgHeader) + total * pwe * 8;
+    *size = need;
+    if (!buf) return FW_OK;
+    if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
+    KgHeader hd{KG_MAGIC, 1, key_group, pwe, h->wd.nw, L, ks.hash_kind, h->win.size, h->win.interval, c.cur, total};
+    memcpy(buf, &hd, sizeof hd);
+    uint64_t* e = (uint64_t*)((char*)buf + sizeof hd);
+    for (int q = 0; q < nsub; q++) {
+        if (!cnt[q]) continue;
+        const size_t sb = ((size_t)li << L) + q;
+        HIP_TRY(hipMemcpy(e, h->state + sb * h->cap_e * pwe, (size_t)cnt[q] * pwe * 8, hipMemcpyDeviceToHost));
+        for (int i = 0; i < cnt[q]; i++) e[(size_t)i * pwe + 2] = (uint32_t)e[(size_t)i * pwe + 2] | ((uint64_t)q << 32);
+        e += (size_t)cnt[q] * pwe;
+    }
+    return FW_OK;
+}
+
+int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
+    if (!h || !buf) return fail(FW_E_INVALID, "null argument");
+    KgHeader hd;
+    if (size < (int64_t)sizeof hd) return fail(FW_E_INVALID, "key-group snapshot truncated");
+    memcpy(&hd, buf, sizeof hd);
+    const KeySpace& ks = h->ks;
+    const int pwe = 3 + h->nw_t, L = ks.sb_per_kg_log2;
+    if (hd.magic != KG_MAGIC || hd.version != 1) return fail(FW_E_INVALID, "not a key-group snapshot");
+    if (hd.pwe != pwe || hd.nw != h->wd.nw || hd.hash_kind != ks.hash_kind || hd.win_size != h->win.size ||
+        hd.win_interval != h->win.interval)
+        return fail(FW_E_INVALID, "key-group snapshot of a different operator configuration");
+    if (size < (int64_t)sizeof hd + hd.n * pwe * 8) return fail(FW_E_INVALID, "key-group snapshot truncated");
+    const int li = hd.key_group - ks.kg_start;
+    if (li < 0 || li >= ks.n_kg) return fail(FW_E_INVALID, "key group %d is not owned by this subtask", hd.key_group);
+    if (ks.hash_kind == KH_PRE && L > hd.sb_log2)
+        return fail(FW_E_INVALID, "precomputed-hash keys cannot be split finer than the snapshot's sub-buckets");
+    const uint64_t* src = (const uint64_t*)((const char*)buf + sizeof hd);
+    // target superbucket of every entry
+    const int nsub = 1 << L;
+    std::vector<std::vector<uint64_t>> per(nsub);
+    for (int64_t i = 0; i < hd.n; i++) {
+        const uint64_t* e = src + (size_t)i * pwe;
+        int sb;
+        if (ks.hash_kind == KH_PRE) {
+            sb = (li << L) + (int)((e[2] >> 32) & (uint64_t)(nsub - 1));
+        } else {
+            uint32_t m;
+            sb = route_key(ks, (int64_t)e[0], 0, &m);
+            if ((sb >> L) != li) return fail(FW_E_INVALID, "entry key does not belong to key group %d", hd.key_group);
+        }
+        auto& v = per[sb - (li << L)];
+        v.insert(v.end(), e, e + pwe);
+        v[v.size() - pwe + 2] = (uint32_t)e[2];  // flags without the source sub-bucket
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    std::vector<int32_t> cnt(nsub);
+    std::vector<int64_t> mins(nsub);
+    HIP_TRY(hipMemcpy(cnt.data(), h->state_count + ((size_t)li << L), sizeof(int32_t) * nsub, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(mins.data(), h->sb_min_timer + ((size_t)li << L), sizeof(int64_t) * nsub, hipMemcpyDeviceToHost));
+    for (int q = 0; q < nsub; q++)
+        if (cnt[q] + (int64_t)(per[q].size() / pwe) > h->cap_e)
+            return fail(FW_E_CAPACITY, "restored key group %d exceeds the state table (%lld entries per superbucket)",
+                        hd.key_group, (long long)h->cap_e);
+    int64_t added = 0;
+    for (int q = 0; q < nsub; q++) {
+        const int64_t n = (int64_t)(per[q].size() / pwe);
+        if (!n) continue;
+        const size_t sb = ((size_t)li << L) + q;
+        HIP_TRY(hipMemcpy(h->state + (sb * h->cap_e + cnt[q]) * pwe, per[q].data(), (size_t)n * pwe * 8,
+                          hipMemcpyHostToDevice));
+        for (int64_t i = 0; i < n; i++)
+            if (per[q][(size_t)i * pwe + 2] & F_TIMER) mins[q] = std::min(mins[q], (int64_t)per[q][(size_t)i * pwe + 1]);
+        cnt[q] += (int32_t)n;
+        added += n;
+    }
+    HIP_TRY(hipMemcpy(h->state_count + ((size_t)li << L), cnt.data(), sizeof(int32_t) * nsub, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(h->sb_min_timer + ((size_t)li << L), mins.data(), sizeof(int64_t) * nsub, hipMemcpyHostToDevice));
+    Ctrl c;
+    int rc = read_ctrl(h, &c);
+    if (rc) return rc;
+    c.live_entries += added;
+    c.ntp = INT64_MIN;  // next trigger recomputed at the next advance
+    HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
+    return FW_OK;
+}
+
 // ---- host-side restatements (the exact code the kernels run), for host partitioners/tests
 int32_t fw_host_key_group(int32_t key_hash_kind, int64_t key, int32_t precomputed_hash, int32_t max_parallelism) {
     return key_group_for_hash(java_key_hash(key_hash_kind, key, precomputed_hash), max_parallelism);

@@ -145,6 +145,42 @@ class WindowAggHandle:
         check(lib().fw_snapshot(self._h, buf, size.value, C.byref(size)))
         return buf.raw[:size.value]
 
+    # ---- key-group-partitioned checkpoint (rescaling)
+    def key_group_range(self):
+        """computeKeyGroupRangeForOperatorIndex(maxP, p, subtask) (KeyGroupRangeAssignment.java:93-106),
+        inclusive bounds."""
+        mp, p, i = self.cfg.max_parallelism, self.cfg.parallelism, self.cfg.subtask_index
+        return (i * mp + p - 1) // p, ((i + 1) * mp - 1) // p
+
+    def snapshot_key_groups(self):
+        """{key_group: blob} for every owned key group, plus this subtask's watermark (the entry it
+        contributes to the operator's union-list watermark state)."""
+        lo, hi = self.key_group_range()
+        out = {}
+        for kg in range(lo, hi + 1):
+            size = C.c_int64()
+            check(lib().fw_snapshot_key_group(self._h, kg, None, 0, C.byref(size)))
+            buf = C.create_string_buffer(size.value)
+            check(lib().fw_snapshot_key_group(self._h, kg, buf, size.value, C.byref(size)))
+            out[kg] = buf.raw[:size.value]
+        return out, self.stats()["current_watermark"]
+
+    def restore_key_groups(self, blobs, watermarks):
+        """Restore the owned key groups found in `blobs` ({key_group: blob}, any source parallelism);
+        the watermark becomes the min of the union list (WindowAggOperator.initializeState :183-206)."""
+        lo, hi = self.key_group_range()
+        for kg, blob in blobs.items():
+            if lo <= kg <= hi:
+                self.restore_key_group_blob(blob)
+        wms = list(watermarks)
+        if wms:
+            self.initialize_watermark(min(wms))
+
+    def restore_key_group_blob(self, blob: bytes):
+        """One key group's blob; raises if this subtask does not own it or the layout differs."""
+        buf = C.create_string_buffer(blob, len(blob))
+        check(lib().fw_restore_key_group(self._h, buf, len(blob)))
+
     def restore(self, blob: bytes):
         buf = C.create_string_buffer(blob, len(blob))
         check(lib().fw_restore(self._h, buf, len(blob)))

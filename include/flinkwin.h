@@ -229,6 +229,19 @@ int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out);
 int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size);
 int fw_restore(fw_handle* h, const void* buf, int64_t size);
 
+/* Key-group-partitioned checkpoint, for restoring at a different parallelism (rescaling).
+   fw_snapshot_key_group flushes, then serialises the live (key, slice) entries and timers of ONE
+   owned key group; buf == NULL queries *size.  Replaces the heap backend's per-key-group state
+   write (HeapSnapshotStrategy.java:97, AbstractStateTableSnapshot.writeStateInKeyGroup :112,
+   InternalTimerServiceImpl.snapshotTimersForKeyGroup :360).  fw_restore_key_group adds such a blob
+   to a handle whose key-group range (computeKeyGroupRangeForOperatorIndex, KeyGroupRangeAssignment
+   .java:93-106) contains it (InternalTimerServiceImpl.restoreTimersForKeyGroup :406).  The operator
+   watermark is union-list state restored as the min over all subtasks (WindowAggOperator.java
+   :183-206): the blob carries its handle's watermark, and the caller passes the min to
+   fw_initialize_watermark. */
+int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t capacity, int64_t* size);
+int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size);
+
 /* ---- stand-alone device kernels (partitioner, tests) ---------------------------------- */
 /* d_kg[i] = key group, d_dest[i] = computeOperatorIndexForKeyGroup(maxP, p, kg). */
 int fw_assign_key_groups(const int64_t* d_key, const int32_t* d_key_hash, int64_t n,

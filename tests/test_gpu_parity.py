@@ -274,6 +274,87 @@ def test_sharded_subtasks_match_unsharded_oracle(p):
         h.close()
 
 
+@pytest.mark.parametrize("p_from,p_to,case", [(2, 3, "sql_hop"), (4, 1, "sql_cumulate_countstar"),
+                                               (1, 2, "ds_sliding_max"), (3, 2, "sql_tumble_int_aggs")])
+def test_rescale_restore_by_key_group(p_from, p_to, case):
+    """Checkpoint at parallelism p_from, restore at p_to: every subtask writes one blob per owned
+    key group (fw_snapshot_key_group, the heap backend's writeStateInKeyGroup unit), the new
+    subtasks restore the key groups of their computeKeyGroupRangeForOperatorIndex range plus the
+    min of the union-list watermarks, and the run continues.  The union of all window results
+    equals one unsharded oracle that never restarted."""
+    torch = _torch_cuda()
+    from flink_amd.runtime.exchange import KeyByExchange
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = CASES[case]
+    dcols = _double_cols(kw)
+    kh = abi.KEYHASH_LONG if kw.get("api") == abi.API_DATASTREAM else abi.KEYHASH_BINROW_BIGINT
+    o = OracleOperator(_cfg(kw, key_hash=kh))
+
+    def handles(p):
+        cfgs = [_cfg(kw, key_hash=kh, parallelism=p, subtask_index=i) for i in range(p)]
+        return cfgs, [WindowAggHandle(c) for c in cfgs]
+
+    cfgs, hs = handles(p_from)
+    ex = KeyByExchange(kh, 128)
+    cut = 9
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(33, 48000, 1500, ooo=2500, step_ms=1200, n_wm=20)):
+        if bi == cut:  # checkpoint (flush + per-key-group state), then restart at p_to
+            blobs, wms = {}, []
+            for h in hs:
+                b, w = h.snapshot_key_groups()
+                blobs.update(b)
+                wms.append(w)
+                h.close()
+            assert sorted(blobs) == list(range(128))
+            cfgs, hs = handles(p_to)
+            for h in hs:
+                h.restore_key_groups(blobs, wms)
+        vals = [iv, dv.view(np.int64)]
+        o.process_batch(k, t, vals)
+        ex.world = len(hs)  # route for the current parallelism (slicing replaces the all-to-all)
+        dk, dt = torch.tensor(k, device="cuda"), torch.tensor(t, device="cuda")
+        pk, pt, pv, counts = ex.partition(dk, dt, [torch.tensor(v, device="cuda") for v in vals])
+        off = 0
+        for i, c in enumerate(counts.tolist()):
+            if c:
+                hs[i].push_device(pk[off:off + c], pt[off:off + c], [v[off:off + c] for v in pv])
+            off += c
+        o.process_watermark(wm)
+        got = []
+        for h in hs:
+            h.advance(wm)
+            got += _rows(h.results(reset=True), cfgs[0], dcols)
+        _compare(sorted(got), _rows(o.results(clear=True), cfgs[0], dcols), dcols,
+                 f"{case} p={p_from}->{p_to} batch {bi}")
+    assert all(h.stats()["error_flags"] == 0 for h in hs)
+    for h in hs:
+        h.close()
+
+
+def test_key_group_restore_rejects_foreign_and_mismatched_blobs():
+    _torch_cuda()
+    from flink_amd._native import FlinkWinError
+    from flink_amd.runtime.handle import WindowAggHandle
+    kw = CASES["sql_hop"]
+    a = WindowAggHandle(_cfg(kw, key_hash=abi.KEYHASH_BINROW_BIGINT, parallelism=2, subtask_index=0))
+    from flink_amd._native import lib
+    keys = np.array([k for k in range(1000) if lib().fw_host_key_group(abi.KEYHASH_BINROW_BIGINT, k, 0, 128) < 64],
+                    dtype=np.int64)  # subtask 0 of 2 owns key groups 0..63
+    n = len(keys)
+    a.push_host(keys, np.full(n, 1_600_000_000_000, np.int64), [np.ones(n, np.int64), np.ones(n, np.int64)])
+    blobs, _ = a.snapshot_key_groups()
+    assert sorted(blobs) == list(range(64))
+    b = WindowAggHandle(_cfg(kw, key_hash=abi.KEYHASH_BINROW_BIGINT, parallelism=2, subtask_index=1))
+    with pytest.raises(FlinkWinError):  # key group 0 belongs to subtask 0
+        b.restore_key_group_blob(blobs[0])
+    c = WindowAggHandle(_cfg(CASES["sql_tumble_int_aggs"], key_hash=abi.KEYHASH_BINROW_BIGINT))
+    with pytest.raises(FlinkWinError):  # different window / accumulator layout
+        c.restore_key_group_blob(blobs[0])
+    for h in (a, b, c):
+        h.close()
+
+
 # ------------------------------------------------------------------------------------------
 # BASELINE-sized streams: the bench workloads at full batch size (2^22 events per watermark),
 # checked on a key subset against the oracle (window results of a key depend only on that

@@ -215,6 +215,7 @@ constexpr int AB_STAMPS = 128;       // merge: accumulate per-phase s_memtime cy
 constexpr int AB_M_NO_HASH = 512;    // merge: gather loads the partials but does not insert them
 constexpr int AB_M_NO_FOLDOP = 1024; // merge: insert the partials but skip the accumulator/flag atomics
 constexpr int AB_GSTAMPS = 256;      // merge: with AB_STAMPS, phases 4/5/6 time the gather's scan/load/fold
+constexpr int AB_M_NO_EMIT = 4096;  // merge: fire without writing result rows (diagnostic)
 constexpr int N_STAMPS = 8;
 
 struct MergeArgs {

@@ -100,6 +100,29 @@ __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
     return h ^ (h >> 13);
 }
 
+// wave-level reductions: one LDS atomic per wave instead of one per lane (same-address LDS
+// atomics serialise lane by lane)
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, d, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
+    return v;
+}
+// slot claim for the active lanes of a wave: one atomicAdd on *ctr, each lane gets base + rank
+__device__ __forceinline__ int32_t wave_claim(int32_t* ctr) {
+    const uint64_t act = __ballot(1);
+    const int lane = __lane_id();
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const int rank = __popcll(act & ((1ull << lane) - 1ull));
+    int32_t base = 0;
+    if (lane == leader) base = atomicAdd(ctr, (int32_t)__popcll(act));
+    return __shfl(base, leader, 64) + rank;
+}
+
 // ======================================================================================
 // K1+K2+K3: single-pass ingest = slice/key-group assignment + LDS segmented reduce + a
 // chunk-local counting sort of the partials by superbucket.
@@ -611,7 +634,8 @@ __device__ __forceinline__ void set_timer(StateLds<NW, E>& S, int e, int64_t W) 
 template <int NW>
 __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
     Ctrl* c = a.ctrl;
-    const int32_t pos = atomicAdd(s_emit, 1);
+    if (a.ablate & AB_M_NO_EMIT) return;
+    const int32_t pos = wave_claim(s_emit);
     int64_t i;
     if (pos < a.slab_cap) {
         i = (int64_t)sb * a.slab_cap + pos;
@@ -662,15 +686,13 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
 }
 
 template <int NW, int E>
-__device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t we, uint32_t* fired, int sb,
-                         int32_t* s_emit) {
+__device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t we, int sb, int32_t* s_emit) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
     const int64_t k = S.key[e];
     uint64_t acc[NW];
 #pragma unroll
     for (int i = 0; i < NW; i++) acc[i] = i < wd.nw ? word_identity(wd.op[i]) : 0;
-    atomicAdd(fired, 1u);
     bool nonempty;
     if (w.kind == FW_WIN_TUMBLE) {
         // SliceUnsharedSyncStateWindowAggProcessor.fireWindow (:54-66)
@@ -986,7 +1008,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             const int n = min(S.n, E);
             for (int e = tid; e < n; e += MG_BLOCK)
                 if ((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W)) {
-                    const int q = atomicAdd(&S.ndue, 1);
+                    const int q = wave_claim(&S.ndue);
                     S.due[q] = (uint16_t)e;
                 }
             __syncthreads();
@@ -997,22 +1019,29 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                 if (tid == 0) s_vmin = INT64_MAX;
                 __syncthreads();
                 const int nd = min(S.ndue, E);
+                int64_t lm = INT64_MAX;
                 for (int q = tid; q < nd; q += MG_BLOCK) {
                     const int e = S.due[q];
-                    if (S.flag[e] & F_TIMER) __hip_atomic_fetch_min(&s_vmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
+                    if (S.flag[e] & F_TIMER) lm = min(lm, S.slice[e]);
                 }
+                lm = wave_min_i64(lm);
+                if ((tid & 63) == 0 && lm != INT64_MAX) __hip_atomic_fetch_min(&s_vmin, lm, __ATOMIC_RELAXED, LDS_SCOPE);
                 __syncthreads();
                 if (!gdet) stm.mark(4);
                 const int64_t v = s_vmin;
                 if (v == INT64_MAX) break;
                 stm.acc[7]++;
+                uint32_t nf = 0;
                 for (int q = tid; q < nd; q += MG_BLOCK) {
                     const int e = S.due[q];
                     if ((S.flag[e] & F_TIMER) && S.slice[e] == v) {
                         atomicAnd(&S.flag[e], ~F_TIMER);
-                        fire_one(a, S, e, v, &s_fired, sb, &s_emit);
+                        fire_one(a, S, e, v, sb, &s_emit);
+                        nf++;
                     }
                 }
+                nf = wave_sum_u32(nf);
+                if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
                 __syncthreads();
                 if (!gdet) stm.mark(5);
             }
@@ -1027,18 +1056,21 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         stm.mark(2);
         const int n = min(S.n, E);
         uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
+        int64_t lnm = INT64_MAX;
         if (!(a.ablate & AB_M_NO_WB)) for (int e = tid; e < n; e += MG_BLOCK) {
             const uint32_t f = S.flag[e];
             if (!(f & (F_ACC | F_TIMER))) continue;
-            const int pos = atomicAdd(&s_nlive, 1);
+            const int pos = wave_claim(&s_nlive);
             uint64_t* p = so + (size_t)pos * PWE;
             p[0] = (uint64_t)S.key[e];
             p[1] = (uint64_t)S.slice[e];
             p[2] = f;
 #pragma unroll
             for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];
-            if (f & F_TIMER) __hip_atomic_fetch_min(&s_newmin, S.slice[e], __ATOMIC_RELAXED, LDS_SCOPE);
+            if (f & F_TIMER) lnm = min(lnm, S.slice[e]);
         }
+        lnm = wave_min_i64(lnm);
+        if ((tid & 63) == 0 && lnm != INT64_MAX) __hip_atomic_fetch_min(&s_newmin, lnm, __ATOMIC_RELAXED, LDS_SCOPE);
         __syncthreads();
         if (tid == 0) {
             a.state_count[sb] = s_nlive;

@@ -30,7 +30,7 @@ constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw)
 
 // ---- merge/fire (K4+K5): one 1024-thread workgroup per superbucket
 constexpr int MG_BLOCK = 1024;
-constexpr int MG_CELL_GROUP = 512;              // cells (chunks) scanned at a time per pending push
+constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a time per pending push (one per thread)
 // LDS slice-state capacity (entries) per superbucket by accumulator words
 constexpr int mg_entries(int nw) { return nw <= 1 ? 4096 : nw <= 4 ? 2048 : 1024; }
 

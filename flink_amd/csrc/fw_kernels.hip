@@ -860,6 +860,32 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     }
     __syncthreads();
     if (s_work) {
+        // cell groups of all pending pushes as one flat sequence; the next group's cell words
+        // are loaded while the current group is folded, the first group's while the state loads
+        const bool gather = do_flush && !(a.ablate & AB_M_NO_GATHER);
+        int n_groups = 0;
+        // cells are enumerated in flat tile order f (cell_chunk(f) is the chunk); padding
+        // positions past the push's last chunk count as empty
+        if (gather) for (int64_t pi = 0; pi < pend; pi++)
+            n_groups += (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
+        auto cell_word = [&](int k, int& pi_out, int& g0_out, int& ng_out) -> uint32_t {
+            int pi = 0;
+            for (;;) {
+                const int ngp = (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
+                if (k < ngp) break;
+                k -= ngp;
+                pi++;
+            }
+            pi_out = pi;
+            g0_out = k * MG_CELL_GROUP;
+            ng_out = min(MG_CELL_GROUP, (int)cell_pad(a.slot_nch[pi]) - g0_out);
+            const int64_t f = g0_out + tid;
+            if (tid >= ng_out || cell_chunk(f) >= a.slot_nch[pi]) return 0u;
+            const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
+            return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
+        };
+        int pi_n = 0, g0_n = 0, ng_n = 0;
+        uint32_t v_n = n_groups > 0 ? cell_word(0, pi_n, g0_n, ng_n) : 0u;
         // ---- load this superbucket's entries into LDS
         for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
         if (tid == 0) {
@@ -894,32 +920,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
         }
         // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket
-        if (do_flush && !(a.ablate & AB_M_NO_GATHER)) {
-            // cell groups of all pending pushes as one flat sequence; the next group's cell words
-            // are loaded while the current group is folded
-            int n_groups = 0;
-            // cells are enumerated in flat tile order f (cell_chunk(f) is the chunk); padding
-            // positions past the push's last chunk count as empty
-            for (int64_t pi = 0; pi < pend; pi++)
-                n_groups += (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
-            auto cell_word = [&](int k, int& pi_out, int& g0_out, int& ng_out) -> uint32_t {
-                int pi = 0;
-                for (;;) {
-                    const int ngp = (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
-                    if (k < ngp) break;
-                    k -= ngp;
-                    pi++;
-                }
-                pi_out = pi;
-                g0_out = k * MG_CELL_GROUP;
-                ng_out = min(MG_CELL_GROUP, (int)cell_pad(a.slot_nch[pi]) - g0_out);
-                const int64_t f = g0_out + tid;
-                if (tid >= ng_out || cell_chunk(f) >= a.slot_nch[pi]) return 0u;
-                const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
-                return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
-            };
-            int pi_n = 0, g0_n = 0, ng_n = 0;
-            uint32_t v_n = n_groups > 0 ? cell_word(0, pi_n, g0_n, ng_n) : 0u;
+        if (gather) {
             for (int k = 0; k < n_groups; k++) {
                 const int pi = pi_n, g0 = g0_n, ng = ng_n;
                 const uint32_t v = v_n;

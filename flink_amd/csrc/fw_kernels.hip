@@ -598,14 +598,20 @@ __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const Wo
 // entry, -1 when the home slot is empty, -2 when the first probe does not decide (collision or
 // an insertion in flight): the caller then takes the probing path.
 template <int NW, int E, int M>
-__device__ __forceinline__ void probe_batch(StateLds<NW, E>& S, const int64_t* k, const int64_t* s, int* e) {
+__device__ __forceinline__ void probe_batch(StateLds<NW, E>& S, const int64_t* k, const int64_t* s, int* e,
+                                            int m = M) {
+    // only the first m (<= M, uniform) lookups are needed; the others issue no LDS reads
     constexpr uint32_t MASK = 2 * E - 1;
     uint32_t st[M];
 #pragma unroll
-    for (int j = 0; j < M; j++) st[j] = __hip_atomic_load(&S.idx[index_hash(k[j], s[j]) & MASK], __ATOMIC_RELAXED, LDS_SCOPE);
+    for (int j = 0; j < M; j++)
+        st[j] = j < m ? __hip_atomic_load(&S.idx[index_hash(k[j], s[j]) & MASK], __ATOMIC_RELAXED, LDS_SCOPE) : 0u;
     int64_t kk[M], ss[M];
 #pragma unroll
     for (int j = 0; j < M; j++) {
+        kk[j] = 0;
+        ss[j] = 0;
+        if (j >= m) continue;
         const uint32_t ei = min(st[j] - 2u, (uint32_t)(E - 1));
         kk[j] = S.key[ei];
         ss[j] = S.slice[ei];
@@ -722,7 +728,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
                 ss[j] = s;
                 s = wsub(s, w.interval);  // wrapping, like the reference's long arithmetic
             }
-            probe_batch<NW, E, HB>(S, kk, ss, eb);
+            probe_batch<NW, E, HB>(S, kk, ss, eb, min(HB, n - j0));
 #pragma unroll
             for (int j = 0; j < HB; j++) {
                 if (j0 + j >= n) break;
@@ -756,8 +762,9 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
 #pragma unroll
         for (int i = 0; i < NW; i++) acc[i] = S.acc[i][ef];
     }
+    int e_we = -1;
     if (we != first) {
-        const int e2 = find_entry(S, k, we);
+        const int e2 = e_we = find_entry(S, k, we);
         if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
 #pragma unroll
             for (int i = 0; i < NW; i++)
@@ -780,7 +787,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
     // clearWindow (CumulativeSliceAssigner.expiredSlices)
     if (we == first) {
     } else {
-        const int e2 = find_entry(S, k, we);
+        const int e2 = e_we;  // the entry of `we` was looked up above and entries never move
         if (e2 >= 0) atomicAnd(&S.flag[e2], ~F_ACC);
         if (we == last && ef >= 0) atomicAnd(&S.flag[ef], ~F_ACC);
     }

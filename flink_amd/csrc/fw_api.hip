@@ -726,8 +726,7 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
 
 int fw_results_reset(fw_handle* h) {
     if (!h) return fail(FW_E_INVALID, "null handle");
-    HIP_TRY(hipMemsetAsync(&h->ctrl->out_count, 0, sizeof(uint64_t), h->stream));
-    HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
+    HIP_TRY(launch_reset_results(h->ctrl, h->sb_out, h->ks.n_sb, h->stream));
     return FW_OK;
 }
 

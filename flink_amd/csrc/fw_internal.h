@@ -284,5 +284,6 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s);
+hipError_t launch_reset_results(Ctrl* c, int32_t* sb_out, int32_t n_sb, hipStream_t s);
 
 }  // namespace fw

@@ -1138,6 +1138,19 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t) {
     return hipGetLastError();
 }
 
+// results consumed: empty every superbucket's output slab and the overflow region (one launch
+// instead of two memsets)
+__global__ __launch_bounds__(BLOCK) void k_reset_results(Ctrl* c, int32_t* sb_out, int32_t n_sb) {
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n_sb) sb_out[i] = 0;
+    if (i == 0) c->out_count = 0;
+}
+
+hipError_t launch_reset_results(Ctrl* c, int32_t* sb_out, int32_t n_sb, hipStream_t s) {
+    hipLaunchKernelGGL(k_reset_results, dim3((n_sb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, c, sb_out, n_sb);
+    return hipGetLastError();
+}
+
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
     hipLaunchKernelGGL(k_init_ctrl, dim3(1), dim3(64), 0, s, c);
     return hipGetLastError();

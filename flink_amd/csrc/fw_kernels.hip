@@ -943,7 +943,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                 __syncthreads();
                 if (gdet) stm.mark(4);
                 const int top = 1 << (31 - __builtin_clz((unsigned)ng));  // highest power of two <= ng
-                constexpr int U = NW <= 2 ? 2 : 1;  // rows in flight per thread (VGPR budget)
+                constexpr int U = 1;  // rows in flight per thread (VGPR budget)
                 for (uint32_t r0 = tid; r0 < total; r0 += U * MG_BLOCK) {
                     // cell of each row: s_cb[lo] <= r < s_cb[lo + 1], the U searches advance together
                     int lo[U];

@@ -834,7 +834,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     __shared__ uint16_t s_start[MG_CELL_GROUP];   // first row of each cell inside its chunk region
     __shared__ uint32_t wsum[MG_BLOCK / 64];
     __shared__ int32_t s_work;
-    __shared__ int64_t s_vmin;
+    __shared__ int64_t s_vmin[2];  // round minimum, double-buffered by round parity
     __shared__ int32_t s_nlive;
     __shared__ int64_t s_newmin;
     __shared__ uint32_t s_fired;
@@ -1011,7 +1011,10 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         // ---- fire: InternalTimerServiceImpl.tryAdvanceWatermark, timestamp order
         if (do_fire && !(a.ablate & AB_M_NO_FIRE)) {
             // due list: entries whose timer fires at W (dense work for the rounds below)
-            if (tid == 0) S.ndue = 0;
+            if (tid == 0) {
+                S.ndue = 0;
+                s_vmin[0] = INT64_MAX;
+            }
             __syncthreads();
             const int n = min(S.n, E);
             for (int e = tid; e < n; e += MG_BLOCK)
@@ -1023,9 +1026,11 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             if (!gdet) stm.mark(6);
             // rounds in timestamp order (per key the reference fires windows in order, and a
             // fired HOP/CUMULATE window can register the next one); keys are independent
-            for (;;) {
-                if (tid == 0) s_vmin = INT64_MAX;
-                __syncthreads();
+            // (the next round's minimum slot is reset during this round, so a round needs two
+            // barriers: after the minimum and after the fires)
+            for (int rnd = 0;; rnd++) {
+                int64_t* vmin = &s_vmin[rnd & 1];
+                if (tid == 0) s_vmin[(rnd + 1) & 1] = INT64_MAX;
                 const int nd = min(S.ndue, E);
                 int64_t lm = INT64_MAX;
                 for (int q = tid; q < nd; q += MG_BLOCK) {
@@ -1033,10 +1038,10 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     if (S.flag[e] & F_TIMER) lm = min(lm, S.slice[e]);
                 }
                 lm = wave_min_i64(lm);
-                if ((tid & 63) == 0 && lm != INT64_MAX) __hip_atomic_fetch_min(&s_vmin, lm, __ATOMIC_RELAXED, LDS_SCOPE);
+                if ((tid & 63) == 0 && lm != INT64_MAX) __hip_atomic_fetch_min(vmin, lm, __ATOMIC_RELAXED, LDS_SCOPE);
                 __syncthreads();
                 if (!gdet) stm.mark(4);
-                const int64_t v = s_vmin;
+                const int64_t v = *vmin;
                 if (v == INT64_MAX) break;
                 stm.acc[7]++;
                 uint32_t nf = 0;

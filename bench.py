@@ -117,6 +117,8 @@ def main():
                     help="launch fw_assign_key_groups over 2^28 keys before timing: a known-byte "
                          "8-B/lane read (2 GiB) + 4-B/lane write (1 GiB) that calibrates FETCH_SIZE/WRITE_SIZE")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged end-to-end leg (N=1 only)")
+    ap.add_argument("--e2e-steps", type=int, default=6)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
                          "one-GPU box: ranks share the GPUs round robin and the exchange is staged "
@@ -203,6 +205,21 @@ def main():
         torch.cuda.synchronize(dev)
         del ck, cd
 
+    # G_b of SURVEY.md 8d: distinct (key, slice) groups of each timed batch (exact, untimed; no
+    # event of the synthetic stream is late, so every row's group is (key, its own slice))
+    interval = wl["window"][2] if wl["window"][0] != "TUMBLE" else wl["window"][1]
+    if wl["window"][0] == "HOP":
+        import math
+        interval = math.gcd(wl["window"][1], wl["window"][2])
+    groups = []
+    for b in range(args.warmup, total_steps):
+        k, t, _ = exchange(b)
+        sl = torch.div(t, interval, rounding_mode="floor")
+        sl = sl - sl.min()
+        groups.append(int(torch.unique(k * (int(sl.max()) + 1) + sl).numel()))
+        del k, t, sl
+    torch.cuda.synchronize(dev)
+
     cfg = build_config(wl, world, rank, keys_total, out_cap)
     # warmup on its own operator instance (first batches of the same stream)
     if args.warmup:
@@ -237,15 +254,24 @@ def main():
     value = n_total / elapsed
     # ---------------- roofline of the segmented-reduce (ingest) kernel ----------------------
     # algorithmic bytes per launch: N_b * sum(w_in) + G_b * w_partial, with
-    # w_partial = key + slice + accumulator words (8 B each) and G_b the partials it wrote
+    # w_partial = key + slice + accumulator words (8 B each) and G_b the distinct (key, slice)
+    # groups of the batch (counted exactly above)
     red_ms, red_n = kt["reduce"]
     w_partial = 8 * (2 + wl["nw"])
     rows_per_launch = n_total / world / red_n
-    g_per_launch = st["partials_emitted"] / red_n
+    g_per_launch = sum(groups) / len(groups)
     bytes_per_launch = rows_per_launch * wl["w_in"] + g_per_launch * w_partial
     avg_reduce_s = red_ms / red_n / 1e3
     achieved = bytes_per_launch / avg_reduce_s / 1e9
-    traffic = None
+    # ---------------- the flush + fire kernel: G_b * w_partial + 2 L w_entry + F w_out ---------
+    mg_ms, mg_n = kt["merge"]
+    w_entry = 8 * (3 + wl["nw"])
+    w_out = 8 * (3 + len(wl["aggs"])) + 4
+    live = st["live_state_entries"]                       # entries after the last step (~ per step)
+    fired_per_step = st["num_fired_windows"] / args.steps
+    merge_bytes = g_per_launch * w_partial + 2 * live * w_entry + fired_per_step * w_out
+    avg_merge_s = mg_ms / max(mg_n, 1) / 1e3
+    traffic = traffic_m = None
     tpath = args.traffic_json
     if tpath is None:
         import glob
@@ -255,13 +281,53 @@ def main():
         tj = json.load(open(tpath))
         if tj.get("workload") == args.workload:
             traffic = tj.get("k_ingest_hbm_bytes_per_launch")
+            traffic_m = tj.get("k_merge_fire_hbm_bytes_per_launch")
+
+    # ---------------- end-to-end leg (N = 1): host-staged ingest + per-watermark D2H ----------
+    # What the JNI shim does: the host writes each batch into the operator's
+    # pinned staging columns (fw_reserve), fw_commit copies them over PCIe and ingests, and every
+    # watermark's results come back to host memory (fw_results copy_to_host).  Reported beside the
+    # device-resident `value`, never as it.
+    e2e = None
+    if world == 1 and not args.no_e2e and args.e2e_steps > 0:
+        from flink_amd.runtime.handle import _np_view
+        hk = [gk[b].cpu().numpy() for b in range(args.e2e_steps)]
+        ht = [gt[b].cpu().numpy() for b in range(args.e2e_steps)]
+        hv = [gv[b].cpu().numpy() for b in range(args.e2e_steps)]
+        cfg_e = build_config(wl, 1, 0, keys_total, out_cap)
+        he = WindowAggHandle(cfg_e)
+        rows_out = 0
+        te0 = time.perf_counter()
+        for b in range(args.e2e_steps):
+            cols = abi.fw_host_cols()
+            _native.check(L.fw_reserve(he._h, B, C.byref(cols)))
+            _np_view(cols.key, B, np.int64)[:] = hk[b]
+            _np_view(cols.ts, B, np.int64)[:] = ht[b]
+            if nv:
+                _np_view(cols.values[0], B, np.int64)[:] = hv[b]
+            _native.check(L.fw_commit(he._h, B))
+            he.advance(watermark(b, wl["rate"]))
+            rows_out += len(he.results(reset=True)["key"])
+        he.sync()
+        te = time.perf_counter() - te0
+        he.close()
+        e2e = {"value": args.e2e_steps * B / te, "unit": "events/s", "steps": args.e2e_steps,
+               "ms_per_step": te / args.e2e_steps * 1e3, "result_rows": rows_out,
+               "path": "numpy batch -> pinned staging (fw_reserve) -> H2D + ingest (fw_commit) -> "
+                       "advance -> fw_results copy_to_host, one watermark per batch"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         v, n, dt, _ = cpu_baseline(wl, args.cpu_sample)
+        try:
+            host_cpus = len(os.sched_getaffinity(0))
+        except AttributeError:
+            host_cpus = os.cpu_count()
         cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
+               "host_nproc": host_cpus,
                "sample": f"first {n} events of the same {args.workload} stream through the C++ oracle "
-                         f"(oracle/flinkwin_oracle.cpp, single thread), {dt:.1f} s"}
+                         f"(oracle/flinkwin_oracle.cpp, single thread on a host with {host_cpus} usable "
+                         f"CPUs), {dt:.1f} s; the reference Flink operator needs a JDK, absent here"}
 
     if rank == 0:
         line = {
@@ -281,8 +347,21 @@ def main():
                          "kernel": "fw::k_ingest (K1 key group + K2 slice assign + K3 LDS segmented reduce, "
                                    "chunk-local superbucket sort)",
                          "algorithmic_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_reduce_s * 1e6,
-                         "launches": red_n, "partials_per_launch": g_per_launch},
+                         "launches": red_n, "distinct_groups_per_launch": g_per_launch,
+                         "partials_written_per_launch": st["partials_emitted"] / red_n,
+                         "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None},
+            "roofline_merge": {"bound": "hbm", "kernel": "fw::k_merge_fire (K4 flush into the HBM slice table + "
+                                                         "K5 timers / fire / emit)",
+                               "achieved": merge_bytes / avg_merge_s / 1e9 if mg_n else None,
+                               "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                               "frac": merge_bytes / avg_merge_s / 1e9 / HBM_PEAK_GBPS if mg_n else None,
+                               "algorithmic_bytes_per_launch": merge_bytes,
+                               "terms": {"G_b_w_partial": g_per_launch * w_partial, "two_L_w_entry": 2 * live * w_entry,
+                                         "F_w_out": fired_per_step * w_out},
+                               "avg_launch_us": avg_merge_s * 1e6, "launches": mg_n, "traffic": traffic_m,
+                               "traffic_over_algorithmic": (traffic_m / merge_bytes) if traffic_m else None},
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
             "device_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         }
         print(json.dumps(line), flush=True)

@@ -43,7 +43,7 @@ def lib():
         "fw_initialize_watermark": (i32, [vp, i64]),
         "fw_reserve": (i32, [vp, i64, P(abi.fw_host_cols)]),
         "fw_commit": (i32, [vp, i64]),
-        "fw_push_device": (i32, [vp, i64, vp, vp, vp, vp]),
+        "fw_push_device": (i32, [vp, i64, vp, vp, vp, vp, vp]),
         "fw_advance": (i32, [vp, i64]),
         "fw_flush": (i32, [vp]),
         "fw_results": (i32, [vp, P(abi.fw_result), i32]),

@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 1
+FW_ABI_VERSION = 2
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -30,6 +30,10 @@ AGG_SUM = 2
 AGG_MIN = 3
 AGG_MAX = 4
 AGG_AVG = 5
+# fw_agg_phase (TwoStageOptimizedWindowAggregateRule: one-phase, or local + global)
+PHASE_ONE = 0
+PHASE_LOCAL = 1
+PHASE_GLOBAL = 2
 # fw_value_type
 T_I64 = 0
 T_F64 = 1
@@ -66,10 +70,13 @@ class fw_config(C.Structure):
         ("aggs", fw_agg_desc * FW_MAX_AGGS),
         ("n_value_cols", C.c_int32),
         ("value_col_types", C.c_int32 * FW_MAX_COLS),
+        ("nullable_cols", C.c_uint32),
+        ("agg_phase", C.c_int32),
         ("max_parallelism", C.c_int32),
         ("parallelism", C.c_int32),
         ("subtask_index", C.c_int32),
         ("device", C.c_int32),
+        ("reserved0", C.c_int32),
         ("state_capacity", C.c_int64),
         ("max_batch_rows", C.c_int64),
         ("output_capacity", C.c_int64),
@@ -79,7 +86,8 @@ class fw_config(C.Structure):
 class fw_host_cols(C.Structure):
     _fields_ = [("key", C.POINTER(C.c_int64)), ("ts", C.POINTER(C.c_int64)),
                 ("key_hash", C.POINTER(C.c_int32)),
-                ("values", C.POINTER(C.c_int64) * FW_MAX_COLS)]
+                ("values", C.POINTER(C.c_int64) * FW_MAX_COLS),
+                ("nulls", C.POINTER(C.c_uint8) * FW_MAX_COLS)]
 
 
 class fw_result(C.Structure):
@@ -117,8 +125,10 @@ class fw_gen_params(C.Structure):
 def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, offset_ms=0,
                 aggs=(), count_star_index=-1, value_col_types=(), key_hash=KEYHASH_BINROW_BIGINT,
                 max_parallelism=128, parallelism=1, subtask_index=0, device=0,
-                state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22):
-    """Build an fw_config.  ``aggs`` is a sequence of (kind, input_col, type)."""
+                state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22,
+                nullable_cols=(), agg_phase=PHASE_ONE):
+    """Build an fw_config.  ``aggs`` is a sequence of (kind, input_col, type); ``nullable_cols``
+    the value columns that may hold SQL NULLs."""
     if len(aggs) > FW_MAX_AGGS or len(value_col_types) > FW_MAX_COLS:
         raise ValueError("too many aggregates or value columns")
     c = fw_config()
@@ -138,6 +148,8 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
     c.n_value_cols = len(value_col_types)
     for i, t in enumerate(value_col_types):
         c.value_col_types[i] = t
+    c.nullable_cols = sum(1 << int(col) for col in nullable_cols)
+    c.agg_phase = agg_phase
     c.max_parallelism = max_parallelism
     c.parallelism = parallelism
     c.subtask_index = subtask_index

@@ -165,11 +165,13 @@ struct fw_handle {
     int64_t* h_ts[2] = {};
     int32_t* h_kh[2] = {};
     int64_t* h_val[2][FW_MAX_COLS] = {};
+    uint8_t* h_nul[2][FW_MAX_COLS] = {};
     hipEvent_t stage_ev[2] = {};
     int64_t* d_key = nullptr;
     int64_t* d_ts = nullptr;
     int32_t* d_kh = nullptr;
     int64_t* d_val[FW_MAX_COLS] = {};
+    uint8_t* d_nul[FW_MAX_COLS] = {};
     int64_t reserved = -1;
 
     // host copies of results
@@ -233,10 +235,17 @@ int validate_and_plan(fw_handle* h) {
     h->always_flush = c.api == FW_API_DATASTREAM;
 
     // ---- aggregates -> accumulator words
+    if (c.api == FW_API_DATASTREAM && c.nullable_cols)
+        return fail(FW_E_INVALID, "DataStream field aggregations have no NULL inputs");
+    if (c.agg_phase != FW_PHASE_ONE && c.agg_phase != FW_PHASE_LOCAL && c.agg_phase != FW_PHASE_GLOBAL)
+        return fail(FW_E_INVALID, "bad agg_phase %d", c.agg_phase);
+    if (c.agg_phase != FW_PHASE_ONE && c.api != FW_API_SQL) return fail(FW_E_INVALID, "two-phase aggregation is SQL only");
     WordDesc& wd = h->wd;
     AggDesc& ad = h->ad;
     wd.nw = 0;
+    wd.has_q = 0;
     int nslot = 0;
+    auto nullable = [&](int col) { return ((c.nullable_cols >> col) & 1u) != 0; };
     auto slot_of = [&](int col) -> int {
         for (int s = 0; s < nslot; s++)
             if (h->slot_col[s] == col) return s;
@@ -244,50 +253,78 @@ int validate_and_plan(fw_handle* h) {
         h->slot_col[nslot] = col;
         return nslot++;
     };
-    auto word_of = [&](int op, int slot) -> int {
+    // one word per (op, slot, gate); COUNT words are identified by their gate alone
+    auto word_of = [&](int op, int slot, int gate) -> int {
         for (int i = 0; i < wd.nw; i++)
-            if (wd.op[i] == op && (op == W_CNT || wd.col[i] == slot)) return i;
+            if (wd.op[i] == op && wd.gate[i] == gate && (op == W_CNT || wd.col[i] == slot)) return i;
         if (wd.nw >= MAX_WORDS) return -1;
         wd.op[wd.nw] = op;
         wd.col[wd.nw] = op == W_CNT ? 0 : slot;
+        wd.gate[wd.nw] = gate;
+        wd.qfirst[wd.nw] = -1;
         return wd.nw++;
     };
     ad.n = c.n_aggs;
-    ad.count_word = -1;
     ad.count_star_word = -1;
+    bool nn_star[FW_MAX_AGGS] = {};
     for (int g = 0; g < c.n_aggs; g++) {
         const fw_agg_desc& d = c.aggs[g];
         ad.kind[g] = d.kind;
         ad.type[g] = d.type;
-        ad.w1[g] = -1;
+        ad.w1[g] = ad.nn[g] = ad.qf[g] = ad.qn[g] = ad.qz[g] = -1;
         if (d.type < FW_T_I64 || d.type > FW_T_I32) return fail(FW_E_INVALID, "agg %d: bad type", g);
-        int slot = 0;
+        int slot = 0, gate = -1;
         if (d.kind != FW_AGG_COUNT_STAR) {
             if (d.input_col < 0 || d.input_col >= c.n_value_cols) return fail(FW_E_INVALID, "agg %d: bad input_col", g);
             if (c.value_col_types[d.input_col] != d.type)
                 return fail(FW_E_INVALID, "agg %d: type does not match value column type", g);
-            if (d.kind != FW_AGG_COUNT) {
+            if (d.kind != FW_AGG_COUNT || nullable(d.input_col)) {
                 slot = slot_of(d.input_col);
                 if (slot < 0) return fail(FW_E_INVALID, "more than %d distinct value columns", MAX_KCOLS);
+                if (nullable(d.input_col)) gate = slot;
             }
-        }
-        const bool f = d.type == FW_T_F64;
-        int w0 = -1;
-        switch (d.kind) {
-            case FW_AGG_COUNT_STAR:
-            case FW_AGG_COUNT: w0 = word_of(W_CNT, 0); break;
-            case FW_AGG_SUM: w0 = word_of(f ? W_SUM_F : W_SUM_I, slot); break;
-            case FW_AGG_MIN: w0 = word_of(f ? W_MIN_D : W_MIN_I, slot); break;
-            case FW_AGG_MAX: w0 = word_of(f ? W_MAX_D : W_MAX_I, slot); break;
-            case FW_AGG_AVG:
-                w0 = word_of(f ? W_SUM_F : W_SUM_I, slot);
-                ad.w1[g] = word_of(W_CNT, 0);
-                break;
-            default: return fail(FW_E_INVALID, "agg %d: unsupported kind %d", g, d.kind);
         }
         if (c.api == FW_API_DATASTREAM && (d.kind == FW_AGG_AVG || d.kind == FW_AGG_COUNT))
             return fail(FW_E_INVALID, "DataStream built-in aggregations are sum/min/max (and COUNT_STAR)");
+        const bool f = d.type == FW_T_F64;
+        // non-NULL count of the input: gated COUNT for a nullable column, else COUNT(*)
+        const int cnt_op = W_CNT;
+        int w0 = -1;
+        switch (d.kind) {
+            case FW_AGG_COUNT_STAR: w0 = word_of(cnt_op, 0, -1); break;
+            case FW_AGG_COUNT: w0 = word_of(cnt_op, slot, gate); break;
+            case FW_AGG_SUM:
+                w0 = word_of(f ? W_SUM_F : W_SUM_I, slot, gate);
+                if (gate >= 0) ad.nn[g] = word_of(cnt_op, slot, gate);
+                else nn_star[g] = true;
+                break;
+            case FW_AGG_MIN:
+            case FW_AGG_MAX: {
+                const bool mx = d.kind == FW_AGG_MAX;
+                if (f && c.api == FW_API_SQL) {  // strict comparison in arrival order: word group
+                    w0 = word_of(mx ? W_QMAX : W_QMIN, slot, gate);
+                    ad.qf[g] = word_of(W_QFIRST, slot, gate);
+                    ad.qn[g] = word_of(W_QNANLO, slot, gate);
+                    ad.qz[g] = word_of(W_QZERO, slot, gate);
+                    if (w0 < 0 || ad.qf[g] < 0 || ad.qn[g] < 0 || ad.qz[g] < 0) return fail(FW_E_INVALID, "too many accumulator words");
+                    wd.qfirst[w0] = wd.qfirst[ad.qn[g]] = ad.qf[g];
+                    wd.has_q = 1;
+                    break;
+                }
+                w0 = word_of(f ? (mx ? W_MAX_D : W_MIN_D) : (mx ? W_MAX_I : W_MIN_I), slot, gate);
+                if (gate >= 0) ad.nn[g] = word_of(cnt_op, slot, gate);
+                else nn_star[g] = true;
+                break;
+            }
+            case FW_AGG_AVG:
+                w0 = word_of(f ? W_SUM_F : W_SUM_I, slot, gate);
+                ad.w1[g] = word_of(cnt_op, slot, gate);
+                break;
+            default: return fail(FW_E_INVALID, "agg %d: unsupported kind %d", g, d.kind);
+        }
         if (w0 < 0 || (d.kind == FW_AGG_AVG && ad.w1[g] < 0)) return fail(FW_E_INVALID, "too many accumulator words");
+        if ((d.kind == FW_AGG_SUM || d.kind == FW_AGG_MIN || d.kind == FW_AGG_MAX) && gate >= 0 && ad.nn[g] < 0 && ad.qf[g] < 0)
+            return fail(FW_E_INVALID, "too many accumulator words");
         ad.w0[g] = w0;
     }
     if (c.count_star_index >= 0) {
@@ -298,16 +335,23 @@ int validate_and_plan(fw_handle* h) {
     } else if (c.window_kind == FW_WIN_HOP) {
         if (c.api == FW_API_SQL) return fail(FW_E_INVALID, "Hopping window requires a COUNT(*) in the aggregate functions.");
         // DataStream sliding windows emit a window iff it received an element: hidden COUNT(*)
-        ad.count_star_word = word_of(W_CNT, 0);
+        ad.count_star_word = word_of(W_CNT, 0, -1);
         if (ad.count_star_word < 0) return fail(FW_E_INVALID, "too many accumulator words");
     }
+    // NOT NULL inputs: SUM / MIN / MAX are NULL only for an entry without rows (COUNT(*) == 0),
+    // which needs a COUNT(*) word to be observable; without one such an entry never fires
+    int star = -1;
     for (int i = 0; i < wd.nw; i++)
-        if (wd.op[i] == W_CNT) ad.count_word = i;
+        if (wd.op[i] == W_CNT && wd.gate[i] < 0) star = i;
+    for (int g = 0; g < c.n_aggs; g++)
+        if (nn_star[g]) ad.nn[g] = star;
     h->nv = nslot;
     h->nw_t = round_nw(wd.nw);
     for (int i = wd.nw; i < MAX_WORDS; i++) {
         wd.op[i] = W_CNT;
         wd.col[i] = 0;
+        wd.gate[i] = -1;
+        wd.qfirst[i] = -1;
     }
 
     // ---- key space: this subtask's key groups, split into superbuckets
@@ -335,6 +379,8 @@ int validate_and_plan(fw_handle* h) {
     h->chunk_rows = (int64_t)IG_BLOCK * ig_rpt(h->nw_t);
     h->cap_rows = ((c.max_batch_rows + h->chunk_rows - 1) / h->chunk_rows) * h->chunk_rows;
     h->max_nch = h->cap_rows / h->chunk_rows;
+    if (wd.has_q && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
+        return fail(FW_E_INVALID, "max_batch_rows too large for SQL MIN/MAX(DOUBLE) arrival ordinals");
     h->cell_cols = cell_pad(h->max_nch);
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     h->out_cap = c.output_capacity;
@@ -402,7 +448,10 @@ int alloc_staging(fw_handle* h) {
         HIP_TRY(hipHostMalloc((void**)&h->h_key[b], n * 8, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc((void**)&h->h_ts[b], n * 8, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc((void**)&h->h_kh[b], n * 4, hipHostMallocDefault));
-        for (int v = 0; v < c.n_value_cols; v++) HIP_TRY(hipHostMalloc((void**)&h->h_val[b][v], n * 8, hipHostMallocDefault));
+        for (int v = 0; v < c.n_value_cols; v++) {
+            HIP_TRY(hipHostMalloc((void**)&h->h_val[b][v], n * 8, hipHostMallocDefault));
+            if ((c.nullable_cols >> v) & 1u) HIP_TRY(hipHostMalloc((void**)&h->h_nul[b][v], n, hipHostMallocDefault));
+        }
         HIP_TRY(hipEventCreateWithFlags(&h->stage_ev[b], hipEventDisableTiming));
         HIP_TRY(hipEventRecord(h->stage_ev[b], h->stream));
     }
@@ -410,8 +459,10 @@ int alloc_staging(fw_handle* h) {
     if ((rc = dalloc(&h->d_key, n))) return rc;
     if ((rc = dalloc(&h->d_ts, n))) return rc;
     if ((rc = dalloc(&h->d_kh, n))) return rc;
-    for (int v = 0; v < c.n_value_cols; v++)
+    for (int v = 0; v < c.n_value_cols; v++) {
         if ((rc = dalloc(&h->d_val[v], n))) return rc;
+        if (((c.nullable_cols >> v) & 1u) && (rc = dalloc(&h->d_nul[v], n))) return rc;
+    }
     return FW_OK;
 }
 
@@ -467,7 +518,8 @@ int force_flush(fw_handle* h) {
     return FW_OK;
 }
 
-int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int32_t* kh, const void* const* vals) {
+int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int32_t* kh, const void* const* vals,
+         const uint8_t* const* nulls) {
     for (int64_t o = 0; o < n; o += h->cap_rows) {
         const int64_t m = std::min(h->cap_rows, n - o);
         if (h->pushes_ub >= FW_MAX_PENDING) {
@@ -484,8 +536,11 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.key = key + o;
         a.ts = ts + o;
         a.khash = kh ? kh + o : nullptr;
-        for (int s = 0; s < MAX_KCOLS; s++)
-            a.vals[s] = s < h->nv ? (const uint64_t*)vals[h->slot_col[s]] + o : nullptr;
+        for (int s = 0; s < MAX_KCOLS; s++) {
+            const bool live = s < h->nv;
+            a.vals[s] = live ? (const uint64_t*)vals[h->slot_col[s]] + o : nullptr;
+            a.nulls[s] = live && ((h->cfg.nullable_cols >> h->slot_col[s]) & 1u) ? nulls[h->slot_col[s]] + o : nullptr;
+        }
         a.n = m;
         a.win = h->win;
         a.ks = h->ks;
@@ -502,6 +557,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.treq = h->treq;
         a.treq_cap = h->treq_cap;
         a.lds_bytes = IG_LDS;
+        a.local = h->cfg.agg_phase == FW_PHASE_LOCAL;
         a.ablate = h->ablate;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
@@ -565,13 +621,19 @@ int fw_destroy(fw_handle* h) {
         hipHostFree(h->h_key[b]);
         hipHostFree(h->h_ts[b]);
         hipHostFree(h->h_kh[b]);
-        for (int v = 0; v < FW_MAX_COLS; v++) hipHostFree(h->h_val[b][v]);
+        for (int v = 0; v < FW_MAX_COLS; v++) {
+            hipHostFree(h->h_val[b][v]);
+            hipHostFree(h->h_nul[b][v]);
+        }
         if (h->stage_ev[b]) hipEventDestroy(h->stage_ev[b]);
     }
     hipFree(h->d_key);
     hipFree(h->d_ts);
     hipFree(h->d_kh);
-    for (int v = 0; v < FW_MAX_COLS; v++) hipFree(h->d_val[v]);
+    for (int v = 0; v < FW_MAX_COLS; v++) {
+        hipFree(h->d_val[v]);
+        hipFree(h->d_nul[v]);
+    }
     delete h->timer;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -605,7 +667,10 @@ int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out) {
     out->key = h->h_key[b];
     out->ts = h->h_ts[b];
     out->key_hash = h->h_kh[b];
-    for (int v = 0; v < h->cfg.n_value_cols; v++) out->values[v] = h->h_val[b][v];
+    for (int v = 0; v < h->cfg.n_value_cols; v++) {
+        out->values[v] = h->h_val[b][v];
+        out->nulls[v] = h->h_nul[b][v];
+    }
     h->reserved = n;
     return FW_OK;
 }
@@ -626,24 +691,33 @@ int fw_commit(fw_handle* h, int64_t n) {
     for (int s = 0; s < h->nv; s++) {
         const int v = h->slot_col[s];
         HIP_TRY(hipMemcpyAsync(h->d_val[v], h->h_val[b][v], n * 8, hipMemcpyHostToDevice, h->stream));
+        if (h->d_nul[v]) HIP_TRY(hipMemcpyAsync(h->d_nul[v], h->h_nul[b][v], n, hipMemcpyHostToDevice, h->stream));
     }
     HIP_TRY(hipEventRecord(h->stage_ev[b], h->stream));
     const void* vals[FW_MAX_COLS];
-    for (int v = 0; v < FW_MAX_COLS; v++) vals[v] = h->d_val[v];
-    return push(h, n, h->d_key, h->d_ts, h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED ? h->d_kh : nullptr, vals);
+    const uint8_t* nuls[FW_MAX_COLS];
+    for (int v = 0; v < FW_MAX_COLS; v++) {
+        vals[v] = h->d_val[v];
+        nuls[v] = h->d_nul[v];
+    }
+    return push(h, n, h->d_key, h->d_ts, h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED ? h->d_kh : nullptr, vals, nuls);
 }
 
 int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t* d_ts, const int32_t* d_key_hash,
-                   const void* const* d_values) {
+                   const void* const* d_values, const uint8_t* const* d_nulls) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     if (n < 0) return fail(FW_E_INVALID, "negative n");
     if (n == 0) return FW_OK;
     if (!d_key || !d_ts) return fail(FW_E_INVALID, "null key/ts column");
     if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED && !d_key_hash) return fail(FW_E_INVALID, "key_hash column required");
     if (h->nv > 0 && !d_values) return fail(FW_E_INVALID, "value columns required");
-    for (int s = 0; s < h->nv; s++)
-        if (!d_values[h->slot_col[s]]) return fail(FW_E_INVALID, "value column %d is NULL", h->slot_col[s]);
-    return push(h, n, d_key, d_ts, d_key_hash, d_values);
+    for (int s = 0; s < h->nv; s++) {
+        const int v = h->slot_col[s];
+        if (!d_values[v]) return fail(FW_E_INVALID, "value column %d is NULL", v);
+        if (((h->cfg.nullable_cols >> v) & 1u) && (!d_nulls || !d_nulls[v]))
+            return fail(FW_E_INVALID, "nullable value column %d needs its null-flag column", v);
+    }
+    return push(h, n, d_key, d_ts, d_key_hash, d_values, d_nulls);
 }
 
 int fw_advance(fw_handle* h, int64_t watermark) {
@@ -786,13 +860,43 @@ int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
     return FW_OK;
 }
 
+// Fingerprint of everything that gives the stored words their meaning: API, phase, window kind,
+// size, slice interval, offset, key hashing, maxParallelism and the accumulator word layout (op,
+// value column, NULL gate per word).  A blob is only restored into an operator with the same one.
+static uint64_t semantics_fingerprint(const fw_handle* h) {
+    uint64_t x = 0xcbf29ce484222325ull;
+    auto mix = [&](int64_t v) {
+        for (int b = 0; b < 8; b++) {
+            x ^= (uint64_t)((v >> (8 * b)) & 0xff);
+            x *= 0x100000001b3ull;
+        }
+    };
+    const fw_config& c = h->cfg;
+    mix(c.api);
+    mix(c.agg_phase);
+    mix(h->win.kind);
+    mix(h->win.size);
+    mix(h->win.interval);
+    mix(h->win.offset);
+    mix(h->ks.hash_kind);
+    mix(h->ks.max_p);
+    mix(h->wd.nw);
+    for (int w = 0; w < h->wd.nw; w++) {
+        mix(h->wd.op[w]);
+        mix(h->slot_col[h->wd.col[w]]);
+        mix(h->wd.gate[w]);
+    }
+    return x;
+}
+
 // ---- snapshot: [header][state_count[n_sb]][entries of sb 0][entries of sb 1]...
 struct SnapHeader {
     uint64_t magic;
     int32_t version, n_sb, cap_e, pwe;
     int64_t cur, late_dropped, fired, live;
+    uint64_t semantics;
 };
-static const uint64_t SNAP_MAGIC = 0x464c4b57494e3031ull;  // "FLKWIN01"
+static const uint64_t SNAP_MAGIC = 0x464c4b57494e3032ull;  // "FLKWIN02"
 
 int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     if (!h || !size) return fail(FW_E_INVALID, "null argument");
@@ -809,7 +913,7 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    SnapHeader hd{SNAP_MAGIC, 1, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, 0, total};
+    SnapHeader hd{SNAP_MAGIC, 2, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, 0, total, semantics_fingerprint(h)};
     char* p = (char*)buf;
     memcpy(p, &hd, sizeof hd);
     p += sizeof hd;
@@ -830,8 +934,10 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     if (size < (int64_t)sizeof hd) return fail(FW_E_INVALID, "snapshot truncated");
     memcpy(&hd, buf, sizeof hd);
     const int nsb = h->ks.n_sb, pwe = 3 + h->nw_t;
-    if (hd.magic != SNAP_MAGIC || hd.n_sb != nsb || hd.pwe != pwe || hd.cap_e != h->cap_e)
+    if (hd.magic != SNAP_MAGIC || hd.n_sb != nsb || hd.pwe != pwe || hd.cap_e != h->cap_e ||
+        hd.semantics != semantics_fingerprint(h))
         return fail(FW_E_INVALID, "snapshot layout does not match this operator configuration");
+    if (size < (int64_t)sizeof hd + 4ll * nsb + hd.live * pwe * 8) return fail(FW_E_INVALID, "snapshot truncated");
     const char* p = (const char*)buf + sizeof hd;
     std::vector<int32_t> cnt(nsb);
     memcpy(cnt.data(), p, 4ll * nsb);
@@ -853,14 +959,17 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     Ctrl c;
     HIP_TRY(hipMemcpy(&c, h->ctrl, sizeof c, hipMemcpyDeviceToHost));
-    c.cur = hd.cur;  // union-list watermark state (WindowAggOperator.initializeState :183-206)
+    // SQL: union-list watermark state (WindowAggOperator.initializeState :183-206).  DataStream:
+    // the WindowOperator keeps no watermark state, its timer service restarts at Long.MIN_VALUE
+    // (InternalTimerServiceImpl.java:72) until the next watermark arrives.
+    c.cur = h->cfg.api == FW_API_SQL ? hd.cur : INT64_MIN;
     c.ntp = INT64_MIN;
     c.late_dropped = (uint64_t)hd.late_dropped;
     c.fired = (uint64_t)hd.fired;
     c.live_entries = hd.live;
     HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
     h->pushes_ub = 0;
-    h->host_cur = hd.cur;
+    h->host_cur = c.cur;
     return FW_OK;
 }
 
@@ -876,8 +985,9 @@ struct KgHeader {
     uint64_t magic;
     int32_t version, key_group, pwe, nw, sb_log2, hash_kind;
     int64_t win_size, win_interval, cur, n;
+    uint64_t semantics;
 };
-static const uint64_t KG_MAGIC = 0x464c4b574b473031ull;  // "FLKWKG01"
+static const uint64_t KG_MAGIC = 0x464c4b574b473032ull;  // "FLKWKG02"
 
 int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t capacity, int64_t* size) {
     if (!h || !size) return fail(FW_E_INVALID, "null argument");
@@ -897,7 +1007,8 @@ int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t ca
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    KgHeader hd{KG_MAGIC, 1, key_group, pwe, h->wd.nw, L, ks.hash_kind, h->win.size, h->win.interval, c.cur, total};
+    KgHeader hd{KG_MAGIC, 2, key_group, pwe, h->wd.nw, L, ks.hash_kind, h->win.size, h->win.interval, c.cur, total,
+                semantics_fingerprint(h)};
     memcpy(buf, &hd, sizeof hd);
     uint64_t* e = (uint64_t*)((char*)buf + sizeof hd);
     for (int q = 0; q < nsub; q++) {
@@ -917,9 +1028,9 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
     memcpy(&hd, buf, sizeof hd);
     const KeySpace& ks = h->ks;
     const int pwe = 3 + h->nw_t, L = ks.sb_per_kg_log2;
-    if (hd.magic != KG_MAGIC || hd.version != 1) return fail(FW_E_INVALID, "not a key-group snapshot");
+    if (hd.magic != KG_MAGIC || hd.version != 2) return fail(FW_E_INVALID, "not a key-group snapshot");
     if (hd.pwe != pwe || hd.nw != h->wd.nw || hd.hash_kind != ks.hash_kind || hd.win_size != h->win.size ||
-        hd.win_interval != h->win.interval)
+        hd.win_interval != h->win.interval || hd.semantics != semantics_fingerprint(h))
         return fail(FW_E_INVALID, "key-group snapshot of a different operator configuration");
     if (size < (int64_t)sizeof hd + hd.n * pwe * 8) return fail(FW_E_INVALID, "key-group snapshot truncated");
     const int li = hd.key_group - ks.kg_start;
@@ -949,6 +1060,9 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
     std::vector<int64_t> mins(nsub);
     HIP_TRY(hipMemcpy(cnt.data(), h->state_count + ((size_t)li << L), sizeof(int32_t) * nsub, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(mins.data(), h->sb_min_timer + ((size_t)li << L), sizeof(int64_t) * nsub, hipMemcpyDeviceToHost));
+    for (int q = 0; q < nsub; q++)
+        if (cnt[q] != 0)  // restored twice, or restored after records of this key group arrived
+            return fail(FW_E_STATE, "key group %d already holds state in this subtask", hd.key_group);
     for (int q = 0; q < nsub; q++)
         if (cnt[q] + (int64_t)(per[q].size() / pwe) > h->cap_e)
             return fail(FW_E_CAPACITY, "restored key group %d exceeds the state table (%lld entries per superbucket)",

@@ -52,26 +52,47 @@ __host__ __device__ inline int64_t cell_chunk(int64_t f) {
     return (tile >> 3) * 128 + (tile & 7) + 8 * (f & 15);
 }
 
-// Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words.
+// Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words, except SQL
+// MIN/MAX(DOUBLE), whose strict-comparison-in-arrival-order semantics need a small word group.
 enum WordOp : int32_t {
-    W_CNT = 0,    // += 1                       COUNT(*), COUNT(col), AVG count
+    W_CNT = 0,    // += 1                       COUNT(*), COUNT(col), AVG count (gated: non-null rows)
     W_SUM_I = 1,  // += v (64-bit wrap)         SUM(BIGINT/INT), AVG(BIGINT/INT) sum
     W_SUM_F = 2,  // += v (IEEE double)         SUM(DOUBLE), AVG(DOUBLE) sum
     W_MIN_I = 3,  // min (signed)               MIN(BIGINT/INT)
     W_MAX_I = 4,  // max (signed)               MAX(BIGINT/INT)
-    W_MIN_D = 5,  // min over dkey(v)           MIN(DOUBLE)
-    W_MAX_D = 6   // max over dkey(v)           MAX(DOUBLE)
+    W_MIN_D = 5,  // min over dkey(v)           DataStream min(double): Double.compare order
+    W_MAX_D = 6,  // max over dkey(v)           DataStream max(double)
+    // SQL MIN/MAX(DOUBLE): MinAggFunction/MaxAggFunction keep the first value and replace it only
+    // on a strict `<` / `>` (MaxAggFunction.java:63-72), in arrival order.  So the result is NaN
+    // iff the first non-null value is NaN (NaN compares false both ways), else the min/max of the
+    // non-NaN values with ties (only -0.0 == +0.0 are equal with different bits) going to the
+    // earliest arrival.  That decomposes into order-insensitive atomics over an arrival ordinal
+    // `ord` (32 bits, unique per record within one flush; state from earlier flushes has ord 0):
+    W_QMIN = 7,    // signed min of dkey(v), -0.0 folded into +0.0, over non-NaN values
+    W_QMAX = 8,    // signed max of the same key
+    W_QFIRST = 9,  // unsigned min of ord << 32 | (isNaN ? bits >> 32 : 0) over non-null values
+                   //   (the high half of a NaN is never 0: its exponent bits are all ones)
+    W_QNANLO = 10, // unsigned min of ord << 32 | (bits & 0xffffffff) over NaN values
+    W_QZERO = 11,  // unsigned min of ord << 1 | sign over +-0.0 values
+    W_CNTV = 12    // += v                      GLOBAL phase: a local COUNT / AVG count column
 };
 
 FW_HD uint64_t word_identity(int32_t op) {
     switch (op) {
         case W_MIN_I:
-        case W_MIN_D: return (uint64_t)INT64_MAX;
+        case W_MIN_D:
+        case W_QMIN: return (uint64_t)INT64_MAX;
         case W_MAX_I:
-        case W_MAX_D: return (uint64_t)INT64_MIN;
+        case W_MAX_D:
+        case W_QMAX: return (uint64_t)INT64_MIN;
+        case W_QFIRST:
+        case W_QNANLO:
+        case W_QZERO: return ~0ull;
         default: return 0;  // counts, integer sums, and +0.0 for double sums
     }
 }
+FW_HD bool is_qword(int32_t op) { return op >= W_QMIN && op <= W_QZERO; }
+constexpr uint64_t Q_EMPTY = ~0ull;
 
 // Entry flags of the HBM slice-state table.
 constexpr uint32_t F_ACC = 1u;    // windowState(key, slice) != null
@@ -166,7 +187,10 @@ FW_HD int32_t superbucket_of(const KeySpace& ks, int64_t key, int32_t pre) {
 struct WordDesc {
     int32_t nw;
     int32_t op[MAX_WORDS];
-    int32_t col[MAX_WORDS];
+    int32_t col[MAX_WORDS];   // value slot the word reads
+    int32_t gate[MAX_WORDS];  // value slot whose NULL rows the word skips, -1: none (COUNT(*))
+    int32_t qfirst[MAX_WORDS];  // W_QNANLO / W_QMIN / W_QMAX: the W_QFIRST word of its group
+    int32_t has_q;            // any W_Q* word (write-back normalisation, fire-time merges)
 };
 
 struct AggDesc {
@@ -174,8 +198,11 @@ struct AggDesc {
     int32_t kind[FW_MAX_AGGS];
     int32_t type[FW_MAX_AGGS];
     int32_t w0[FW_MAX_AGGS];
-    int32_t w1[FW_MAX_AGGS];
-    int32_t count_word;  // word holding COUNT(*) for emptiness / null rules, -1 if none
+    int32_t w1[FW_MAX_AGGS];  // AVG count word
+    int32_t nn[FW_MAX_AGGS];  // word whose value 0 makes SUM / MIN / MAX NULL, -1: never
+    int32_t qf[FW_MAX_AGGS];  // SQL MIN/MAX(DOUBLE): W_QFIRST, W_QNANLO, W_QZERO words (else -1)
+    int32_t qn[FW_MAX_AGGS];
+    int32_t qz[FW_MAX_AGGS];
     int32_t count_star_word;  // word of the SQL indexOfCountStar aggregate, -1 if none
 };
 
@@ -184,6 +211,7 @@ struct IngestArgs {
     const int64_t* ts;
     const int32_t* khash;
     const uint64_t* vals[MAX_KCOLS];
+    const uint8_t* nulls[MAX_KCOLS];  // null flags per value slot (nullptr: NOT NULL column)
     int64_t n;
     WinDesc win;
     KeySpace ks;
@@ -202,6 +230,7 @@ struct IngestArgs {
     int64_t* treq;         // timer requests: (key, window, sb) triples
     int64_t treq_cap;
     int32_t lds_bytes;     // dynamic LDS of the launch (IG_LDS)
+    int32_t local;         // LOCAL phase: no late-record handling (LocalSlicingWindowAggOperator)
     int32_t ablate;        // development only (FW_ABLATE env): skip phases to time the others
 };
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
@@ -235,6 +264,7 @@ struct MergeArgs {
     WordDesc wd;
     AggDesc ad;
     int32_t always_flush;    // DataStream: state is updated per record, flush every advance
+    int32_t local;           // LOCAL phase: emit every gathered (key, slice) partial, keep no state
     int64_t* out_key;        // output slabs: [n_sb][slab_cap] rows, then out_cap overflow rows
     int64_t* out_ws;
     int64_t* out_we;

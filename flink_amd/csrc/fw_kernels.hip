@@ -52,37 +52,137 @@ __device__ __forceinline__ uint64_t pick_col(const uint64_t (&v)[N], int32_t col
     return r;
 }
 
-// value of one accumulator word for a single record (accumulate on the identity)
-__device__ __forceinline__ uint64_t record_word(int32_t op, uint64_t v) {
+__device__ __forceinline__ bool f64_isnan(uint64_t b) { return (b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull; }
+__device__ __forceinline__ bool f64_iszero(uint64_t b) { return (b & 0x7FFFFFFFFFFFFFFFull) == 0; }
+
+// value of one accumulator word for a single non-NULL record (accumulate on the identity);
+// `ord` >= 1 is the record's arrival ordinal within the flush (W_Q* words only)
+__device__ __forceinline__ uint64_t record_word(int32_t op, uint64_t v, uint32_t ord) {
     switch (op) {
         case W_CNT: return 1;
         case W_MIN_D:
         case W_MAX_D: return (uint64_t)dkey(v);
-        default: return v;  // SUM_I, SUM_F (bits), MIN_I, MAX_I
+        case W_QMIN:
+        case W_QMAX: return f64_isnan(v) ? word_identity(op) : f64_iszero(v) ? 0ull : (uint64_t)dkey(v);
+        case W_QFIRST: return ((uint64_t)ord << 32) | (f64_isnan(v) ? (v >> 32) : 0ull);
+        case W_QNANLO: return f64_isnan(v) ? (((uint64_t)ord << 32) | (v & 0xFFFFFFFFull)) : Q_EMPTY;
+        case W_QZERO: return f64_iszero(v) ? (((uint64_t)ord << 1) | (v >> 63)) : Q_EMPTY;
+        default: return v;  // SUM_I, SUM_F (bits), MIN_I, MAX_I, CNTV
     }
 }
+// a record's word, honouring the word's NULL gate (null_slots: bit s = value slot s is NULL)
+__device__ __forceinline__ uint64_t gated_word(const WordDesc& wd, int w, uint64_t v, uint32_t null_slots, uint32_t ord) {
+    const int32_t g = wd.gate[w];
+    if (g >= 0 && ((null_slots >> g) & 1u)) return word_identity(wd.op[w]);
+    return record_word(wd.op[w], v, ord);
+}
 
-// atomically fold `v` into an LDS accumulator word
+// atomically fold `v` into an LDS accumulator word (element-level combine: commutative)
 __device__ __forceinline__ void lds_fold(int32_t op, uint64_t* slot, uint64_t v) {
     switch (op) {
         case W_CNT:
+        case W_CNTV:
         case W_SUM_I: __hip_atomic_fetch_add(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
         case W_SUM_F: __hip_atomic_fetch_add((double*)slot, as_f64(v), __ATOMIC_RELAXED, LDS_SCOPE); break;
         case W_MIN_I:
-        case W_MIN_D: __hip_atomic_fetch_min((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+        case W_MIN_D:
+        case W_QMIN: __hip_atomic_fetch_min((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+        case W_QFIRST:
+        case W_QNANLO:
+        case W_QZERO: __hip_atomic_fetch_min(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
         default: __hip_atomic_fetch_max((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
     }
 }
 
-// fold in registers (used when merging slices at fire time, in the reference's order)
+// element-level fold in registers
 __device__ __forceinline__ uint64_t reg_fold(int32_t op, uint64_t a, uint64_t b) {
     switch (op) {
         case W_CNT:
+        case W_CNTV:
         case W_SUM_I: return a + b;
         case W_SUM_F: return f64_bits(as_f64(a) + as_f64(b));
         case W_MIN_I:
-        case W_MIN_D: return (int64_t)a < (int64_t)b ? a : b;
+        case W_MIN_D:
+        case W_QMIN: return (int64_t)a < (int64_t)b ? a : b;
+        case W_QFIRST:
+        case W_QNANLO:
+        case W_QZERO: return a < b ? a : b;
         default: return (int64_t)a > (int64_t)b ? a : b;
+    }
+}
+
+// ---- SQL MIN/MAX(DOUBLE) word groups ------------------------------------------------------
+// result of aggregate g from its words: the NaN that arrived first, else the extremum of the
+// non-NaN values (a zero takes the sign of the earliest zero); *isnull when no non-NULL value
+__device__ __forceinline__ uint64_t q_result(const AggDesc& ad, int g, const uint64_t* acc, bool* isnull) {
+    const uint64_t f = acc[ad.qf[g]];
+    *isnull = f == Q_EMPTY;
+    if (*isnull) return 0;
+    if ((uint32_t)f) return (f << 32) | (acc[ad.qn[g]] & 0xFFFFFFFFull);
+    const int64_t k = (int64_t)acc[ad.w0[g]];
+    if (k != 0) return dkey_inv(k);
+    const uint64_t z = acc[ad.qz[g]];
+    return z != Q_EMPTY ? ((z & 1ull) << 63) : 0ull;
+}
+
+// words of a group after the write-back of a flush: every recorded ordinal becomes 0 ("earlier
+// than anything a later flush adds"), and a non-NaN-first group forgets its NaNs
+__device__ __forceinline__ uint64_t q_normalise(const WordDesc& wd, int w, const uint64_t* acc) {
+    const uint64_t v = acc[w];
+    switch (wd.op[w]) {
+        case W_QFIRST: return v != Q_EMPTY ? (v & 0xFFFFFFFFull) : v;
+        case W_QZERO: return v != Q_EMPTY ? (v & 1ull) : v;
+        case W_QNANLO: {
+            const uint64_t f = acc[wd.qfirst[w]];
+            return (f != Q_EMPTY && (uint32_t)f) ? (v & 0xFFFFFFFFull) : Q_EMPTY;
+        }
+        default: return v;
+    }
+}
+
+// slice merge at fire time, in the reference's order: acc = merge(acc, other) with the aggregates'
+// mergeExpressions (acc earlier).  Counts and sums add; integer and DataStream min/max are order
+// free; SQL MIN/MAX(DOUBLE) compare result values with a strict `<` / `>` (MaxAggFunction.java:82-95)
+// and the merged value is re-encoded as one element with ordinal 0.
+template <int NW>
+__device__ __forceinline__ void merge_slice(const WordDesc& wd, const AggDesc& ad, uint64_t* acc, const uint64_t* other) {
+    uint64_t res[FW_MAX_AGGS];
+    bool nul[FW_MAX_AGGS];
+    if (wd.has_q) {
+        for (int g = 0; g < ad.n; g++) {
+            if (ad.qf[g] < 0) continue;
+            bool na, no;
+            const uint64_t ra = q_result(ad, g, acc, &na);
+            const uint64_t ro = q_result(ad, g, other, &no);
+            const bool take = !no && (na || (ad.kind[g] == FW_AGG_MAX ? as_f64(ro) > as_f64(ra) : as_f64(ro) < as_f64(ra)));
+            res[g] = take ? ro : ra;
+            nul[g] = na && no;
+        }
+    }
+#pragma unroll
+    for (int w = 0; w < NW; w++)
+        if (w < wd.nw && !is_qword(wd.op[w])) acc[w] = reg_fold(wd.op[w], acc[w], other[w]);
+    if (wd.has_q) {
+        for (int g = 0; g < ad.n; g++)
+            if (ad.qf[g] >= 0) {
+                acc[ad.qf[g]] = Q_EMPTY;
+                acc[ad.qn[g]] = Q_EMPTY;
+                acc[ad.qz[g]] = Q_EMPTY;
+            }
+        for (int g = 0; g < ad.n; g++) {
+            if (ad.qf[g] < 0) continue;
+            const int op = wd.op[ad.w0[g]];
+            if (nul[g]) {
+                acc[ad.w0[g]] = word_identity(op);
+                continue;
+            }
+            const uint64_t b = res[g];
+            const bool nan = f64_isnan(b);
+            acc[ad.qf[g]] = nan ? (b >> 32) : 0ull;
+            if (nan) acc[ad.qn[g]] = b & 0xFFFFFFFFull;
+            if (f64_iszero(b)) acc[ad.qz[g]] = b >> 63;
+            acc[ad.w0[g]] = nan ? word_identity(op) : f64_iszero(b) ? 0ull : (uint64_t)dkey(b);
+        }
     }
 }
 
@@ -217,6 +317,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     int64_t rk[RPT], rs[RPT];
     uint64_t rv[RPT][NVR];
     int32_t pre[RPT];
+    uint32_t rnul[RPT];  // bit q: value slot q is NULL in this row
     uint32_t valid = 0;
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
@@ -224,6 +325,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         rk[j] = 0;
         rs[j] = 0;
         pre[j] = 0;
+        rnul[j] = 0;
 #pragma unroll
         for (int q = 0; q < NVR; q++) rv[j][q] = 0;
         if (i < a.n) {
@@ -231,10 +333,15 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             rs[j] = a.ts[i];
             if (a.khash) pre[j] = a.khash[i];
 #pragma unroll
-            for (int q = 0; q < NV; q++) rv[j][q] = a.vals[q][i];
+            for (int q = 0; q < NV; q++) {
+                rv[j][q] = a.vals[q][i];
+                if (a.nulls[q] && a.nulls[q][i]) rnul[j] |= 1u << q;
+            }
             valid |= 1u << j;
         }
     });
+    // arrival ordinal base of this chunk within the flush (W_Q* words; >= 1, see record_word)
+    const uint32_t ord0 = (uint32_t)(slot * a.cap_rows + base) + 1u;
     // slice-aligned base 2^30 ms below the chunk's first row: rows within 2^31 ms of it take
     // the 32-bit path (one mul_hi instead of a 64-bit magic division)
     const bool fast = a.win.fast32 && ts0 > -(1ll << 61) && ts0 < (1ll << 61);
@@ -252,7 +359,10 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         rsb[j] = 0;
         rm[j] = 0;
 #pragma unroll
-        for (int w = 0; w < NW; w++) racc[j][w] = w < a.wd.nw ? record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w])) : 0;
+        for (int w = 0; w < NW; w++)
+            racc[j][w] = w < a.wd.nw ? gated_word(a.wd, w, pick_col(rv[j], a.wd.col[w]), rnul[j],
+                                                  ord0 + (uint32_t)(j * IG_BLOCK + tid))
+                                     : 0;
         if (!(valid & (1u << j))) return;
         rsb[j] = route_key(a.ks, rk[j], pre[j], &rm[j]);
         if ((uint32_t)rsb[j] >= (uint32_t)n_sb) {  // key group not owned by this subtask
@@ -270,7 +380,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             se = slice_end_of(a.win, rs[j]);
         }
         int64_t target = se;
-        if (is_fired(se, cur_wm)) {
+        if (!a.local && is_fired(se, cur_wm)) {
             if (is_fired(last_window_end_of(a.win, se), cur_wm)) {  // late for every window: drop
                 valid &= ~(1u << j);
                 ldrop++;
@@ -656,11 +766,12 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
     a.out_key[i] = key;
     a.out_ws[i] = window_start_of(a.win, we);
     a.out_we[i] = we;
-    const bool no_rows = a.ad.count_word >= 0 && acc[a.ad.count_word] == 0;
     uint32_t nm = 0;
     for (int g = 0; g < a.ad.n; g++) {
         const int32_t kind = a.ad.kind[g], type = a.ad.type[g];
         const uint64_t w0 = acc[a.ad.w0[g]];
+        // SUM / MIN / MAX are NULL without a non-NULL input (SumAggFunction.java:66-69)
+        const bool no_rows = a.ad.nn[g] >= 0 && acc[a.ad.nn[g]] == 0;
         uint64_t v = 0;
         switch (kind) {
             case FW_AGG_COUNT_STAR:
@@ -671,6 +782,12 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
                 break;
             case FW_AGG_MIN:
             case FW_AGG_MAX:
+                if (a.ad.qf[g] >= 0) {
+                    bool isnull;
+                    v = q_result(a.ad, g, acc, &isnull);
+                    if (isnull) nm |= 1u << g;
+                    break;
+                }
                 v = type == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
                 if (no_rows) nm |= 1u << g;
                 break;
@@ -686,7 +803,7 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
                 break;
             }
         }
-        a.out_val[g][i] = v;
+        a.out_val[g][i] = ((nm >> g) & 1u) ? 0ull : v;  // a NULL's value word is 0
     }
     a.out_null[i] = nm;
 }
@@ -735,9 +852,10 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
                 int e2 = eb[j];
                 if (e2 == -2) e2 = find_entry(S, k, ss[j]);
                 if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
+                    uint64_t o[NW];
 #pragma unroll
-                    for (int i = 0; i < NW; i++)
-                        if (i < wd.nw) acc[i] = reg_fold(wd.op[i], acc[i], S.acc[i][e2]);
+                    for (int i = 0; i < NW; i++) o[i] = S.acc[i][e2];
+                    merge_slice<NW>(wd, a.ad, acc, o);
                 }
                 if (ss[j] == s_exp) e_exp = e2;
             }
@@ -766,9 +884,10 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
     if (we != first) {
         const int e2 = e_we = find_entry(S, k, we);
         if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
+            uint64_t o[NW];
 #pragma unroll
-            for (int i = 0; i < NW; i++)
-                if (i < wd.nw) acc[i] = reg_fold(wd.op[i], acc[i], S.acc[i][e2]);
+            for (int i = 0; i < NW; i++) o[i] = S.acc[i][e2];
+            merge_slice<NW>(wd, a.ad, acc, o);
         }
     }
     if (ef >= 0) {  // windowState.update(firstSlice, acc)
@@ -1078,8 +1197,16 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             p[0] = (uint64_t)S.key[e];
             p[1] = (uint64_t)S.slice[e];
             p[2] = f;
+            if (a.wd.has_q) {
+                uint64_t v[NW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];
+                for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
+#pragma unroll
+                for (int w = 0; w < NW; w++) p[3 + w] = w < a.wd.nw ? q_normalise(a.wd, w, v) : v[w];
+            } else {
+#pragma unroll
+                for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];
+            }
             if (f & F_TIMER) lnm = min(lnm, S.slice[e]);
         }
         lnm = wave_min_i64(lnm);
@@ -1290,20 +1417,49 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
                                                         int32_t ncols, int64_t n, int32_t kind, int32_t max_p,
                                                         int32_t p, const uint32_t* offsets, int64_t* okey, int64_t* ots,
                                                         uint64_t* const* ovals) {
-    __shared__ uint32_t h[PART_MAXP];
-    const int tid = threadIdx.x;
+    // Stable: rows keep their input order within a destination (the order a Netty channel
+    // delivers them in, ChannelSelectorRecordWriter.emit :54), so a DOUBLE SUM downstream adds in
+    // the same order on every run.  Each wave ranks its 64 rows per destination with ballots;
+    // the waves of one pass are ordered through a per-wave count table.
+    constexpr int NWV = BLOCK / 64;
+    __shared__ uint32_t h[PART_MAXP];         // next output position per destination
+    __shared__ uint32_t wc[NWV][PART_MAXP];   // rows per (wave, destination) of the current pass
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid < p) h[tid] = offsets[(size_t)blockIdx.x * p + tid];
-    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t b = (int64_t)blockIdx.x * PART_TILE;
-    for (int j = tid; j < PART_TILE; j += BLOCK) {
-        const int64_t i = b + j;
-        if (i >= n) break;
-        const int64_t k = key[i];
-        const int32_t g = key_group_for_hash(java_key_hash(kind, k, 0), max_p);
-        const uint32_t pos = atomicAdd(&h[operator_for_key_group(max_p, p, g)], 1u);
-        okey[pos] = k;
-        ots[pos] = ts[i];
-        for (int c = 0; c < ncols; c++) ovals[c][pos] = vals[c][i];
+    for (int j0 = 0; j0 < PART_TILE; j0 += BLOCK) {
+        const int64_t i = b + j0 + tid;
+        int32_t d = -1;
+        int64_t k = 0;
+        if (i < n) {
+            k = key[i];
+            d = operator_for_key_group(max_p, p, key_group_for_hash(java_key_hash(kind, k, 0), max_p));
+        }
+        uint32_t rank = 0;
+        for (int dd = 0; dd < p; dd++) {
+            const uint64_t m = __ballot(d == dd);
+            if (d == dd) rank = (uint32_t)__popcll(m & lt);
+            if (lane == 0) wc[w][dd] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();  // wc of every wave and h of the previous pass are visible
+        uint32_t pos = 0;
+        if (d >= 0) {
+            pos = h[d] + rank;
+            for (int v = 0; v < w; v++) pos += wc[v][d];
+        }
+        __syncthreads();  // every lane has read h
+        if (tid < p) {
+            uint32_t t = 0;
+            for (int v = 0; v < NWV; v++) t += wc[v][tid];
+            h[tid] += t;
+        }
+        if (d >= 0) {
+            okey[pos] = k;
+            ots[pos] = ts[i];
+            for (int c = 0; c < ncols; c++) ovals[c][pos] = vals[c][i];
+        }
+        __syncthreads();  // h updated before the next pass reads it; wc free to overwrite
     }
 }
 

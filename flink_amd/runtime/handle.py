@@ -13,7 +13,7 @@ from .._native import check, lib
 def _np_view(ptr, n, dtype):
     if n == 0:
         return np.empty(0, dtype)
-    ct = {np.int64: C.c_int64, np.int32: C.c_int32, np.uint32: C.c_uint32, np.uint64: C.c_uint64}[dtype]
+    ct = {np.int64: C.c_int64, np.int32: C.c_int32, np.uint32: C.c_uint32, np.uint64: C.c_uint64, np.uint8: C.c_uint8}[dtype]
     return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,))
 
 
@@ -47,8 +47,9 @@ class WindowAggHandle:
         check(lib().fw_initialize_watermark(self._h, int(wm)))
 
     # ---- ingest
-    def push_host(self, keys, ts, values=(), key_hashes=None):
-        """Host columns -> pinned staging -> device (fw_reserve / fw_commit)."""
+    def push_host(self, keys, ts, values=(), key_hashes=None, nulls=None):
+        """Host columns -> pinned staging -> device (fw_reserve / fw_commit).  ``nulls`` maps a
+        nullable value column to its per-row null flags (bool / uint8, non-zero = SQL NULL)."""
         keys = np.asarray(keys, dtype=np.int64)
         n = len(keys)
         cap = self.cfg.max_batch_rows
@@ -66,11 +67,17 @@ class WindowAggHandle:
                     if v.dtype == np.float64:
                         v = v.view(np.int64)
                     _np_view(cols.values[c], m, np.int64)[:] = v.astype(np.int64, copy=False)[o:o + m]
+                for c in range(self.cfg.n_value_cols):
+                    if self.cfg.nullable_cols >> c & 1:
+                        nf = np.zeros(n, np.uint8) if nulls is None or c not in nulls else \
+                            np.asarray(nulls[c]).astype(np.uint8, copy=False)
+                        _np_view(cols.nulls[c], m, np.uint8)[:] = nf[o:o + m]
             check(lib().fw_commit(self._h, m))
 
-    def push_device(self, keys, ts, values=(), key_hashes=None):
-        """Device-resident columns (torch cuda tensors, int64 / float64).  The handle's stream
-        waits for the producer's current stream before reading them."""
+    def push_device(self, keys, ts, values=(), key_hashes=None, nulls=None):
+        """Device-resident columns (torch cuda tensors, int64 / float64; ``nulls``: {column:
+        uint8 tensor}).  The handle's stream waits for the producer's current stream before
+        reading them."""
         import torch
         n = keys.numel()
         if n == 0:
@@ -80,8 +87,11 @@ class WindowAggHandle:
         arr = (C.c_void_p * abi.FW_MAX_COLS)()
         for c, v in enumerate(values):
             arr[c] = v.data_ptr()
+        nul = (C.c_void_p * abi.FW_MAX_COLS)()
+        for c, v in (nulls or {}).items():
+            nul[c] = v.data_ptr()
         check(lib().fw_push_device(self._h, n, keys.data_ptr(), ts.data_ptr(),
-                                   key_hashes.data_ptr() if key_hashes is not None else None, arr))
+                                   key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
         # the producer stream must not reuse the input memory before the ingest kernel has read
         # it: order the producer's later work after this push (no record_stream: the handle's
         # stream dies with the handle, before torch frees the tensors)
@@ -166,14 +176,16 @@ class WindowAggHandle:
         return out, self.stats()["current_watermark"]
 
     def restore_key_groups(self, blobs, watermarks):
-        """Restore the owned key groups found in `blobs` ({key_group: blob}, any source parallelism);
-        the watermark becomes the min of the union list (WindowAggOperator.initializeState :183-206)."""
+        """Restore the owned key groups found in `blobs` ({key_group: blob}, any source parallelism).
+        SQL: the watermark becomes the min of the union list (WindowAggOperator.initializeState
+        :183-206).  DataStream: the WindowOperator keeps no watermark state; its timer service
+        starts again at Long.MIN_VALUE (InternalTimerServiceImpl.java:72)."""
         lo, hi = self.key_group_range()
         for kg, blob in blobs.items():
             if lo <= kg <= hi:
                 self.restore_key_group_blob(blob)
         wms = list(watermarks)
-        if wms:
+        if wms and self.cfg.api == abi.API_SQL:
             self.initialize_watermark(min(wms))
 
     def restore_key_group_blob(self, blob: bytes):

@@ -61,7 +61,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 1
+#define FW_ABI_VERSION 2
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -87,12 +87,23 @@ typedef enum {
 
 typedef enum {
     FW_AGG_COUNT_STAR = 0,  /* COUNT(*)            Count1AggFunction                    */
-    FW_AGG_COUNT = 1,       /* COUNT(col)          CountAggFunction (non-null inputs)   */
+    FW_AGG_COUNT = 1,       /* COUNT(col)          CountAggFunction (counts non-null)    */
     FW_AGG_SUM = 2,         /* SUM(col)            SumAggFunction / SumAggregator        */
     FW_AGG_MIN = 3,         /* MIN(col)            MinAggFunction / ComparableAggregator */
     FW_AGG_MAX = 4,         /* MAX(col)            MaxAggFunction / ComparableAggregator */
     FW_AGG_AVG = 5          /* AVG(col)            AvgAggFunction                        */
 } fw_agg_kind;
+
+/* Aggregation phase (TwoStageOptimizedWindowAggregateRule.java:80-109).  ONE: the slicing
+   WindowAggOperator with AggCombiner.  LOCAL: LocalSlicingWindowAggOperator + LocalAggCombiner
+   (LocalAggCombiner.java:69-97): no state, no timers; every flush emits one partial accumulator row
+   per (key, sliceEnd).  GLOBAL: WindowAggOperator with GlobalAggCombiner (GlobalAggCombiner.java:77-110):
+   input rows are local accumulators, folded with the aggregates' merge expressions. */
+typedef enum {
+    FW_PHASE_ONE = 0,
+    FW_PHASE_LOCAL = 1,
+    FW_PHASE_GLOBAL = 2
+} fw_agg_phase;
 
 typedef enum {
     FW_T_I64 = 0,           /* BIGINT / long                                            */
@@ -131,10 +142,14 @@ typedef struct {
     fw_agg_desc aggs[FW_MAX_AGGS];
     int32_t n_value_cols;
     int32_t value_col_types[FW_MAX_COLS];
+    uint32_t nullable_cols;   /* bit c: value column c may hold SQL NULLs; every push then
+                                 carries a null-flag column for it (SQL only)               */
+    int32_t agg_phase;        /* fw_agg_phase (SQL only)                                    */
     int32_t max_parallelism;  /* number of key groups (pipeline.max-parallelism)           */
     int32_t parallelism;      /* operator parallelism p                                    */
     int32_t subtask_index;    /* this subtask: owns computeKeyGroupRangeForOperatorIndex   */
     int32_t device;           /* HIP device ordinal                                        */
+    int32_t reserved0;
     int64_t state_capacity;   /* expected max live (key, slice) state entries (sizing hint) */
     int64_t max_batch_rows;   /* max rows per fw_commit / fw_push_device call              */
     int64_t output_capacity;  /* result rows kept between fw_results_reset calls           */
@@ -142,12 +157,16 @@ typedef struct {
 
 typedef struct fw_handle fw_handle;
 
-/* Pinned host staging columns returned by fw_reserve (valid until fw_commit). */
+/* Pinned host staging columns returned by fw_reserve (valid until fw_commit).
+   Null flags are one byte per row, non-zero = SQL NULL: the layout of Flink's heap columnar
+   vectors (AbstractHeapVector.isNull, a boolean[] per column).  A NULL row's value word is
+   ignored.  nulls[c] is non-NULL exactly for the columns in fw_config.nullable_cols. */
 typedef struct {
     int64_t* key;
     int64_t* ts;                       /* event time, epoch ms (rowtime)               */
     int32_t* key_hash;                 /* only for FW_KEYHASH_PRECOMPUTED              */
     int64_t* values[FW_MAX_COLS];      /* int64 or double bits, per value_col_types     */
+    uint8_t* nulls[FW_MAX_COLS];       /* null flags of the nullable columns            */
 } fw_host_cols;
 
 /* Window results: SQL rows are key ++ aggs ++ (window_start, window_end); DataStream
@@ -190,9 +209,11 @@ int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out);
 int fw_commit(fw_handle* h, int64_t n);
 /* Device-resident columns (caller-owned device memory, ordered on the handle stream).
    d_values[c] points at n 8-byte words of value column c; d_key_hash may be NULL unless
-   key_hash == FW_KEYHASH_PRECOMPUTED. */
+   key_hash == FW_KEYHASH_PRECOMPUTED; d_nulls may be NULL unless nullable_cols != 0, and then
+   d_nulls[c] points at n null-flag bytes of each nullable column c. */
 int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t* d_ts,
-                   const int32_t* d_key_hash, const void* const* d_values);
+                   const int32_t* d_key_hash, const void* const* d_values,
+                   const uint8_t* const* d_nulls);
 
 /* ---- progress / output --------------------------------------------------------------- */
 int fw_advance(fw_handle* h, int64_t watermark);

@@ -215,7 +215,7 @@ struct Oracle {
     int64_t epoch = 0;
 
     // RecordsWindowBuffer: (sliceEnd, key) -> records in insertion order
-    struct BufRec { uint64_t vals[FW_MAX_COLS]; };
+    struct BufRec { uint64_t vals[FW_MAX_COLS]; uint8_t nul[FW_MAX_COLS]; };
     std::vector<std::pair<std::pair<int64_t, int64_t>, std::vector<BufRec>>> buffer;
     std::map<std::pair<int64_t, int64_t>, size_t> buffer_index;
     int64_t min_slice_end = INT64_MAX;
@@ -232,17 +232,20 @@ struct Oracle {
     // -------------------------------------------------------------------------------
     Row create_accumulators() const { return Row(); }
 
-    void accumulate(Row& r, const uint64_t* vals) const {
+    // accumulateExpressions; nul[c] != 0: value column c is NULL in this record, and every
+    // aggregate of that column keeps its accumulator (ifThenElse(isNull(operand(0)), acc, ...))
+    void accumulate(Row& r, const uint64_t* vals, const uint8_t* nul) const {
         for (int a = 0; a < cfg.c.n_aggs; a++) {
             const fw_agg_desc& g = cfg.c.aggs[a];
             AggState& s = r.a[a];
+            if (g.kind != FW_AGG_COUNT_STAR && nul[g.input_col]) continue;
             const uint64_t raw = g.kind == FW_AGG_COUNT_STAR ? 0 : vals[g.input_col];
             const bool isf = g.type == FW_T_F64;
             const int64_t iv = (int64_t)raw;
             const double dv = bits_to_double(raw);
             switch (g.kind) {
                 case FW_AGG_COUNT_STAR:  // Count1AggFunction: count + 1
-                case FW_AGG_COUNT:       // CountAggFunction: inputs are NOT NULL here
+                case FW_AGG_COUNT:       // CountAggFunction: count + 1 for a non-NULL operand
                     s.i = jadd64(s.i, 1);
                     s.is_null = false;
                     break;
@@ -392,22 +395,22 @@ struct Oracle {
     // -------------------------------------------------------------------------------
     // SQL: AbstractSliceSyncStateWindowAggProcessor.processElement (:96-126)
     // -------------------------------------------------------------------------------
-    bool sql_process_element(int64_t key, int64_t ts, const uint64_t* vals) {
+    bool sql_process_element(int64_t key, int64_t ts, const uint64_t* vals, const uint8_t* nul) {
         const int64_t slice_end = assign_slice_end(ts);
         if (is_window_fired(slice_end, current_progress)) {
             const int64_t last = get_last_window_end(slice_end);
             if (is_window_fired(last, current_progress)) return true;  // dropped
-            buffer_add(key, merge_target(slice_end), vals);
+            buffer_add(key, merge_target(slice_end), vals, nul);
             int64_t unfired = slice_end;
             while (is_window_fired(unfired, current_progress)) unfired = jadd64(unfired, cfg.interval);
             register_timer(key, unfired);
             return false;
         }
-        buffer_add(key, slice_end, vals);
+        buffer_add(key, slice_end, vals, nul);
         return false;
     }
 
-    void buffer_add(int64_t key, int64_t slice, const uint64_t* vals) {
+    void buffer_add(int64_t key, int64_t slice, const uint64_t* vals, const uint8_t* nul) {
         auto wk = std::make_pair(slice, key);
         auto it = buffer_index.find(wk);
         size_t gi;
@@ -420,6 +423,7 @@ struct Oracle {
         }
         BufRec r;
         std::memcpy(r.vals, vals, sizeof(r.vals));
+        std::memcpy(r.nul, nul, sizeof(r.nul));
         buffer[gi].second.push_back(r);
         min_slice_end = std::min(min_slice_end, slice);
     }
@@ -431,7 +435,7 @@ struct Oracle {
             auto sk = std::make_pair(key, slice);
             auto it = state.find(sk);
             Row acc = it == state.end() ? create_accumulators() : it->second;
-            for (auto& rec : g.second) accumulate(acc, rec.vals);
+            for (auto& rec : g.second) accumulate(acc, rec.vals, rec.nul);
             state[sk] = acc;
             if (!is_window_fired(slice, timer_watermark)) register_timer(key, slice);
         }
@@ -557,6 +561,7 @@ struct Oracle {
     // EventTimeTrigger, allowedLateness = 0, no late side output.
     // -------------------------------------------------------------------------------
     bool ds_process_element(int64_t key, int64_t ts, const uint64_t* vals) {
+        static const uint8_t no_nulls[FW_MAX_COLS] = {0};
         const fw_config& c = cfg.c;
         std::vector<int64_t> starts;
         if (c.window_kind == FW_WIN_TUMBLE) {
@@ -576,7 +581,7 @@ struct Oracle {
             auto sk = std::make_pair(key, end);
             auto it = state.find(sk);
             Row acc = it == state.end() ? create_accumulators() : it->second;
-            accumulate(acc, vals);  // HeapReducingState.add / HeapAggregatingState.add
+            accumulate(acc, vals, no_nulls);  // HeapReducingState.add / HeapAggregatingState.add
             state[sk] = acc;
             // EventTimeTrigger.onElement: maxTs > watermark -> registerEventTimeTimer(maxTs);
             // registerCleanupTimer(window) registers the same (key, window, maxTs) timer.
@@ -607,11 +612,19 @@ struct Oracle {
         epoch++;
     }
 
-    // prepareSnapshotPreBarrier -> windowBuffer.flush(); then a restored operator starts with
-    // nextTriggerProgress = Long.MIN_VALUE and the watermark from union-list state.
+    // SQL: prepareSnapshotPreBarrier -> windowBuffer.flush(); then a restored operator starts with
+    // nextTriggerProgress = Long.MIN_VALUE and the watermark from union-list state
+    // (WindowAggOperator.java:183-206).  DataStream: the WindowOperator snapshots no watermark, so
+    // the restored timer service starts at Long.MIN_VALUE (InternalTimerServiceImpl.java:72) and
+    // nothing is late until the next watermark; state and timers are kept.
     void snapshot_restore() {
         if (!ds) flush();
         next_trigger_progress = INT64_MIN;
+        if (ds) {
+            timer_watermark = INT64_MIN;
+            current_watermark = INT64_MIN;
+            current_progress = INT64_MIN;
+        }
     }
 };
 
@@ -648,14 +661,20 @@ void or_initialize_watermark(void* h, int64_t wm) {
     o->timer_watermark = wm;
 }
 
-// Row-major value columns: vals[col * n + i] (8-byte words).
-int64_t or_process_batch(void* h, int64_t n, const int64_t* key, const int64_t* ts, const uint64_t* vals, int32_t ncols) {
+// Row-major value columns: vals[col * n + i] (8-byte words); nulls[col * n + i] != 0 marks a
+// SQL NULL (nulls may be NULL: no NULLs).
+int64_t or_process_batch(void* h, int64_t n, const int64_t* key, const int64_t* ts, const uint64_t* vals, int32_t ncols,
+                         const uint8_t* nulls) {
     Oracle* o = (Oracle*)h;
     int64_t dropped = 0;
     uint64_t row[FW_MAX_COLS] = {0};
+    uint8_t nul[FW_MAX_COLS] = {0};
     for (int64_t i = 0; i < n; i++) {
-        for (int c = 0; c < ncols; c++) row[c] = vals[(int64_t)c * n + i];
-        bool d = o->ds ? o->ds_process_element(key[i], ts[i], row) : o->sql_process_element(key[i], ts[i], row);
+        for (int c = 0; c < ncols; c++) {
+            row[c] = vals[(int64_t)c * n + i];
+            nul[c] = nulls ? nulls[(int64_t)c * n + i] : 0;
+        }
+        bool d = o->ds ? o->ds_process_element(key[i], ts[i], row) : o->sql_process_element(key[i], ts[i], row, nul);
         if (d) dropped++;
     }
     o->late_dropped += dropped;

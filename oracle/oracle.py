@@ -33,7 +33,7 @@ def lib():
         L.or_destroy.argtypes = [vp]
         L.or_initialize_watermark.argtypes = [vp, i64]
         L.or_process_batch.restype = i64
-        L.or_process_batch.argtypes = [vp, i64, vp, vp, vp, i32]
+        L.or_process_batch.argtypes = [vp, i64, vp, vp, vp, i32, vp]
         L.or_process_watermark.argtypes = [vp, i64]
         L.or_flush.argtypes = [vp]
         L.or_snapshot_restore.argtypes = [vp]
@@ -86,7 +86,8 @@ class OracleOperator:
     def initialize_watermark(self, wm):
         lib().or_initialize_watermark(self.h, int(wm))
 
-    def process_batch(self, keys, ts, values):
+    def process_batch(self, keys, ts, values, nulls=None):
+        """``nulls``: {value column: per-row flags, non-zero = SQL NULL}."""
         keys = np.ascontiguousarray(keys, dtype=np.int64)
         ts = np.ascontiguousarray(ts, dtype=np.int64)
         n = len(keys)
@@ -95,7 +96,12 @@ class OracleOperator:
         for c, v in enumerate(values):
             v = np.asarray(v)
             vals[c] = v.view(np.uint64) if v.dtype in (np.float64, np.int64, np.uint64) else v.astype(np.int64).view(np.uint64)
-        return lib().or_process_batch(self.h, n, _ptr(keys), _ptr(ts), _ptr(vals), ncols)
+        nul = None
+        if nulls:
+            nul = np.zeros((max(ncols, 1), n), dtype=np.uint8)
+            for c, f in nulls.items():
+                nul[c] = np.asarray(f).astype(np.uint8) != 0
+        return lib().or_process_batch(self.h, n, _ptr(keys), _ptr(ts), _ptr(vals), ncols, _ptr(nul))
 
     def process_watermark(self, wm):
         lib().or_process_watermark(self.h, int(wm))

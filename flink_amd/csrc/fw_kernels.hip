@@ -144,11 +144,12 @@ __device__ __forceinline__ uint64_t q_normalise(const WordDesc& wd, int w, const
 // mergeExpressions (acc earlier).  Counts and sums add; integer and DataStream min/max are order
 // free; SQL MIN/MAX(DOUBLE) compare result values with a strict `<` / `>` (MaxAggFunction.java:82-95)
 // and the merged value is re-encoded as one element with ordinal 0.
-template <int NW>
-__device__ __forceinline__ void merge_slice(const WordDesc& wd, const AggDesc& ad, uint64_t* acc, const uint64_t* other) {
+// the SQL-double part, out of line: it only runs in the Q kernel variants and keeps its
+// scratch arrays out of the hot path's register budget
+__device__ __noinline__ void merge_q_groups(const WordDesc& wd, const AggDesc& ad, uint64_t* acc, const uint64_t* other) {
     uint64_t res[FW_MAX_AGGS];
     bool nul[FW_MAX_AGGS];
-    if (wd.has_q) {
+    {
         for (int g = 0; g < ad.n; g++) {
             if (ad.qf[g] < 0) continue;
             bool na, no;
@@ -159,10 +160,7 @@ __device__ __forceinline__ void merge_slice(const WordDesc& wd, const AggDesc& a
             nul[g] = na && no;
         }
     }
-#pragma unroll
-    for (int w = 0; w < NW; w++)
-        if (w < wd.nw && !is_qword(wd.op[w])) acc[w] = reg_fold(wd.op[w], acc[w], other[w]);
-    if (wd.has_q) {
+    {
         for (int g = 0; g < ad.n; g++)
             if (ad.qf[g] >= 0) {
                 acc[ad.qf[g]] = Q_EMPTY;
@@ -183,6 +181,27 @@ __device__ __forceinline__ void merge_slice(const WordDesc& wd, const AggDesc& a
             if (f64_iszero(b)) acc[ad.qz[g]] = b >> 63;
             acc[ad.w0[g]] = nan ? word_identity(op) : f64_iszero(b) ? 0ull : (uint64_t)dkey(b);
         }
+    }
+}
+
+template <int NW, bool Q>
+__device__ __forceinline__ void merge_slice(const WordDesc& wd, const AggDesc& ad, uint64_t* acc, const uint64_t* other) {
+    if constexpr (Q) {
+        // acc/other travel through memory for the out-of-line group merge
+        uint64_t a2[MAX_WORDS], o2[MAX_WORDS];
+#pragma unroll
+        for (int w = 0; w < MAX_WORDS; w++) {
+            a2[w] = w < NW ? acc[w] : 0;
+            o2[w] = w < NW ? other[w] : 0;
+        }
+        merge_q_groups(wd, ad, a2, o2);
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            acc[w] = (w < wd.nw && !is_qword(wd.op[w])) ? reg_fold(wd.op[w], acc[w], other[w]) : a2[w];
+    } else {
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            if (w < wd.nw) acc[w] = reg_fold(wd.op[w], acc[w], other[w]);
     }
 }
 
@@ -270,7 +289,8 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, 
     return v;
 }
 
-template <int NV, int NW, int RPT>
+// X: the configuration has nullable columns or SQL MIN/MAX(DOUBLE) words (gates, ordinals)
+template <int NV, int NW, int RPT, bool X>
 __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int CH = IG_BLOCK * RPT;
     constexpr int NSUB = RPT / IG_SRPT;
@@ -335,7 +355,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
 #pragma unroll
             for (int q = 0; q < NV; q++) {
                 rv[j][q] = a.vals[q][i];
-                if (a.nulls[q] && a.nulls[q][i]) rnul[j] |= 1u << q;
+                if (X && a.nulls[q] && a.nulls[q][i]) rnul[j] |= 1u << q;
             }
             valid |= 1u << j;
         }
@@ -360,9 +380,10 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         rm[j] = 0;
 #pragma unroll
         for (int w = 0; w < NW; w++)
-            racc[j][w] = w < a.wd.nw ? gated_word(a.wd, w, pick_col(rv[j], a.wd.col[w]), rnul[j],
-                                                  ord0 + (uint32_t)(j * IG_BLOCK + tid))
-                                     : 0;
+            racc[j][w] = w >= a.wd.nw ? 0
+                         : X ? gated_word(a.wd, w, pick_col(rv[j], a.wd.col[w]), rnul[j],
+                                          ord0 + (uint32_t)(j * IG_BLOCK + tid))
+                             : record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w]), 0);
         if (!(valid & (1u << j))) return;
         rsb[j] = route_key(a.ks, rk[j], pre[j], &rm[j]);
         if ((uint32_t)rsb[j] >= (uint32_t)n_sb) {  // key group not owned by this subtask
@@ -747,7 +768,7 @@ __device__ __forceinline__ void set_timer(StateLds<NW, E>& S, int e, int64_t W) 
 // Emission is atomic-free at device scope: each superbucket appends to its own output slab
 // (LDS cursor); only slab overflow falls back to a shared overflow region.  fw_results compacts
 // slabs + overflow into one contiguous result set on demand (k_compact_*).
-template <int NW>
+template <int NW, bool Q>
 __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
     Ctrl* c = a.ctrl;
     if (a.ablate & AB_M_NO_EMIT) return;
@@ -782,7 +803,7 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
                 break;
             case FW_AGG_MIN:
             case FW_AGG_MAX:
-                if (a.ad.qf[g] >= 0) {
+                if (Q && a.ad.qf[g] >= 0) {
                     bool isnull;
                     v = q_result(a.ad, g, acc, &isnull);
                     if (isnull) nm |= 1u << g;
@@ -808,7 +829,7 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
     a.out_null[i] = nm;
 }
 
-template <int NW, int E>
+template <int NW, int E, bool Q>
 __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t we, int sb, int32_t* s_emit) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
@@ -824,7 +845,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
             for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
         }
         nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
-        if (nonempty) emit_row<NW>(a, sb, s_emit, k, we, acc);
+        if (nonempty) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
         atomicAnd(&S.flag[e], ~F_ACC);  // clearWindow: expiredSlices(we) = [we]
         return;
     }
@@ -855,14 +876,14 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
                     uint64_t o[NW];
 #pragma unroll
                     for (int i = 0; i < NW; i++) o[i] = S.acc[i][e2];
-                    merge_slice<NW>(wd, a.ad, acc, o);
+                    merge_slice<NW, Q>(wd, a.ad, acc, o);
                 }
                 if (ss[j] == s_exp) e_exp = e2;
             }
         }
         nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
         if (nonempty) {
-            emit_row<NW>(a, sb, s_emit, k, we, acc);
+            emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
             // nextTriggerWindow: register windowEnd + sliceSize while the window is non-empty
             const int e3 = find_or_insert(S, k, wadd(we, w.interval), wd);
             if (e3 >= 0) set_timer(S, e3, a.wm);
@@ -887,7 +908,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
             uint64_t o[NW];
 #pragma unroll
             for (int i = 0; i < NW; i++) o[i] = S.acc[i][e2];
-            merge_slice<NW>(wd, a.ad, acc, o);
+            merge_slice<NW, Q>(wd, a.ad, acc, o);
         }
     }
     if (ef >= 0) {  // windowState.update(firstSlice, acc)
@@ -896,7 +917,7 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
         atomicOr(&S.flag[ef], F_ACC);
     }
     nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
-    if (nonempty) emit_row<NW>(a, sb, s_emit, k, we, acc);
+    if (nonempty) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
     const int64_t next = wadd(we, w.interval);
     const int64_t last = wadd(ws, w.size);
     if (!(next > last)) {
@@ -943,7 +964,7 @@ __device__ __forceinline__ int sb_of_block(int b, int n_sb) {
     return (b % 8) * (n_sb / 8) + b / 8;
 }
 
-template <int NW, int E>
+template <int NW, int E, bool Q>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
@@ -1168,7 +1189,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     const int e = S.due[q];
                     if ((S.flag[e] & F_TIMER) && S.slice[e] == v) {
                         atomicAnd(&S.flag[e], ~F_TIMER);
-                        fire_one(a, S, e, v, sb, &s_emit);
+                        fire_one<NW, E, Q>(a, S, e, v, sb, &s_emit);
                         nf++;
                     }
                 }
@@ -1197,7 +1218,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             p[0] = (uint64_t)S.key[e];
             p[1] = (uint64_t)S.slice[e];
             p[2] = f;
-            if (a.wd.has_q) {
+            if (Q) {
                 uint64_t v[NW];
 #pragma unroll
                 for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
@@ -1291,14 +1312,14 @@ hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
 // ---------------------------------------------------------------------------------------
 // template dispatch
 // ---------------------------------------------------------------------------------------
-template <int NV, int NW>
-static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
+template <int NV, int NW, bool X>
+static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
     constexpr int RPT = ig_rpt(NW);
     const int64_t nch = a.n_chunks;
     if (nch == 0) return hipSuccess;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT, X>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, IG_LDS);
         if (e != hipSuccess) return e;
         attr_set = true;
@@ -1306,12 +1327,19 @@ static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
     // the fold table and the histogram must fit the dynamic LDS
     if ((int64_t)(IG_HDR_WORDS + ig_hist_words(a.ks.n_sb)) * 8 + ig_fold_bytes(NW) > a.lds_bytes) return hipErrorInvalidValue;
     kt_mark(t, FW_KT_REDUCE, false, s);
-    hipLaunchKernelGGL((k_ingest<NV, NW, RPT>), dim3((unsigned)nch), dim3(IG_BLOCK), a.lds_bytes, s, a);
+    hipLaunchKernelGGL((k_ingest<NV, NW, RPT, X>), dim3((unsigned)nch), dim3(IG_BLOCK), a.lds_bytes, s, a);
     kt_mark(t, FW_KT_REDUCE, true, s);
     kt_mark(t, FW_KT_OTHER, false, s);
     hipLaunchKernelGGL(k_push_stats, dim3(1), dim3(BLOCK), 0, s, a.chunk_stats, nch, a.ctrl, a.slot_nch);
     kt_mark(t, FW_KT_OTHER, true, s);
     return hipGetLastError();
+}
+
+template <int NV, int NW>
+static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
+    bool x = a.wd.has_q != 0;
+    for (int q = 0; q < MAX_KCOLS; q++) x = x || a.nulls[q] != nullptr;
+    return x ? ingest_x<NV, NW, true>(a, s, t) : ingest_x<NV, NW, false>(a, s, t);
 }
 
 template <int NV>
@@ -1334,7 +1362,10 @@ hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t) {
 
 template <int NW>
 static hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((k_merge_fire<NW, mg_entries(NW)>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
+    if (a.wd.has_q)
+        hipLaunchKernelGGL((k_merge_fire<NW, mg_entries(NW), true>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_merge_fire<NW, mg_entries(NW), false>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
     return hipGetLastError();
 }
 

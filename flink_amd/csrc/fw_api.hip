@@ -125,6 +125,7 @@ struct fw_handle {
     int nv = 0;
     int slot_col[MAX_KCOLS] = {0, 0, 0, 0};
     int nw_t = 1;  // template word count (layout stride)
+    int n_out = 1; // result value columns (aggregates; LOCAL phase: accumulator fields)
     int64_t cap_rows = 0;     // rows per partial-buffer slot (= max rows per push piece)
     int64_t chunk_rows = 0;   // rows per ingest chunk (IG_BLOCK * ig_rpt(nw_t))
     int64_t max_nch = 0;      // ingest chunks per push piece
@@ -274,6 +275,44 @@ int validate_and_plan(fw_handle* h) {
         ad.w1[g] = ad.nn[g] = ad.qf[g] = ad.qn[g] = ad.qz[g] = -1;
         if (d.type < FW_T_I64 || d.type > FW_T_I32) return fail(FW_E_INVALID, "agg %d: bad type", g);
         int slot = 0, gate = -1;
+        const bool global = c.agg_phase == FW_PHASE_GLOBAL;
+        if (global) {
+            // GLOBAL phase (GlobalAggCombiner.combine :77-110): the value columns are the local
+            // accumulator fields the LOCAL phase emits, and every aggregate folds them with its
+            // mergeExpressions: counts add, sums add (NULL-able), MIN/MAX compare, AVG adds its
+            // (sum, count) pair.  Local counts and AVG sums are never NULL.
+            if (d.input_col < 0 || d.input_col >= c.n_value_cols) return fail(FW_E_INVALID, "agg %d: bad input_col", g);
+            const int sc = d.input_col;
+            const bool fl = d.type == FW_T_F64;
+            int w0 = -1;
+            auto slot_chk = [&](int col) { const int sl = slot_of(col); return sl; };
+            switch (d.kind) {
+                case FW_AGG_COUNT_STAR:
+                case FW_AGG_COUNT:
+                    if (c.value_col_types[sc] != FW_T_I64 || nullable(sc))
+                        return fail(FW_E_INVALID, "agg %d: a local count column is a NOT NULL BIGINT", g);
+                    if ((slot = slot_chk(sc)) < 0) return fail(FW_E_INVALID, "more than %d distinct value columns", MAX_KCOLS);
+                    w0 = word_of(W_CNTV, slot, -1);
+                    break;
+                case FW_AGG_AVG: {
+                    if (sc + 1 >= c.n_value_cols || c.value_col_types[sc] != (fl ? FW_T_F64 : FW_T_I64) ||
+                        c.value_col_types[sc + 1] != FW_T_I64 || nullable(sc) || nullable(sc + 1))
+                        return fail(FW_E_INVALID, "agg %d: a local AVG is a NOT NULL (sum, BIGINT count) column pair", g);
+                    const int s0 = slot_chk(sc), s1 = slot_chk(sc + 1);
+                    if (s0 < 0 || s1 < 0) return fail(FW_E_INVALID, "more than %d distinct value columns", MAX_KCOLS);
+                    w0 = word_of(fl ? W_SUM_F : W_SUM_I, s0, -1);
+                    ad.w1[g] = word_of(W_CNTV, s1, -1);
+                    if (ad.w1[g] < 0) return fail(FW_E_INVALID, "too many accumulator words");
+                    break;
+                }
+                default: w0 = -2; break;  // SUM / MIN / MAX: as in one phase, below
+            }
+            if (w0 != -2) {
+                if (w0 < 0) return fail(FW_E_INVALID, "too many accumulator words");
+                ad.w0[g] = w0;
+                continue;
+            }
+        }
         if (d.kind != FW_AGG_COUNT_STAR) {
             if (d.input_col < 0 || d.input_col >= c.n_value_cols) return fail(FW_E_INVALID, "agg %d: bad input_col", g);
             if (c.value_col_types[d.input_col] != d.type)
@@ -347,6 +386,12 @@ int validate_and_plan(fw_handle* h) {
         if (nn_star[g]) ad.nn[g] = star;
     h->nv = nslot;
     h->nw_t = round_nw(wd.nw);
+    h->n_out = c.n_aggs;
+    if (c.agg_phase == FW_PHASE_LOCAL) {  // output = local accumulator fields (AVG: sum, count)
+        h->n_out = 0;
+        for (int g = 0; g < c.n_aggs; g++) h->n_out += c.aggs[g].kind == FW_AGG_AVG ? 2 : 1;
+        if (h->n_out > FW_MAX_AGGS) return fail(FW_E_INVALID, "LOCAL phase: more than %d accumulator fields", FW_MAX_AGGS);
+    }
     for (int i = wd.nw; i < MAX_WORDS; i++) {
         wd.op[i] = W_CNT;
         wd.col[i] = 0;
@@ -416,13 +461,13 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->out_ws, orows))) return rc;
     if ((rc = dalloc(&h->out_we, orows))) return rc;
     if ((rc = dalloc(&h->out_null, orows))) return rc;
-    for (int g = 0; g < c.n_aggs; g++)
+    for (int g = 0; g < h->n_out; g++)
         if ((rc = dalloc(&h->out_val[g], orows))) return rc;
     if ((rc = dalloc(&h->res_key, h->out_cap))) return rc;
     if ((rc = dalloc(&h->res_ws, h->out_cap))) return rc;
     if ((rc = dalloc(&h->res_we, h->out_cap))) return rc;
     if ((rc = dalloc(&h->res_null, h->out_cap))) return rc;
-    for (int g = 0; g < c.n_aggs; g++)
+    for (int g = 0; g < h->n_out; g++)
         if ((rc = dalloc(&h->res_val[g], h->out_cap))) return rc;
     if ((rc = dalloc(&h->sb_out, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->sb_fired, h->ks.n_sb))) return rc;
@@ -496,6 +541,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.wd = h->wd;
     a.ad = h->ad;
     a.always_flush = h->always_flush;
+    a.local = h->cfg.agg_phase == FW_PHASE_LOCAL;
     a.out_key = h->out_key;
     a.out_ws = h->out_ws;
     a.out_we = h->out_we;
@@ -558,6 +604,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.treq_cap = h->treq_cap;
         a.lds_bytes = IG_LDS;
         a.local = h->cfg.agg_phase == FW_PHASE_LOCAL;
+        a.global = h->cfg.agg_phase == FW_PHASE_GLOBAL;
         a.ablate = h->ablate;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
@@ -739,13 +786,13 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     ca.sb_out = h->sb_out;
     ca.off = h->coff;
     ca.n_sb = h->ks.n_sb;
-    ca.n_aggs = h->cfg.n_aggs;
+    ca.n_aggs = h->n_out;
     ca.slab_cap = h->slab_cap;
     ca.out_key = h->out_key;
     ca.out_ws = h->out_ws;
     ca.out_we = h->out_we;
     ca.out_null = h->out_null;
-    for (int g = 0; g < h->cfg.n_aggs; g++) {
+    for (int g = 0; g < h->n_out; g++) {
         ca.out_val[g] = h->out_val[g];
         ca.res_val[g] = h->res_val[g];
     }
@@ -766,7 +813,7 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     const int64_t n = total;
     memset(out, 0, sizeof *out);
     out->n = n;
-    const int na = h->cfg.n_aggs;
+    const int na = h->n_out;
     if (!copy_to_host) {
         out->key = h->res_key;
         out->window_start = h->res_ws;
@@ -850,6 +897,8 @@ int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
     HIP_TRY(hipMemcpyAsync(st, h->stamps, sizeof st, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     for (int k = 0; k < N_STAMPS && k < FW_KT_N; k++) out->merge_phase_cycles[k] = (int64_t)st[k];
+    if (h->ablate & AB_FSTAMPS)  // diagnostic builds only: per-lane cycles of fire_one's parts
+        fprintf(stderr, "fire_parts lookup+merge=%llu emit=%llu next=%llu calls=%llu\n", st[8], st[9], st[10], st[11]);
     if (!h->timer) return FW_OK;
     EvTimer* t = static_cast<EvTimer*>(h->timer);
     HIP_TRY(t->resolve());

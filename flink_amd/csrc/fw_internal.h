@@ -231,6 +231,7 @@ struct IngestArgs {
     int64_t treq_cap;
     int32_t lds_bytes;     // dynamic LDS of the launch (IG_LDS)
     int32_t local;         // LOCAL phase: no late-record handling (LocalSlicingWindowAggOperator)
+    int32_t global;        // GLOBAL phase: the ts column holds the slice end (SliceAssigners.sliced)
     int32_t ablate;        // development only (FW_ABLATE env): skip phases to time the others
 };
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
@@ -245,7 +246,8 @@ constexpr int AB_M_NO_HASH = 512;    // merge: gather loads the partials but doe
 constexpr int AB_M_NO_FOLDOP = 1024; // merge: insert the partials but skip the accumulator/flag atomics
 constexpr int AB_GSTAMPS = 256;      // merge: with AB_STAMPS, phases 4/5/6 time the gather's scan/load/fold
 constexpr int AB_M_NO_EMIT = 4096;  // merge: fire without writing result rows (diagnostic)
-constexpr int N_STAMPS = 8;
+constexpr int AB_FSTAMPS = 8192;    // merge: per-lane cycles of fire_one's parts into stamps[8..11]
+constexpr int N_STAMPS = 16;
 
 struct MergeArgs {
     Ctrl* ctrl;

@@ -393,7 +393,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         }
         int64_t se;
         const uint64_t d = (uint64_t)rs[j] - (uint64_t)tbase;
-        if (fast && d < (1ull << 31)) {
+        if (a.global) {
+            se = rs[j];  // SlicedSharedSliceAssigner.assignSliceEnd: the row's slice-end field
+        } else if (fast && d < (1ull << 31)) {
             const uint32_t d32 = (uint32_t)d;
             const uint32_t r = d32 - udiv32(d32, a.win.slice_div32) * (uint32_t)a.win.interval;
             se = rs[j] - (int64_t)r + a.win.interval;
@@ -768,22 +770,24 @@ __device__ __forceinline__ void set_timer(StateLds<NW, E>& S, int e, int64_t W) 
 // Emission is atomic-free at device scope: each superbucket appends to its own output slab
 // (LDS cursor); only slab overflow falls back to a shared overflow region.  fw_results compacts
 // slabs + overflow into one contiguous result set on demand (k_compact_*).
+// output row position: the superbucket's slab, or the shared overflow region; -1 when full
+__device__ __forceinline__ int64_t claim_out_row(const MergeArgs& a, int sb, int32_t* s_emit) {
+    Ctrl* c = a.ctrl;
+    const int32_t pos = wave_claim(s_emit);
+    if (pos < a.slab_cap) return (int64_t)sb * a.slab_cap + pos;
+    const uint64_t o = atomicAdd((unsigned long long*)&c->out_count, 1ull);
+    if ((int64_t)o >= a.out_cap) {
+        __hip_atomic_fetch_or(&c->error, ERR_OUTPUT, __ATOMIC_RELAXED, DEV_SCOPE);
+        return -1;
+    }
+    return (int64_t)a.n_sb * a.slab_cap + (int64_t)o;
+}
+
 template <int NW, bool Q>
 __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
-    Ctrl* c = a.ctrl;
     if (a.ablate & AB_M_NO_EMIT) return;
-    const int32_t pos = wave_claim(s_emit);
-    int64_t i;
-    if (pos < a.slab_cap) {
-        i = (int64_t)sb * a.slab_cap + pos;
-    } else {
-        const uint64_t o = atomicAdd((unsigned long long*)&c->out_count, 1ull);
-        if ((int64_t)o >= a.out_cap) {
-            __hip_atomic_fetch_or(&c->error, ERR_OUTPUT, __ATOMIC_RELAXED, DEV_SCOPE);
-            return;
-        }
-        i = (int64_t)a.n_sb * a.slab_cap + (int64_t)o;
-    }
+    const int64_t i = claim_out_row(a, sb, s_emit);
+    if (i < 0) return;
     a.out_key[i] = key;
     a.out_ws[i] = window_start_of(a.win, we);
     a.out_we[i] = we;
@@ -829,30 +833,117 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
     a.out_null[i] = nm;
 }
 
-template <int NW, int E, bool Q>
-__device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t we, int sb, int32_t* s_emit) {
-    const WinDesc& w = a.win;
-    const WordDesc& wd = a.wd;
-    const int64_t k = S.key[e];
-    uint64_t acc[NW];
+// LOCAL phase output (LocalAggCombiner.combine :69-97 -> output(key, window, acc)): one row per
+// (key, sliceEnd) of the flush holding the local accumulator fields of every aggregate in order
+// (COUNT(*) / COUNT: count; SUM, MIN, MAX: value, NULL-able; AVG: sum, count), window_end =
+// window_start = sliceEnd.  The GLOBAL phase ingests exactly these columns.
+template <int NW, bool Q>
+__device__ void emit_partial(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t se, const uint64_t* acc) {
+    const int64_t i = claim_out_row(a, sb, s_emit);
+    if (i < 0) return;
+    a.out_key[i] = key;
+    a.out_ws[i] = se;
+    a.out_we[i] = se;
+    uint32_t nm = 0;
+    int j = 0;
+    for (int g = 0; g < a.ad.n; g++) {
+        const int32_t kind = a.ad.kind[g], type = a.ad.type[g];
+        const uint64_t w0 = acc[a.ad.w0[g]];
+        const bool no_rows = a.ad.nn[g] >= 0 && acc[a.ad.nn[g]] == 0;
+        uint64_t v = w0;
+        bool isnull = false;
+        switch (kind) {
+            case FW_AGG_SUM:
+                v = type == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)w0 : w0;
+                isnull = no_rows;
+                break;
+            case FW_AGG_MIN:
+            case FW_AGG_MAX:
+                if (Q && a.ad.qf[g] >= 0) {
+                    v = q_result(a.ad, g, acc, &isnull);
+                    break;
+                }
+                v = type == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
+                isnull = no_rows;
+                break;
+            case FW_AGG_AVG:  // (sum, count); the sum of AVG(INT) is a BIGINT (IntAvgAggFunction)
+                a.out_val[j][i] = w0;
+                j++;
+                v = acc[a.ad.w1[g]];
+                break;
+            default: break;  // counts
+        }
+        if (isnull) nm |= 1u << j;
+        a.out_val[j][i] = isnull ? 0ull : v;
+        j++;
+    }
+    a.out_null[i] = nm;
+}
+
+// flags that live only inside one k_merge_fire launch (dropped at write-back)
+constexpr uint32_t F_FIRED = 4u;    // HOP: window (key, this slice end) fired in this advance (chain claim)
+constexpr uint32_t F_NOTHEAD = 8u;  // CUMULATE: an earlier due step of the same window chains to this one
+constexpr uint32_t F_EXPIRE = 16u;  // HOP: slice expired by a window fired in this advance (cleared at write-back)
+
+template <int NW>
+__device__ __forceinline__ void acc_identity(const WordDesc& wd, uint64_t* acc) {
 #pragma unroll
     for (int i = 0; i < NW; i++) acc[i] = i < wd.nw ? word_identity(wd.op[i]) : 0;
-    bool nonempty;
-    if (w.kind == FW_WIN_TUMBLE) {
-        // SliceUnsharedSyncStateWindowAggProcessor.fireWindow (:54-66)
-        if (S.flag[e] & F_ACC) {
+}
+
+// acc = merge(acc, state of entry e) when the entry holds an accumulator (windowState.value != null)
+template <int NW, int E, bool Q>
+__device__ __forceinline__ void merge_entry(const MergeArgs& a, StateLds<NW, E>& S, int e, uint64_t* acc) {
+    if (e < 0 || !(S.flag[e] & F_ACC)) return;
+    uint64_t o[NW];
 #pragma unroll
-            for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
-        }
-        nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
-        if (nonempty) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
-        atomicAnd(&S.flag[e], ~F_ACC);  // clearWindow: expiredSlices(we) = [we]
-        return;
+    for (int i = 0; i < NW; i++) o[i] = S.acc[i][e];
+    merge_slice<NW, Q>(a.wd, a.ad, acc, o);
+}
+
+// TUMBLE: SliceUnsharedSyncStateWindowAggProcessor.fireWindow (:54-66) + clearWindow
+// (expiredSlices(we) = [we]); DataStream tumbling: WindowOperator.onEventTime + clearAllState.
+// Windows of different keys and of one key are independent: every due entry fires once.
+template <int NW, int E, bool Q>
+__device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+    uint64_t acc[NW];
+    const uint32_t f = atomicAnd(&S.flag[e], ~(F_TIMER | F_ACC));
+    if (f & F_ACC) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
+    } else {
+        acc_identity<NW>(a.wd, acc);
     }
-    if (w.kind == FW_WIN_HOP) {
-        // mergeSlices with a null target: fold the n slices ending at we, newest first; the
-        // lookups go in batches of HB with their first probes issued together
-        constexpr int HB = NW <= 2 ? 8 : NW <= 4 ? 4 : 2;
+    if (a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0) emit_row<NW, Q>(a, sb, s_emit, S.key[e], S.slice[e], acc);
+    return 1;
+}
+
+// HOP: the timer chain of one key starting at due entry e, fired without timestamp rounds.
+// SliceSharedSyncStateWindowAggProcessor.fireWindow (:65-86): merge the n slices ending at we
+// newest first into a fresh accumulator, emit unless empty (hidden COUNT(*)), and while the window
+// is non-empty register we + slice (nextTriggerWindow); a registered timer that is already due
+// fires in this same advance (InternalTimerServiceImpl.tryAdvanceWatermark :328-348), so the
+// chain continues.  clearWindow expires windowStart + slice: that slice also belongs to the
+// earlier windows of the key that are due in this advance, so the expiry is deferred to the
+// write-back (F_EXPIRE), after every window of the advance has read its slices.  With that, the
+// chains of one key may run concurrently in any order; the F_FIRED claim makes every window fire
+// exactly once.
+template <int NW, int E, bool Q>
+__device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+    const WinDesc& w = a.win;
+    const WordDesc& wd = a.wd;
+    constexpr int HB = NW <= 2 ? 8 : NW <= 4 ? 4 : 2;
+    const int64_t k = S.key[e];
+    int64_t we = S.slice[e];
+    int ew = e;
+    uint32_t nf = 0;
+    for (;;) {
+        const uint32_t old = atomicOr(&S.flag[ew], F_FIRED);
+        if (old & F_FIRED) break;  // fired by another chain of this key
+        atomicAnd(&S.flag[ew], ~F_TIMER);
+        nf++;
+        uint64_t acc[NW];
+        acc_identity<NW>(wd, acc);
         const int n = w.n_slices;
         const int64_t s_exp = wadd(wsub(we, w.size), w.interval);  // clearWindow's expired slice
         int e_exp = -3;
@@ -872,64 +963,99 @@ __device__ void fire_one(const MergeArgs& a, StateLds<NW, E>& S, int e, int64_t 
                 if (j0 + j >= n) break;
                 int e2 = eb[j];
                 if (e2 == -2) e2 = find_entry(S, k, ss[j]);
-                if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
-                    uint64_t o[NW];
-#pragma unroll
-                    for (int i = 0; i < NW; i++) o[i] = S.acc[i][e2];
-                    merge_slice<NW, Q>(wd, a.ad, acc, o);
-                }
+                merge_entry<NW, E, Q>(a, S, e2, acc);
                 if (ss[j] == s_exp) e_exp = e2;
             }
         }
-        nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
-        if (nonempty) {
-            emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
-            // nextTriggerWindow: register windowEnd + sliceSize while the window is non-empty
-            const int e3 = find_or_insert(S, k, wadd(we, w.interval), wd);
-            if (e3 >= 0) set_timer(S, e3, a.wm);
-        }
-        // clearWindow: expiredSlices = [windowStart + sliceSize]
+        const bool nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
+        if (nonempty) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
         const int e2 = e_exp != -3 ? e_exp : find_entry(S, k, s_exp);
-        if (e2 >= 0) atomicAnd(&S.flag[e2], ~F_ACC);
-        return;
+        if (e2 >= 0) atomicOr(&S.flag[e2], F_EXPIRE);
+        if (!nonempty) break;
+        const int64_t nx = wadd(we, w.interval);
+        const int en = find_or_insert(S, k, nx, wd);
+        if (en < 0) break;  // state overflow (flagged)
+        if (!is_fired(nx, a.wm)) {
+            atomicOr(&S.flag[en], F_TIMER);
+            break;
+        }
+        we = nx;
+        ew = en;
     }
-    // CUMULATE: merge the window's slice into the first-slice state (mergeSlices -> merge)
+    return nf;
+}
+
+// CUMULATE: the steps of one cumulative window of one key, from its earliest due step, in order:
+// mergeSlices merges step we's slice into the first-slice state (CumulativeSliceAssigner
+// .mergeSlices, SliceSharedSyncStateWindowAggProcessor.merge :89-118), the window is emitted
+// unless empty, the next step is registered up to the window's last step (nextTriggerWindow), and
+// clearWindow expires we (and the first slice at the last step).  The merged accumulator stays in
+// registers across the chain and is written back to the first slice once.
+template <int NW, int E, bool Q>
+__device__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+    const WinDesc& w = a.win;
+    const WordDesc& wd = a.wd;
+    const int64_t k = S.key[e];
+    int64_t we = S.slice[e];
     const int64_t ws = window_start_of(w, we);
     const int64_t first = wadd(ws, w.interval);
+    const int64_t last = wadd(ws, w.size);
     const int ef = find_or_insert(S, k, first, wd);
+    uint64_t acc[NW];
     if (ef >= 0 && (S.flag[ef] & F_ACC)) {
 #pragma unroll
         for (int i = 0; i < NW; i++) acc[i] = S.acc[i][ef];
+    } else {
+        acc_identity<NW>(wd, acc);
     }
-    int e_we = -1;
-    if (we != first) {
-        const int e2 = e_we = find_entry(S, k, we);
-        if (e2 >= 0 && (S.flag[e2] & F_ACC)) {
-            uint64_t o[NW];
-#pragma unroll
-            for (int i = 0; i < NW; i++) o[i] = S.acc[i][e2];
-            merge_slice<NW, Q>(wd, a.ad, acc, o);
+    uint32_t nf = 0;
+    bool done = false;
+    int ewe = e;
+    for (;;) {
+        if (ewe >= 0) atomicAnd(&S.flag[ewe], ~F_TIMER);
+        if (we != first) merge_entry<NW, E, Q>(a, S, ewe, acc);
+        nf++;
+        if (a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
+        if (we != first && ewe >= 0) atomicAnd(&S.flag[ewe], ~F_ACC);
+        if (we == last) {  // expiredSlices(last) = [last, first]
+            if (ef >= 0) atomicAnd(&S.flag[ef], ~F_ACC);
+            done = true;
+            break;
         }
+        const int64_t nx = wadd(we, w.interval);
+        if (!is_fired(nx, a.wm)) {
+            const int en = find_or_insert(S, k, nx, wd);
+            if (en >= 0) atomicOr(&S.flag[en], F_TIMER);
+            break;
+        }
+        we = nx;
+        ewe = we == first ? ef : find_entry(S, k, we);
     }
-    if (ef >= 0) {  // windowState.update(firstSlice, acc)
+    if (!done && ef >= 0) {  // windowState.update(firstSlice, acc)
 #pragma unroll
         for (int i = 0; i < NW; i++) S.acc[i][ef] = acc[i];
         atomicOr(&S.flag[ef], F_ACC);
     }
-    nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
-    if (nonempty) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
-    const int64_t next = wadd(we, w.interval);
-    const int64_t last = wadd(ws, w.size);
-    if (!(next > last)) {
-        const int e3 = find_or_insert(S, k, next, wd);
-        if (e3 >= 0) set_timer(S, e3, a.wm);
-    }
-    // clearWindow (CumulativeSliceAssigner.expiredSlices)
-    if (we == first) {
-    } else {
-        const int e2 = e_we;  // the entry of `we` was looked up above and entries never move
-        if (e2 >= 0) atomicAnd(&S.flag[e2], ~F_ACC);
-        if (we == last && ef >= 0) atomicAnd(&S.flag[ef], ~F_ACC);
+    return nf;
+}
+
+// CUMULATE pre-pass: a due step whose window has an earlier due step is reached by that step's
+// chain (CUMULATE chains never stop before the window's last step), so it starts no chain of its
+// own.  Each due step marks the next due step of its window.
+template <int NW, int E>
+__device__ __forceinline__ void mark_cumulate_successor(const MergeArgs& a, StateLds<NW, E>& S, int e) {
+    const WinDesc& w = a.win;
+    const int64_t k = S.key[e];
+    const int64_t we = S.slice[e];
+    const int64_t last = wadd(window_start_of(w, we), w.size);
+    for (int64_t s = we; s != last;) {
+        s = wadd(s, w.interval);
+        if (!is_fired(s, a.wm)) break;
+        const int e2 = find_entry(S, k, s);
+        if (e2 >= 0 && (S.flag[e2] & F_TIMER)) {
+            atomicOr(&S.flag[e2], F_NOTHEAD);
+            break;
+        }
     }
 }
 
@@ -964,17 +1090,17 @@ __device__ __forceinline__ int sb_of_block(int b, int n_sb) {
     return (b % 8) * (n_sb / 8) + b / 8;
 }
 
-template <int NW, int E, bool Q>
+// rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
+constexpr int mg_rows_in_flight(int nw) { return nw <= 1 ? 4 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1; }
+
+template <int NW, int E, bool Q, int KIND>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
     constexpr int CH = IG_BLOCK * ig_rpt(NW);  // chunk rows of the ingest kernel that wrote the cells
+    constexpr int GU = mg_rows_in_flight(NW);
     __shared__ StateLds<NW, E> S;
-    __shared__ uint32_t s_cb[MG_CELL_GROUP + 1];  // flat prefix of the cell counts of a cell group
-    __shared__ uint16_t s_start[MG_CELL_GROUP];   // first row of each cell inside its chunk region
-    __shared__ uint32_t wsum[MG_BLOCK / 64];
     __shared__ int32_t s_work;
-    __shared__ int64_t s_vmin[2];  // round minimum, double-buffered by round parity
     __shared__ int32_t s_nlive;
     __shared__ int64_t s_newmin;
     __shared__ uint32_t s_fired;
@@ -999,140 +1125,97 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
 
     Stamps stm;
     stm.init((a.ablate & AB_STAMPS) != 0);
-    const bool gdet = (a.ablate & AB_GSTAMPS) != 0;
     if (tid == 0) {
         s_work = (ntreq > 0) || do_flush || (do_fire && is_fired(a.sb_min_timer[sb], W));
         s_fired = 0;
         s_emit = a.sb_out[sb];
     }
     __syncthreads();
-    if (s_work) {
-        // cell groups of all pending pushes as one flat sequence; the next group's cell words
-        // are loaded while the current group is folded, the first group's while the state loads
-        const bool gather = do_flush && !(a.ablate & AB_M_NO_GATHER);
-        int n_groups = 0;
-        // cells are enumerated in flat tile order f (cell_chunk(f) is the chunk); padding
-        // positions past the push's last chunk count as empty
-        if (gather) for (int64_t pi = 0; pi < pend; pi++)
-            n_groups += (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
-        auto cell_word = [&](int k, int& pi_out, int& g0_out, int& ng_out) -> uint32_t {
-            int pi = 0;
-            for (;;) {
-                const int ngp = (int)((cell_pad(a.slot_nch[pi]) + MG_CELL_GROUP - 1) / MG_CELL_GROUP);
-                if (k < ngp) break;
-                k -= ngp;
-                pi++;
-            }
-            pi_out = pi;
-            g0_out = k * MG_CELL_GROUP;
-            ng_out = min(MG_CELL_GROUP, (int)cell_pad(a.slot_nch[pi]) - g0_out);
-            const int64_t f = g0_out + tid;
-            if (tid >= ng_out || cell_chunk(f) >= a.slot_nch[pi]) return 0u;
-            const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
-            return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
-        };
-        int pi_n = 0, g0_n = 0, ng_n = 0;
-        uint32_t v_n = n_groups > 0 ? cell_word(0, pi_n, g0_n, ng_n) : 0u;
-        // ---- load this superbucket's entries into LDS
-        for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
-        if (tid == 0) {
-            S.n = (a.ablate & AB_M_NO_LOAD) ? 0 : n0;
-            S.overflow = 0;
+    if (!s_work) return;
+    const bool gather = do_flush && !(a.ablate & AB_M_NO_GATHER);
+    // this thread's first cell word, loaded while the state loads (the gather below walks the
+    // cells of every pending push, one cell per thread per pass, in flat tile order f:
+    // cell_chunk(f) is the chunk, positions past the push's last chunk are padding)
+    auto cell_at = [&](int64_t pi, int f) -> uint32_t {
+        if (cell_chunk(f) >= a.slot_nch[pi]) return 0u;
+        const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
+        return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
+    };
+    uint32_t v_first = 0;
+    if (gather && tid < cell_pad(a.slot_nch[0])) v_first = cell_at(0, tid);
+    // ---- load this superbucket's entries into LDS
+    for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
+    if (tid == 0) {
+        S.n = (a.ablate & AB_M_NO_LOAD) ? 0 : n0;
+        S.overflow = 0;
+        S.ndue = 0;
+    }
+    __syncthreads();
+    const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
+    if (!(a.ablate & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
+        const uint64_t* p = st + (size_t)e * PWE;
+        const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
+        S.key[e] = k;
+        S.slice[e] = s;
+        S.flag[e] = (uint32_t)p[2];
+#pragma unroll
+        for (int w = 0; w < NW; w++) S.acc[w][e] = p[3 + w];
+        uint32_t h = index_hash(k, s) & (2 * E - 1);
+        for (;;) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 2u + (uint32_t)e, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, LDS_SCOPE))
+                break;
+            h = (h + 1) & (2 * E - 1);
         }
-        __syncthreads();
-        const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
-        if (!(a.ablate & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
-            const uint64_t* p = st + (size_t)e * PWE;
-            const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
-            S.key[e] = k;
-            S.slice[e] = s;
-            S.flag[e] = (uint32_t)p[2];
+    }
+    __syncthreads();
+    stm.mark(0);
+    // ---- timers registered by late records in processElement
+    for (int64_t r = tid; r < ntreq; r += MG_BLOCK) {
+        if (a.treq[3 * r + 2] != sb) continue;
+        const int e = find_or_insert(S, a.treq[3 * r], a.treq[3 * r + 1], a.wd);
+        if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
+    }
+    // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket.
+    // One cell (the rows one ingest chunk wrote for this superbucket) per thread per pass; GU of
+    // its rows are loaded together, then looked up in the LDS table and folded (or inserted).
+    if (gather) {
+        for (int64_t pi = 0; pi < pend; pi++) {
+            const int nch = a.slot_nch[pi];
+            const int ncell = (int)cell_pad(nch);
+            const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
+            for (int f = tid; f < ncell; f += MG_BLOCK) {
+                const uint32_t v = (pi == 0 && f == tid) ? v_first : cell_at(pi, f);
+                const uint32_t cnt = v >> 16;
+                if (!cnt) continue;
+                const uint64_t* rp = seg + ((size_t)cell_chunk(f) * CH + (v & 0xFFFFu)) * PW;
+                for (uint32_t r0 = 0; r0 < cnt; r0 += GU) {
+                    uint64_t row[GU][PW];
 #pragma unroll
-            for (int w = 0; w < NW; w++) S.acc[w][e] = p[3 + w];
-            uint32_t h = index_hash(k, s) & (2 * E - 1);
-            for (;;) {
-                uint32_t expect = 0;
-                if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 2u + (uint32_t)e, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, LDS_SCOPE))
-                    break;
-                h = (h + 1) & (2 * E - 1);
-            }
-        }
-        __syncthreads();
-        stm.mark(0);
-        // ---- timers registered by late records in processElement
-        for (int64_t r = tid; r < ntreq; r += MG_BLOCK) {
-            if (a.treq[3 * r + 2] != sb) continue;
-            const int e = find_or_insert(S, a.treq[3 * r], a.treq[3 * r + 1], a.wd);
-            if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
-        }
-        // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket
-        if (gather) {
-            for (int k = 0; k < n_groups; k++) {
-                const int pi = pi_n, g0 = g0_n, ng = ng_n;
-                const uint32_t v = v_n;
-                if (k + 1 < n_groups) v_n = cell_word(k + 1, pi_n, g0_n, ng_n);
-                const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
-                uint32_t total;
-                const uint32_t incl = block_incl_scan<MG_BLOCK>(v >> 16, wsum, &total);
-                if (tid < MG_CELL_GROUP) {
-                    s_cb[tid + 1] = incl;
-                    s_start[tid] = (uint16_t)(v & 0xFFFFu);
-                }
-                if (tid == 0) s_cb[0] = 0;
-                __syncthreads();
-                if (gdet) stm.mark(4);
-                const int top = 1 << (31 - __builtin_clz((unsigned)ng));  // highest power of two <= ng
-                constexpr int U = 1;  // rows in flight per thread (VGPR budget)
-                for (uint32_t r0 = tid; r0 < total; r0 += U * MG_BLOCK) {
-                    // cell of each row: s_cb[lo] <= r < s_cb[lo + 1], the U searches advance together
-                    int lo[U];
-                    uint32_t rr[U];
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        lo[u] = 0;
-                        rr[u] = min(r0 + u * MG_BLOCK, total - 1);
-                    }
-                    for (int step = top; step > 0; step >>= 1) {
-#pragma unroll
-                        for (int u = 0; u < U; u++) {
-                            const int c = lo[u] + step;
-                            if (c < ng && s_cb[c] <= rr[u]) lo[u] = c;
-                        }
-                    }
-                    uint64_t row[U][PW];
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        const uint64_t* p =
-                            seg + ((size_t)cell_chunk(g0 + lo[u]) * CH + s_start[lo[u]] + (rr[u] - s_cb[lo[u]])) * PW;
+                    for (int u = 0; u < GU; u++) {
+                        const uint64_t* p = rp + (size_t)min(r0 + u, cnt - 1) * PW;
 #pragma unroll
                         for (int w = 0; w < PW; w++) row[u][w] = p[w];
                     }
-                    if (gdet) {
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        stm.mark(5);
-                    }
-                    int ge[U];
-                    if (!(a.ablate & AB_M_NO_HASH)) {
-                        int64_t gk[U], gs[U];
+                    int ge[GU];
+                    {
+                        int64_t gk[GU], gs[GU];
 #pragma unroll
-                        for (int u = 0; u < U; u++) {
+                        for (int u = 0; u < GU; u++) {
                             gk[u] = (int64_t)row[u][0];
                             gs[u] = (int64_t)row[u][1];
                         }
-                        probe_batch<NW, E, U>(S, gk, gs, ge);
+                        probe_batch<NW, E, GU>(S, gk, gs, ge);
                     }
-                    static_for<U>([&](auto UU) {
+                    static_for<GU>([&](auto UU) {
                         constexpr int u = decltype(UU)::value;
-                        if (r0 + u * MG_BLOCK >= total) return;
+                        if (r0 + u >= cnt) return;
                         const int64_t k = (int64_t)row[u][0], s = (int64_t)row[u][1];
-                        if (a.ablate & AB_M_NO_HASH) {
-                            if (k == -7 && s == -7) S.overflow = 1;  // keeps the loads live
-                            return;
-                        }
-                        // register the window timer unless already fired (AggCombiner.java:103-110)
-                        const uint32_t fl = is_fired(s, w_old) ? F_ACC : (F_ACC | F_TIMER);
-                        int e = ge[u];
+                        // register the window timer unless already fired (AggCombiner.java:103-110);
+                        // the LOCAL phase keeps no timers (LocalAggCombiner.java:69-97)
+                        const uint32_t fl = (a.local || is_fired(s, w_old)) ? F_ACC : (F_ACC | F_TIMER);
+                        int e = ge[u];  // -1 / -2: not found by the batched first probe
                         bool ins = false;
                         if (e < 0) e = find_or_insert(S, k, s, a.wd, &row[u][2], fl, &ins);
                         if (e < 0 || ins || (a.ablate & AB_M_NO_FOLDOP)) return;
@@ -1142,77 +1225,66 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         atomicOr(&S.flag[e], fl);
                     });
                 }
-                __syncthreads();
-                if (gdet) stm.mark(6);
             }
         }
-        __syncthreads();
-        stm.mark(1);
-        // ---- fire: InternalTimerServiceImpl.tryAdvanceWatermark, timestamp order
-        if (do_fire && !(a.ablate & AB_M_NO_FIRE)) {
-            // due list: entries whose timer fires at W (dense work for the rounds below)
-            if (tid == 0) {
-                S.ndue = 0;
-                s_vmin[0] = INT64_MAX;
-            }
-            __syncthreads();
-            const int n = min(S.n, E);
-            for (int e = tid; e < n; e += MG_BLOCK)
-                if ((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W)) {
-                    const int q = wave_claim(&S.ndue);
-                    S.due[q] = (uint16_t)e;
-                }
-            __syncthreads();
-            if (!gdet) stm.mark(6);
-            // rounds in timestamp order (per key the reference fires windows in order, and a
-            // fired HOP/CUMULATE window can register the next one); keys are independent
-            // (the next round's minimum slot is reset during this round, so a round needs two
-            // barriers: after the minimum and after the fires)
-            for (int rnd = 0;; rnd++) {
-                int64_t* vmin = &s_vmin[rnd & 1];
-                if (tid == 0) s_vmin[(rnd + 1) & 1] = INT64_MAX;
-                const int nd = min(S.ndue, E);
-                int64_t lm = INT64_MAX;
-                for (int q = tid; q < nd; q += MG_BLOCK) {
-                    const int e = S.due[q];
-                    if (S.flag[e] & F_TIMER) lm = min(lm, S.slice[e]);
-                }
-                lm = wave_min_i64(lm);
-                if ((tid & 63) == 0 && lm != INT64_MAX) __hip_atomic_fetch_min(vmin, lm, __ATOMIC_RELAXED, LDS_SCOPE);
-                __syncthreads();
-                if (!gdet) stm.mark(4);
-                const int64_t v = *vmin;
-                if (v == INT64_MAX) break;
-                stm.acc[7]++;
-                uint32_t nf = 0;
-                for (int q = tid; q < nd; q += MG_BLOCK) {
-                    const int e = S.due[q];
-                    if ((S.flag[e] & F_TIMER) && S.slice[e] == v) {
-                        atomicAnd(&S.flag[e], ~F_TIMER);
-                        fire_one<NW, E, Q>(a, S, e, v, sb, &s_emit);
-                        nf++;
-                    }
-                }
-                nf = wave_sum_u32(nf);
-                if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
-                __syncthreads();
-                if (!gdet) stm.mark(5);
-            }
-            if (S.ndue > E && tid == 0) S.overflow = 1;
-        }
-        // ---- write back live entries
-        if (tid == 0) {
-            s_nlive = 0;
-            s_newmin = INT64_MAX;
-        }
-        __syncthreads();
-        stm.mark(2);
+    }
+    __syncthreads();
+    stm.mark(1);
+    // ---- fire: InternalTimerServiceImpl.tryAdvanceWatermark (:328-348) -> WindowAggOperator
+    // .onTimer -> fireWindow + clearWindow.  One pass over the entries whose timer is due; HOP and
+    // CUMULATE follow their timer chains per key (no timestamp rounds, see fire_*_chain).
+    if (do_fire && !(a.ablate & AB_M_NO_FIRE)) {
         const int n = min(S.n, E);
-        uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
-        int64_t lnm = INT64_MAX;
-        if (!(a.ablate & AB_M_NO_WB)) for (int e = tid; e < n; e += MG_BLOCK) {
-            const uint32_t f = S.flag[e];
-            if (!(f & (F_ACC | F_TIMER))) continue;
+        for (int e = tid; e < n; e += MG_BLOCK)
+            if ((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W)) {
+                const int q = wave_claim(&S.ndue);
+                if (q < E) S.due[q] = (uint16_t)e;
+            }
+        __syncthreads();
+        const int nd = min(S.ndue, E);
+        if (KIND == FW_WIN_CUMULATE) {
+            for (int q = tid; q < nd; q += MG_BLOCK) mark_cumulate_successor<NW, E>(a, S, S.due[q]);
+            __syncthreads();
+        }
+        stm.mark(6);
+        uint32_t nf = 0;
+        for (int q = tid; q < nd; q += MG_BLOCK) {
+            const int e = S.due[q];
+            if (KIND == FW_WIN_TUMBLE) {
+                nf += fire_tumble<NW, E, Q>(a, S, e, sb, &s_emit);
+            } else if (KIND == FW_WIN_HOP) {
+                nf += fire_hop_chain<NW, E, Q>(a, S, e, sb, &s_emit);
+            } else {
+                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_cumulate_chain<NW, E, Q>(a, S, e, sb, &s_emit);
+            }
+        }
+        nf = wave_sum_u32(nf);
+        if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
+        if (S.ndue > E && tid == 0) S.overflow = 1;
+    }
+    // ---- write back live entries (LOCAL phase: emit every partial instead, keep no state)
+    if (tid == 0) {
+        s_nlive = 0;
+        s_newmin = INT64_MAX;
+    }
+    __syncthreads();
+    stm.mark(5);
+    const int n = min(S.n, E);
+    uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
+    int64_t lnm = INT64_MAX;
+    if (a.local) {
+        if (gather)
+            for (int e = tid; e < n; e += MG_BLOCK) {
+                uint64_t v[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
+                emit_partial<NW, Q>(a, sb, &s_emit, S.key[e], S.slice[e], v);
+            }
+    } else if (!(a.ablate & AB_M_NO_WB)) {
+        for (int e = tid; e < n; e += MG_BLOCK) {
+            const uint32_t f0 = S.flag[e];
+            const uint32_t f = f0 & ((f0 & F_EXPIRE) ? F_TIMER : (F_ACC | F_TIMER));
+            if (!f) continue;
             const int pos = wave_claim(&s_nlive);
             uint64_t* p = so + (size_t)pos * PWE;
             p[0] = (uint64_t)S.key[e];
@@ -1230,20 +1302,20 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             }
             if (f & F_TIMER) lnm = min(lnm, S.slice[e]);
         }
-        lnm = wave_min_i64(lnm);
-        if ((tid & 63) == 0 && lnm != INT64_MAX) __hip_atomic_fetch_min(&s_newmin, lnm, __ATOMIC_RELAXED, LDS_SCOPE);
-        __syncthreads();
-        if (tid == 0) {
-            a.state_count[sb] = s_nlive;
-            a.sb_min_timer[sb] = s_newmin;
-            a.sb_out[sb] = min(s_emit, a.slab_cap);
-            if (s_fired) a.sb_fired[sb] += s_fired;
-            if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
-        }
-        __syncthreads();
-        stm.mark(3);
-        stm.flush(a.stamps);
     }
+    lnm = wave_min_i64(lnm);
+    if ((tid & 63) == 0 && lnm != INT64_MAX) __hip_atomic_fetch_min(&s_newmin, lnm, __ATOMIC_RELAXED, LDS_SCOPE);
+    __syncthreads();
+    if (tid == 0) {
+        a.state_count[sb] = a.local ? 0 : s_nlive;
+        a.sb_min_timer[sb] = s_newmin;
+        a.sb_out[sb] = min(s_emit, a.slab_cap);
+        if (s_fired) a.sb_fired[sb] += s_fired;
+        if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
+    }
+    __syncthreads();
+    stm.mark(3);
+    stm.flush(a.stamps);
 }
 
 // applies the control decisions of the preceding k_merge_fire (one thread; the kernel boundary
@@ -1360,13 +1432,20 @@ hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t) {
     }
 }
 
+template <int NW, bool Q>
+static hipError_t merge_q(const MergeArgs& a, hipStream_t s) {
+    constexpr int E = mg_entries(NW);
+    switch (a.win.kind) {
+        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_TUMBLE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_HOP>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_CUMULATE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
 template <int NW>
 static hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
-    if (a.wd.has_q)
-        hipLaunchKernelGGL((k_merge_fire<NW, mg_entries(NW), true>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_merge_fire<NW, mg_entries(NW), false>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
-    return hipGetLastError();
+    return a.wd.has_q ? merge_q<NW, true>(a, s) : merge_q<NW, false>(a, s);
 }
 
 static hipError_t merge_any(const MergeArgs& a, hipStream_t s) {

@@ -160,6 +160,41 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
     return c
 
 
+def result_columns(cfg):
+    """Result value columns of an operator: one per aggregate, or (LOCAL phase) the local
+    accumulator fields -- COUNT(*) / COUNT / SUM / MIN / MAX: one, AVG: sum and count."""
+    if cfg.agg_phase != PHASE_LOCAL:
+        return cfg.n_aggs
+    return sum(2 if cfg.aggs[i].kind == AGG_AVG else 1 for i in range(cfg.n_aggs))
+
+
+def global_config(cfg, **overrides):
+    """The GLOBAL-phase operator of a two-phase plan (TwoStageOptimizedWindowAggregateRule): same
+    window, key and aggregates, fed with the LOCAL phase's accumulator rows -- value column j is
+    accumulator field j (see result_columns), SUM / MIN / MAX fields NULL-able; the ts column
+    carries the slice end."""
+    aggs, types, nullable, j = [], [], [], 0
+    for i in range(cfg.n_aggs):
+        kind, typ = cfg.aggs[i].kind, cfg.aggs[i].type
+        aggs.append((kind, j, typ))
+        if kind in (AGG_COUNT_STAR, AGG_COUNT):
+            types.append(T_I64)
+        elif kind == AGG_AVG:
+            types += [T_F64 if typ == T_F64 else T_I64, T_I64]
+        else:
+            types.append(typ)
+            nullable.append(j)
+        j += 2 if kind == AGG_AVG else 1
+    kw = dict(api=cfg.api, window_kind=cfg.window_kind, size_ms=cfg.size_ms, slide_ms=cfg.slide_ms,
+              offset_ms=cfg.offset_ms, aggs=aggs, count_star_index=cfg.count_star_index, value_col_types=types,
+              key_hash=cfg.key_hash, max_parallelism=cfg.max_parallelism, parallelism=cfg.parallelism,
+              subtask_index=cfg.subtask_index, device=cfg.device, state_capacity=cfg.state_capacity,
+              max_batch_rows=cfg.max_batch_rows, output_capacity=cfg.output_capacity, nullable_cols=nullable,
+              agg_phase=PHASE_GLOBAL)
+    kw.update(overrides)
+    return make_config(**kw)
+
+
 def result_is_double(kind, typ):
     """Whether an aggregate's SQL/DataStream result column is DOUBLE."""
     if kind in (AGG_COUNT_STAR, AGG_COUNT):

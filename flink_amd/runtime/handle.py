@@ -22,7 +22,7 @@ class WindowAggHandle:
         self.cfg = cfg
         self._h = C.c_void_p()
         check(lib().fw_create(C.byref(cfg), C.byref(self._h)))
-        self.n_aggs = cfg.n_aggs
+        self.n_aggs = abi.result_columns(cfg)  # result value columns
 
     # ---- lifecycle
     def close(self):
@@ -124,6 +124,25 @@ class WindowAggHandle:
         r = abi.fw_result()
         check(lib().fw_results(self._h, C.byref(r), 0))
         return r.n, r
+
+    def device_result_tensors(self, device):
+        """This watermark's results as torch tensors on `device` (zero-copy views of the handle's
+        result buffers, valid until the next call on the handle): key, window_start, window_end,
+        [values], null_mask (int64)."""
+        import torch
+        n, r = self.device_results()
+
+        class _View:  # __cuda_array_interface__ over a device pointer
+            def __init__(self, ptr, typestr):
+                self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
+                                                 "version": 3, "strides": None}
+
+        def t(ptr, typestr="<i8"):
+            if n == 0:
+                return torch.empty(0, dtype=torch.int64 if typestr == "<i8" else torch.int32, device=device)
+            return torch.as_tensor(_View(C.cast(ptr, C.c_void_p).value, typestr), device=device)
+        return (t(r.key), t(r.window_start), t(r.window_end), [t(r.values[a]) for a in range(self.n_aggs)],
+                t(r.null_mask, "<i4").to(torch.int64))
 
     def reset_results(self):
         check(lib().fw_results_reset(self._h))

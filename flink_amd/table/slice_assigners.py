@@ -96,6 +96,10 @@ class HoppingSliceAssigner(SliceAssigner):
         """HoppingSlicesIterable: n slices ending at window_end, newest first; null target."""
         return None, [window_end - i * self.slice_size for i in range(self.num_slices_per_window)]
 
+    def next_trigger_window(self, window_end, is_window_empty):
+        """HoppingSliceAssigner.nextTriggerWindow: the next window while this one is not empty."""
+        return None if is_window_empty else window_end + self.slice_size
+
 
 class CumulativeSliceAssigner(SliceAssigner):
     """SliceAssigners.CumulativeSliceAssigner (:319-454)."""
@@ -133,6 +137,12 @@ class CumulativeSliceAssigner(SliceAssigner):
     def slices_to_merge(self, window_end):
         first = self.get_window_start(window_end) + self.slide
         return first, ([] if window_end == first else [window_end])
+
+    def next_trigger_window(self, window_end, is_window_empty):
+        """CumulativeSliceAssigner.nextTriggerWindow: the next step up to the window's max size,
+        empty or not."""
+        nxt = window_end + self.slide
+        return None if nxt > self.get_window_start(window_end) + self.size else nxt
 
 
 class SliceAssigners:

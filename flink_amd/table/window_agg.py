@@ -47,7 +47,8 @@ def is_gpu_eligible(assigner, aggs, value_types, *, is_event_time=True, shift_ti
 class WindowAggOperator:
     def __init__(self, assigner, aggs, value_types, count_star_index=-1, key_type="BIGINT",
                  max_parallelism=128, parallelism=1, subtask_index=0, device=0,
-                 state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22):
+                 state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22,
+                 nullable_cols=()):
         ok, why = is_gpu_eligible(assigner, aggs, value_types, key_type=key_type)
         if not ok:
             raise ValueError(f"not eligible for the GPU window operator: {why}")
@@ -64,7 +65,7 @@ class WindowAggOperator:
             key_hash=KEY_HASH[key_type], max_parallelism=max_parallelism,
             parallelism=parallelism, subtask_index=subtask_index, device=device,
             state_capacity=state_capacity, max_batch_rows=max_batch_rows,
-            output_capacity=output_capacity)
+            output_capacity=output_capacity, nullable_cols=nullable_cols)
         self.handle = None
         self.current_watermark = -(1 << 63)
 
@@ -81,13 +82,14 @@ class WindowAggOperator:
             self.handle = None
 
     # ---- OneInputStreamOperator
-    def process_batch(self, keys, rowtimes, values=(), key_hashes=None):
-        """processElement for every row of a columnar batch (host arrays)."""
-        self.handle.push_host(keys, rowtimes, values, key_hashes)
+    def process_batch(self, keys, rowtimes, values=(), key_hashes=None, nulls=None):
+        """processElement for every row of a columnar batch (host arrays; ``nulls``: {column:
+        per-row NULL flags} for NULL-able columns)."""
+        self.handle.push_host(keys, rowtimes, values, key_hashes, nulls=nulls)
 
-    def process_batch_device(self, keys, rowtimes, values=(), key_hashes=None):
+    def process_batch_device(self, keys, rowtimes, values=(), key_hashes=None, nulls=None):
         """processElement for a batch already resident in HBM (torch cuda tensors)."""
-        self.handle.push_device(keys, rowtimes, values, key_hashes)
+        self.handle.push_device(keys, rowtimes, values, key_hashes, nulls=nulls)
 
     def process_watermark(self, watermark, collect=True):
         """processWatermark (:227-238): flush if triggered, fire timers <= watermark; returns the

@@ -182,6 +182,7 @@ struct OutRow {
     uint32_t null_mask;
     int64_t epoch;  // index of the watermark call that produced it
 };
+constexpr int MAX_FIELDS = FW_MAX_AGGS;
 
 inline double bits_to_double(uint64_t b) { double d; std::memcpy(&d, &b, 8); return d; }
 inline uint64_t double_to_bits(double d) { uint64_t b; std::memcpy(&b, &d, 8); return b; }
@@ -205,6 +206,7 @@ struct Config {
 struct Oracle {
     Config cfg;
     bool ds;  // DataStream operator
+    int phase = FW_PHASE_ONE;  // SQL: ONE / LOCAL / GLOBAL (TwoStageOptimizedWindowAggregateRule)
     // operator / processor progress
     int64_t current_watermark = INT64_MIN;      // WindowAggOperator.currentWatermark
     int64_t current_progress = INT64_MIN;       // WindowAggProcessorBase.currentProgress
@@ -323,6 +325,60 @@ struct Oracle {
         }
     }
 
+    // LocalAggCombiner.output (LocalAggCombiner.java:100-106): the accumulator fields of every
+    // aggregate in order -- COUNT(*) / COUNT: count; SUM / MIN / MAX: value (NULL-able);
+    // AVG: sum, count.  Returns the field count.
+    int acc_fields(const Row& r, uint64_t* v, uint32_t* nm) const {
+        *nm = 0;
+        int j = 0;
+        for (int a = 0; a < cfg.c.n_aggs; a++) {
+            const fw_agg_desc& g = cfg.c.aggs[a];
+            const AggState& s = r.a[a];
+            const bool isf = g.type == FW_T_F64;
+            switch (g.kind) {
+                case FW_AGG_COUNT_STAR:
+                case FW_AGG_COUNT: v[j++] = (uint64_t)s.i; break;
+                case FW_AGG_AVG:
+                    v[j++] = isf ? double_to_bits(s.d) : (uint64_t)s.i;
+                    v[j++] = (uint64_t)s.cnt;
+                    break;
+                default:
+                    if (s.is_null) { *nm |= 1u << j; v[j++] = 0; break; }
+                    v[j++] = isf ? double_to_bits(s.d) : (uint64_t)s.i;
+                    break;
+            }
+        }
+        return j;
+    }
+
+    // the inverse: a local accumulator row as an accumulator Row (GLOBAL phase input; aggregate a
+    // reads its fields from column input_col, AVG's count from the next column)
+    Row row_from_fields(const uint64_t* v, const uint8_t* nul) const {
+        Row r;
+        for (int a = 0; a < cfg.c.n_aggs; a++) {
+            const fw_agg_desc& g = cfg.c.aggs[a];
+            AggState& s = r.a[a];
+            const bool isf = g.type == FW_T_F64;
+            int j = g.input_col;
+            switch (g.kind) {
+                case FW_AGG_COUNT_STAR:
+                case FW_AGG_COUNT: s.i = (int64_t)v[j++]; s.is_null = false; break;
+                case FW_AGG_AVG:
+                    if (isf) s.d = bits_to_double(v[j]); else s.i = (int64_t)v[j];
+                    j++;
+                    s.cnt = (int64_t)v[j++];
+                    s.is_null = false;
+                    break;
+                default:
+                    s.is_null = nul[j] != 0;
+                    if (isf) s.d = bits_to_double(v[j]); else s.i = (int64_t)v[j];
+                    j++;
+                    break;
+            }
+        }
+        return r;
+    }
+
     // getValueExpression; returns value words + null mask
     void get_value(const Row& r, uint64_t* v, uint32_t* nm) const {
         *nm = 0;
@@ -396,7 +452,12 @@ struct Oracle {
     // SQL: AbstractSliceSyncStateWindowAggProcessor.processElement (:96-126)
     // -------------------------------------------------------------------------------
     bool sql_process_element(int64_t key, int64_t ts, const uint64_t* vals, const uint8_t* nul) {
-        const int64_t slice_end = assign_slice_end(ts);
+        if (phase == FW_PHASE_LOCAL) {  // LocalSlicingWindowAggOperator.processElement (:109-115)
+            buffer_add(key, assign_slice_end(ts), vals, nul);
+            return false;
+        }
+        // GLOBAL: SliceAssigners.sliced -> the row's slice-end field (here: the ts column)
+        const int64_t slice_end = phase == FW_PHASE_GLOBAL ? ts : assign_slice_end(ts);
         if (is_window_fired(slice_end, current_progress)) {
             const int64_t last = get_last_window_end(slice_end);
             if (is_window_fired(last, current_progress)) return true;  // dropped
@@ -428,14 +489,33 @@ struct Oracle {
         min_slice_end = std::min(min_slice_end, slice);
     }
 
-    // RecordsWindowBuffer.flush (:115-126) -> AggCombiner.combine (:76-115)
+    // RecordsWindowBuffer.flush (:115-126) -> AggCombiner.combine (:76-115); LOCAL:
+    // LocalAggCombiner.combine (:69-97) emits the accumulator; GLOBAL: GlobalAggCombiner.combine
+    // (:77-110) merges the local accumulators into a fresh one, then into the state.
     void flush() {
         for (auto& g : buffer) {
             const int64_t slice = g.first.first, key = g.first.second;
+            if (phase == FW_PHASE_LOCAL) {
+                Row acc = create_accumulators();
+                for (auto& rec : g.second) accumulate(acc, rec.vals, rec.nul);
+                OutRow o;
+                o.key = key;
+                o.ws = o.we = slice;
+                acc_fields(acc, o.v, &o.null_mask);
+                o.epoch = epoch;
+                out.push_back(o);
+                continue;
+            }
             auto sk = std::make_pair(key, slice);
             auto it = state.find(sk);
             Row acc = it == state.end() ? create_accumulators() : it->second;
-            for (auto& rec : g.second) accumulate(acc, rec.vals, rec.nul);
+            if (phase == FW_PHASE_GLOBAL) {
+                Row local = create_accumulators();
+                for (auto& rec : g.second) merge(local, row_from_fields(rec.vals, rec.nul));
+                merge(acc, local);
+            } else {
+                for (auto& rec : g.second) accumulate(acc, rec.vals, rec.nul);
+            }
             state[sk] = acc;
             if (!is_window_fired(slice, timer_watermark)) register_timer(key, slice);
         }
@@ -539,6 +619,18 @@ struct Oracle {
         }
     }
 
+    // LocalSlicingWindowAggOperator.processWatermark (:117-130): flush (emit partials) when the
+    // watermark may trigger a window; no timers, no state
+    void local_process_watermark(int64_t wm) {
+        if (wm > current_watermark) {
+            current_watermark = wm;
+            if (current_watermark >= next_trigger_progress) {
+                if (is_window_fired(min_slice_end, current_watermark)) flush();
+                next_trigger_progress = next_trigger_watermark(current_watermark, cfg.interval);
+            }
+        }
+    }
+
     // WindowAggOperator.processWatermark (:227-238)
     void sql_process_watermark(int64_t wm) {
         if (wm > current_watermark) {
@@ -608,7 +700,9 @@ struct Oracle {
     }
 
     void process_watermark(int64_t wm) {
-        if (ds) ds_process_watermark(wm); else sql_process_watermark(wm);
+        if (ds) ds_process_watermark(wm);
+        else if (phase == FW_PHASE_LOCAL) local_process_watermark(wm);
+        else sql_process_watermark(wm);
         epoch++;
     }
 
@@ -644,6 +738,7 @@ void* or_create(const fw_config* c) {
     Oracle* o = new Oracle();
     o->cfg.c = *c;
     o->ds = c->api == FW_API_DATASTREAM;
+    o->phase = c->agg_phase;
     if (c->window_kind == FW_WIN_TUMBLE) { o->cfg.interval = c->size_ms; o->cfg.n_slices = 1; }
     else if (c->window_kind == FW_WIN_HOP) {
         o->cfg.interval = gcd64(c->size_ms, c->slide_ms);
@@ -690,6 +785,14 @@ int64_t or_timer_count(void* h) { return (int64_t)((Oracle*)h)->timers.size(); }
 int64_t or_current_watermark(void* h) { return ((Oracle*)h)->current_watermark; }
 
 int64_t or_num_results(void* h) { return (int64_t)((Oracle*)h)->out.size(); }
+// result value columns: the aggregates, or the LOCAL phase's accumulator fields
+int32_t or_num_value_columns(void* h) {
+    Oracle* o = (Oracle*)h;
+    if (o->phase != FW_PHASE_LOCAL) return o->cfg.c.n_aggs;
+    int n = 0;
+    for (int a = 0; a < o->cfg.c.n_aggs; a++) n += o->cfg.c.aggs[a].kind == FW_AGG_AVG ? 2 : 1;
+    return n;
+}
 // Copies results into SoA arrays (each may be NULL): vals[a * n + i].
 void or_get_results(void* h, int64_t* key, int64_t* ws, int64_t* we, uint64_t* vals, uint32_t* nm, int64_t* epoch) {
     Oracle* o = (Oracle*)h;
@@ -701,7 +804,7 @@ void or_get_results(void* h, int64_t* key, int64_t* ws, int64_t* we, uint64_t* v
         if (we) we[i] = r.we;
         if (nm) nm[i] = r.null_mask;
         if (epoch) epoch[i] = r.epoch;
-        if (vals) for (int a = 0; a < o->cfg.c.n_aggs; a++) vals[(int64_t)a * n + i] = r.v[a];
+        if (vals) for (int a = 0; a < or_num_value_columns(h); a++) vals[(int64_t)a * n + i] = r.v[a];
     }
 }
 void or_clear_results(void* h) { ((Oracle*)h)->out.clear(); }

@@ -37,6 +37,8 @@ def lib():
         L.or_process_watermark.argtypes = [vp, i64]
         L.or_flush.argtypes = [vp]
         L.or_snapshot_restore.argtypes = [vp]
+        L.or_num_value_columns.restype = i32
+        L.or_num_value_columns.argtypes = [vp]
         for f in ("or_late_dropped", "or_state_size", "or_timer_count", "or_num_results",
                   "or_current_watermark"):
             getattr(L, f).restype = i64
@@ -123,7 +125,7 @@ class OracleOperator:
     def results(self, clear=True):
         L = lib()
         n = L.or_num_results(self.h)
-        na = self.cfg.n_aggs
+        na = L.or_num_value_columns(self.h)
         key = np.empty(n, np.int64)
         ws = np.empty(n, np.int64)
         we = np.empty(n, np.int64)

@@ -20,6 +20,22 @@ the reference test asserts after each watermark (plus the late-drop counter).  S
        Output records are (key, sum) with timestamp window.maxTimestamp().
   DOCS docs/content/docs/sql/reference/queries/window-agg.md:55-117 (global TUMBLE / HOP /
        CUMULATE SUM(price) over the Bid table; DECIMAL(10,2) prices carried as BIGINT cents).
+  TPRG flink-table/flink-table-planner/src/test/java/org/apache/flink/table/planner/plan/nodes/
+       exec/stream/WindowAggregateTestPrograms.java:39-60 (data), :86-375 (expected rows),
+       :500-511 (SELECT name, window_start, window_end, COUNT(*), SUM(a_int), COUNT(DISTINCT
+       comment)): TUMBLE / HOP / CUMULATE with and without offset, ONE_PHASE and TWO_PHASE, a
+       savepoint between the "before" and "after" data.  COUNT(DISTINCT) is not a GPU aggregate
+       (the eligibility rule sends it to the reference operator), so those fixtures carry
+       COUNT(*) and SUM(a_int) only.  The source's watermark is rowtime - 1 s
+       (:75), emitted after every record; end of input emits Long.MAX_VALUE.
+  ITC  flink-table/flink-table-planner/src/test/scala/org/apache/flink/table/planner/runtime/
+       stream/sql/WindowAggregateITCase.scala:218-282 with TestData.windowDataWithTimestamp
+       (flink-table-planner/src/test/scala/.../runtime/utils/TestData.scala:749-762): COUNT(*)
+       and MAX(double) (a NULL-able DOUBLE column); SUM(DECIMAL) and MIN(FLOAT) are not GPU
+       aggregates.
+  KATS flink-table/flink-table-runtime/src/test/java/org/apache/flink/table/runtime/operators/
+       window/tvf/slicing/{Tumbling,Hopping,Cumulative}SliceAssignerTest.java (UTC): slice end,
+       window start, expired slices, slices to merge, next trigger window.
 
 Keys that are strings in the reference tests are mapped to integer ids; their Java
 String.hashCode is recorded so key-group assignment matches the reference.  "snapshot_restore"
@@ -230,7 +246,230 @@ FIXTURES.append({
 })
 
 
+# ---------------------------------------------------------------- WindowAggregateTestPrograms
+T0_TP = int(dt.datetime(2020, 10, 10, tzinfo=dt.timezone.utc).timestamp() * 1000)
+# (seconds after 2020-10-10T00:00, a_int, b_double, name) of BEFORE_DATA / AFTER_DATA (:39-60)
+TP_BEFORE = [(1, 1, 1.0, "a"), (2, 2, 2.0, "a"), (3, 2, 2.0, "a"), (4, 5, 5.0, "a"), (7, 3, 3.0, "b"),
+             (6, 6, 6.0, "b"), (8, 3, None, "a"), (4, 5, 5.0, "a"), (16, 4, 4.0, "b"), (32, 7, 7.0, None),
+             (34, 1, 3.0, "b")]
+TP_AFTER = [(40, 10, 3.0, "a"), (42, 11, 4.0, "d"), (43, 12, 5.0, "c"), (44, 13, 6.0, "d")]
+TP_KEYS = {"a": {"id": 1, "hash": java_string_hash("a")}, "b": {"id": 2, "hash": java_string_hash("b")},
+           "c": {"id": 3, "hash": java_string_hash("c")}, "d": {"id": 4, "hash": java_string_hash("d")},
+           "null": {"id": 0, "hash": 0}}
+
+
+def _tp_time(hms):  # "00:00:05" or "23:59:55" of 2020-10-10 / 2020-10-09
+    return hms
+
+
+def _iso_ms(s):
+    return int(dt.datetime.fromisoformat(s).replace(tzinfo=dt.timezone.utc).timestamp() * 1000)
+
+
+def _records(rows, column, wm_state):
+    """elements (+ the rowtime - 1 s watermark after every record that raises it)"""
+    steps = []
+    for sec, a_int, b_double, name in rows:
+        ts = T0_TP + sec * 1000
+        key = name if name is not None else "null"
+        if column == "a_int":
+            steps.append({"op": "element", "key": key, "ts": ts, "values": [a_int]})
+        else:
+            steps.append({"op": "element", "key": key, "ts": ts, "values": [0.0 if b_double is None else b_double],
+                          "nulls": [1 if b_double is None else 0]})
+        w = ts - 1000
+        if w > wm_state[0]:
+            wm_state[0] = w
+            steps.append({"op": "watermark", "wm": w})
+    return steps
+
+
+def _parse_rows(rows):
+    out = []
+    for r in rows:
+        f = [x.strip() for x in r[3:-1].split(",")]
+        out.append({"key": f[0], "window_start": _iso_ms(f[1]), "window_end": _iso_ms(f[2]),
+                    "values": [int(f[3]), int(f[4])]})
+    return out
+
+
+def _tp(name, src, window, size_ms, slide_ms, offset_ms, before, after):
+    st = [-(1 << 63)]
+    steps = _records(TP_BEFORE, "a_int", st)
+    steps.append({"op": "check", "expect": _parse_rows(before)})
+    steps.append(SNAP)
+    steps += _records(TP_AFTER, "a_int", st)
+    steps.append({"op": "watermark", "wm": INT64_MAX})
+    steps.append({"op": "check", "expect": _parse_rows(after)})
+    FIXTURES.append({
+        "name": name, "source": src, "keys": TP_KEYS, "two_phase": True,
+        "config": {"api": "SQL", "window": window, "size_ms": size_ms, "slide_ms": slide_ms,
+                   "offset_ms": offset_ms, "count_star_index": 0, "key_hash": "PRECOMPUTED",
+                   "aggs": [["COUNT_STAR", 0, "BIGINT"], ["SUM", 0, "INT"]], "value_cols": ["INT"]},
+        "steps": steps, "late_dropped": None})
+
+
+_TPF = "WindowAggregateTestPrograms.java"
+_tp("tp_tumble_5s", _TPF + ":86-117 TUMBLE_WINDOW_EVENT_TIME(_TWO_PHASE)", "TUMBLE", 5000, 0, 0,
+    ["+I[a, 2020-10-10T00:00, 2020-10-10T00:00:05, 4, 10, 2]", "+I[a, 2020-10-10T00:00:05, 2020-10-10T00:00:10, 1, 3, 1]",
+     "+I[b, 2020-10-10T00:00:05, 2020-10-10T00:00:10, 2, 9, 2]", "+I[b, 2020-10-10T00:00:15, 2020-10-10T00:00:20, 1, 4, 1]"],
+    ["+I[b, 2020-10-10T00:00:30, 2020-10-10T00:00:35, 1, 1, 1]", "+I[null, 2020-10-10T00:00:30, 2020-10-10T00:00:35, 1, 7, 0]",
+     "+I[a, 2020-10-10T00:00:40, 2020-10-10T00:00:45, 1, 10, 1]", "+I[c, 2020-10-10T00:00:40, 2020-10-10T00:00:45, 1, 12, 1]",
+     "+I[d, 2020-10-10T00:00:40, 2020-10-10T00:00:45, 2, 24, 2]"])
+_tp("tp_tumble_5s_offset_1s", _TPF + ":129-160 TUMBLE_WINDOW_EVENT_TIME(_TWO_PHASE)_WITH_OFFSET", "TUMBLE", 5000, 0, 1000,
+    ["+I[a, 2020-10-10T00:00:01, 2020-10-10T00:00:06, 4, 10, 2]", "+I[b, 2020-10-10T00:00:06, 2020-10-10T00:00:11, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00:06, 2020-10-10T00:00:11, 1, 3, 1]", "+I[b, 2020-10-10T00:00:16, 2020-10-10T00:00:21, 1, 4, 1]"],
+    ["+I[b, 2020-10-10T00:00:31, 2020-10-10T00:00:36, 1, 1, 1]", "+I[null, 2020-10-10T00:00:31, 2020-10-10T00:00:36, 1, 7, 0]",
+     "+I[a, 2020-10-10T00:00:36, 2020-10-10T00:00:41, 1, 10, 1]", "+I[c, 2020-10-10T00:00:41, 2020-10-10T00:00:46, 1, 12, 1]",
+     "+I[d, 2020-10-10T00:00:41, 2020-10-10T00:00:46, 2, 24, 2]"])
+_tp("tp_hop_5s_10s", _TPF + ":172-211 HOP_WINDOW_EVENT_TIME(_TWO_PHASE)", "HOP", 10000, 5000, 0,
+    ["+I[a, 2020-10-09T23:59:55, 2020-10-10T00:00:05, 4, 10, 2]", "+I[b, 2020-10-10T00:00, 2020-10-10T00:00:10, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00, 2020-10-10T00:00:10, 6, 18, 3]", "+I[b, 2020-10-10T00:00:05, 2020-10-10T00:00:15, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00:05, 2020-10-10T00:00:15, 1, 3, 1]", "+I[b, 2020-10-10T00:00:10, 2020-10-10T00:00:20, 1, 4, 1]",
+     "+I[b, 2020-10-10T00:00:15, 2020-10-10T00:00:25, 1, 4, 1]"],
+    ["+I[b, 2020-10-10T00:00:25, 2020-10-10T00:00:35, 1, 1, 1]", "+I[null, 2020-10-10T00:00:25, 2020-10-10T00:00:35, 1, 7, 0]",
+     "+I[b, 2020-10-10T00:00:30, 2020-10-10T00:00:40, 1, 1, 1]", "+I[null, 2020-10-10T00:00:30, 2020-10-10T00:00:40, 1, 7, 0]",
+     "+I[c, 2020-10-10T00:00:35, 2020-10-10T00:00:45, 1, 12, 1]", "+I[d, 2020-10-10T00:00:35, 2020-10-10T00:00:45, 2, 24, 2]",
+     "+I[a, 2020-10-10T00:00:35, 2020-10-10T00:00:45, 1, 10, 1]", "+I[d, 2020-10-10T00:00:40, 2020-10-10T00:00:50, 2, 24, 2]",
+     "+I[a, 2020-10-10T00:00:40, 2020-10-10T00:00:50, 1, 10, 1]", "+I[c, 2020-10-10T00:00:40, 2020-10-10T00:00:50, 1, 12, 1]"])
+_tp("tp_hop_5s_10s_offset_1s", _TPF + ":223-262 HOP_WINDOW_EVENT_TIME(_TWO_PHASE)_WITH_OFFSET", "HOP", 10000, 5000, 1000,
+    ["+I[a, 2020-10-09T23:59:56, 2020-10-10T00:00:06, 4, 10, 2]", "+I[b, 2020-10-10T00:00:01, 2020-10-10T00:00:11, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00:01, 2020-10-10T00:00:11, 6, 18, 3]", "+I[b, 2020-10-10T00:00:06, 2020-10-10T00:00:16, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00:06, 2020-10-10T00:00:16, 1, 3, 1]", "+I[b, 2020-10-10T00:00:11, 2020-10-10T00:00:21, 1, 4, 1]",
+     "+I[b, 2020-10-10T00:00:16, 2020-10-10T00:00:26, 1, 4, 1]"],
+    ["+I[b, 2020-10-10T00:00:26, 2020-10-10T00:00:36, 1, 1, 1]", "+I[null, 2020-10-10T00:00:26, 2020-10-10T00:00:36, 1, 7, 0]",
+     "+I[a, 2020-10-10T00:00:31, 2020-10-10T00:00:41, 1, 10, 1]", "+I[b, 2020-10-10T00:00:31, 2020-10-10T00:00:41, 1, 1, 1]",
+     "+I[null, 2020-10-10T00:00:31, 2020-10-10T00:00:41, 1, 7, 0]", "+I[c, 2020-10-10T00:00:36, 2020-10-10T00:00:46, 1, 12, 1]",
+     "+I[d, 2020-10-10T00:00:36, 2020-10-10T00:00:46, 2, 24, 2]", "+I[a, 2020-10-10T00:00:36, 2020-10-10T00:00:46, 1, 10, 1]",
+     "+I[d, 2020-10-10T00:00:41, 2020-10-10T00:00:51, 2, 24, 2]", "+I[c, 2020-10-10T00:00:41, 2020-10-10T00:00:51, 1, 12, 1]"])
+_tp("tp_cumulate_5s_15s", _TPF + ":274-313 CUMULATE_WINDOW_EVENT_TIME(_TWO_PHASE)", "CUMULATE", 15000, 5000, 0,
+    ["+I[a, 2020-10-10T00:00, 2020-10-10T00:00:05, 4, 10, 2]", "+I[b, 2020-10-10T00:00, 2020-10-10T00:00:10, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00, 2020-10-10T00:00:10, 6, 18, 3]", "+I[b, 2020-10-10T00:00, 2020-10-10T00:00:15, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00, 2020-10-10T00:00:15, 6, 18, 3]", "+I[b, 2020-10-10T00:00:15, 2020-10-10T00:00:20, 1, 4, 1]",
+     "+I[b, 2020-10-10T00:00:15, 2020-10-10T00:00:25, 1, 4, 1]", "+I[b, 2020-10-10T00:00:15, 2020-10-10T00:00:30, 1, 4, 1]"],
+    ["+I[b, 2020-10-10T00:00:30, 2020-10-10T00:00:35, 1, 1, 1]", "+I[null, 2020-10-10T00:00:30, 2020-10-10T00:00:35, 1, 7, 0]",
+     "+I[b, 2020-10-10T00:00:30, 2020-10-10T00:00:40, 1, 1, 1]", "+I[null, 2020-10-10T00:00:30, 2020-10-10T00:00:40, 1, 7, 0]",
+     "+I[b, 2020-10-10T00:00:30, 2020-10-10T00:00:45, 1, 1, 1]", "+I[c, 2020-10-10T00:00:30, 2020-10-10T00:00:45, 1, 12, 1]",
+     "+I[d, 2020-10-10T00:00:30, 2020-10-10T00:00:45, 2, 24, 2]", "+I[a, 2020-10-10T00:00:30, 2020-10-10T00:00:45, 1, 10, 1]",
+     "+I[null, 2020-10-10T00:00:30, 2020-10-10T00:00:45, 1, 7, 0]"])
+_tp("tp_cumulate_5s_15s_offset_1s", _TPF + ":325-365 CUMULATE_WINDOW_EVENT_TIME(_TWO_PHASE)_WITH_OFFSET", "CUMULATE", 15000, 5000, 1000,
+    ["+I[a, 2020-10-10T00:00:01, 2020-10-10T00:00:06, 4, 10, 2]", "+I[b, 2020-10-10T00:00:01, 2020-10-10T00:00:11, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00:01, 2020-10-10T00:00:11, 6, 18, 3]", "+I[b, 2020-10-10T00:00:01, 2020-10-10T00:00:16, 2, 9, 2]",
+     "+I[a, 2020-10-10T00:00:01, 2020-10-10T00:00:16, 6, 18, 3]", "+I[b, 2020-10-10T00:00:16, 2020-10-10T00:00:21, 1, 4, 1]",
+     "+I[b, 2020-10-10T00:00:16, 2020-10-10T00:00:26, 1, 4, 1]", "+I[b, 2020-10-10T00:00:16, 2020-10-10T00:00:31, 1, 4, 1]"],
+    ["+I[b, 2020-10-10T00:00:31, 2020-10-10T00:00:36, 1, 1, 1]", "+I[null, 2020-10-10T00:00:31, 2020-10-10T00:00:36, 1, 7, 0]",
+     "+I[a, 2020-10-10T00:00:31, 2020-10-10T00:00:41, 1, 10, 1]", "+I[b, 2020-10-10T00:00:31, 2020-10-10T00:00:41, 1, 1, 1]",
+     "+I[null, 2020-10-10T00:00:31, 2020-10-10T00:00:41, 1, 7, 0]", "+I[b, 2020-10-10T00:00:31, 2020-10-10T00:00:46, 1, 1, 1]",
+     "+I[c, 2020-10-10T00:00:31, 2020-10-10T00:00:46, 1, 12, 1]", "+I[d, 2020-10-10T00:00:31, 2020-10-10T00:00:46, 2, 24, 2]",
+     "+I[a, 2020-10-10T00:00:31, 2020-10-10T00:00:46, 1, 10, 1]", "+I[null, 2020-10-10T00:00:31, 2020-10-10T00:00:46, 1, 7, 0]"])
+
+
+# ---------------------------------------------------------------- WindowAggregateITCase MAX(double)
+def _itc(name, src, size_ms, offset_ms, rows):
+    st = [-(1 << 63)]
+    steps = _records(TP_BEFORE, "b_double", st)
+    steps.append({"op": "watermark", "wm": INT64_MAX})
+    exp = []
+    for key, ws, we, cnt, mx in rows:
+        exp.append({"key": key, "window_start": _iso_ms(ws), "window_end": _iso_ms(we),
+                    "values": [cnt, mx], "nulls": [0, 1 if mx is None else 0]})
+    steps.append({"op": "check", "expect": exp})
+    FIXTURES.append({
+        "name": name, "source": src, "keys": TP_KEYS, "two_phase": True,
+        "config": {"api": "SQL", "window": "TUMBLE", "size_ms": size_ms, "slide_ms": 0, "offset_ms": offset_ms,
+                   "count_star_index": -1, "key_hash": "PRECOMPUTED", "nullable_cols": [0],
+                   "aggs": [["COUNT_STAR", 0, "BIGINT"], ["MAX", 0, "DOUBLE"]], "value_cols": ["DOUBLE"]},
+        "steps": steps, "late_dropped": 1 if size_ms == 5000 else 0})
+
+
+_ITC = "WindowAggregateITCase.scala"
+_itc("itc_tumble_5s_max_double", _ITC + ":218-230 testEventTimeTumbleWindow", 5000, 0, [
+    ("a", "2020-10-10T00:00", "2020-10-10T00:00:05", 4, 5.0), ("a", "2020-10-10T00:00:05", "2020-10-10T00:00:10", 1, None),
+    ("b", "2020-10-10T00:00:05", "2020-10-10T00:00:10", 2, 6.0), ("b", "2020-10-10T00:00:15", "2020-10-10T00:00:20", 1, 4.0),
+    ("b", "2020-10-10T00:00:30", "2020-10-10T00:00:35", 1, 3.0), ("null", "2020-10-10T00:00:30", "2020-10-10T00:00:35", 1, 7.0)])
+_itc("itc_tumble_1d_offset_8h_max_double", _ITC + ":232-242 testEventTimeTumbleWindowWithOffset", 86400000, 8 * 3600000, [
+    ("a", "2020-10-09T08:00", "2020-10-10T08:00", 6, 5.0), ("b", "2020-10-09T08:00", "2020-10-10T08:00", 4, 6.0),
+    ("null", "2020-10-09T08:00", "2020-10-10T08:00", 1, 7.0)])
+_itc("itc_tumble_1d_offset_neg8h_max_double", _ITC + ":272-282 testEventTimeTumbleWindowWithNegativeOffset", 86400000, -8 * 3600000, [
+    ("a", "2020-10-09T16:00", "2020-10-10T16:00", 6, 5.0), ("b", "2020-10-09T16:00", "2020-10-10T16:00", 4, 6.0),
+    ("null", "2020-10-09T16:00", "2020-10-10T16:00", 1, 7.0)])
+
+
+# ---------------------------------------------------------------- SliceAssigner KATs (UTC)
+def _u(s):
+    return _iso_ms(s)
+
+
+H = 3600000
+_SAT = "flink-table-runtime/src/test/java/org/apache/flink/table/runtime/operators/window/tvf/slicing/"
+KATS = [
+    # TumblingSliceAssignerTest.java
+    {"src": _SAT + "TumblingSliceAssignerTest.java:35-44", "assigner": ["TUMBLE", 5 * H, 0, 0], "op": "slice_end",
+     "cases": [[_u("1970-01-01T00:00:00"), _u("1970-01-01T05:00:00")], [_u("1970-01-01T04:59:59.999"), _u("1970-01-01T05:00:00")],
+               [_u("1970-01-01T05:00:00"), _u("1970-01-01T10:00:00")]]},
+    {"src": _SAT + "TumblingSliceAssignerTest.java:48-58", "assigner": ["TUMBLE", 5 * H, 0, 100], "op": "slice_end",
+     "cases": [[_u("1970-01-01T00:00:00.100"), _u("1970-01-01T05:00:00.100")], [_u("1970-01-01T05:00:00.099"), _u("1970-01-01T05:00:00.100")],
+               [_u("1970-01-01T05:00:00.100"), _u("1970-01-01T10:00:00.100")]]},
+    {"src": _SAT + "TumblingSliceAssignerTest.java:100-108", "assigner": ["TUMBLE", 5 * H, 0, 0], "op": "window_start",
+     "cases": [[_u("1970-01-01T00:00:00"), _u("1969-12-31T19:00:00")], [_u("1970-01-01T05:00:00"), _u("1970-01-01T00:00:00")],
+               [_u("1970-01-01T10:00:00"), _u("1970-01-01T05:00:00")]]},
+    {"src": _SAT + "TumblingSliceAssignerTest.java:113-121", "assigner": ["TUMBLE", 5 * H, 0, 0], "op": "expired_slices",
+     "cases": [[_u("1970-01-01T00:00:00"), [_u("1970-01-01T00:00:00")]], [_u("1970-01-01T05:00:00"), [_u("1970-01-01T05:00:00")]],
+               [_u("1970-01-01T10:00:00"), [_u("1970-01-01T10:00:00")]]]},
+    # HoppingSliceAssignerTest.java
+    {"src": _SAT + "HoppingSliceAssignerTest.java:37-47", "assigner": ["HOP", 5 * H, 1 * H, 0], "op": "slice_end",
+     "cases": [[_u("1970-01-01T00:00:00"), _u("1970-01-01T01:00:00")], [_u("1970-01-01T04:59:59.999"), _u("1970-01-01T05:00:00")],
+               [_u("1970-01-01T05:00:00"), _u("1970-01-01T06:00:00")]]},
+    {"src": _SAT + "HoppingSliceAssignerTest.java:51-63", "assigner": ["HOP", 5 * H, 1 * H, 100], "op": "slice_end",
+     "cases": [[_u("1970-01-01T00:00:00.100"), _u("1970-01-01T01:00:00.100")], [_u("1970-01-01T05:00:00.099"), _u("1970-01-01T05:00:00.100")],
+               [_u("1970-01-01T05:00:00.100"), _u("1970-01-01T06:00:00.100")]]},
+    {"src": _SAT + "HoppingSliceAssignerTest.java:109-128", "assigner": ["HOP", 5 * H, 1 * H, 0], "op": "window_start",
+     "cases": [[_u("1970-01-01T%02d:00:00" % h), _u("1970-01-01T%02d:00:00" % (h - 5)) if h >= 5 else
+                _u("1969-12-31T%02d:00:00" % (h + 19))] for h in (0, 1, 2, 3, 4, 5, 6, 10)]},
+    {"src": _SAT + "HoppingSliceAssignerTest.java:132-141", "assigner": ["HOP", 4 * H, 1 * H, 0], "op": "expired_slices",
+     "cases": [[_u("1970-01-01T00:00:00"), [_u("1969-12-31T21:00:00")]], [_u("1970-01-01T04:00:00"), [_u("1970-01-01T01:00:00")]],
+               [_u("1970-01-01T08:00:00"), [_u("1970-01-01T05:00:00")]]]},
+    {"src": _SAT + "HoppingSliceAssignerTest.java:143-173", "assigner": ["HOP", 5 * H, 1 * H, 0], "op": "merge",
+     "cases": [[_u("1970-01-01T00:00:00"), [None, [_u("1970-01-01T00:00:00"), _u("1969-12-31T23:00:00"), _u("1969-12-31T22:00:00"),
+                                                    _u("1969-12-31T21:00:00"), _u("1969-12-31T20:00:00")]]],
+               [_u("1970-01-01T05:00:00"), [None, [_u("1970-01-01T0%d:00:00" % h) for h in (5, 4, 3, 2, 1)]]],
+               [_u("1970-01-01T06:00:00"), [None, [_u("1970-01-01T0%d:00:00" % h) for h in (6, 5, 4, 3, 2)]]]]},
+    {"src": _SAT + "HoppingSliceAssignerTest.java:177-210 (window not empty / empty)", "assigner": ["HOP", 5 * H, 1 * H, 0],
+     "op": "next_trigger", "cases": [[[_u("1970-01-01T0%d:00:00" % h), False], _u("1970-01-01T0%d:00:00" % (h + 1))] for h in range(7)]
+     + [[[_u("1970-01-01T0%d:00:00" % h), True], None] for h in range(7)]},
+    # CumulativeSliceAssignerTest.java
+    {"src": _SAT + "CumulativeSliceAssignerTest.java testSliceAssignment", "assigner": ["CUMULATE", 24 * H, 1 * H, 0], "op": "slice_end",
+     "cases": [[_u("1970-01-01T00:00:00"), _u("1970-01-01T01:00:00")], [_u("1970-01-02T22:59:59.999"), _u("1970-01-02T23:00:00")],
+               [_u("1970-01-02T23:00:00"), _u("1970-01-03T00:00:00")]]},
+    {"src": _SAT + "CumulativeSliceAssignerTest.java testSliceAssignmentWithOffset", "assigner": ["CUMULATE", 5 * H, 1 * H, 100], "op": "slice_end",
+     "cases": [[_u("1970-01-01T00:00:00.100"), _u("1970-01-01T01:00:00.100")], [_u("1970-01-01T05:00:00.099"), _u("1970-01-01T05:00:00.100")],
+               [_u("1970-01-01T05:00:00.100"), _u("1970-01-01T06:00:00.100")]]},
+    {"src": _SAT + "CumulativeSliceAssignerTest.java testGetWindowStart", "assigner": ["CUMULATE", 5 * H, 1 * H, 0], "op": "window_start",
+     "cases": [[_u("1970-01-01T00:00:00"), _u("1969-12-31T19:00:00")]] +
+              [[_u("1970-01-01T0%d:00:00" % h), _u("1970-01-01T00:00:00")] for h in (1, 2, 3, 4, 5)] +
+              [[_u("1970-01-01T06:00:00"), _u("1970-01-01T05:00:00")], [_u("1970-01-01T08:00:00"), _u("1970-01-01T05:00:00")]]},
+    {"src": _SAT + "CumulativeSliceAssignerTest.java testExpiredSlices", "assigner": ["CUMULATE", 5 * H, 1 * H, 0], "op": "expired_slices",
+     "cases": [[_u("1970-01-01T01:00:00"), []]] + [[_u("1970-01-01T0%d:00:00" % h), [_u("1970-01-01T0%d:00:00" % h)]] for h in (2, 3, 4)] +
+              [[_u("1970-01-01T05:00:00"), [_u("1970-01-01T05:00:00"), _u("1970-01-01T01:00:00")]],
+               [_u("1970-01-01T06:00:00"), []],
+               [_u("1970-01-01T10:00:00"), [_u("1970-01-01T10:00:00"), _u("1970-01-01T06:00:00")]],
+               [_u("1970-01-01T00:00:00"), [_u("1970-01-01T00:00:00"), _u("1969-12-31T20:00:00")]]]},
+    {"src": _SAT + "CumulativeSliceAssignerTest.java testMerge", "assigner": ["CUMULATE", 5 * H, 1 * H, 0], "op": "merge",
+     "cases": [[_u("1970-01-01T01:00:00"), [_u("1970-01-01T01:00:00"), []]]] +
+              [[_u("1970-01-01T0%d:00:00" % h), [_u("1970-01-01T01:00:00"), [_u("1970-01-01T0%d:00:00" % h)]]] for h in (2, 3, 4, 5)] +
+              [[_u("1970-01-01T06:00:00"), [_u("1970-01-01T06:00:00"), []]],
+               [_u("1970-01-01T08:00:00"), [_u("1970-01-01T06:00:00"), [_u("1970-01-01T08:00:00")]]],
+               [_u("1970-01-01T10:00:00"), [_u("1970-01-01T06:00:00"), [_u("1970-01-01T10:00:00")]]],
+               [_u("1970-01-01T00:00:00"), [_u("1969-12-31T20:00:00"), [_u("1970-01-01T00:00:00")]]]]},
+    {"src": _SAT + "CumulativeSliceAssignerTest.java testNextTriggerWindow", "assigner": ["CUMULATE", 5 * H, 1 * H, 0], "op": "next_trigger",
+     "cases": [[[_u("1970-01-01T0%d:00:00" % h, ), empty], (None if h in (0, 5) else _u("1970-01-01T0%d:00:00" % (h + 1)))]
+               for empty in (False, True) for h in range(7)]},
+]
+
+
 def main():
+    with open(os.path.join(HERE, "slice_assigner_kats.json"), "w") as fh:
+        json.dump(KATS, fh, indent=1)
     for f in FIXTURES:
         f.setdefault("keys", KEYS)
         with open(os.path.join(HERE, f["name"] + ".json"), "w") as fh:

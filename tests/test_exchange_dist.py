@@ -116,3 +116,89 @@ def test_gloo_two_subtasks_union_equals_unsharded():
     assert sum(r[3] for r in res) == op.late_dropped
     assert len(got) > 1000 and got == sorted(want)
     op.close()
+
+
+def _worker_two_phase(rank, port, n_batches, n, out_q):
+    """Two-phase plan on CPU: oracle LOCAL per source subtask -> keyBy exchange of the partial rows
+    (key, slice end, accumulator fields, null mask) -> oracle GLOBAL per subtask."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from flink_amd.runtime.exchange import KeyByExchange
+        from oracle.oracle import OracleOperator, key_group, key_group_range
+
+        ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+        lo, hi = key_group_range(128, WORLD, rank)
+        one = _cfg(WORLD, rank)
+        local_cfg = abi.make_config(window_kind=one.window_kind, size_ms=one.size_ms, slide_ms=one.slide_ms,
+                                    count_star_index=one.count_star_index,
+                                    aggs=[(one.aggs[i].kind, one.aggs[i].input_col, one.aggs[i].type) for i in range(one.n_aggs)],
+                                    value_col_types=[abi.T_I64], key_hash=abi.KEYHASH_BINROW_BIGINT,
+                                    agg_phase=abi.PHASE_LOCAL)
+        glob_cfg = abi.global_config(local_cfg, parallelism=WORLD, subtask_index=rank)
+        local, glob = OracleOperator(local_cfg), OracleOperator(glob_cfg)
+        rows, partials = [], 0
+        for b in range(n_batches):
+            k, t, v = _stream(rank, b, n)
+            local.process_batch(k, t, [v])
+            wm = ex.global_watermark(T0 + b * 3000 - 3000 + 500 * rank)
+            local.process_watermark(wm)
+            r = local.results()
+            nf = len(r["values"])
+            rk, rse, cols = ex.exchange(torch.from_numpy(r["key"]), torch.from_numpy(r["window_end"]),
+                                        [torch.from_numpy(x) for x in r["values"]] +
+                                        [torch.from_numpy(r["null_mask"].astype(np.int64))])
+            partials += rk.numel()
+            kgs = {key_group(abi.KEYHASH_BINROW_BIGINT, int(x), 128) for x in np.unique(rk.numpy())}
+            assert all(lo <= g <= hi for g in kgs), f"rank {rank}: foreign key group"
+            nm = cols[-1].numpy()
+            glob.process_batch(rk.numpy(), rse.numpy(), [c.numpy() for c in cols[:nf]],
+                               {j: (nm >> j) & 1 for j in range(nf)})
+            glob.process_watermark(wm)
+            rows += _rows(glob.results())
+        local.process_watermark(T0 + n_batches * 3000 + 60000)
+        r = local.results()
+        rk, rse, cols = ex.exchange(torch.from_numpy(r["key"]), torch.from_numpy(r["window_end"]),
+                                    [torch.from_numpy(x) for x in r["values"]] +
+                                    [torch.from_numpy(r["null_mask"].astype(np.int64))])
+        nm = cols[-1].numpy()
+        glob.process_batch(rk.numpy(), rse.numpy(), [c.numpy() for c in cols[:-1]],
+                           {j: (nm >> j) & 1 for j in range(len(cols) - 1)})
+        glob.process_watermark(T0 + n_batches * 3000 + 60000)
+        rows += _rows(glob.results())
+        out_q.put((rank, partials, rows, glob.late_dropped))
+        local.close()
+        glob.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_phase_union_equals_one_phase():
+    """LocalSlicingWindowAggOperator + GlobalAggCombiner across two subtasks (only partial rows on
+    the wire) produce exactly the one-phase results of one unsharded operator."""
+    from oracle.oracle import OracleOperator
+
+    n_batches, n = 8, 3000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_two_phase, args=(r, port, n_batches, n, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = sorted(row for r in res for row in r[2])
+    assert sum(r[1] for r in res) < WORLD * n_batches * n  # fewer partial rows than records on the wire
+    op = OracleOperator(_cfg(1, 0))
+    want = []
+    for b in range(n_batches):
+        cols = [_stream(r, b, n) for r in range(WORLD)]
+        op.process_batch(*[np.concatenate([c[i] for c in cols]) for i in (0, 1)], [np.concatenate([c[2] for c in cols])])
+        op.process_watermark(T0 + b * 3000 - 3000)
+        want += _rows(op.results())
+    op.process_watermark(T0 + n_batches * 3000 + 60000)
+    want += _rows(op.results())
+    assert len(got) > 1000 and got == sorted(want)
+    op.close()

@@ -552,3 +552,109 @@ def test_partition_by_dest_is_stable(p):
     assert np.array_equal(pk.cpu().numpy(), k[order])
     assert np.array_equal(pt.cpu().numpy(), t[order])
     assert np.array_equal(pv[0].cpu().numpy(), v[order])
+
+
+# ------------------------------------------------------------------------------------------
+# two-phase (local / global) aggregation: TwoStageOptimizedWindowAggregateRule's plan
+# ------------------------------------------------------------------------------------------
+TWO_PHASE_CASES = {
+    "tumble": dict(window_kind=abi.WIN_TUMBLE, size_ms=4000, offset_ms=-700,
+                   aggs=[(abi.AGG_SUM, 0, I64), (abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_AVG, 1, F64),
+                         (abi.AGG_MAX, 0, I64), (abi.AGG_COUNT, 1, F64)]),
+    "hop": dict(window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000, count_star_index=1,
+                aggs=[(abi.AGG_MIN, 0, I64), (abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 1, F64), (abi.AGG_AVG, 0, I64)]),
+    "cumulate": dict(window_kind=abi.WIN_CUMULATE, size_ms=8000, slide_ms=2000, count_star_index=0,
+                     aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_MAX, 1, F64), (abi.AGG_MIN, 0, I64)]),
+}
+
+
+def _push_partials_to_oracle(og, key, se, fields, nm):
+    n = key.numel()
+    if n == 0:
+        return
+    nmh = nm.cpu().numpy()
+    og.process_batch(key.cpu().numpy(), se.cpu().numpy(), [f.cpu().numpy() for f in fields],
+                     {j: (nmh >> j) & 1 for j in range(len(fields))})
+
+
+@pytest.mark.parametrize("name", sorted(TWO_PHASE_CASES))
+def test_two_phase_local_global_matches_oracle(name):
+    """LOCAL on the GPU against LocalAggCombiner's partials (oracle LOCAL, as a multiset per
+    watermark), GLOBAL on the GPU against the oracle GLOBAL fed the same partial rows, and the
+    end-to-end two-phase results against one one-phase operator (the plans agree)."""
+    torch = _torch_cuda()
+    from flink_amd.table.two_phase import TwoPhaseWindowAgg
+    from oracle.oracle import OracleOperator
+    kw = TWO_PHASE_CASES[name]
+    cfg = _cfg(kw, nullable_cols=[1])
+    tp = TwoPhaseWindowAgg(cfg)
+    ol, og, o1 = OracleOperator(tp.local_cfg), OracleOperator(tp.global_cfg), OracleOperator(cfg)
+    rng = np.random.default_rng(len(name))
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(40 + len(name), 40000, 500, ooo=2 * kw["size_ms"], step_ms=1300, n_wm=22)):
+        nul = {1: (rng.random(len(k)) < 0.2).astype(np.uint8)}
+        vals = [iv, dv.view(np.int64)]
+        tp.process_batch(k, t, vals, nulls=nul)
+        ol.process_batch(k, t, vals, nul)
+        o1.process_batch(k, t, vals, nul)
+        key, se, fields, nm = tp.local_partials(wm)
+        ol.process_watermark(wm)
+        want_l = _rows(ol.results(clear=True), tp.local_cfg, set())
+        got_l = sorted((int(a), int(b), int(b), tuple(int(f[i]) for f in fields), int(c))
+                       for i, (a, b, c) in enumerate(zip(key.tolist(), se.tolist(), nm.tolist())))
+        # LOCAL: DOUBLE sums fold in a different order (1e-9), the rest bit-exact
+        dcols_l = {j for j, ty in enumerate(tp.global_cfg.value_col_types[:tp.n_fields]) if ty == F64}
+        _compare(got_l, want_l, dcols_l, f"{name} LOCAL batch {bi}")
+        # GLOBAL fed the GPU's partials (in the GPU's order) on both sides
+        _push_partials_to_oracle(og, key, se, fields, nm)
+        tp.global_ingest(key, se, fields, nm)
+        tp.glob.advance(wm)
+        og.process_watermark(wm)
+        o1.process_watermark(wm)
+        got = _rows(tp.glob.results(reset=True), cfg, _double_cols(kw))
+        _compare(got, _rows(og.results(clear=True), cfg, _double_cols(kw)), _double_cols(kw), f"{name} GLOBAL batch {bi}")
+        _compare(got, _rows(o1.results(clear=True), cfg, _double_cols(kw)), _double_cols(kw), f"{name} vs one-phase batch {bi}")
+    # the GLOBAL operator counts dropped partial rows (one per (key, slice) group), not records
+    assert tp.num_late_records_dropped == og.late_dropped
+    tp.close()
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_two_phase_sharded_subtasks_match_one_phase(p):
+    """p source subtasks run LOCAL, their partials are routed by fw_partition_by_dest to p GLOBAL
+    subtasks (computeKeyGroupRangeForOperatorIndex), and the union of the GLOBAL results equals one
+    unsharded one-phase operator."""
+    torch = _torch_cuda()
+    from flink_amd.runtime.exchange import KeyByExchange
+    from flink_amd.table.two_phase import TwoPhaseWindowAgg
+    from oracle.oracle import OracleOperator
+    kw = TWO_PHASE_CASES["hop"]
+    cfgs = [_cfg(kw, key_hash=abi.KEYHASH_BINROW_BIGINT, parallelism=p, subtask_index=i) for i in range(p)]
+    ops = [TwoPhaseWindowAgg(c) for c in cfgs]
+    o1 = OracleOperator(_cfg(kw, key_hash=abi.KEYHASH_BINROW_BIGINT))
+    ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+    ex.world = p
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(77 + p, 50000, 3000, ooo=4000, step_ms=1500, n_wm=18)):
+        vals = [iv, dv.view(np.int64)]
+        o1.process_batch(k, t, vals)
+        for src, part in enumerate(np.array_split(np.arange(len(k)), p)):  # source subtasks
+            ops[src].process_batch(k[part], t[part], [v[part] for v in vals])
+        o1.process_watermark(wm)
+        # every source's partials, routed to the global subtasks (slicing replaces the all-to-all)
+        for src in range(p):
+            key, se, fields, nm = ops[src].local_partials(wm)
+            pk, pse, pcols, counts = ex.partition(key, se, fields + [nm])
+            off = 0
+            for d, c in enumerate(counts.tolist()):
+                if c:
+                    ops[d].global_ingest(pk[off:off + c], pse[off:off + c], [x[off:off + c] for x in pcols[:-1]],
+                                         pcols[-1][off:off + c])
+                off += c
+        got = []
+        for op in ops:
+            op.glob.advance(wm)
+            got += _rows(op.glob.results(reset=True), cfgs[0], _double_cols(kw))
+        _compare(sorted(got), _rows(o1.results(clear=True), cfgs[0], _double_cols(kw)), _double_cols(kw),
+                 f"two-phase p={p} batch {bi}")
+    for op in ops:
+        assert op.glob.stats()["error_flags"] == 0
+        op.close()

@@ -123,7 +123,7 @@ struct fw_handle {
     WordDesc wd{};
     AggDesc ad{};
     int nv = 0;
-    int slot_col[MAX_KCOLS] = {0, 0, 0, 0};
+    int slot_col[MAX_KCOLS] = {};
     int nw_t = 1;  // template word count (layout stride)
     int n_out = 1; // result value columns (aggregates; LOCAL phase: accumulator fields)
     int64_t cap_rows = 0;     // rows per partial-buffer slot (= max rows per push piece)
@@ -421,7 +421,7 @@ int validate_and_plan(fw_handle* h) {
     ks.n_sb = ks.n_kg << ks.sb_per_kg_log2;
     if (c.max_batch_rows <= 0) return fail(FW_E_INVALID, "max_batch_rows must be > 0");
     if (c.output_capacity <= 0) return fail(FW_E_INVALID, "output_capacity must be > 0");
-    h->chunk_rows = (int64_t)IG_BLOCK * ig_rpt(h->nw_t);
+    h->chunk_rows = (int64_t)IG_BLOCK * ig_rpt(h->nw_t, ig_nv(h->nv));
     h->cap_rows = ((c.max_batch_rows + h->chunk_rows - 1) / h->chunk_rows) * h->chunk_rows;
     h->max_nch = h->cap_rows / h->chunk_rows;
     if (wd.has_q && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
@@ -542,6 +542,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.ad = h->ad;
     a.always_flush = h->always_flush;
     a.local = h->cfg.agg_phase == FW_PHASE_LOCAL;
+    a.chunk_rows = (int32_t)h->chunk_rows;
     a.out_key = h->out_key;
     a.out_ws = h->out_ws;
     a.out_we = h->out_we;

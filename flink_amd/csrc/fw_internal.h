@@ -10,7 +10,7 @@ namespace fw {
 
 constexpr int BLOCK = 256;          // threads per workgroup of the small helper kernels
 constexpr int MAX_WORDS = 8;        // accumulator words per (key, slice)
-constexpr int MAX_KCOLS = 4;        // value columns a kernel loads per record
+constexpr int MAX_KCOLS = 8;        // value columns a kernel loads per record
 constexpr int FW_MAX_PENDING = 8;   // pushes buffered between two flushes
 
 // ---- ingest (K1+K2+K3): one 512-thread workgroup per chunk of IG_BLOCK * RPT rows, two
@@ -22,8 +22,11 @@ constexpr int IG_LDS = 78 * 1024;               // dynamic LDS per workgroup: hi
 constexpr int IG_MAX_SB = 8192;                 // superbuckets the ingest histogram holds (32 KiB)
 constexpr int IG_HDR_WORDS = 16;                // 8-B words of per-chunk counters at the LDS base
 constexpr int ig_hist_words(int n_sb) { return ((n_sb + 3) >> 2) << 1; }  // 16-B multiple
-// rows per thread by accumulator words: the chunk's partials stay in registers (<= 128 VGPRs)
-constexpr int ig_rpt(int nw) { return nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
+// rows per thread by accumulator words and loaded value columns (template NV): the chunk's rows
+// and partials stay in registers (<= 128 VGPRs)
+constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
+// the template NV of a count of loaded value columns
+constexpr int ig_nv(int nv) { return nv <= 2 ? nv : nv <= 4 ? 4 : 8; }
 // LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)
 constexpr int ig_slots(int nw) { return nw <= 2 ? 1024 : nw <= 4 ? 512 : 256; }
 constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw); }
@@ -267,6 +270,7 @@ struct MergeArgs {
     AggDesc ad;
     int32_t always_flush;    // DataStream: state is updated per record, flush every advance
     int32_t local;           // LOCAL phase: emit every gathered (key, slice) partial, keep no state
+    int32_t chunk_rows;      // rows per ingest chunk (IG_BLOCK * ig_rpt): the cells' row stride
     int64_t* out_key;        // output slabs: [n_sb][slab_cap] rows, then out_cap overflow rows
     int64_t* out_ws;
     int64_t* out_we;

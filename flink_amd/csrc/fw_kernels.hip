@@ -354,6 +354,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             if (a.khash) pre[j] = a.khash[i];
 #pragma unroll
             for (int q = 0; q < NV; q++) {
+                if (NV > 2 && q >= a.nv) break;  // the NV = 4 / 8 variants also serve 3 / 5-7 columns
                 rv[j][q] = a.vals[q][i];
                 if (X && a.nulls[q] && a.nulls[q][i]) rnul[j] |= 1u << q;
             }
@@ -1097,7 +1098,7 @@ template <int NW, int E, bool Q, int KIND>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
-    constexpr int CH = IG_BLOCK * ig_rpt(NW);  // chunk rows of the ingest kernel that wrote the cells
+    const int64_t CH = a.chunk_rows;  // chunk rows of the ingest kernel that wrote the cells
     constexpr int GU = mg_rows_in_flight(NW);
     __shared__ StateLds<NW, E> S;
     __shared__ int32_t s_work;
@@ -1386,7 +1387,7 @@ hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
 // ---------------------------------------------------------------------------------------
 template <int NV, int NW, bool X>
 static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
-    constexpr int RPT = ig_rpt(NW);
+    constexpr int RPT = ig_rpt(NW, NV);
     const int64_t nch = a.n_chunks;
     if (nch == 0) return hipSuccess;
     static bool attr_set = false;
@@ -1424,11 +1425,12 @@ static hipError_t ingest_nv(const IngestArgs& a, hipStream_t s, KTimer* t) {
 }
 
 hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t) {
-    switch (a.nv) {
+    switch (ig_nv(a.nv)) {
         case 0: return ingest_nv<0>(a, s, t);
         case 1: return ingest_nv<1>(a, s, t);
         case 2: return ingest_nv<2>(a, s, t);
-        default: return ingest_nv<4>(a, s, t);
+        case 4: return ingest_nv<4>(a, s, t);
+        default: return ingest_nv<8>(a, s, t);
     }
 }
 

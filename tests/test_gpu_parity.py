@@ -612,7 +612,14 @@ def test_two_phase_local_global_matches_oracle(name):
         o1.process_watermark(wm)
         got = _rows(tp.glob.results(reset=True), cfg, _double_cols(kw))
         _compare(got, _rows(og.results(clear=True), cfg, _double_cols(kw)), _double_cols(kw), f"{name} GLOBAL batch {bi}")
-        _compare(got, _rows(o1.results(clear=True), cfg, _double_cols(kw)), _double_cols(kw), f"{name} vs one-phase batch {bi}")
+        want1 = _rows(o1.results(clear=True), cfg, _double_cols(kw))
+        if not kw.get("offset_ms"):
+            # The plans agree on slice-aligned trigger grids.  With an offset they need not: both
+            # operators flush their buffers only when the watermark crosses the trigger grid of
+            # TimeWindowUtil.getNextTriggerWatermark, which ignores the window offset, so a LOCAL
+            # flush can reach the GLOBAL operator after its slice fired (then it drops as late),
+            # where the one-phase operator had accepted those records at arrival.
+            _compare(got, want1, _double_cols(kw), f"{name} vs one-phase batch {bi}")
     # the GLOBAL operator counts dropped partial rows (one per (key, slice) group), not records
     assert tp.num_late_records_dropped == og.late_dropped
     tp.close()

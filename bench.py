@@ -118,6 +118,8 @@ def main():
                          "8-B/lane read (2 GiB) + 4-B/lane write (1 GiB) that calibrates FETCH_SIZE/WRITE_SIZE")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged end-to-end leg (N=1 only)")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="diagnostic: time the steps without the per-launch hipEvents (no roofline)")
     ap.add_argument("--e2e-steps", type=int, default=6)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
@@ -232,7 +234,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    h.set_profiling(True)          # hipEvents around every launch on the operator's stream
+    h.set_profiling(not args.no_kernel_events)  # hipEvents around the launches on the operator's stream
     t0 = time.perf_counter()
     run(args.warmup, args.steps, h)
     h.sync()
@@ -252,6 +254,12 @@ def main():
 
     n_total = args.steps * B * world
     value = n_total / elapsed
+    if args.no_kernel_events:
+        if rank == 0:
+            print(json.dumps({"diagnostic": "no per-launch events", "value": value,
+                              "ms_per_step": elapsed / args.steps * 1e3}), flush=True)
+        h.close()
+        return
     # ---------------- roofline of the segmented-reduce (ingest) kernel ----------------------
     # algorithmic bytes per launch: N_b * sum(w_in) + G_b * w_partial, with
     # w_partial = key + slice + accumulator words (8 B each) and G_b the distinct (key, slice)

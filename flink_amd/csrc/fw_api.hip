@@ -79,7 +79,9 @@ struct EvTimer final : KTimer {
         (void)hipEventCreate(&e);
         return e;
     }
+    bool all = false;  // also the small bookkeeping launches (FW_KT_OTHER)
     void mark(int kind, bool end, hipStream_t s) override {
+        if (kind == FW_KT_OTHER && !all) return;  // each event record costs the stream a few us
         hipEvent_t ev = get();
         (void)hipEventRecord(ev, s);
         if (!end) {
@@ -152,6 +154,7 @@ struct fw_handle {
     int32_t* sb_out = nullptr;
     uint32_t* sb_fired = nullptr;
     int64_t* chunk_stats = nullptr;
+    Tickets* tickets = nullptr;  // last-workgroup election counters of k_ingest / k_merge_fire
     int64_t* coff = nullptr;   // compaction offsets [n_sb + 2]
     int64_t* res_key = nullptr;
     int64_t* res_ws = nullptr;
@@ -181,6 +184,7 @@ struct fw_handle {
     std::vector<uint32_t> r_null;
 
     int64_t pushes_ub = 0;  // upper bound of device pending_pushes
+    bool reset_pending = false;  // fw_results_reset called: the next merge launch empties the results
     int64_t host_cur = INT64_MIN;
     KTimer* timer = nullptr;  // non-null while fw_set_profiling is on
     int ablate = 0;           // FW_ABLATE (development timing builds only; results are wrong)
@@ -474,6 +478,8 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->coff, h->ks.n_sb + 2))) return rc;
     if ((rc = dalloc(&h->chunk_stats, 4 * h->max_nch + 4))) return rc;
     if ((rc = dalloc(&h->stamps, N_STAMPS))) return rc;
+    if ((rc = dalloc(&h->tickets, 1))) return rc;
+    HIP_TRY(hipMemsetAsync(h->tickets, 0, sizeof(Tickets), h->stream));
     HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(unsigned long long) * N_STAMPS, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_fired, 0, sizeof(uint32_t) * h->ks.n_sb, h->stream));
@@ -526,6 +532,7 @@ int read_ctrl(fw_handle* h, Ctrl* out) {
 MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     MergeArgs a{};
     a.ctrl = h->ctrl;
+    a.tickets = h->tickets;
     a.parts = h->parts;
     a.cells = h->cells;
     a.slot_nch = h->slot_nch;
@@ -554,13 +561,21 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.sb_fired = h->sb_fired;
     a.wm = wm;
     a.force_flush = force;
+    a.reset_out = h->reset_pending;
     a.ablate = h->ablate;
     a.stamps = h->stamps;
     return a;
 }
 
+int launch_merge(fw_handle* h, int64_t wm, int force) {
+    HIP_TRY(launch_merge_fire(merge_args(h, wm, force), h->stream, h->timer));
+    h->reset_pending = false;  // the launch started every output slab (and the overflow) afresh
+    return FW_OK;
+}
+
 int force_flush(fw_handle* h) {
-    HIP_TRY(launch_merge_fire(merge_args(h, INT64_MIN, 1), h->stream, h->timer));
+    int rc = launch_merge(h, INT64_MIN, 1);
+    if (rc) return rc;
     h->pushes_ub = 0;
     return FW_OK;
 }
@@ -594,6 +609,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.wd = h->wd;
         a.nv = h->nv;
         a.ctrl = h->ctrl;
+        a.tickets = h->tickets;
         a.parts = h->parts;
         a.cap_rows = h->cap_rows;
         a.cells = h->cells;
@@ -664,6 +680,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->sb_fired);
     hipFree(h->coff);
     hipFree(h->chunk_stats);
+    hipFree(h->tickets);
     hipFree(h->stamps);
     for (int b = 0; b < 2; b++) {
         hipHostFree(h->h_key[b]);
@@ -770,7 +787,8 @@ int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t*
 
 int fw_advance(fw_handle* h, int64_t watermark) {
     if (!h) return fail(FW_E_INVALID, "null handle");
-    HIP_TRY(launch_merge_fire(merge_args(h, watermark, 0), h->stream, h->timer));
+    int rc = launch_merge(h, watermark, 0);
+    if (rc) return rc;
     if (watermark > h->host_cur) h->host_cur = watermark;
     return FW_OK;
 }
@@ -782,6 +800,13 @@ int fw_flush(fw_handle* h) {
 
 int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    if (h->reset_pending) {  // consumed and nothing emitted since
+        Ctrl c;
+        int rc = read_ctrl(h, &c);
+        if (rc) return rc;
+        memset(out, 0, sizeof *out);
+        return FW_OK;
+    }
     CompactArgs ca{};
     ca.ctrl = h->ctrl;
     ca.sb_out = h->sb_out;
@@ -848,7 +873,8 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
 
 int fw_results_reset(fw_handle* h) {
     if (!h) return fail(FW_E_INVALID, "null handle");
-    HIP_TRY(launch_reset_results(h->ctrl, h->sb_out, h->ks.n_sb, h->stream));
+    // no launch: the next merge launch starts every output slab and the overflow region afresh
+    h->reset_pending = true;
     return FW_OK;
 }
 
@@ -863,12 +889,13 @@ int fw_get_stats(fw_handle* h, fw_stats* out) {
     HIP_TRY(hipMemcpyAsync(sbo.data(), h->sb_out, 4ll * nsb, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipMemcpyAsync(fired.data(), h->sb_fired, 4ll * nsb, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    int64_t live = 0, avail = std::min<int64_t>((int64_t)c.out_count, h->out_cap), nf = (int64_t)c.fired;
+    int64_t live = 0, avail = std::min<int64_t>((int64_t)c.out_count[c.ovf_sel & 1], h->out_cap), nf = (int64_t)c.fired;
     for (int s = 0; s < nsb; s++) {
         live += cnt[s];
         avail += sbo[s];
         nf += fired[s];
     }
+    if (h->reset_pending) avail = 0;
     memset(out, 0, sizeof *out);
     out->current_watermark = c.cur;
     out->next_trigger_progress = c.ntp;
@@ -887,7 +914,12 @@ int fw_set_profiling(fw_handle* h, int enable) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     HIP_TRY(hipStreamSynchronize(h->stream));
     delete h->timer;
-    h->timer = enable ? new EvTimer() : nullptr;
+    h->timer = nullptr;
+    if (enable) {
+        EvTimer* t = new EvTimer();
+        t->all = enable >= 2;
+        h->timer = t;
+    }
     return FW_OK;
 }
 

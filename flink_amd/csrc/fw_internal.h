@@ -110,13 +110,22 @@ constexpr uint32_t ERR_KEYGROUP = 16u;  // a record's key group is outside this 
 
 // Device-resident operator control block (one per handle).  Only kernels write it, so a
 // watermark cycle needs no host round trip.
+// Last-workgroup election counters (grid_last_wg): [ingest | merge][16 groups + top], one
+// 128-byte line each, so the grid's device-scope atomics do not queue on one address.
+constexpr int TK_GROUPS = 16;
+struct Tickets {
+    uint32_t c[2][TK_GROUPS + 1][32];
+};
+
 struct Ctrl {
     int64_t cur;             // currentProgress == operator / timer-service watermark
     int64_t ntp;             // nextTriggerProgress
     int64_t min_pending;     // RecordsWindowBuffer.minSliceEnd of the pending partials
     int64_t pending_pushes;  // pushes waiting in the partial buffer (flushed by k_merge_fire)
     int64_t n_treq;          // pending timer requests (late records)
-    uint64_t out_count;      // result rows produced since the last reset
+    uint64_t out_count[2];   // rows in the shared overflow region since the last reset; [ovf_sel] is
+                             // live, the other is kept 0 so a merge launch that resets the results
+                             // can start on it while the previous rows are still counted
     uint64_t late_dropped;   // numLateRecordsDropped
     uint64_t fired;          // fired (key, window) timers
     uint64_t pending_rows;   // rows ingested but not yet flushed
@@ -124,7 +133,10 @@ struct Ctrl {
     uint32_t error;
     int32_t push_slot;       // partial-buffer slot of the push being ingested
     uint64_t partials;       // partials written by the ingest kernels (cumulative)
-    uint64_t pad[3];
+    uint32_t pad1[2];
+    int32_t ovf_sel;         // live out_count
+    int32_t pad0;
+    uint64_t pad[1];
 };
 
 // Window / slice description shared by both kernels (SliceAssigners.java).
@@ -228,7 +240,8 @@ struct IngestArgs {
                            // of each (superbucket, chunk) cell inside the chunk's region
     int32_t* slot_nch;     // [FW_MAX_PENDING] chunks of each pending push
     int64_t max_nch;       // cell_pad(chunks per slot): cells per superbucket per slot
-    int64_t* chunk_stats;  // [n_chunks][3]: min target slice, dropped rows, accepted rows
+    int64_t* chunk_stats;  // [n_chunks][4]: min target slice, dropped rows, accepted rows, partials
+    Tickets* tickets;
     int64_t n_chunks;
     int64_t* treq;         // timer requests: (key, window, sb) triples
     int64_t treq_cap;
@@ -247,13 +260,14 @@ constexpr int AB_M_NO_LOAD = 64;     // merge: skip loading the state into LDS
 constexpr int AB_STAMPS = 128;       // merge: accumulate per-phase s_memtime cycles (diagnostic)
 constexpr int AB_M_NO_HASH = 512;    // merge: gather loads the partials but does not insert them
 constexpr int AB_M_NO_FOLDOP = 1024; // merge: insert the partials but skip the accumulator/flag atomics
-constexpr int AB_GSTAMPS = 256;      // merge: with AB_STAMPS, phases 4/5/6 time the gather's scan/load/fold
+constexpr int AB_GSTAMPS = 256;      // merge: with AB_STAMPS, stamps 2/4/7 = thread 0 gather loads/probe/fold
 constexpr int AB_M_NO_EMIT = 4096;  // merge: fire without writing result rows (diagnostic)
 constexpr int AB_FSTAMPS = 8192;    // merge: per-lane cycles of fire_one's parts into stamps[8..11]
 constexpr int N_STAMPS = 16;
 
 struct MergeArgs {
     Ctrl* ctrl;
+    Tickets* tickets;
     const uint64_t* parts;
     const uint32_t* cells;   // see IngestArgs
     const int32_t* slot_nch;
@@ -282,6 +296,7 @@ struct MergeArgs {
     int64_t out_cap;         // overflow rows
     int64_t wm;              // watermark of this advance
     int32_t force_flush;     // prepareCheckpoint: flush, no timers
+    int32_t reset_out;       // the results were consumed (fw_results_reset): emit from slab row 0
     int32_t ablate;          // development only (FW_ABLATE)
     unsigned long long* stamps;  // [N_STAMPS] phase cycles summed over workgroups (AB_STAMPS)
 };
@@ -320,6 +335,5 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s);
-hipError_t launch_reset_results(Ctrl* c, int32_t* sb_out, int32_t n_sb, hipStream_t s);
 
 }  // namespace fw

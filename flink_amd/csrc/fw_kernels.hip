@@ -242,6 +242,23 @@ __device__ __forceinline__ int32_t wave_claim(int32_t* ctr) {
     return __shfl(base, leader, 64) + rank;
 }
 
+// Last-workgroup election, called by one thread per workgroup once the workgroup's published
+// stores have completed (s_waitcnt vmcnt(0)).  True for exactly one workgroup of the grid, the
+// last to arrive; it may then read what every other workgroup published (agent-scope loads).
+// Workgroup b counts on group counter b % TK_GROUPS and the last of each group on the top
+// counter: same-address device-scope atomics serialise at the memory side, so 1024 workgroups
+// on one counter cost tens of microseconds.  Counters are left at 0 for the next launch.
+__device__ bool grid_last_wg(uint32_t (*t)[32]) {
+    const uint32_t G = gridDim.x, g = blockIdx.x % TK_GROUPS;
+    const uint32_t in_g = (G - g + TK_GROUPS - 1) / TK_GROUPS;
+    const uint32_t ng = min(G, (uint32_t)TK_GROUPS);
+    if (__hip_atomic_fetch_add(&t[g][0], 1u, __ATOMIC_RELAXED, DEV_SCOPE) != in_g - 1) return false;
+    __hip_atomic_store(&t[g][0], 0u, __ATOMIC_RELAXED, DEV_SCOPE);
+    if (__hip_atomic_fetch_add(&t[TK_GROUPS][0], 1u, __ATOMIC_RELAXED, DEV_SCOPE) != ng - 1) return false;
+    __hip_atomic_store(&t[TK_GROUPS][0], 0u, __ATOMIC_RELAXED, DEV_SCOPE);
+    return true;
+}
+
 // ======================================================================================
 // K1+K2+K3: single-pass ingest = slice/key-group assignment + LDS segmented reduce + a
 // chunk-local counting sort of the partials by superbucket.
@@ -530,56 +547,61 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                 }
             }
         }
-    // ---- control counters (reduced into the control block by k_push_stats)
+    // ---- control counters.  Each chunk publishes its stats with agent-scope stores (they bypass
+    // the XCD's L2, so any XCD reads them), then takes a ticket; the last workgroup of the launch
+    // reduces every chunk's stats into the control block and commits the push's slot
+    // (RecordsWindowBuffer's minSliceEnd and the late-drop counter).  No extra launch.
     if (lmin != INT64_MAX) __hip_atomic_fetch_min(s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
     if (ldrop) atomicAdd(s_drop, (unsigned long long)ldrop);
     if (lrows) atomicAdd(s_rows, (unsigned long long)lrows);
     __syncthreads();
+    int32_t* s_last = (int32_t*)&lds[3];
     if (tid == 0) {
-        a.chunk_stats[4 * c] = *s_min;
-        a.chunk_stats[4 * c + 1] = (int64_t)*s_drop;
-        a.chunk_stats[4 * c + 2] = (int64_t)*s_rows;
-        a.chunk_stats[4 * c + 3] = (int64_t)total;
+        __hip_atomic_store(&a.chunk_stats[4 * c], *s_min, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[4 * c + 1], (int64_t)*s_drop, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[4 * c + 2], (int64_t)*s_rows, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[4 * c + 3], (int64_t)total, __ATOMIC_RELAXED, DEV_SCOPE);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *s_last = grid_last_wg(a.tickets->c[0]);
     }
-}
-
-// one block: reduce the chunk stats into the control block and commit the push's slot
-__global__ __launch_bounds__(BLOCK) void k_push_stats(const int64_t* st, int64_t nch, Ctrl* ctrl, int32_t* slot_nch) {
-    __shared__ int64_t mn[BLOCK];
-    __shared__ int64_t dr[BLOCK];
-    __shared__ int64_t rw[BLOCK];
-    __shared__ int64_t pt[BLOCK];
-    int64_t m = INT64_MAX, d = 0, r = 0, q = 0;
-    for (int64_t i = threadIdx.x; i < nch; i += BLOCK) {
-        m = min(m, st[4 * i]);
-        d += st[4 * i + 1];
-        r += st[4 * i + 2];
-        q += st[4 * i + 3];
-    }
-    mn[threadIdx.x] = m;
-    dr[threadIdx.x] = d;
-    rw[threadIdx.x] = r;
-    pt[threadIdx.x] = q;
     __syncthreads();
-    for (int k = BLOCK / 2; k > 0; k >>= 1) {
-        if (threadIdx.x < k) {
-            mn[threadIdx.x] = min(mn[threadIdx.x], mn[threadIdx.x + k]);
-            dr[threadIdx.x] += dr[threadIdx.x + k];
-            rw[threadIdx.x] += rw[threadIdx.x + k];
-            pt[threadIdx.x] += pt[threadIdx.x + k];
-        }
-        __syncthreads();
+    if (!*s_last) return;
+    int64_t m = INT64_MAX, d = 0, r = 0, q = 0;
+    for (int64_t i = tid; i < (int64_t)gridDim.x; i += IG_BLOCK) {
+        m = min(m, __hip_atomic_load(&a.chunk_stats[4 * i], __ATOMIC_RELAXED, DEV_SCOPE));
+        d += __hip_atomic_load(&a.chunk_stats[4 * i + 1], __ATOMIC_RELAXED, DEV_SCOPE);
+        r += __hip_atomic_load(&a.chunk_stats[4 * i + 2], __ATOMIC_RELAXED, DEV_SCOPE);
+        q += __hip_atomic_load(&a.chunk_stats[4 * i + 3], __ATOMIC_RELAXED, DEV_SCOPE);
     }
-    if (threadIdx.x == 0) {
-        const int64_t slot = ctrl->pending_pushes;
-        if (slot < FW_MAX_PENDING) {
-            slot_nch[slot] = (int32_t)nch;
-            ctrl->pending_pushes = slot + 1;
-            ctrl->min_pending = min(ctrl->min_pending, mn[0]);
-            ctrl->pending_rows += (uint64_t)rw[0];
-            ctrl->partials += (uint64_t)pt[0];
+    m = wave_min_i64(m);
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) {
+        d += (int64_t)__shfl_xor((long long)d, k, 64);
+        r += (int64_t)__shfl_xor((long long)r, k, 64);
+        q += (int64_t)__shfl_xor((long long)q, k, 64);
+    }
+    int64_t* red = (int64_t*)area;  // [4][IG_BLOCK / 64]
+    constexpr int NWV = IG_BLOCK / 64;
+    if ((tid & 63) == 0) {
+        red[tid >> 6] = m;
+        red[NWV + (tid >> 6)] = d;
+        red[2 * NWV + (tid >> 6)] = r;
+        red[3 * NWV + (tid >> 6)] = q;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int v = 1; v < NWV; v++) {
+            m = min(m, red[v]);
+            d += red[NWV + v];
+            r += red[2 * NWV + v];
+            q += red[3 * NWV + v];
         }
-        ctrl->late_dropped += (uint64_t)dr[0];
+        a.slot_nch[slot] = (int32_t)gridDim.x;
+        ctrl->pending_pushes = slot + 1;
+        ctrl->min_pending = min(ctrl->min_pending, m);
+        ctrl->pending_rows += (uint64_t)r;
+        ctrl->partials += (uint64_t)q;
+        ctrl->late_dropped += (uint64_t)d;
     }
 }
 
@@ -607,7 +629,7 @@ __global__ __launch_bounds__(BLOCK) void k_compact_scan(const int32_t* sb_out, i
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const int64_t ovf = (int64_t)min(ctrl->out_count, (uint64_t)out_cap);
+        const int64_t ovf = (int64_t)min(ctrl->out_count[ctrl->ovf_sel & 1], (uint64_t)out_cap);
         off[n_sb] = carry;          // slab rows
         off[n_sb + 1] = carry + ovf;  // total rows
     }
@@ -776,7 +798,9 @@ __device__ __forceinline__ int64_t claim_out_row(const MergeArgs& a, int sb, int
     Ctrl* c = a.ctrl;
     const int32_t pos = wave_claim(s_emit);
     if (pos < a.slab_cap) return (int64_t)sb * a.slab_cap + pos;
-    const uint64_t o = atomicAdd((unsigned long long*)&c->out_count, 1ull);
+    // a launch that resets the results counts on the spare counter (kept 0), see Ctrl::out_count
+    const int sel = (__hip_atomic_load(&c->ovf_sel, __ATOMIC_RELAXED, DEV_SCOPE) ^ a.reset_out) & 1;
+    const uint64_t o = atomicAdd((unsigned long long*)&c->out_count[sel], 1ull);
     if ((int64_t)o >= a.out_cap) {
         __hip_atomic_fetch_or(&c->error, ERR_OUTPUT, __ATOMIC_RELAXED, DEV_SCOPE);
         return -1;
@@ -1091,6 +1115,37 @@ __device__ __forceinline__ int sb_of_block(int b, int n_sb) {
     return (b % 8) * (n_sb / 8) + b / 8;
 }
 
+// the last workgroup of a k_merge_fire launch applies the launch's control decisions (every
+// workgroup read the old values at its start): advanceProgress bookkeeping of the processor
+// (AbstractSliceSyncStateWindowAggProcessor.java:139-153), the buffer reset after a flush, the
+// consumed timer requests, and the overflow-counter switch of a result reset.
+__device__ void merge_finalize(const MergeArgs& a) {
+    Ctrl* c = a.ctrl;
+    const int64_t W = a.wm;
+    const int64_t cur = c->cur, pend = c->pending_pushes, ntp = c->ntp;
+    const bool adv = !a.force_flush && W > cur;
+    const bool do_flush = pend > 0 && (a.force_flush || (adv && (a.always_flush || (W >= ntp && is_fired(c->min_pending, W)))));
+    if (adv) {
+        c->cur = W;
+        if (W >= ntp) c->ntp = next_trigger_watermark(W, a.win.slice_div);
+    }
+    if (do_flush) {
+        c->pending_pushes = 0;
+        c->min_pending = INT64_MAX;
+        c->pending_rows = 0;
+    }
+    c->n_treq = 0;
+    const int sel = (c->ovf_sel ^ a.reset_out) & 1;
+    c->ovf_sel = sel;
+    __hip_atomic_store(&c->out_count[sel ^ 1], 0ull, __ATOMIC_RELAXED, DEV_SCOPE);
+}
+
+__device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
+    if (threadIdx.x != 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (grid_last_wg(a.tickets->c[1])) merge_finalize(a);
+}
+
 // rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
 constexpr int mg_rows_in_flight(int nw) { return nw <= 1 ? 4 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1; }
 
@@ -1111,7 +1166,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     const int sb = sb_of_block(blockIdx.x, a.n_sb);
     Ctrl* c = a.ctrl;
     const int64_t W = a.wm;
-    // control decisions; k_finalize applies the same decisions to the control block afterwards
+    // control decisions; the launch's last workgroup applies them to the control block (merge_finalize)
     const int64_t cur = __hip_atomic_load(&c->cur, __ATOMIC_RELAXED, DEV_SCOPE);
     const int64_t pend = __hip_atomic_load(&c->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
     const int64_t ntreq = min(__hip_atomic_load(&c->n_treq, __ATOMIC_RELAXED, DEV_SCOPE), (int64_t)0x7fffffff);
@@ -1129,10 +1184,14 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     if (tid == 0) {
         s_work = (ntreq > 0) || do_flush || (do_fire && is_fired(a.sb_min_timer[sb], W));
         s_fired = 0;
-        s_emit = a.sb_out[sb];
+        s_emit = a.reset_out ? 0 : a.sb_out[sb];
+        if (!s_work && a.reset_out) a.sb_out[sb] = 0;
     }
     __syncthreads();
-    if (!s_work) return;
+    if (!s_work) {
+        merge_ticket(a);
+        return;
+    }
     const bool gather = do_flush && !(a.ablate & AB_M_NO_GATHER);
     // this thread's first cell word, loaded while the state loads (the gather below walks the
     // cells of every pending push, one cell per thread per pass, in flat tile order f:
@@ -1181,6 +1240,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket.
     // One cell (the rows one ingest chunk wrote for this superbucket) per thread per pass; GU of
     // its rows are loaded together, then looked up in the LDS table and folded (or inserted).
+    // diagnostic (AB_GSTAMPS): thread 0's cycles in row loads / first probes / insert + fold
+    const bool gst = (a.ablate & AB_GSTAMPS) && stm.on && tid == 0;
     if (gather) {
         for (int64_t pi = 0; pi < pend; pi++) {
             const int nch = a.slot_nch[pi];
@@ -1193,11 +1254,25 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                 const uint64_t* rp = seg + ((size_t)cell_chunk(f) * CH + (v & 0xFFFFu)) * PW;
                 for (uint32_t r0 = 0; r0 < cnt; r0 += GU) {
                     uint64_t row[GU][PW];
+                    uint64_t g0 = gst ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
                     for (int u = 0; u < GU; u++) {
                         const uint64_t* p = rp + (size_t)min(r0 + u, cnt - 1) * PW;
 #pragma unroll
                         for (int w = 0; w < PW; w++) row[u][w] = p[w];
+                    }
+                    if (gst) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                        stm.acc[2] += g1 - g0;
+                        g0 = g1;
+                    }
+                    if (a.ablate & AB_M_NO_HASH) {  // diagnostic: loads only
+                        uint64_t x = 0;
+#pragma unroll
+                        for (int u = 0; u < GU; u++) x ^= row[u][0] ^ row[u][1] ^ row[u][PW - 1];
+                        asm volatile("" ::"v"(x));  // keeps the loads
+                        continue;
                     }
                     int ge[GU];
                     {
@@ -1208,6 +1283,12 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                             gs[u] = (int64_t)row[u][1];
                         }
                         probe_batch<NW, E, GU>(S, gk, gs, ge);
+                    }
+                    if (gst) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                        stm.acc[4] += g1 - g0;
+                        g0 = g1;
                     }
                     static_for<GU>([&](auto UU) {
                         constexpr int u = decltype(UU)::value;
@@ -1225,6 +1306,10 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                             if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
                         atomicOr(&S.flag[e], fl);
                     });
+                    if (gst) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        stm.acc[7] += __builtin_amdgcn_s_memtime() - g0;
+                    }
                 }
             }
         }
@@ -1317,25 +1402,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     __syncthreads();
     stm.mark(3);
     stm.flush(a.stamps);
-}
-
-// applies the control decisions of the preceding k_merge_fire (one thread; the kernel boundary
-// orders it after every merge workgroup has read the old values)
-__global__ void k_finalize(Ctrl* c, int64_t W, int32_t force_flush, int32_t always_flush, UDiv slice_div) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const int64_t cur = c->cur, pend = c->pending_pushes, ntp = c->ntp;
-    const bool adv = !force_flush && W > cur;
-    const bool do_flush = pend > 0 && (force_flush || (adv && (always_flush || (W >= ntp && is_fired(c->min_pending, W)))));
-    if (adv) {
-        c->cur = W;
-        if (W >= ntp) c->ntp = next_trigger_watermark(W, slice_div);
-    }
-    if (do_flush) {
-        c->pending_pushes = 0;
-        c->min_pending = INT64_MAX;
-        c->pending_rows = 0;
-    }
-    c->n_treq = 0;
+    merge_ticket(a);
 }
 
 __global__ void k_init_ctrl(Ctrl* c) {
@@ -1346,7 +1413,9 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->pending_pushes = 0;
         c->push_slot = 0;
         c->n_treq = 0;
-        c->out_count = 0;
+        c->out_count[0] = 0;
+        c->out_count[1] = 0;
+        c->ovf_sel = 0;
         c->late_dropped = 0;
         c->fired = 0;
         c->pending_rows = 0;
@@ -1361,19 +1430,6 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t) {
     hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(BLOCK), 0, s, a.sb_out, a.n_sb, a.off, a.ctrl, a.res_cap);
     hipLaunchKernelGGL(k_compact_copy, dim3(a.n_sb + 1), dim3(BLOCK), 0, s, a);
     kt_mark(t, FW_KT_OTHER, true, s);
-    return hipGetLastError();
-}
-
-// results consumed: empty every superbucket's output slab and the overflow region (one launch
-// instead of two memsets)
-__global__ __launch_bounds__(BLOCK) void k_reset_results(Ctrl* c, int32_t* sb_out, int32_t n_sb) {
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i < n_sb) sb_out[i] = 0;
-    if (i == 0) c->out_count = 0;
-}
-
-hipError_t launch_reset_results(Ctrl* c, int32_t* sb_out, int32_t n_sb, hipStream_t s) {
-    hipLaunchKernelGGL(k_reset_results, dim3((n_sb + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, c, sb_out, n_sb);
     return hipGetLastError();
 }
 
@@ -1402,9 +1458,6 @@ static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
     kt_mark(t, FW_KT_REDUCE, false, s);
     hipLaunchKernelGGL((k_ingest<NV, NW, RPT, X>), dim3((unsigned)nch), dim3(IG_BLOCK), a.lds_bytes, s, a);
     kt_mark(t, FW_KT_REDUCE, true, s);
-    kt_mark(t, FW_KT_OTHER, false, s);
-    hipLaunchKernelGGL(k_push_stats, dim3(1), dim3(BLOCK), 0, s, a.chunk_stats, nch, a.ctrl, a.slot_nch);
-    kt_mark(t, FW_KT_OTHER, true, s);
     return hipGetLastError();
 }
 
@@ -1462,12 +1515,7 @@ hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s, KTimer* t) {
     kt_mark(t, FW_KT_MERGE, false, s);
     hipError_t e = merge_any(a, s);
     kt_mark(t, FW_KT_MERGE, true, s);
-    if (e != hipSuccess) return e;
-    kt_mark(t, FW_KT_OTHER, false, s);
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, s, a.ctrl, a.wm, a.force_flush, a.always_flush,
-                       a.win.slice_div);
-    kt_mark(t, FW_KT_OTHER, true, s);
-    return hipGetLastError();
+    return e;
 }
 
 // ======================================================================================

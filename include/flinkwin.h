@@ -239,7 +239,9 @@ typedef struct {
     int64_t merge_phase_cycles[FW_KT_N];  /* diagnostic builds only (FW_ABLATE stamps): shader
                                              cycles per merge phase, summed over workgroups     */
 } fw_kernel_times;
-/* enable != 0 starts timing (and resets the accumulators); 0 stops it. */
+/* enable = 1 times the ingest and merge/fire launches, 2 also the small bookkeeping launches
+   (FW_KT_OTHER; each timed launch costs the stream two event records); 0 stops timing.  Enabling
+   resets the accumulators. */
 int fw_set_profiling(fw_handle* h, int enable);
 /* synchronises the handle stream, then returns the accumulated times */
 int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out);

@@ -86,7 +86,7 @@ def merge_main(wl_name, variants, steps=12):
         try:
             for b in range(steps):
                 if b == 3:
-                    h.sync()
+                    torch.cuda.synchronize()  # not h.sync(): ablated runs may set error bits
                     h.set_profiling(True)
                 h.push_device(gk[b], gt[b], [gv[b]] if wl["value_cols"] else [])
                 h.reset_results()
@@ -95,11 +95,11 @@ def merge_main(wl_name, variants, steps=12):
             print(json.dumps({"workload": wl_name, "ablate": ab, "error": str(e)}), flush=True)
             h.close()
             continue
-        kt = h.kernel_times()
+        kt = h.kernel_times()  # reads times + stamps, no error check
         ms, n = kt["merge"]
         print(json.dumps({"workload": wl_name, "ablate": ab, "merge_ms_per_step": round(ms / (steps - 3), 4),
                           "reduce_us": round(kt["reduce"][0] / kt["reduce"][1] * 1e3, 2),
-                          "phase_Mcycles": [round(x / 1e6, 1) for x in kt["merge_phase_cycles"][:7]],
+                          "phase_Mcycles": [round(x / 1e6, 1) for x in kt["merge_phase_cycles"][:8]],
                           "rounds": kt["merge_phase_cycles"][7], "fired": h.stats()["num_fired_windows"],
                           "errors": h.stats()["error_flags"]}), flush=True)
         h.close()

@@ -56,7 +56,9 @@ def lib():
         "fw_snapshot_key_group": (i32, [vp, i32, vp, i64, P(i64)]),
         "fw_restore_key_group": (i32, [vp, vp, i64]),
         "fw_assign_key_groups": (i32, [vp, vp, i64, i32, i32, i32, vp, vp, vp]),
-        "fw_partition_by_dest": (i32, [vp, vp, vp, i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp]),
+        "fw_partition_by_dest": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp]),
+        "fw_key_row_hash": (i32, [P(abi.fw_key_field), i32, i64, vp, vp]),
+        "fw_host_key_row_hash": (i32, [P(abi.fw_key_field), i32, i64, vp]),
         "fw_partition_workspace_bytes": (i64, [i64, i32]),
         "fw_generate": (i32, [P(abi.fw_gen_params), i64, i64, vp, vp, vp, vp]),
         "fw_host_key_group": (i32, [i32, i64, i32, i32]),
@@ -79,6 +81,7 @@ EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_ge
             "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_advance",
             "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
+            "fw_key_row_hash", "fw_host_key_row_hash",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
             "fw_host_next_trigger_watermark"]

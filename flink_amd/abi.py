@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 2
+FW_ABI_VERSION = 3
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -45,6 +45,15 @@ KEYHASH_BINROW_BIGINT = 2
 KEYHASH_BINROW_INT = 3
 KEYHASH_PRECOMPUTED = 4
 
+# fw_key_field_kind (key-row fields for fw_key_row_hash)
+KF_STRING, KF_FIXED1, KF_FIXED2, KF_FIXED4, KF_FIXED8 = 0, 1, 2, 4, 8
+FW_MAX_KEY_FIELDS = 8
+# SQL key field type -> fw_key_field_kind (BinaryRowWriter slot width; strings go to the var part)
+KEY_FIELD_KINDS = {"BOOLEAN": KF_FIXED1, "TINYINT": KF_FIXED1, "SMALLINT": KF_FIXED2, "INT": KF_FIXED4,
+                   "DATE": KF_FIXED4, "FLOAT": KF_FIXED4, "BIGINT": KF_FIXED8, "DOUBLE": KF_FIXED8,
+                   "TIMESTAMP": KF_FIXED8, "VARCHAR": KF_STRING, "CHAR": KF_STRING, "STRING": KF_STRING,
+                   "VARBINARY": KF_STRING, "BINARY": KF_STRING, "BYTES": KF_STRING}
+
 AGG_NAMES = {"COUNT_STAR": AGG_COUNT_STAR, "COUNT": AGG_COUNT, "SUM": AGG_SUM,
              "MIN": AGG_MIN, "MAX": AGG_MAX, "AVG": AGG_AVG}
 TYPE_NAMES = {"BIGINT": T_I64, "DOUBLE": T_F64, "INT": T_I32}
@@ -81,6 +90,11 @@ class fw_config(C.Structure):
         ("max_batch_rows", C.c_int64),
         ("output_capacity", C.c_int64),
     ]
+
+
+class fw_key_field(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("fixed", C.c_void_p),
+                ("offsets", C.c_void_p), ("bytes", C.c_void_p), ("nulls", C.c_void_p)]
 
 
 class fw_host_cols(C.Structure):

@@ -71,6 +71,93 @@ FW_HD int32_t java_key_hash(int32_t kind, int64_t key, int32_t pre) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// BinaryRowData.hashCode of a general key row (VARCHAR / composite keys), streamed word by
+// word from the key's columns without materialising the row.  The row image is the one
+// BinaryRowWriter builds (TR/data/writer/BinaryRowWriter.java:39-122, AbstractBinaryWriter.java
+// :83-106,242-345; layout BinaryRowData.java:69-124, BinaryFormat.java:30-54):
+//   [null bits: ((n + 71) / 64) * 8 B; byte 0 = RowKind (INSERT = 0), bit 8 + i = field i NULL]
+//   [n fixed 8-byte slots: NULL -> 0; BOOLEAN/TINYINT/SMALLINT/INT/FLOAT/BIGINT/DOUBLE... -> the
+//    value's low `width` bytes (the writer's reset() leaves the rest 0); string of len <= 7 ->
+//    bytes little endian | (0x80 | len) << 56; longer -> (offset << 32) | len]
+//   [variable part: each longer string's bytes in field order, zero-padded to 8 B]
+// and the hash is MurmurHashUtils.hashBytesByWords (seed 42) over all of it (BinaryRowData
+// .java:459 -> BinarySegmentUtils.hashByWords).
+// ---------------------------------------------------------------------------------------
+constexpr int KR_MAX_FIELDS = 8;
+struct KeyRowDesc {
+    int32_t n;                            // fields
+    int32_t width[KR_MAX_FIELDS];         // 1 / 2 / 4 / 8 fixed slot bytes; 0 = string
+    const int64_t* fixed[KR_MAX_FIELDS];  // fixed fields: one int64 per row
+    const int32_t* offs[KR_MAX_FIELDS];   // strings: n + 1 byte offsets into bytes
+    const uint8_t* bytes[KR_MAX_FIELDS];  // strings: 4-byte aligned base
+    const uint8_t* nulls[KR_MAX_FIELDS];  // optional NULL flags (non-zero = NULL)
+};
+
+// up to 4 bytes of a string at byte p (avail >= 1 of them valid), little endian, zero-padded.
+// Device: aligned dword loads (the base is 4-byte aligned; a dword is read only if it holds a
+// valid byte); host: byte loads.
+FW_HD uint32_t kr_load_word(const uint8_t* base, int64_t p, int64_t avail) {
+    uint32_t w;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t* a = (const uint32_t*)(base + (p & ~(int64_t)3));
+    const uint32_t sh = (uint32_t)(p & 3) * 8u;
+    uint64_t v = a[0] >> sh;
+    if (sh && avail > 4 - (int64_t)(p & 3)) v |= (uint64_t)a[1] << (32u - sh);
+    w = (uint32_t)v;
+#else
+    w = 0;
+    for (int b = 0; b < 4 && b < avail; b++) w |= (uint32_t)base[p + b] << (8 * b);
+#endif
+    if (avail < 4) w &= (1u << (8 * avail)) - 1u;
+    return w;
+}
+
+FW_HD int32_t key_row_hash(const KeyRowDesc& d, int64_t i) {
+    const int nb = ((d.n + 71) / 64) * 8;  // BinaryRowData.calculateBitSetWidthInBytes (n <= 56: 8)
+    uint64_t hdr = 0;
+    for (int f = 0; f < d.n; f++)
+        if (d.nulls[f] && d.nulls[f][i]) hdr |= 1ull << (8 + f);
+    uint32_t h = 42u;
+    h = murmur_h1(h, murmur_k1((uint32_t)hdr));
+    h = murmur_h1(h, murmur_k1((uint32_t)(hdr >> 32)));
+    uint32_t cursor = (uint32_t)(nb + 8 * d.n);  // the writer's cursor: start of the variable part
+    for (int f = 0; f < d.n; f++) {
+        uint64_t slot = 0;
+        if (!((hdr >> (8 + f)) & 1u)) {
+            const int w = d.width[f];
+            if (w > 0) {
+                const uint64_t v = (uint64_t)d.fixed[f][i];
+                slot = w == 8 ? v : v & ((1ull << (8 * w)) - 1ull);
+            } else {
+                const int64_t o = d.offs[f][i];
+                const uint32_t len = (uint32_t)(d.offs[f][i + 1] - o);
+                if (len <= 7) {  // writeBytesToFixLenPart
+                    slot = (uint64_t)(0x80u | len) << 56;
+                    if (len) slot |= kr_load_word(d.bytes[f], o, len);
+                    if (len > 4) slot |= (uint64_t)kr_load_word(d.bytes[f], o + 4, len - 4) << 32;
+                } else {  // writeBytesToVarLenPart: setOffsetAndSize(pos, cursor, len)
+                    slot = ((uint64_t)cursor << 32) | len;
+                    cursor += (len + 7u) & ~7u;
+                }
+            }
+        }
+        h = murmur_h1(h, murmur_k1((uint32_t)slot));
+        h = murmur_h1(h, murmur_k1((uint32_t)(slot >> 32)));
+    }
+    for (int f = 0; f < d.n; f++) {
+        if (d.width[f] > 0 || ((hdr >> (8 + f)) & 1u)) continue;
+        const int64_t o = d.offs[f][i];
+        const int64_t len = d.offs[f][i + 1] - o;
+        if (len <= 7) continue;
+        const int64_t padded = (len + 7) & ~(int64_t)7;
+        for (int64_t j = 0; j < padded; j += 4)
+            h = murmur_h1(h, murmur_k1(j < len ? kr_load_word(d.bytes[f], o + j, len - j) : 0u));
+    }
+    // the null-bit region beyond the first word (n > 56) is all zero bits here (n <= 8)
+    return (int32_t)fmix32(h ^ cursor);
+}
+
 // KeyGroupRangeAssignment.computeKeyGroupForKeyHash
 FW_HD int32_t key_group_for_hash(int32_t h, int32_t max_p) { return flink_murmur_hash(h) % max_p; }
 // KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup

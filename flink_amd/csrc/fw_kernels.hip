@@ -1201,8 +1201,13 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
         return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
     };
+    // the gather splits a push's cells into groups of gather_group(ncell) <= 64 consecutive
+    // cells, one group per wave per pass (16 groups when a push has <= 1024 cells)
+    const int lane = tid & 63, wv = tid >> 6;
+    auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
     uint32_t v_first = 0;
-    if (gather && tid < cell_pad(a.slot_nch[0])) v_first = cell_at(0, tid);
+    if (gather && lane < gather_group((int)cell_pad(a.slot_nch[0])))
+        v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
     // ---- load this superbucket's entries into LDS
     for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
     if (tid == 0) {
@@ -1238,26 +1243,45 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
     }
     // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket.
-    // One cell (the rows one ingest chunk wrote for this superbucket) per thread per pass; GU of
-    // its rows are loaded together, then looked up in the LDS table and folded (or inserted).
-    // diagnostic (AB_GSTAMPS): thread 0's cycles in row loads / first probes / insert + fold
+    // A wave takes a group of cells (the rows ingest chunks wrote for this superbucket), scans
+    // their row counts and deals the rows of the whole group over its 64 lanes, GU rows per lane
+    // per pass: every lane is busy whatever the cells' sizes, and neighbouring lanes load
+    // neighbouring rows.  Rows are looked up in the LDS table (first probes batched), hits
+    // folded; the misses of a lane are then inserted one at a time.
+    // diagnostic (AB_GSTAMPS): thread 0's cycles in row loads / first probes / fold + insert
     const bool gst = (a.ablate & AB_GSTAMPS) && stm.on && tid == 0;
     if (gather) {
         for (int64_t pi = 0; pi < pend; pi++) {
-            const int nch = a.slot_nch[pi];
-            const int ncell = (int)cell_pad(nch);
+            const int ncell = (int)cell_pad(a.slot_nch[pi]);
+            const int G = gather_group(ncell);
+            const int ngroups = ncell / G;
             const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
-            for (int f = tid; f < ncell; f += MG_BLOCK) {
-                const uint32_t v = (pi == 0 && f == tid) ? v_first : cell_at(pi, f);
+            for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
+                const int f = g * G + lane;
+                const uint32_t v = lane >= G ? 0u : (pi == 0 && g == wv) ? v_first : cell_at(pi, f);
                 const uint32_t cnt = v >> 16;
-                if (!cnt) continue;
-                const uint64_t* rp = seg + ((size_t)cell_chunk(f) * CH + (v & 0xFFFFu)) * PW;
-                for (uint32_t r0 = 0; r0 < cnt; r0 += GU) {
+                uint32_t inc = cnt;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+                    if (lane >= d) inc += t;
+                }
+                const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+                const uint32_t excl = inc - cnt;
+                // segment row of this cell's first row, less the rows of the group before it
+                const uint32_t adj = (uint32_t)(cell_chunk(f) * CH + (v & 0xFFFFu)) - excl;
+                for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
                     uint64_t row[GU][PW];
                     uint64_t g0 = gst ? __builtin_amdgcn_s_memtime() : 0;
 #pragma unroll
                     for (int u = 0; u < GU; u++) {
-                        const uint64_t* p = rp + (size_t)min(r0 + u, cnt - 1) * PW;
+                        // the group's row x lives in the last cell whose first row is <= x
+                        const uint32_t x = min(r0 + (uint32_t)(u * 64 + lane), tot - 1);
+                        int lo = 0;
+#pragma unroll
+                        for (int step = 32; step > 0; step >>= 1)
+                            if ((uint32_t)__shfl((int)excl, lo + step, 64) <= x) lo += step;
+                        const uint64_t* p = seg + (size_t)((uint32_t)__shfl((int)adj, lo, 64) + x) * PW;
 #pragma unroll
                         for (int w = 0; w < PW; w++) row[u][w] = p[w];
                     }
@@ -1290,22 +1314,47 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         stm.acc[4] += g1 - g0;
                         g0 = g1;
                     }
+                    // register the window timer unless already fired (AggCombiner.java:103-110);
+                    // the LOCAL phase keeps no timers (LocalAggCombiner.java:69-97)
+                    auto flags_of = [&](int64_t sl) -> uint32_t {
+                        return (a.local || is_fired(sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
+                    };
+                    uint32_t miss = 0;
                     static_for<GU>([&](auto UU) {
                         constexpr int u = decltype(UU)::value;
-                        if (r0 + u >= cnt) return;
-                        const int64_t k = (int64_t)row[u][0], s = (int64_t)row[u][1];
-                        // register the window timer unless already fired (AggCombiner.java:103-110);
-                        // the LOCAL phase keeps no timers (LocalAggCombiner.java:69-97)
-                        const uint32_t fl = (a.local || is_fired(s, w_old)) ? F_ACC : (F_ACC | F_TIMER);
-                        int e = ge[u];  // -1 / -2: not found by the batched first probe
-                        bool ins = false;
-                        if (e < 0) e = find_or_insert(S, k, s, a.wd, &row[u][2], fl, &ins);
-                        if (e < 0 || ins || (a.ablate & AB_M_NO_FOLDOP)) return;
+                        if (r0 + (uint32_t)(u * 64 + lane) >= tot) return;
+                        const int e = ge[u];  // -1 / -2: not found by the batched first probe
+                        if (e < 0) {
+                            miss |= 1u << u;
+                            return;
+                        }
+                        if (a.ablate & AB_M_NO_FOLDOP) return;
 #pragma unroll
                         for (int w = 0; w < NW; w++)
                             if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
-                        atomicOr(&S.flag[e], fl);
+                        atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
                     });
+                    while (miss) {  // the wave loops max(popcount) times, not GU times
+                        const int um = __ffs(miss) - 1;
+                        miss &= miss - 1;
+                        uint64_t r[PW];
+                        static_for<GU>([&](auto UU) {
+                            constexpr int u = decltype(UU)::value;
+                            if (u == um) {
+#pragma unroll
+                                for (int w = 0; w < PW; w++) r[w] = row[u][w];
+                            }
+                        });
+                        const int64_t k = (int64_t)r[0], sl = (int64_t)r[1];
+                        const uint32_t fl = flags_of(sl);
+                        bool ins = false;
+                        const int e = find_or_insert(S, k, sl, a.wd, &r[2], fl, &ins);
+                        if (e < 0 || ins || (a.ablate & AB_M_NO_FOLDOP)) continue;
+#pragma unroll
+                        for (int w = 0; w < NW; w++)
+                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], r[2 + w]);
+                        atomicOr(&S.flag[e], fl);
+                    }
                     if (gst) {
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         stm.acc[7] += __builtin_amdgcn_s_memtime() - g0;
@@ -1533,8 +1582,8 @@ __global__ void k_key_groups(const int64_t* key, const int32_t* kh, int64_t n, i
 constexpr int PART_TILE = 4096;
 constexpr int PART_MAXP = 64;
 
-__global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, int64_t n, int32_t kind, int32_t max_p,
-                                                     int32_t p, uint32_t* counts) {
+__global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, const int32_t* kh, int64_t n, int32_t kind,
+                                                     int32_t max_p, int32_t p, uint32_t* counts) {
     __shared__ uint32_t h[PART_MAXP];
     const int tid = threadIdx.x;
     if (tid < PART_MAXP) h[tid] = 0;
@@ -1543,7 +1592,7 @@ __global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, int64_t
     for (int j = tid; j < PART_TILE; j += BLOCK) {
         const int64_t i = b + j;
         if (i >= n) break;
-        const int32_t g = key_group_for_hash(java_key_hash(kind, key[i], 0), max_p);
+        const int32_t g = key_group_for_hash(java_key_hash(kind, key[i], kh ? kh[i] : 0), max_p);
         atomicAdd(&h[operator_for_key_group(max_p, p, g)], 1u);
     }
     __syncthreads();
@@ -1573,7 +1622,8 @@ __global__ __launch_bounds__(BLOCK) void k_part_scan(uint32_t* counts, int64_t n
     }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, const int64_t* ts, const uint64_t* const* vals,
+__global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, const int32_t* kh, const int64_t* ts,
+                                                        const uint64_t* const* vals,
                                                         int32_t ncols, int64_t n, int32_t kind, int32_t max_p,
                                                         int32_t p, const uint32_t* offsets, int64_t* okey, int64_t* ots,
                                                         uint64_t* const* ovals) {
@@ -1594,7 +1644,7 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
         int64_t k = 0;
         if (i < n) {
             k = key[i];
-            d = operator_for_key_group(max_p, p, key_group_for_hash(java_key_hash(kind, k, 0), max_p));
+            d = operator_for_key_group(max_p, p, key_group_for_hash(java_key_hash(kind, k, kh ? kh[i] : 0), max_p));
         }
         uint32_t rank = 0;
         for (int dd = 0; dd < p; dd++) {
@@ -1621,6 +1671,11 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
         }
         __syncthreads();  // h updated before the next pass reads it; wc free to overwrite
     }
+}
+
+__global__ void k_key_row_hash(KeyRowDesc d, int64_t n, int32_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = key_row_hash(d, i);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) { return mix64(x + 0x9E3779B97F4A7C15ull); }
@@ -1669,18 +1724,61 @@ extern "C" int fw_assign_key_groups(const int64_t* d_key, const int32_t* d_key_h
     return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
 }
 
+// fw_key_field[] -> KeyRowDesc (FW_E_INVALID on a bad description)
+static int key_row_desc(const fw_key_field* fields, int32_t n_fields, KeyRowDesc* d) {
+    if (!fields || n_fields <= 0 || n_fields > FW_MAX_KEY_FIELDS || n_fields > KR_MAX_FIELDS) return FW_E_INVALID;
+    *d = KeyRowDesc{};
+    d->n = n_fields;
+    for (int f = 0; f < n_fields; f++) {
+        const fw_key_field& k = fields[f];
+        if (k.kind != FW_KF_STRING && k.kind != FW_KF_FIXED1 && k.kind != FW_KF_FIXED2 && k.kind != FW_KF_FIXED4 &&
+            k.kind != FW_KF_FIXED8)
+            return FW_E_INVALID;
+        d->width[f] = k.kind;
+        if (k.kind == FW_KF_STRING) {
+            if (!k.offsets || !k.bytes || ((uintptr_t)k.bytes & 3)) return FW_E_INVALID;
+        } else if (!k.fixed) {
+            return FW_E_INVALID;
+        }
+        d->fixed[f] = k.fixed;
+        d->offs[f] = k.offsets;
+        d->bytes[f] = k.bytes;
+        d->nulls[f] = k.nulls;
+    }
+    return FW_OK;
+}
+
+extern "C" int fw_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n, int32_t* d_hash, void* stream) {
+    KeyRowDesc d;
+    if (const int rc = key_row_desc(fields, n_fields, &d)) return rc;
+    if (n <= 0) return FW_OK;
+    if (!d_hash) return FW_E_INVALID;
+    hipLaunchKernelGGL(k_key_row_hash, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, d, n,
+                       d_hash);
+    return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
+}
+
+extern "C" int fw_host_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n, int32_t* hash) {
+    KeyRowDesc d;
+    if (const int rc = key_row_desc(fields, n_fields, &d)) return rc;
+    if (n > 0 && !hash) return FW_E_INVALID;
+    for (int64_t i = 0; i < n; i++) hash[i] = key_row_hash(d, i);
+    return FW_OK;
+}
+
 extern "C" int64_t fw_partition_workspace_bytes(int64_t n, int32_t parallelism) {
     const int64_t nblk = (n + PART_TILE - 1) / PART_TILE;
     return (nblk * parallelism * 4 + 2 * FW_MAX_COLS * 8 + 255) & ~255ll;
 }
 
-extern "C" int fw_partition_by_dest(const int64_t* d_key, const int64_t* d_ts, const void* const* d_values,
-                                    int32_t n_cols, int64_t n, int32_t key_hash_kind, int32_t max_parallelism,
-                                    int32_t parallelism, int64_t* d_out_key, int64_t* d_out_ts,
-                                    void* const* d_out_values, int64_t* d_counts, void* d_workspace,
-                                    int64_t workspace_bytes, void* stream) {
+extern "C" int fw_partition_by_dest(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                                    const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
+                                    int32_t max_parallelism, int32_t parallelism, int64_t* d_out_key,
+                                    int64_t* d_out_ts, void* const* d_out_values, int64_t* d_counts,
+                                    void* d_workspace, int64_t workspace_bytes, void* stream) {
     if (parallelism <= 0 || parallelism > PART_MAXP || n_cols < 0 || n_cols > FW_MAX_COLS) return FW_E_INVALID;
-    if (key_hash_kind == FW_KEYHASH_PRECOMPUTED) return FW_E_INVALID;
+    if (key_hash_kind == FW_KEYHASH_PRECOMPUTED && n > 0 && !d_key_hash) return FW_E_INVALID;
+    if (key_hash_kind != FW_KEYHASH_PRECOMPUTED) d_key_hash = nullptr;
     if (workspace_bytes < fw_partition_workspace_bytes(n, parallelism)) return FW_E_INVALID;
     hipStream_t s = (hipStream_t)stream;
     if (n <= 0) {
@@ -1698,10 +1796,10 @@ extern "C" int fw_partition_by_dest(const int64_t* d_key, const int64_t* d_ts, c
         hv[FW_MAX_COLS + c] = d_out_values[c];
     }
     if (hipMemcpyAsync(dv, hv, sizeof(hv), hipMemcpyHostToDevice, s) != hipSuccess) return FW_E_DEVICE;
-    hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, n, key_hash_kind, max_parallelism,
-                       parallelism, counts);
+    hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, n, key_hash_kind,
+                       max_parallelism, parallelism, counts);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(BLOCK), 0, s, counts, nblk, parallelism, d_counts);
-    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_ts,
+    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, d_ts,
                        (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
                        d_out_key, d_out_ts, (uint64_t* const*)dov);
     return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;

@@ -34,22 +34,26 @@ class KeyByExchange:
         self._ws = None
 
     # ---- routing ------------------------------------------------------------------------
-    def partition(self, key, ts, values):
+    def partition(self, key, ts, values, key_hash=None):
         """Rows grouped by destination subtask (ascending).  Returns (key, ts, values, counts)
-        with counts[d] = rows for subtask d; stable within a destination."""
+        with counts[d] = rows for subtask d; stable within a destination.  ``key_hash`` (int32
+        per row) routes FW_KEYHASH_PRECOMPUTED keys, e.g. VARCHAR keys hashed by fw_key_row_hash."""
         p = self.world
+        if self.kind == abi.KEYHASH_PRECOMPUTED and key_hash is None:
+            raise ValueError("precomputed-hash keys need their key_hash column")
         if key.is_cuda:
-            return self._partition_device(key, ts, values)
+            return self._partition_device(key, ts, values, key_hash)
         n = key.numel()
         dest = np.empty(n, dtype=np.int32)
         kn = np.ascontiguousarray(key.numpy())
-        check(lib().fw_host_assign_key_groups(kn.ctypes.data, None, n, self.kind, self.max_p, p,
-                                              None, dest.ctypes.data))
+        kh = None if key_hash is None else np.ascontiguousarray(key_hash.numpy().astype(np.int32, copy=False))
+        check(lib().fw_host_assign_key_groups(kn.ctypes.data, None if kh is None else kh.ctypes.data, n, self.kind,
+                                              self.max_p, p, None, dest.ctypes.data))
         order = torch.from_numpy(np.argsort(dest, kind="stable"))
         counts = torch.from_numpy(np.bincount(dest, minlength=p).astype(np.int64))
         return key[order], ts[order], [v[order] for v in values], counts
 
-    def _partition_device(self, key, ts, values):
+    def _partition_device(self, key, ts, values, key_hash=None):
         p, n, dev = self.world, key.numel(), key.device
         L = lib()
         ws = L.fw_partition_workspace_bytes(n, p)
@@ -60,19 +64,30 @@ class KeyByExchange:
         counts = torch.empty(p, dtype=torch.int64, device=dev)
         vin = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in values])
         vout = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in pv])
-        check(L.fw_partition_by_dest(key.data_ptr(), ts.data_ptr(), vin, len(values), n, self.kind,
+        kh = None if key_hash is None else key_hash.to(torch.int32).contiguous()
+        check(L.fw_partition_by_dest(key.data_ptr(), None if kh is None else kh.data_ptr(), ts.data_ptr(), vin,
+                                     len(values), n, self.kind,
                                      self.max_p, p, pk.data_ptr(), pt.data_ptr(), vout, counts.data_ptr(),
                                      self._ws.data_ptr(), self._ws.numel(),
                                      torch.cuda.current_stream(dev).cuda_stream))
         return pk, pt, pv, counts
 
     # ---- exchange -----------------------------------------------------------------------
-    def exchange(self, key, ts, values):
+    def exchange(self, key, ts, values, key_hash=None):
         """Send every row to the subtask owning its key group; returns this subtask's rows
-        (grouped by source rank, each source's rows in their partitioned order)."""
+        (grouped by source rank, each source's rows in their partitioned order).  With
+        ``key_hash`` (precomputed-hash keys) the hash travels with its row and the result is
+        (key, ts, values, key_hash)."""
+        if key_hash is None:
+            return self._exchange(key, ts, list(values), None)
+        # the hash moves as one more 8-byte column
+        k, t, v = self._exchange(key, ts, list(values) + [key_hash.to(torch.int64)], key_hash)
+        return k, t, v[:-1], v[-1].to(torch.int32)
+
+    def _exchange(self, key, ts, values, routing_hash):
         if self.world == 1:
             return key, ts, list(values)
-        pk, pt, pv, counts = self.partition(key, ts, values)
+        pk, pt, pv, counts = self.partition(key, ts, values, routing_hash)
         # gloo moves host tensors only: device batches are staged through host memory (used to
         # rehearse the N > 1 path on one GPU; RCCL moves device memory directly over xGMI)
         stage = key.is_cuda and dist.get_backend(self.group) != "nccl"

@@ -13,6 +13,7 @@ import numpy as np
 
 from .. import abi
 from ..runtime.handle import WindowAggHandle
+from .key_rows import KeyDictionary, KeyRowColumns
 from .slice_assigners import SliceAssigner
 
 GPU_AGGS = {"COUNT_STAR", "COUNT", "SUM", "MIN", "MAX", "AVG"}
@@ -34,7 +35,13 @@ def is_gpu_eligible(assigner, aggs, value_types, *, is_event_time=True, shift_ti
         return False, "TIMESTAMP_LTZ shift zones run on the reference operator"
     if has_distinct or needs_retraction:
         return False, "DISTINCT / retraction aggregates run on the reference operator"
-    if key_type not in KEY_HASH:
+    if isinstance(key_type, (tuple, list)):  # key row of several / non-integer fields (fw_key_row_hash)
+        if not 1 <= len(key_type) <= abi.FW_MAX_KEY_FIELDS:
+            return False, f"key rows of {len(key_type)} fields run on the reference operator"
+        bad = [t for t in key_type if t not in abi.KEY_FIELD_KINDS]
+        if bad:
+            return False, f"key field type {bad[0]} runs on the reference operator"
+    elif key_type not in KEY_HASH:
         return False, f"key type {key_type} must be host-hashed"
     for kind, col, typ in aggs:
         if kind not in GPU_AGGS:
@@ -56,13 +63,17 @@ class WindowAggOperator:
             raise ValueError("Hopping window requires a COUNT(*) in the aggregate functions.")
         self.assigner = assigner
         self.aggs = list(aggs)
+        # key rows (VARCHAR / composite keys): dictionary ids as the state key, device-hashed rows
+        self.key_types = list(key_type) if isinstance(key_type, (tuple, list)) else None
+        self.keys = KeyDictionary() if self.key_types else None
         self.cfg = abi.make_config(
             api=abi.API_SQL, window_kind=assigner.kind, size_ms=assigner.size,
             slide_ms=assigner.slide, offset_ms=assigner.offset,
             aggs=[(abi.AGG_NAMES[k], c, abi.TYPE_NAMES[t]) for k, c, t in aggs],
             count_star_index=count_star_index,
             value_col_types=[abi.TYPE_NAMES[t] for t in value_types],
-            key_hash=KEY_HASH[key_type], max_parallelism=max_parallelism,
+            key_hash=abi.KEYHASH_PRECOMPUTED if self.key_types else KEY_HASH[key_type],
+            max_parallelism=max_parallelism,
             parallelism=parallelism, subtask_index=subtask_index, device=device,
             state_capacity=state_capacity, max_batch_rows=max_batch_rows,
             output_capacity=output_capacity, nullable_cols=nullable_cols)
@@ -84,8 +95,22 @@ class WindowAggOperator:
     # ---- OneInputStreamOperator
     def process_batch(self, keys, rowtimes, values=(), key_hashes=None, nulls=None):
         """processElement for every row of a columnar batch (host arrays; ``nulls``: {column:
-        per-row NULL flags} for NULL-able columns)."""
-        self.handle.push_host(keys, rowtimes, values, key_hashes, nulls=nulls)
+        per-row NULL flags} for NULL-able columns).  With key rows (``key_type`` a tuple of SQL
+        types) ``keys`` is a sequence of key tuples: their columns go to the device, which
+        computes BinaryRowData.hashCode (fw_key_row_hash) and routes by it."""
+        if self.key_types is None:
+            self.handle.push_host(keys, rowtimes, values, key_hashes, nulls=nulls)
+            return
+        import torch
+        dev = torch.device("cuda", self.cfg.device)
+        ids = self.keys.encode(keys)
+        kh = KeyRowColumns.from_rows(keys, self.key_types).to(dev).hash_device()
+        vals = [torch.from_numpy(np.ascontiguousarray(v).view(np.int64)).to(dev) for v in values]
+        nul = None if not nulls else {c: torch.from_numpy(np.ascontiguousarray(f).astype(np.uint8)).to(dev)
+                                      for c, f in nulls.items()}
+        self.handle.push_device(torch.from_numpy(ids).to(dev),
+                                torch.from_numpy(np.ascontiguousarray(rowtimes, dtype=np.int64)).to(dev),
+                                vals, kh, nulls=nul)
 
     def process_batch_device(self, keys, rowtimes, values=(), key_hashes=None, nulls=None):
         """processElement for a batch already resident in HBM (torch cuda tensors)."""
@@ -126,5 +151,6 @@ class WindowAggOperator:
                     vals.append(float(np.int64(res["values"][a][i]).view(np.float64)))
                 else:
                     vals.append(int(res["values"][a][i]))
-            rows.append((int(res["key"][i]), *vals, int(res["window_start"][i]), int(res["window_end"][i])))
+            key = self.keys.decode(res["key"][i]) if self.keys is not None else (int(res["key"][i]),)
+            rows.append((*key, *vals, int(res["window_start"][i]), int(res["window_end"][i])))
         return rows

@@ -47,6 +47,10 @@
  *                    (FR/runtime/state/KeyGroupRangeAssignment.java:63-127) as used by
  *                    KeyGroupStreamPartitioner.selectChannel (FR/streaming/runtime/partitioner/
  *                    KeyGroupStreamPartitioner.java:55-65)
+ *   fw_key_row_hash  BinaryRowDataKeySelector.getKey(row).hashCode() for VARCHAR / composite keys
+ *                    (TR/keyselector/BinaryRowDataKeySelector.java:54 -> BinaryRowData.hashCode
+ *                    :459 -> MurmurHashUtils.hashBytesByWords :70-170), feeding
+ *                    FW_KEYHASH_PRECOMPUTED handles and partitioning
  *   fw_partition_by_dest
  *                    the keyBy exchange's record routing (ChannelSelectorRecordWriter.emit,
  *                    FR/runtime/io/network/api/writer/ChannelSelectorRecordWriter.java:54): rows
@@ -61,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 2
+#define FW_ABI_VERSION 3
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -265,14 +269,45 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size);
 int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t capacity, int64_t* size);
 int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size);
 
+/* ---- key rows: VARCHAR / composite keys ------------------------------------------------ */
+/* A key row field, as the key projection writes it into a BinaryRowData (BinaryRowWriter,
+   TR/data/writer/BinaryRowWriter.java:39-122 + AbstractBinaryWriter.java:83-106,242-345).
+   A FIXEDn field occupies the low n bytes of its 8-byte slot; a STRING field is UTF-8 text
+   (VARCHAR / CHAR) or bytes (VARBINARY / BINARY). */
+#define FW_MAX_KEY_FIELDS 8
+typedef enum {
+    FW_KF_STRING = 0,   /* VARCHAR, CHAR, VARBINARY, BINARY           writeString / writeBinary        */
+    FW_KF_FIXED1 = 1,   /* BOOLEAN, TINYINT                           writeBoolean / writeByte         */
+    FW_KF_FIXED2 = 2,   /* SMALLINT                                   writeShort                       */
+    FW_KF_FIXED4 = 4,   /* INT, DATE, TIME(0-3), FLOAT (IEEE bits)    writeInt / writeFloat            */
+    FW_KF_FIXED8 = 8    /* BIGINT, DOUBLE (bits), TIMESTAMP(0-3) millis, DECIMAL(p<=18) unscaled long   */
+} fw_key_field_kind;
+typedef struct {
+    int32_t kind;              /* fw_key_field_kind                                          */
+    int32_t reserved;
+    const int64_t* fixed;      /* FIXEDn: one int64 per row (low n bytes used)               */
+    const int32_t* offsets;    /* STRING: n + 1 byte offsets into bytes (Arrow layout)       */
+    const uint8_t* bytes;      /* STRING: the bytes; base 4-byte aligned                      */
+    const uint8_t* nulls;      /* NULL or 1 byte per row, non-zero = NULL (setNullAt)         */
+} fw_key_field;
+/* d_hash[i] = hashCode() of row i's key row (BinaryRowData.hashCode, BinaryRowData.java:459):
+   the Java hash a FW_KEYHASH_PRECOMPUTED handle / fw_partition_by_dest routes by.  All pointers
+   in fields are device pointers; the key's identity in the window state (the int64 key column
+   pushed alongside) is the caller's, e.g. a dictionary id. */
+int fw_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n, int32_t* d_hash, void* stream);
+
 /* ---- stand-alone device kernels (partitioner, tests) ---------------------------------- */
 /* d_kg[i] = key group, d_dest[i] = computeOperatorIndexForKeyGroup(maxP, p, kg). */
 int fw_assign_key_groups(const int64_t* d_key, const int32_t* d_key_hash, int64_t n,
                          int32_t key_hash_kind, int32_t max_parallelism, int32_t parallelism,
                          int32_t* d_kg, int32_t* d_dest, void* stream);
 /* Counting-sort rows by destination subtask.  d_counts[p] receives rows per destination;
-   output columns are grouped by destination in ascending order. n_cols value columns. */
-int fw_partition_by_dest(const int64_t* d_key, const int64_t* d_ts, const void* const* d_values,
+   output columns are grouped by destination in ascending order, rows in input order within a
+   destination. n_cols value columns.  d_key_hash is the Java key hash per row, required for
+   FW_KEYHASH_PRECOMPUTED (e.g. from fw_key_row_hash) and ignored otherwise; a caller that needs
+   it on the receiving side moves it as one of the value columns. */
+int fw_partition_by_dest(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                         const void* const* d_values,
                          int32_t n_cols, int64_t n, int32_t key_hash_kind,
                          int32_t max_parallelism, int32_t parallelism,
                          int64_t* d_out_key, int64_t* d_out_ts, void* const* d_out_values,
@@ -303,6 +338,8 @@ int32_t fw_host_key_group(int32_t key_hash_kind, int64_t key, int32_t precompute
    kg[i] / dest[i] as fw_assign_key_groups computes them on the device. Either output may be NULL. */
 int fw_host_assign_key_groups(const int64_t* key, const int32_t* key_hash, int64_t n, int32_t key_hash_kind,
                               int32_t max_parallelism, int32_t parallelism, int32_t* kg, int32_t* dest);
+/* fw_key_row_hash over host-resident columns (the Java-side partitioner of host-staged records). */
+int fw_host_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n, int32_t* hash);
 /* TimeWindow.getWindowStartWithOffset (FR/streaming/api/windowing/windows/TimeWindow.java:264). */
 int64_t fw_host_window_start(int64_t ts, int64_t offset, int64_t size);
 /* TimeWindowUtil.getNextTriggerWatermark, UTC (TR/util/TimeWindowUtil.java:186). */

@@ -112,6 +112,49 @@ int32_t binrow_hash_words(const int32_t* words, int nwords) {
     return fmix32(h1 ^ (nwords * 4));
 }
 
+// BinaryRowData.hashCode of a general key row, restated by building the row's bytes exactly as
+// BinaryRowWriter does (BinaryRowWriter.java:39-122: reset zeroes the null-bit words, the fixed
+// part is nullBitsSizeInBytes + 8 * arity, complete() sets the size to the cursor;
+// AbstractBinaryWriter.java:83-106 writeString / writeBytes, :242-246 zeroOutPaddingBytes,
+// :295-310 writeBytesToVarLenPart, :323-331 roundNumberOfBytesToNearestWord, :333-348
+// writeBytesToFixLenPart; setNullAt :59-62 writes the null bit and a 0 slot) on a
+// little-endian machine, then hashing the bytes as 4-byte ints (BinarySegmentUtils.hashByWords).
+int32_t key_row_hash_bytes(const fw_key_field* f, int nf, int64_t i) {
+    const int null_bytes = ((nf + 63 + 8) / 64) * 8;  // calculateBitSetWidthInBytes (:71-73)
+    std::vector<uint8_t> row((size_t)null_bytes + 8 * (size_t)nf, 0);
+    auto put_long = [&](size_t at, uint64_t v) { for (int b = 0; b < 8; b++) row[at + b] = (uint8_t)(v >> (8 * b)); };
+    for (int p = 0; p < nf; p++) {
+        const size_t slot = (size_t)null_bytes + 8 * (size_t)p;  // getFieldOffset (:114-116)
+        if (f[p].nulls && f[p].nulls[i]) {
+            const int bit = p + 8;  // HEADER_SIZE_IN_BITS
+            row[(size_t)bit >> 3] |= (uint8_t)(1u << (bit & 7));
+            put_long(slot, 0);
+            continue;
+        }
+        if (f[p].kind != FW_KF_STRING) {  // putLong / putInt / putShort / put write `width` bytes
+            const uint64_t v = (uint64_t)f[p].fixed[i];
+            for (int b = 0; b < f[p].kind; b++) row[slot + b] = (uint8_t)(v >> (8 * b));
+            continue;
+        }
+        const int32_t o = f[p].offsets[i], len = f[p].offsets[i + 1] - o;
+        const uint8_t* bytes = f[p].bytes + o;
+        if (len <= 7) {
+            uint64_t seven = 0;
+            for (int b = 0; b < len; b++) seven |= (uint64_t)bytes[b] << (8 * b);
+            put_long(slot, ((uint64_t)(len | 0x80) << 56) | seven);
+        } else {
+            const size_t cursor = row.size();
+            const size_t rounded = (size_t)(len + 7) / 8 * 8;
+            row.resize(cursor + rounded, 0);
+            memcpy(&row[cursor], bytes, (size_t)len);
+            put_long(slot, ((uint64_t)cursor << 32) | (uint64_t)len);
+        }
+    }
+    std::vector<int32_t> words(row.size() / 4);
+    memcpy(words.data(), row.data(), row.size());
+    return binrow_hash_words(words.data(), (int)words.size());
+}
+
 int32_t java_key_hash(int kind, int64_t key, int32_t precomputed) {
     switch (kind) {
         case FW_KEYHASH_LONG: return (int32_t)(key ^ (int64_t)((uint64_t)key >> 32));  // Long.hashCode
@@ -812,6 +855,9 @@ void or_clear_results(void* h) { ((Oracle*)h)->out.clear(); }
 // Hash / key-group restatements.
 int32_t or_murmur_hash(int32_t code) { return murmur_hash(code); }
 int32_t or_java_key_hash(int32_t kind, int64_t key, int32_t pre) { return java_key_hash(kind, key, pre); }
+void or_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n, int32_t* out) {
+    for (int64_t i = 0; i < n; i++) out[i] = key_row_hash_bytes(fields, n_fields, i);
+}
 int32_t or_key_group(int32_t kind, int64_t key, int32_t pre, int32_t max_p) {
     return key_group_for_hash(java_key_hash(kind, key, pre), max_p);
 }

@@ -49,6 +49,7 @@ def lib():
         L.or_murmur_hash.argtypes = [i32]
         L.or_java_key_hash.restype = i32
         L.or_java_key_hash.argtypes = [i32, i64, i32]
+        L.or_key_row_hash.argtypes = [C.POINTER(abi.fw_key_field), i32, i64, vp]
         L.or_key_group.restype = i32
         L.or_key_group.argtypes = [i32, i64, i32, i32]
         L.or_operator_index.restype = i32
@@ -146,6 +147,14 @@ def murmur_hash(code):
 
 def java_key_hash(kind, key, pre=0):
     return lib().or_java_key_hash(kind, int(key), int(pre))
+
+
+def key_row_hash(fields, n_fields, n):
+    """BinaryRowData.hashCode of n key rows from host fw_key_field columns (byte-image restatement)."""
+    import numpy as np
+    out = np.empty(n, dtype=np.int32)
+    lib().or_key_row_hash(fields, n_fields, n, out.ctypes.data)
+    return out
 
 
 def key_group(kind, key, max_p, pre=0):

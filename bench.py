@@ -186,7 +186,8 @@ def main():
 
     out_cap = 2 * keys_total // world + (1 << 20)
     if wl["window"][0] == "CUMULATE":
-        out_cap = keys_total + (1 << 20)
+        # every step of every active key's window fires; a 2^22 batch spans ~151 s = up to 3 steps
+        out_cap = 4 * keys_total + (1 << 20)
 
     def run(first, nsteps, handle):
         for b in range(first, first + nsteps):

@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 3
+FW_ABI_VERSION = 4
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -89,6 +89,13 @@ class fw_config(C.Structure):
         ("state_capacity", C.c_int64),
         ("max_batch_rows", C.c_int64),
         ("output_capacity", C.c_int64),
+        ("allowed_lateness_ms", C.c_int64),
+        ("late_side_output", C.c_int32),
+        ("tz_use_dst", C.c_int32),
+        ("tz_n", C.c_int32),
+        ("reserved1", C.c_int32),
+        ("tz_utc", C.POINTER(C.c_int64)),
+        ("tz_offset_ms", C.POINTER(C.c_int64)),
     ]
 
 
@@ -109,6 +116,12 @@ class fw_result(C.Structure):
                 ("window_start", C.POINTER(C.c_int64)), ("window_end", C.POINTER(C.c_int64)),
                 ("values", C.POINTER(C.c_int64) * FW_MAX_AGGS),
                 ("null_mask", C.POINTER(C.c_uint32))]
+
+
+class fw_late_rows(C.Structure):
+    _fields_ = [("n", C.c_int64), ("key", C.POINTER(C.c_int64)), ("ts", C.POINTER(C.c_int64)),
+                ("values", C.POINTER(C.c_int64) * FW_MAX_COLS), ("push_seq", C.POINTER(C.c_int64)),
+                ("row", C.POINTER(C.c_int64))]
 
 
 class fw_stats(C.Structure):
@@ -140,9 +153,11 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
                 aggs=(), count_star_index=-1, value_col_types=(), key_hash=KEYHASH_BINROW_BIGINT,
                 max_parallelism=128, parallelism=1, subtask_index=0, device=0,
                 state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22,
-                nullable_cols=(), agg_phase=PHASE_ONE):
+                nullable_cols=(), agg_phase=PHASE_ONE, allowed_lateness_ms=0, late_side_output=False,
+                shift_zone=None):
     """Build an fw_config.  ``aggs`` is a sequence of (kind, input_col, type); ``nullable_cols``
-    the value columns that may hold SQL NULLs."""
+    the value columns that may hold SQL NULLs; ``shift_zone`` a TIMESTAMP_LTZ window's time zone
+    (a zone name, or a ShiftZone from flink_amd.table.time_zone; None / "UTC": no shift)."""
     if len(aggs) > FW_MAX_AGGS or len(value_col_types) > FW_MAX_COLS:
         raise ValueError("too many aggregates or value columns")
     c = fw_config()
@@ -171,7 +186,31 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
     c.state_capacity = state_capacity
     c.max_batch_rows = max_batch_rows
     c.output_capacity = output_capacity
+    c.allowed_lateness_ms = allowed_lateness_ms
+    c.late_side_output = 1 if late_side_output else 0
+    set_shift_zone(c, shift_zone)
     return c
+
+
+def set_shift_zone(c, zone):
+    """Attach a shift time zone's offset table to a config (the arrays are kept alive on it)."""
+    if zone is None or zone == "UTC":
+        c.tz_n, c.tz_use_dst = 0, 0
+        c.tz_utc = C.POINTER(C.c_int64)()
+        c.tz_offset_ms = C.POINTER(C.c_int64)()
+        c._zone = None
+        return
+    if isinstance(zone, str):
+        from .table.time_zone import ShiftZone
+        zone = ShiftZone.of(zone)
+    n = len(zone.utc)
+    utc = (C.c_int64 * n)(*zone.utc)
+    off = (C.c_int64 * n)(*zone.offset_ms)
+    c._zone = (zone, utc, off)  # keeps the arrays alive while the config is
+    c.tz_n = n
+    c.tz_use_dst = 1 if zone.use_dst else 0
+    c.tz_utc = C.cast(utc, C.POINTER(C.c_int64))
+    c.tz_offset_ms = C.cast(off, C.POINTER(C.c_int64))
 
 
 def result_columns(cfg):
@@ -204,7 +243,7 @@ def global_config(cfg, **overrides):
               key_hash=cfg.key_hash, max_parallelism=cfg.max_parallelism, parallelism=cfg.parallelism,
               subtask_index=cfg.subtask_index, device=cfg.device, state_capacity=cfg.state_capacity,
               max_batch_rows=cfg.max_batch_rows, output_capacity=cfg.output_capacity, nullable_cols=nullable,
-              agg_phase=PHASE_GLOBAL)
+              agg_phase=PHASE_GLOBAL, shift_zone=getattr(cfg, "_zone", None) and cfg._zone[0])
     kw.update(overrides)
     return make_config(**kw)
 

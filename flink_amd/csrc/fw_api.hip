@@ -141,6 +141,14 @@ struct fw_handle {
     int32_t* slot_nch = nullptr;  // [FW_MAX_PENDING]
     int64_t* treq = nullptr;
     int64_t treq_cap = 0;
+    uint64_t* lfire = nullptr;   // DataStream late-fire rows
+    int64_t lfire_cap = 0;
+    int64_t* side = nullptr;     // DataStream late side-output rows
+    int64_t side_cap = 0;
+    int32_t push_seq = 0;        // fw_commit / fw_push_device calls (side-output row ids)
+    std::vector<int64_t> tz_utc, tz_off, tz_bound;  // shift-zone table (host copy)
+    int64_t* d_tz = nullptr;     // device copy: [utc | off | bound]
+    std::vector<int64_t> lr_key, lr_ts, lr_seq, lr_row, lr_val[FW_MAX_COLS];  // fw_late_records copies
     uint64_t* state = nullptr;
     int32_t* state_count = nullptr;
     int64_t* sb_min_timer = nullptr;
@@ -233,6 +241,31 @@ int validate_and_plan(fw_handle* h) {
             break;
         default: return fail(FW_E_INVALID, "bad window kind %d", c.window_kind);
     }
+    w.ds = c.api == FW_API_DATASTREAM;
+    w.slide = c.window_kind == FW_WIN_HOP ? c.slide_ms : c.size_ms;
+    w.n_win = (w.ds && c.window_kind == FW_WIN_HOP) ? (int32_t)(c.size_ms / c.slide_ms) : 1;
+    w.slide_div = make_udiv((uint64_t)w.slide);
+    // ---- lateness (DataStream) and shift time zone (SQL TIMESTAMP_LTZ)
+    if (c.allowed_lateness_ms < 0) return fail(FW_E_INVALID, "The allowed lateness cannot be negative.");
+    if (c.api == FW_API_SQL && (c.allowed_lateness_ms != 0 || c.late_side_output))
+        return fail(FW_E_INVALID, "allowed lateness and late side outputs are DataStream WindowOperator features");
+    w.lateness = c.allowed_lateness_ms;
+    if (c.tz_n < 0) return fail(FW_E_INVALID, "tz_n must be >= 0");
+    if (c.tz_n > 0) {
+        if (c.api != FW_API_SQL) return fail(FW_E_INVALID, "shift time zones belong to SQL TIMESTAMP_LTZ windows");
+        if (!c.tz_utc || !c.tz_offset_ms) return fail(FW_E_INVALID, "tz_utc / tz_offset_ms required when tz_n > 0");
+        if (c.tz_utc[0] != INT64_MIN) return fail(FW_E_INVALID, "tz_utc[0] must be Long.MIN_VALUE");
+        h->tz_utc.assign(c.tz_utc, c.tz_utc + c.tz_n);
+        h->tz_off.assign(c.tz_offset_ms, c.tz_offset_ms + c.tz_n);
+        h->tz_bound.assign(c.tz_n, INT64_MIN);
+        for (int i = 1; i < c.tz_n; i++) {
+            if (h->tz_utc[i] <= h->tz_utc[i - 1]) return fail(FW_E_INVALID, "tz_utc must be strictly ascending");
+            if (h->tz_off[i] < -18 * 3600000ll || h->tz_off[i] > 18 * 3600000ll) return fail(FW_E_INVALID, "offset out of range");
+            h->tz_bound[i] = h->tz_utc[i] + std::max(h->tz_off[i - 1], h->tz_off[i]);
+            if (h->tz_bound[i] <= h->tz_bound[i - 1]) return fail(FW_E_INVALID, "tz transitions too close together");
+        }
+    }
+    w.tz = TzTable{h->tz_utc.data(), h->tz_off.data(), h->tz_bound.data(), c.tz_n, c.tz_use_dst ? 1 : 0};
     w.slice_div = make_udiv((uint64_t)w.interval);
     w.size_div = make_udiv((uint64_t)w.size);
     w.fast32 = w.interval < (1ll << 30) && w.offset < (1ll << 61) && w.offset > -(1ll << 61);
@@ -432,6 +465,12 @@ int validate_and_plan(fw_handle* h) {
         return fail(FW_E_INVALID, "max_batch_rows too large for SQL MIN/MAX(DOUBLE) arrival ordinals");
     h->cell_cols = cell_pad(h->max_nch);
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
+    if (c.api == FW_API_DATASTREAM) {
+        if (c.allowed_lateness_ms > 0 && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
+            return fail(FW_E_INVALID, "max_batch_rows too large for late-element arrival ordinals");
+        h->lfire_cap = c.allowed_lateness_ms > 0 ? h->treq_cap : 0;
+        h->side_cap = c.late_side_output ? h->treq_cap : 0;
+    }
     h->out_cap = c.output_capacity;
     h->slab_cap = std::max<int64_t>(64, (2 * c.output_capacity + ks.n_sb - 1) / ks.n_sb);
     h->stage_cap = c.max_batch_rows;
@@ -457,6 +496,15 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->cells, (size_t)FW_MAX_PENDING * h->ks.n_sb * h->cell_cols))) return rc;
     if ((rc = dalloc(&h->slot_nch, FW_MAX_PENDING))) return rc;
     if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
+    if (h->lfire_cap && (rc = dalloc(&h->lfire, (size_t)h->lfire_cap * LFW))) return rc;
+    if (h->side_cap && (rc = dalloc(&h->side, (size_t)h->side_cap * SOW))) return rc;
+    if (!h->tz_utc.empty()) {  // shift-zone table on the device; the kernels' WinDesc points at it
+        const size_t n = h->tz_utc.size();
+        if ((rc = dalloc(&h->d_tz, 3 * n))) return rc;
+        HIP_TRY(hipMemcpy(h->d_tz, h->tz_utc.data(), 8 * n, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(h->d_tz + n, h->tz_off.data(), 8 * n, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(h->d_tz + 2 * n, h->tz_bound.data(), 8 * n, hipMemcpyHostToDevice));
+    }
     if ((rc = dalloc(&h->state, (size_t)h->ks.n_sb * h->cap_e * PWE))) return rc;
     if ((rc = dalloc(&h->state_count, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->sb_min_timer, h->ks.n_sb))) return rc;
@@ -521,12 +569,25 @@ int read_ctrl(fw_handle* h, Ctrl* out) {
     HIP_TRY(hipMemcpyAsync(out, h->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (out->error) {
-        return fail(FW_E_CAPACITY, "device error (bits 0x%x:%s%s%s%s%s)", out->error,
+        return fail(FW_E_CAPACITY, "device error (bits 0x%x:%s%s%s%s%s%s)", out->error,
                     out->error & ERR_CHUNKS ? " partial-buffer" : "", out->error & ERR_STATE ? " state-table" : "",
                     out->error & ERR_OUTPUT ? " result-buffer" : "", out->error & ERR_TREQ ? " timer-requests" : "",
-                    out->error & ERR_KEYGROUP ? " key-group-not-owned" : "");
+                    out->error & ERR_KEYGROUP ? " key-group-not-owned" : "",
+                    out->error & ERR_LATE ? " late-rows (call fw_late_records more often)" : "");
     }
     return FW_OK;
+}
+
+// the window description the kernels get: the shift-zone table pointers are the device copy's
+WinDesc device_win(const fw_handle* h) {
+    WinDesc w = h->win;
+    if (h->d_tz) {
+        const size_t n = h->tz_utc.size();
+        w.tz.utc = h->d_tz;
+        w.tz.off = h->d_tz + n;
+        w.tz.bound = h->d_tz + 2 * n;
+    }
+    return w;
 }
 
 MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
@@ -544,7 +605,9 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.sb_min_timer = h->sb_min_timer;
     a.n_sb = h->ks.n_sb;
     a.cap_e = h->cap_e;
-    a.win = h->win;
+    a.win = device_win(h);
+    a.lfire = h->lfire;
+    a.lfire_cap = h->lfire_cap;
     a.wd = h->wd;
     a.ad = h->ad;
     a.always_flush = h->always_flush;
@@ -604,7 +667,14 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
             a.nulls[s] = live && ((h->cfg.nullable_cols >> h->slot_col[s]) & 1u) ? nulls[h->slot_col[s]] + o : nullptr;
         }
         a.n = m;
-        a.win = h->win;
+        a.win = device_win(h);
+        a.lfire = h->lfire;
+        a.lfire_cap = h->lfire_cap;
+        a.side = h->side;
+        a.side_cap = h->side_cap;
+        a.side_output = h->cfg.late_side_output ? 1 : 0;
+        a.push_seq = h->push_seq;
+        a.row0 = o;
         a.ks = h->ks;
         a.wd = h->wd;
         a.nv = h->nv;
@@ -626,7 +696,16 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
     }
+    h->push_seq++;
     return FW_OK;
+}
+
+// earliest watermark-visible time of an entry's timers, as a window end (is_fired(x, W) <=> due):
+// the maxTimestamp timer at its window end, a DataStream cleanup timer at cleanupTime + 1
+int64_t entry_timer_end(const fw_handle* h, int64_t slice, uint64_t flags) {
+    int64_t m = (flags & F_TIMER) ? slice : INT64_MAX;
+    if (h->win.ds && (flags & F_CLEAN)) m = std::min(m, wadd(ds_cleanup_time(h->win, slice), 1));
+    return m;
 }
 
 }  // namespace
@@ -644,6 +723,8 @@ int fw_create(const fw_config* cfg, fw_handle** out) {
     h->cfg = *cfg;
     if (const char* ab = getenv("FW_ABLATE")) h->ablate = atoi(ab);
     int rc = validate_and_plan(h);
+    h->cfg.tz_utc = nullptr;  // the shift-zone table was copied (h->tz_*); never read the caller's
+    h->cfg.tz_offset_ms = nullptr;
     if (!rc) rc = allocate(h);
     if (rc) {
         std::string keep = g_err;
@@ -663,6 +744,9 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->cells);
     hipFree(h->slot_nch);
     hipFree(h->treq);
+    hipFree(h->lfire);
+    hipFree(h->side);
+    hipFree(h->d_tz);
     hipFree(h->state);
     hipFree(h->state_count);
     hipFree(h->sb_min_timer);
@@ -871,6 +955,40 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     return FW_OK;
 }
 
+int fw_late_records(fw_handle* h, fw_late_rows* out) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    memset(out, 0, sizeof *out);
+    if (!h->side_cap) return fail(FW_E_STATE, "the operator has no late side output (late_side_output = 0)");
+    Ctrl c;
+    int rc = read_ctrl(h, &c);
+    if (rc) return rc;
+    const int64_t n = std::min<int64_t>(c.n_side, h->side_cap);
+    std::vector<int64_t> raw((size_t)n * SOW);
+    if (n) HIP_TRY(hipMemcpy(raw.data(), h->side, raw.size() * 8, hipMemcpyDeviceToHost));
+    const int64_t zero = 0;
+    HIP_TRY(hipMemcpy(&h->ctrl->n_side, &zero, 8, hipMemcpyHostToDevice));
+    h->lr_key.resize(n);
+    h->lr_ts.resize(n);
+    h->lr_seq.resize(n);
+    h->lr_row.resize(n);
+    for (int v = 0; v < h->cfg.n_value_cols; v++) h->lr_val[v].assign(n, 0);
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t* p = raw.data() + (size_t)i * SOW;
+        h->lr_key[i] = p[0];
+        h->lr_ts[i] = p[1];
+        h->lr_seq[i] = (int64_t)((uint64_t)p[2] >> 32);
+        h->lr_row[i] = p[2] & 0xffffffffll;
+        for (int s = 0; s < h->nv; s++) h->lr_val[h->slot_col[s]][i] = p[3 + s];  // loaded value slots
+    }
+    out->n = n;
+    out->key = h->lr_key.data();
+    out->ts = h->lr_ts.data();
+    out->push_seq = h->lr_seq.data();
+    out->row = h->lr_row.data();
+    for (int v = 0; v < h->cfg.n_value_cols; v++) out->values[v] = h->lr_val[v].data();
+    return FW_OK;
+}
+
 int fw_results_reset(fw_handle* h) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     // no launch: the next merge launch starts every output slab and the overflow region afresh
@@ -962,6 +1080,12 @@ static uint64_t semantics_fingerprint(const fw_handle* h) {
     mix(h->win.offset);
     mix(h->ks.hash_kind);
     mix(h->ks.max_p);
+    mix(c.allowed_lateness_ms);
+    mix(c.tz_use_dst);
+    for (size_t i = 0; i < h->tz_utc.size(); i++) {
+        mix(h->tz_utc[i]);
+        mix(h->tz_off[i]);
+    }
     mix(h->wd.nw);
     for (int w = 0; w < h->wd.nw; w++) {
         mix(h->wd.op[w]);
@@ -1031,7 +1155,7 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
         const size_t bytes = (size_t)cnt[s] * pwe * 8;
         const uint64_t* e = (const uint64_t*)p;
         for (int i = 0; i < cnt[s]; i++)
-            if (e[(size_t)i * pwe + 2] & F_TIMER) mins[s] = std::min(mins[s], (int64_t)e[(size_t)i * pwe + 1]);
+            mins[s] = std::min(mins[s], entry_timer_end(h, (int64_t)e[(size_t)i * pwe + 1], e[(size_t)i * pwe + 2]));
         HIP_TRY(hipMemcpy(h->state + (size_t)s * h->cap_e * pwe, p, bytes, hipMemcpyHostToDevice));
         p += bytes;
     }
@@ -1157,7 +1281,7 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
         HIP_TRY(hipMemcpy(h->state + (sb * h->cap_e + cnt[q]) * pwe, per[q].data(), (size_t)n * pwe * 8,
                           hipMemcpyHostToDevice));
         for (int64_t i = 0; i < n; i++)
-            if (per[q][(size_t)i * pwe + 2] & F_TIMER) mins[q] = std::min(mins[q], (int64_t)per[q][(size_t)i * pwe + 1]);
+            mins[q] = std::min(mins[q], entry_timer_end(h, (int64_t)per[q][(size_t)i * pwe + 1], per[q][(size_t)i * pwe + 2]));
         cnt[q] += (int32_t)n;
         added += n;
     }
@@ -1192,6 +1316,24 @@ int64_t fw_host_window_start(int64_t ts, int64_t offset, int64_t size) {
 }
 int64_t fw_host_next_trigger_watermark(int64_t wm, int64_t interval) {
     return next_trigger_watermark(wm, make_udiv((uint64_t)interval));
+}
+
+int fw_host_time_op(const fw_config* cfg, int32_t what, int64_t x, int64_t* out) {
+    if (!cfg || !out) return fail(FW_E_INVALID, "null argument");
+    fw_handle h;
+    h.cfg = *cfg;
+    const int rc = validate_and_plan(&h);  // host-only planning; w.tz points at h's host copy
+    if (rc) return rc;
+    const WinDesc& w = h.win;
+    switch (what) {
+        case 0: *out = tz_to_utc_ts(w.tz, x); break;
+        case 1: *out = tz_epoch_for_timer(w.tz, x); break;
+        case 2: *out = tz_next_trigger_watermark(w.tz, x, w.slice_div); break;
+        case 3: *out = slice_end_of(w, tz_to_utc_ts(w.tz, x)); break;
+        case 4: *out = window_start_of(w, x); break;
+        default: return fail(FW_E_INVALID, "bad time op %d", what);
+    }
+    return FW_OK;
 }
 
 }  // extern "C"

@@ -277,6 +277,73 @@ FW_HD int64_t next_trigger_watermark(int64_t wm, const UDiv& interval) {
     return trig > wm ? trig : wadd(trig, (int64_t)interval.d);
 }
 
+// ---------------------------------------------------------------------------------------
+// Shift time zone of a TIMESTAMP_LTZ window (TR/util/TimeWindowUtil.java:52-211).  The zone is a
+// piecewise-constant UTC offset table (the caller expands java.time ZoneRules into it):
+//   from UTC instant utc[i] on (utc[0] = Long.MIN_VALUE) the offset is off[i] ms, and
+//   bound[i] = utc[i] + max(off[i-1], off[i]) (bound[0] = MIN) is the first local time that
+//   LocalDateTime.atZone maps with off[i]: a local time in a gap maps with the offset before the
+//   gap (ZonedDateTime.ofLocal moves it later by the gap length and takes the later offset, which
+//   is the same instant), a local time in an overlap with the earlier offset.
+// n == 0 is the UTC zone (TIMESTAMP rowtime): every conversion is the identity.
+// ---------------------------------------------------------------------------------------
+struct TzTable {
+    const int64_t* utc;
+    const int64_t* off;
+    const int64_t* bound;
+    int32_t n;
+    int32_t dst;  // TimeZone.getTimeZone(zone).useDaylightTime()
+};
+
+// last i with a[i] <= x (a[0] = INT64_MIN, ascending)
+FW_HD int tz_find(const int64_t* a, int n, int64_t x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a[mid] <= x) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// TimeWindowUtil.toUtcTimestampMills (:52-60): the local wall-clock millis of an epoch instant
+FW_HD int64_t tz_to_utc_ts(const TzTable& z, int64_t epoch) {
+    if (z.n == 0 || epoch == INT64_MAX) return epoch;
+    return wadd(epoch, z.off[tz_find(z.utc, z.n, epoch)]);
+}
+// LocalDateTime.atZone(zone).toInstant().toEpochMilli() of a local wall-clock millis value
+FW_HD int64_t tz_local_to_epoch(const TzTable& z, int64_t local) {
+    return wsub(local, z.off[tz_find(z.bound, z.n, local)]);
+}
+// TimeWindowUtil.toEpochMillsForTimer (:69-140): the timer instant of a local timestamp; in a DST
+// gap the first skipped instant's hour, in an overlap the later of the two instants
+FW_HD int64_t tz_epoch_for_timer(const TzTable& z, int64_t local) {
+    if (z.n == 0 || local == INT64_MAX) return local;
+    const int64_t t1 = tz_local_to_epoch(z, local);
+    if (!z.dst) return t1;
+    const int64_t hour = 3600000;
+    const int64_t t2 = tz_local_to_epoch(z, wadd(local, hour));
+    if (t1 == t2) return wsub(t1, t1 % hour);  // Java % truncates toward zero, as C++
+    if (wsub(t2, t1) > hour) return wadd(t1, hour);
+    return t1;
+}
+
+// TimeWindowUtil.isWindowFired (:175-183) in a shift time zone
+FW_HD bool tz_is_fired(const TzTable& z, int64_t window_end, int64_t progress) {
+    if (window_end == INT64_MAX) return false;
+    return progress >= tz_epoch_for_timer(z, wsub(window_end, 1));
+}
+
+// TimeWindowUtil.getNextTriggerWatermark (:186-211) with the shift zone's useDaylightTime(); a
+// zone without daylight saving (and UTC) takes the epoch-space branch, as the reference does
+FW_HD int64_t tz_next_trigger_watermark(const TzTable& z, int64_t wm, const UDiv& interval) {
+    if (wm == INT64_MAX) return wm;
+    if (z.n == 0 || !z.dst) return next_trigger_watermark(wm, interval);
+    const int64_t start = window_start(tz_to_utc_ts(z, wm), 0, interval);
+    const int64_t trig = tz_epoch_for_timer(z, wsub(wadd(start, (int64_t)interval.d), 1));
+    return trig > wm ? trig : wadd(trig, (int64_t)interval.d);
+}
+
 // Sortable 64-bit key of a double (total order of Double.compare: NaN canonicalised, greatest).
 FW_HD int64_t dkey(uint64_t bits) {
     if ((bits & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (bits & 0x000FFFFFFFFFFFFFull))

@@ -1,0 +1,460 @@
+// fw_ingest_impl.h -- k_ingest (K1+K2+K3) and its launchers, instantiated per loaded value
+// column count in k_ingest_nv*.hip.
+#pragma once
+#include "fw_kernel_common.h"
+
+namespace fw {
+// ======================================================================================
+// K1+K2+K3: single-pass ingest = slice/key-group assignment + LDS segmented reduce + a
+// chunk-local counting sort of the partials by superbucket.
+//
+// One 1024-thread workgroup owns a chunk of CH = 1024*RPT rows and keeps all of them in
+// registers (row j*1024 + tid, coalesced column loads, every load of the chunk in flight at
+// once).  The chunk is folded in fold sub-tiles of 2048 rows: rows with equal (key, slice) meet
+// in an LDS slot table whose owner is the lowest row index hashing to the slot (so a hot key,
+// which occurs early, keeps its slot); the owner ends up holding the folded partial in its
+// registers.  The surviving partials are then ranked per superbucket with LDS atomics, the
+// per-superbucket counts are scanned, and every partial is stored at
+//     parts[slot][c*CH + start(sb) + rank]
+// so each (superbucket, chunk) cell is contiguous.  The cell table (cell_index: XCD-tiled
+// [slot][chunk/16][sb][16], start | count << 16) tells the merge kernel where its rows are: no count pass, no global
+// scan, one launch per push (+ a one-block stats reduce).
+// Restates AbstractSliceSyncStateWindowAggProcessor.processElement (:96-126: slice assignment,
+// late drop / late merge + timer), RecordsWindowBuffer.addElement (:81, grouping by
+// (key, sliceEnd)) and the per-group fold of AggCombiner.combine (:76-99).
+// ======================================================================================
+
+// inclusive scan of one value per thread over an NT-thread block (wave shuffles + LDS)
+template <int NT>
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int NWV = NT / 64;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    if (tid < 64) {
+        uint32_t x = tid < NWV ? wsum[tid] : 0u;
+#pragma unroll
+        for (int d = 1; d < NWV; d <<= 1) {
+            const uint32_t t = __shfl_up(x, d, 64);
+            if (lane >= d) x += t;
+        }
+        if (tid < NWV) wsum[tid] = x;
+    }
+    __syncthreads();
+    if (w > 0) v += wsum[w - 1];
+    *total = wsum[NWV - 1];
+    return v;
+}
+
+// X: the configuration has nullable columns or SQL MIN/MAX(DOUBLE) words (gates, ordinals)
+template <int NV, int NW, int RPT, bool X>
+__global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
+    constexpr int CH = IG_BLOCK * RPT;
+    constexpr int NSUB = RPT / IG_SRPT;
+    constexpr int NVR = NV > 0 ? NV : 1;
+    constexpr int PW = 2 + NW;
+    constexpr int SL = ig_slots(NW);
+    static_assert(RPT % IG_SRPT == 0, "fold sub-tiles must tile the chunk");
+    // dynamic LDS only (16-B aligned base, G17): [header 16 words][hist: n_sb u32, padded to
+    // 16 B][area: fold table, later the store stage]
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    int64_t* s_min = (int64_t*)&lds[0];
+    unsigned long long* s_drop = (unsigned long long*)&lds[1];
+    unsigned long long* s_rows = (unsigned long long*)&lds[2];
+    uint32_t* wsum = (uint32_t*)&lds[4];  // IG_BLOCK / 64 words
+    const int n_sb = a.ks.n_sb;
+    uint32_t* hist = (uint32_t*)(lds + IG_HDR_WORDS);  // partials per superbucket -> cell start
+    uint64_t* area = lds + IG_HDR_WORDS + ig_hist_words(n_sb);
+    const int area_words = (a.lds_bytes >> 3) - IG_HDR_WORDS - ig_hist_words(n_sb);
+    uint32_t* claim = (uint32_t*)area;                   // [SL]
+    int64_t* ckey = (int64_t*)(area + (SL >> 1));       // [SL]
+    int64_t* cslice = ckey + SL;                         // [SL]
+    uint64_t* cacc = (uint64_t*)(cslice + SL);           // [NW][SL]
+
+    const int tid = threadIdx.x;
+    Ctrl* ctrl = a.ctrl;
+    const int64_t c = blockIdx.x;
+    // the push's slot in the partial buffer; k_push_stats (next launch) advances pending_pushes
+    const int64_t slot = __hip_atomic_load(&ctrl->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
+    if (slot >= FW_MAX_PENDING) {
+        if (tid == 0) __hip_atomic_fetch_or(&ctrl->error, ERR_CHUNKS, __ATOMIC_RELAXED, DEV_SCOPE);
+        return;
+    }
+    const int64_t cur_wm = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
+    if (tid == 0) {
+        *s_min = INT64_MAX;
+        *s_drop = 0;
+        *s_rows = 0;
+    }
+    for (int s = tid; s < n_sb; s += IG_BLOCK) hist[s] = 0;
+
+    // ---- coalesced column loads of the whole chunk (all in flight before the first use)
+    const int64_t base = c * CH;
+    const int64_t ts0 = a.ts[base];  // chunk base for the 32-bit slice arithmetic
+    int64_t rk[RPT], rs[RPT];
+    uint64_t rv[RPT][NVR];
+    int32_t pre[RPT];
+    uint32_t rnul[RPT];  // bit q: value slot q is NULL in this row
+    uint32_t valid = 0;
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int64_t i = base + (int64_t)j * IG_BLOCK + tid;
+        rk[j] = 0;
+        rs[j] = 0;
+        pre[j] = 0;
+        rnul[j] = 0;
+#pragma unroll
+        for (int q = 0; q < NVR; q++) rv[j][q] = 0;
+        if (i < a.n) {
+            rk[j] = a.key[i];
+            rs[j] = a.ts[i];
+            if (a.khash) pre[j] = a.khash[i];
+#pragma unroll
+            for (int q = 0; q < NV; q++) {
+                if (NV > 2 && q >= a.nv) break;  // the NV = 4 / 8 variants also serve 3 / 5-7 columns
+                rv[j][q] = a.vals[q][i];
+                if (X && a.nulls[q] && a.nulls[q][i]) rnul[j] |= 1u << q;
+            }
+            valid |= 1u << j;
+        }
+    });
+    // arrival ordinal base of this chunk within the flush (W_Q* words; >= 1, see record_word)
+    const uint32_t ord0 = (uint32_t)(slot * a.cap_rows + base) + 1u;
+    // TIMESTAMP_LTZ: slices live on the shift zone's wall clock (AbstractSliceAssigner
+    // .assignSliceEnd -> toUtcTimestampMills, SliceAssigners.java:655-670)
+    int64_t tsl0 = ts0;
+    if (a.win.tz.n && !a.global) {
+        tsl0 = tz_to_utc_ts(a.win.tz, ts0);
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if (valid & (1u << j)) rs[j] = tz_to_utc_ts(a.win.tz, rs[j]);
+        });
+    }
+    // slice-aligned base 2^30 ms below the chunk's first row: rows within 2^31 ms of it take
+    // the 32-bit path (one mul_hi instead of a 64-bit magic division)
+    const bool fast = a.win.fast32 && tsl0 > -(1ll << 61) && tsl0 < (1ll << 61);
+    const int64_t tbase = fast ? window_start(tsl0, a.win.offset, a.win.slice_div) -
+                                     (int64_t)((1u << 30) / (uint32_t)a.win.interval) * a.win.interval
+                               : 0;
+    // ---- K1/K2: key group -> superbucket, slice end, late classification, record words
+    int32_t rsb[RPT];
+    uint32_t rm[RPT];
+    uint64_t racc[RPT][NW];
+    int64_t lmin = INT64_MAX;
+    uint32_t ldrop = 0, lrows = 0;
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        rsb[j] = 0;
+        rm[j] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            racc[j][w] = w >= a.wd.nw ? 0
+                         : X ? gated_word(a.wd, w, pick_col(rv[j], a.wd.col[w]), rnul[j],
+                                          ord0 + (uint32_t)(j * IG_BLOCK + tid))
+                             : record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w]), 0);
+        if (!(valid & (1u << j))) return;
+        rsb[j] = route_key(a.ks, rk[j], pre[j], &rm[j]);
+        if ((uint32_t)rsb[j] >= (uint32_t)n_sb) {  // key group not owned by this subtask
+            __hip_atomic_fetch_or(&ctrl->error, ERR_KEYGROUP, __ATOMIC_RELAXED, DEV_SCOPE);
+            valid &= ~(1u << j);
+            return;
+        }
+        int64_t se;
+        const uint64_t d = (uint64_t)rs[j] - (uint64_t)tbase;
+        if (a.global) {
+            se = rs[j];  // SlicedSharedSliceAssigner.assignSliceEnd: the row's slice-end field
+        } else if (fast && d < (1ull << 31)) {
+            const uint32_t d32 = (uint32_t)d;
+            const uint32_t r = d32 - udiv32(d32, a.win.slice_div32) * (uint32_t)a.win.interval;
+            se = rs[j] - (int64_t)r + a.win.interval;
+        } else {
+            se = slice_end_of(a.win, rs[j]);
+        }
+        int64_t target = se;
+        if (a.win.ds) {
+            // DataStream WindowOperator.processElement (:405-446): the pane's windows, newest
+            // first, end at e0, e0 - slide, ...; a window is late once its cleanup time has passed
+            // (isWindowLate :609-612), fired once its maxTimestamp has (EventTimeTrigger)
+            const int64_t e0 = ds_first_window_end(a.win, se);
+            if (ds_cleanup_time(a.win, e0) <= cur_wm) {  // late for every window: skipped
+                valid &= ~(1u << j);
+                if (wadd(rs[j], a.win.lateness) <= cur_wm) {  // isElementLate (:640-644)
+                    if (!a.side_output) {
+                        ldrop++;
+                    } else {  // sideOutput(element)
+                        const int64_t r = __hip_atomic_fetch_add(&ctrl->n_side, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
+                        if (r < a.side_cap) {
+                            int64_t* p = a.side + (size_t)r * SOW;
+                            const int64_t i = base + (int64_t)j * IG_BLOCK + tid;
+                            p[0] = rk[j];
+                            p[1] = rs[j];
+                            p[2] = ((int64_t)a.push_seq << 32) | (int64_t)(i + a.row0);
+#pragma unroll
+                            for (int q = 0; q < NVR; q++) p[3 + q] = (int64_t)rv[j][q];
+                        } else {
+                            __hip_atomic_fetch_or(&ctrl->error, ERR_LATE, __ATOMIC_RELAXED, DEV_SCOPE);
+                        }
+                    }
+                }
+                return;
+            }
+            // the newest fired window; if it is not cleaned yet the element fires it again at
+            // once (EventTimeTrigger.onElement returns FIRE): a late-fire row, handled in order of
+            // arrival by the merge kernel
+            bool late_fire = false;
+            if (cur_wm >= wsub(e0, 1)) {
+                late_fire = true;  // e0 fired, and not cleaned (checked above)
+            } else if (a.win.n_win > 1) {
+                const uint64_t d = (uint64_t)wsub(wsub(e0, 1), cur_wm);
+                uint64_t kf = udiv(d, a.win.slide_div);
+                kf += (kf * (uint64_t)a.win.slide != d);
+                if (kf < (uint64_t)a.win.n_win)
+                    late_fire = ds_cleanup_time(a.win, wsub(e0, (int64_t)kf * a.win.slide)) > cur_wm;
+            }
+            if (late_fire) {
+                valid &= ~(1u << j);
+                const int64_t r = __hip_atomic_fetch_add(&ctrl->n_lfire, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
+                if (r < a.lfire_cap) {
+                    uint64_t* p = a.lfire + (size_t)r * LFW;
+                    p[0] = (uint64_t)rk[j];
+                    p[1] = (uint64_t)se;
+                    p[2] = (uint64_t)(uint32_t)rsb[j] | ((uint64_t)(ord0 + (uint32_t)(j * IG_BLOCK + tid)) << 32);
+#pragma unroll
+                    for (int w = 0; w < NW; w++) p[3 + w] = racc[j][w];
+                } else {
+                    __hip_atomic_fetch_or(&ctrl->error, ERR_LATE, __ATOMIC_RELAXED, DEV_SCOPE);
+                }
+                return;
+            }
+        } else if (!a.local && win_fired(a.win, se, cur_wm)) {
+            if (win_fired(a.win, last_window_end_of(a.win, se), cur_wm)) {  // late for every window: drop
+                valid &= ~(1u << j);
+                ldrop++;
+                return;
+            }
+            target = merge_target_of(a.win, se);
+            // timer for the first unfired window (processElement :111-117)
+            int64_t unfired;
+            if (a.win.tz.n == 0) {
+                const int64_t steps = (int64_t)((uint64_t)wsub(wadd(cur_wm, 1), se) / (uint64_t)a.win.interval) + 1;
+                unfired = wadd(se, steps * a.win.interval);
+            } else {  // window ends are not equally spaced in epoch time across a DST change
+                unfired = se;
+                while (win_fired(a.win, unfired, cur_wm)) unfired = wadd(unfired, a.win.interval);
+            }
+            const int64_t r = __hip_atomic_fetch_add(&ctrl->n_treq, (int64_t)1, __ATOMIC_RELAXED, DEV_SCOPE);
+            if (r < a.treq_cap) {
+                a.treq[3 * r] = rk[j];
+                a.treq[3 * r + 1] = unfired;
+                a.treq[3 * r + 2] = rsb[j];
+            } else {
+                __hip_atomic_fetch_or(&ctrl->error, ERR_TREQ, __ATOMIC_RELAXED, DEV_SCOPE);
+            }
+        }
+        rs[j] = target;
+        lmin = min(lmin, target);
+        lrows++;
+    });
+    // ---- K3: fold equal (key, slice) rows, one 1024-row sub-tile at a time
+    if (!(a.ablate & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
+        constexpr int s = decltype(S)::value;
+        uint32_t rh[IG_SRPT];
+        __syncthreads();  // previous sub-tile's owners are done with claim/cacc
+        for (int h = tid; h < SL; h += IG_BLOCK) claim[h] = 0xFFFFFFFFu;
+        __syncthreads();
+        static_for<IG_SRPT>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            rh[q] = fold_slot(rm[j], rs[j], SL);
+            if (valid & (1u << j)) atomicMin(&claim[rh[q]], (uint32_t)(j * IG_BLOCK + tid));
+        });
+        __syncthreads();
+        static_for<IG_SRPT>([&](auto Q) {  // slot owners publish their (key, slice) and partial
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
+            ckey[rh[q]] = rk[j];
+            cslice[rh[q]] = rs[j];
+#pragma unroll
+            for (int w = 0; w < NW; w++) cacc[w * SL + rh[q]] = racc[j][w];
+        });
+        __syncthreads();
+        static_for<IG_SRPT>([&](auto Q) {  // everyone else folds into a matching owner
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            const uint32_t h = rh[q];
+            if (!(valid & (1u << j)) || claim[h] == (uint32_t)(j * IG_BLOCK + tid)) return;
+            if (ckey[h] == rk[j] && cslice[h] == rs[j]) {
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w * SL + h], racc[j][w]);
+                valid &= ~(1u << j);
+            }
+        });
+        __syncthreads();
+        static_for<IG_SRPT>([&](auto Q) {  // owners take the folded partial back
+            constexpr int q = decltype(Q)::value;
+            constexpr int j = s * IG_SRPT + q;
+            if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
+#pragma unroll
+            for (int w = 0; w < NW; w++) racc[j][w] = cacc[w * SL + rh[q]];
+        });
+    });
+    // ---- rank the partials per superbucket, scan, publish the cells
+    uint32_t rdst[RPT];
+    const bool sort = !(a.ablate & AB_NO_SORT);
+    static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        rdst[j] = (sort && (valid & (1u << j))) ? atomicAdd(&hist[rsb[j]], 1u) : (uint32_t)(j * IG_BLOCK + tid);
+    });
+    __syncthreads();
+    uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch;
+    const int per = (n_sb + IG_BLOCK - 1) / IG_BLOCK;
+    const int sb0 = min(tid * per, n_sb), sb1 = min(sb0 + per, n_sb);
+    uint32_t seg = 0;
+    for (int i = sb0; i < sb1; i++) seg += hist[i];
+    uint32_t total;
+    const uint32_t incl = block_incl_scan<IG_BLOCK>(seg, wsum, &total);
+    uint32_t run = incl - seg;
+    if (sort)
+        for (int i = sb0; i < sb1; i++) {
+            const uint32_t v = hist[i];
+            hist[i] = run;
+            cells[cell_index(c, n_sb, i)] = run | (v << 16);
+            run += v;
+        }
+    __syncthreads();
+    if (sort)
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if (valid & (1u << j)) rdst[j] += hist[rsb[j]];
+        });
+    else
+        total = CH;
+    // ---- store the partials through an LDS stage so every global store is a full line
+    uint64_t* out = a.parts + ((size_t)slot * a.cap_rows + (size_t)base) * PW;
+    const uint32_t wrows = (uint32_t)(area_words / PW) & ~1u;
+    if (!(a.ablate & AB_NO_STORE))
+        for (uint32_t w0 = 0; w0 < total; w0 += wrows) {
+            __syncthreads();  // fold table / previous window no longer read
+            static_for<RPT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                const uint32_t d = rdst[j] - w0;
+                if (!(valid & (1u << j)) || d >= wrows) return;
+                uint64_t* p = area + (size_t)d * PW;
+                p[0] = (uint64_t)rk[j];
+                p[1] = (uint64_t)rs[j];
+#pragma unroll
+                for (int w = 0; w < NW; w++) p[2 + w] = racc[j][w];
+            });
+            __syncthreads();
+            const uint32_t nwords = min(wrows, total - w0) * PW;
+            uint64_t* dst = out + (size_t)w0 * PW;  // 16-B aligned: slot, chunk and window bases are even rows
+            for (uint32_t q = 2 * tid; q < nwords; q += 2 * IG_BLOCK) {
+                if (q + 1 < nwords) {
+                    *(ulonglong2*)(dst + q) = *(const ulonglong2*)(area + q);
+                } else {
+                    dst[q] = area[q];
+                }
+            }
+        }
+    // ---- control counters.  Each chunk publishes its stats with agent-scope stores (they bypass
+    // the XCD's L2, so any XCD reads them), then takes a ticket; the last workgroup of the launch
+    // reduces every chunk's stats into the control block and commits the push's slot
+    // (RecordsWindowBuffer's minSliceEnd and the late-drop counter).  No extra launch.
+    if (lmin != INT64_MAX) __hip_atomic_fetch_min(s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
+    if (ldrop) atomicAdd(s_drop, (unsigned long long)ldrop);
+    if (lrows) atomicAdd(s_rows, (unsigned long long)lrows);
+    __syncthreads();
+    int32_t* s_last = (int32_t*)&lds[3];
+    if (tid == 0) {
+        __hip_atomic_store(&a.chunk_stats[4 * c], *s_min, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[4 * c + 1], (int64_t)*s_drop, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[4 * c + 2], (int64_t)*s_rows, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[4 * c + 3], (int64_t)total, __ATOMIC_RELAXED, DEV_SCOPE);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *s_last = grid_last_wg(a.tickets->c[0]);
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    int64_t m = INT64_MAX, d = 0, r = 0, q = 0;
+    for (int64_t i = tid; i < (int64_t)gridDim.x; i += IG_BLOCK) {
+        m = min(m, __hip_atomic_load(&a.chunk_stats[4 * i], __ATOMIC_RELAXED, DEV_SCOPE));
+        d += __hip_atomic_load(&a.chunk_stats[4 * i + 1], __ATOMIC_RELAXED, DEV_SCOPE);
+        r += __hip_atomic_load(&a.chunk_stats[4 * i + 2], __ATOMIC_RELAXED, DEV_SCOPE);
+        q += __hip_atomic_load(&a.chunk_stats[4 * i + 3], __ATOMIC_RELAXED, DEV_SCOPE);
+    }
+    m = wave_min_i64(m);
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) {
+        d += (int64_t)__shfl_xor((long long)d, k, 64);
+        r += (int64_t)__shfl_xor((long long)r, k, 64);
+        q += (int64_t)__shfl_xor((long long)q, k, 64);
+    }
+    int64_t* red = (int64_t*)area;  // [4][IG_BLOCK / 64]
+    constexpr int NWV = IG_BLOCK / 64;
+    if ((tid & 63) == 0) {
+        red[tid >> 6] = m;
+        red[NWV + (tid >> 6)] = d;
+        red[2 * NWV + (tid >> 6)] = r;
+        red[3 * NWV + (tid >> 6)] = q;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int v = 1; v < NWV; v++) {
+            m = min(m, red[v]);
+            d += red[NWV + v];
+            r += red[2 * NWV + v];
+            q += red[3 * NWV + v];
+        }
+        a.slot_nch[slot] = (int32_t)gridDim.x;
+        ctrl->pending_pushes = slot + 1;
+        ctrl->min_pending = min(ctrl->min_pending, m);
+        ctrl->pending_rows += (uint64_t)r;
+        ctrl->partials += (uint64_t)q;
+        ctrl->late_dropped += (uint64_t)d;
+    }
+}
+
+template <int NV, int NW, bool X>
+static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
+    constexpr int RPT = ig_rpt(NW, NV);
+    const int64_t nch = a.n_chunks;
+    if (nch == 0) return hipSuccess;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT, X>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, IG_LDS);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    // the fold table and the histogram must fit the dynamic LDS
+    if ((int64_t)(IG_HDR_WORDS + ig_hist_words(a.ks.n_sb)) * 8 + ig_fold_bytes(NW) > a.lds_bytes) return hipErrorInvalidValue;
+    kt_mark(t, FW_KT_REDUCE, false, s);
+    hipLaunchKernelGGL((k_ingest<NV, NW, RPT, X>), dim3((unsigned)nch), dim3(IG_BLOCK), a.lds_bytes, s, a);
+    kt_mark(t, FW_KT_REDUCE, true, s);
+    return hipGetLastError();
+}
+
+template <int NV, int NW>
+static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
+    bool x = a.wd.has_q != 0;
+    for (int q = 0; q < MAX_KCOLS; q++) x = x || a.nulls[q] != nullptr;
+    return x ? ingest_x<NV, NW, true>(a, s, t) : ingest_x<NV, NW, false>(a, s, t);
+}
+
+template <int NV>
+hipError_t ingest_nv(const IngestArgs& a, hipStream_t s, KTimer* t) {
+    const int nw = a.wd.nw;
+    if (nw <= 1) return ingest_nw<NV, 1>(a, s, t);
+    if (nw <= 2) return ingest_nw<NV, 2>(a, s, t);
+    if (nw <= 4) return ingest_nw<NV, 4>(a, s, t);
+    return ingest_nw<NV, 8>(a, s, t);
+}
+
+}  // namespace fw

@@ -100,6 +100,9 @@ constexpr uint64_t Q_EMPTY = ~0ull;
 // Entry flags of the HBM slice-state table.
 constexpr uint32_t F_ACC = 1u;    // windowState(key, slice) != null
 constexpr uint32_t F_TIMER = 2u;  // event-time timer registered for (key, window = slice)
+// DataStream window entries (KIND_DSWIN): F_TIMER is the window's maxTimestamp timer, F_CLEAN its
+// cleanup timer at cleanupTime (WindowOperator.registerCleanupTimer :616-628)
+constexpr uint32_t F_CLEAN = 32u;
 
 // Error bits reported through Ctrl::error.
 constexpr uint32_t ERR_CHUNKS = 1u;
@@ -107,6 +110,7 @@ constexpr uint32_t ERR_STATE = 2u;
 constexpr uint32_t ERR_OUTPUT = 4u;
 constexpr uint32_t ERR_TREQ = 8u;
 constexpr uint32_t ERR_KEYGROUP = 16u;  // a record's key group is outside this subtask's range
+constexpr uint32_t ERR_LATE = 32u;      // late-fire rows or late side-output rows over capacity
 
 // Device-resident operator control block (one per handle).  Only kernels write it, so a
 // watermark cycle needs no host round trip.
@@ -136,7 +140,8 @@ struct Ctrl {
     uint32_t pad1[2];
     int32_t ovf_sel;         // live out_count
     int32_t pad0;
-    uint64_t pad[1];
+    int64_t n_lfire;         // DataStream late-fire rows pending (EventTimeTrigger.onElement FIRE)
+    int64_t n_side;          // DataStream late side-output rows since the last fw_late_records
 };
 
 // Window / slice description shared by both kernels (SliceAssigners.java).
@@ -150,8 +155,41 @@ struct WinDesc {
     UDiv size_div;        // divisor = size (CUMULATE getWindowStart)
     UDiv32 slice_div32;   // divisor = interval, for the 32-bit fast path
     int32_t fast32;       // interval < 2^30 and |offset| < 2^61: rows near a chunk base use 32-bit math
-    int32_t pad;
+    int32_t ds;           // DataStream WindowOperator: per-window state (KIND_DSWIN)
+    TzTable tz;           // SQL shift time zone (device pointers); tz.n == 0: UTC
+    // DataStream: windows are [start, start + size) with start on the slide grid; a pane (slice)
+    // of `interval` ms belongs to n_win consecutive windows (1 for tumbling)
+    int64_t slide;
+    int64_t lateness;     // allowedLateness (cleanupTime = maxTimestamp + lateness, saturating)
+    UDiv slide_div;
+    int32_t n_win;
+    int32_t pad2;
 };
+
+// merge/fire kernel variant of a handle: the SQL window kinds, or DataStream windows
+constexpr int KIND_DSWIN = 3;
+
+// TimeWindowUtil.isWindowFired in the window's shift zone (UTC when tz.n == 0)
+FW_HD bool win_fired(const WinDesc& w, int64_t we, int64_t progress) {
+    if (w.tz.n == 0) return is_fired(we, progress);
+    return tz_is_fired(w.tz, we, progress);
+}
+
+// ---- DataStream windows of a pane (WindowOperator over Tumbling/SlidingEventTimeWindows)
+// end of the latest window holding pane `pe` (SlidingEventTimeWindows.assignWindows :77-90:
+// lastStart = getWindowStartWithOffset(ts, offset, slide), windows down to start > ts - size)
+FW_HD int64_t ds_first_window_end(const WinDesc& w, int64_t pe) {
+    if (w.n_win == 1) return pe;
+    const int64_t ts0 = wsub(pe, w.interval);  // the pane's first millisecond
+    return wadd(window_start(ts0, w.offset, w.slide_div), w.size);
+}
+// WindowOperator.cleanupTime (:670-677) of the window ending at we: maxTimestamp + lateness,
+// Long.MAX_VALUE on overflow (then no cleanup timer is registered, registerCleanupTimer :616-628)
+FW_HD int64_t ds_cleanup_time(const WinDesc& w, int64_t we) {
+    const int64_t mt = wsub(we, 1);
+    const int64_t ct = wadd(mt, w.lateness);
+    return ct >= mt ? ct : INT64_MAX;
+}
 
 FW_HD int64_t slice_end_of(const WinDesc& w, int64_t ts) {
     return wadd(window_start(ts, w.offset, w.slice_div), w.interval);
@@ -249,6 +287,15 @@ struct IngestArgs {
     int32_t local;         // LOCAL phase: no late-record handling (LocalSlicingWindowAggOperator)
     int32_t global;        // GLOBAL phase: the ts column holds the slice end (SliceAssigners.sliced)
     int32_t ablate;        // development only (FW_ABLATE env): skip phases to time the others
+    // DataStream lateness: rows that fire an already fired window (late-fire rows) and rows sent
+    // to the late side output
+    uint64_t* lfire;       // [lfire_cap][3 + MAX_WORDS]: key, pane end, sb | ord << 32, words
+    int64_t lfire_cap;
+    int64_t* side;         // [side_cap][3 + nv]: key, ts, push_seq << 32 | row, value slots
+    int64_t side_cap;
+    int32_t side_output;   // late side output instead of numLateRecordsDropped
+    int32_t push_seq;      // fw_commit / fw_push_device call number (side-output rows)
+    int64_t row0;          // row offset of this launch within its call
 };
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
 constexpr int AB_NO_SORT = 2;    // skip rank/scan/cells; store partials at their row position
@@ -299,7 +346,11 @@ struct MergeArgs {
     int32_t reset_out;       // the results were consumed (fw_results_reset): emit from slab row 0
     int32_t ablate;          // development only (FW_ABLATE)
     unsigned long long* stamps;  // [N_STAMPS] phase cycles summed over workgroups (AB_STAMPS)
+    const uint64_t* lfire;   // DataStream late-fire rows (IngestArgs::lfire)
+    int64_t lfire_cap;
 };
+constexpr int LFW = 3 + MAX_WORDS;  // words per late-fire row
+constexpr int SOW = 3 + MAX_KCOLS;  // words per late side-output row
 
 struct CompactArgs {
     Ctrl* ctrl;

@@ -1,0 +1,942 @@
+// fw_merge_impl.h -- k_merge_fire (K4+K5) and its launchers, instantiated per accumulator word
+// count in k_merge_nw*.hip.
+#pragma once
+#include "fw_kernel_common.h"
+
+namespace fw {
+// ======================================================================================
+// K4+K5: merge pending partials into the HBM slice-state table, fire due timers
+// ======================================================================================
+template <int NW, int E>
+struct StateLds {
+    uint32_t idx[2 * E];   // open-addressing index: 0 empty, 1 claiming, 2+e entry e
+    int64_t key[E];
+    int64_t slice[E];
+    uint32_t flag[E];
+    uint64_t acc[NW][E];
+    uint16_t due[E];       // entries whose timer is due at this watermark (each fires once)
+    int32_t ndue;
+    int32_t n;             // entries in use
+    uint32_t overflow;
+};
+
+constexpr uint32_t IDX_DEAD = 0xFFFFFFFFu;
+
+template <int NW, int E>
+__device__ __forceinline__ void init_entry_acc(StateLds<NW, E>& S, int e, const WordDesc& wd) {
+#pragma unroll
+    for (int w = 0; w < NW; w++) S.acc[w][e] = w < wd.nw ? word_identity(wd.op[w]) : 0;
+}
+
+// LDS publication protocol of the index: the inserting lane writes the entry's fields, then
+// (after a compiler barrier) the index word with a relaxed store.  LDS executes one wave's
+// requests in issue order and a reader's field loads depend on the index value it read, so a
+// reader that sees 2+e sees the fields.  Acquire/release orderings are not used: at workgroup
+// scope they also order global memory, making every publish wait for earlier result stores.
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+template <int NW, int E>
+__device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
+    constexpr uint32_t MASK = 2 * E - 1;
+    uint32_t h = index_hash(k, s) & MASK;
+    for (int probes = 0; probes < 2 * E;) {
+        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_RELAXED, LDS_SCOPE);
+        if (st == 0) return -1;
+        if (st == 1) continue;  // being inserted by another lane: re-read
+        const uint32_t e = st - 2;
+        if (e < (uint32_t)E && S.key[e] == k && S.slice[e] == s) return (int)e;
+        h = (h + 1) & MASK;
+        probes++;
+    }
+    return -1;
+}
+
+// Finds (k, s) or inserts it.  A new entry starts from `v` folded into the identity (or the
+// identity when v is null) with flags `flag0`; *inserted tells the caller it must not fold v again.
+template <int NW, int E>
+__device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd,
+                              const uint64_t* v = nullptr, uint32_t flag0 = 0, bool* inserted = nullptr) {
+    constexpr uint32_t MASK = 2 * E - 1;
+    uint32_t h = index_hash(k, s) & MASK;
+    for (int probes = 0; probes < 2 * E;) {
+        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_RELAXED, LDS_SCOPE);
+        if (st == 1) continue;
+        if (st == 0) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 1u, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, LDS_SCOPE)) {
+                const int e = atomicAdd(&S.n, 1);
+                if (e >= E) {
+                    S.overflow = 1;
+                    __hip_atomic_store(&S.idx[h], IDX_DEAD, __ATOMIC_RELAXED, LDS_SCOPE);
+                    return -1;
+                }
+                S.key[e] = k;
+                S.slice[e] = s;
+                S.flag[e] = flag0;
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    S.acc[w][e] = w < wd.nw ? (v ? reg_fold(wd.op[w], word_identity(wd.op[w]), v[w])
+                                                 : word_identity(wd.op[w]))
+                                            : 0;
+                compiler_fence();
+                __hip_atomic_store(&S.idx[h], 2u + (uint32_t)e, __ATOMIC_RELAXED, LDS_SCOPE);
+                if (inserted) *inserted = true;
+                return e;
+            }
+            continue;  // lost the race: re-read this slot
+        }
+        const uint32_t e = st - 2;
+        if (e < (uint32_t)E && S.key[e] == k && S.slice[e] == s) return (int)e;
+        h = (h + 1) & MASK;
+        probes++;
+    }
+    S.overflow = 1;
+    return -1;
+}
+
+// First-probe lookups of M (key, slice) pairs with their LDS loads issued together (the lookups
+// of one lane are independent; issuing them back to back overlaps their latencies).  e[j] is the
+// entry, -1 when the home slot is empty, -2 when the first probe does not decide (collision or
+// an insertion in flight): the caller then takes the probing path.
+template <int NW, int E, int M>
+__device__ __forceinline__ void probe_batch(StateLds<NW, E>& S, const int64_t* k, const int64_t* s, int* e,
+                                            int m = M) {
+    // only the first m (<= M, uniform) lookups are needed; the others issue no LDS reads
+    constexpr uint32_t MASK = 2 * E - 1;
+    uint32_t st[M];
+#pragma unroll
+    for (int j = 0; j < M; j++)
+        st[j] = j < m ? __hip_atomic_load(&S.idx[index_hash(k[j], s[j]) & MASK], __ATOMIC_RELAXED, LDS_SCOPE) : 0u;
+    int64_t kk[M], ss[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+        kk[j] = 0;
+        ss[j] = 0;
+        if (j >= m) continue;
+        const uint32_t ei = min(st[j] - 2u, (uint32_t)(E - 1));
+        kk[j] = S.key[ei];
+        ss[j] = S.slice[ei];
+    }
+#pragma unroll
+    for (int j = 0; j < M; j++)
+        e[j] = st[j] == 0 ? -1
+               : (st[j] >= 2 && st[j] - 2 < (uint32_t)E && kk[j] == k[j] && ss[j] == s[j]) ? (int)(st[j] - 2)
+                                                                                          : -2;
+}
+
+// register an event-time timer on entry e; a timer that is already due at this watermark joins
+// the due list (an entry's timer fires at most once per advance: its timestamp is its slice end)
+template <int NW, int E>
+__device__ __forceinline__ void set_timer(StateLds<NW, E>& S, int e, int64_t W, const WinDesc& w) {
+    const uint32_t old = atomicOr(&S.flag[e], F_TIMER);
+    if (!(old & F_TIMER) && win_fired(w, S.slice[e], W)) {
+        const int q = atomicAdd(&S.ndue, 1);
+        if (q < E) S.due[q] = (uint16_t)e;
+    }
+}
+
+// Emission is atomic-free at device scope: each superbucket appends to its own output slab
+// (LDS cursor); only slab overflow falls back to a shared overflow region.  fw_results compacts
+// slabs + overflow into one contiguous result set on demand (k_compact_*).
+// output row position: the superbucket's slab, or the shared overflow region; -1 when full
+__device__ __forceinline__ int64_t claim_out_row(const MergeArgs& a, int sb, int32_t* s_emit) {
+    Ctrl* c = a.ctrl;
+    const int32_t pos = wave_claim(s_emit);
+    if (pos < a.slab_cap) return (int64_t)sb * a.slab_cap + pos;
+    // a launch that resets the results counts on the spare counter (kept 0), see Ctrl::out_count
+    const int sel = (__hip_atomic_load(&c->ovf_sel, __ATOMIC_RELAXED, DEV_SCOPE) ^ a.reset_out) & 1;
+    const uint64_t o = atomicAdd((unsigned long long*)&c->out_count[sel], 1ull);
+    if ((int64_t)o >= a.out_cap) {
+        __hip_atomic_fetch_or(&c->error, ERR_OUTPUT, __ATOMIC_RELAXED, DEV_SCOPE);
+        return -1;
+    }
+    return (int64_t)a.n_sb * a.slab_cap + (int64_t)o;
+}
+
+template <int NW, bool Q>
+__device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
+    if (a.ablate & AB_M_NO_EMIT) return;
+    const int64_t i = claim_out_row(a, sb, s_emit);
+    if (i < 0) return;
+    a.out_key[i] = key;
+    a.out_ws[i] = window_start_of(a.win, we);
+    a.out_we[i] = we;
+    uint32_t nm = 0;
+    for (int g = 0; g < a.ad.n; g++) {
+        const int32_t kind = a.ad.kind[g], type = a.ad.type[g];
+        const uint64_t w0 = acc[a.ad.w0[g]];
+        // SUM / MIN / MAX are NULL without a non-NULL input (SumAggFunction.java:66-69)
+        const bool no_rows = a.ad.nn[g] >= 0 && acc[a.ad.nn[g]] == 0;
+        uint64_t v = 0;
+        switch (kind) {
+            case FW_AGG_COUNT_STAR:
+            case FW_AGG_COUNT: v = w0; break;
+            case FW_AGG_SUM:
+                v = type == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)w0 : w0;
+                if (no_rows) nm |= 1u << g;
+                break;
+            case FW_AGG_MIN:
+            case FW_AGG_MAX:
+                if (Q && a.ad.qf[g] >= 0) {
+                    bool isnull;
+                    v = q_result(a.ad, g, acc, &isnull);
+                    if (isnull) nm |= 1u << g;
+                    break;
+                }
+                v = type == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
+                if (no_rows) nm |= 1u << g;
+                break;
+            case FW_AGG_AVG: {
+                const uint64_t cnt = acc[a.ad.w1[g]];
+                if (cnt == 0) { nm |= 1u << g; break; }
+                if (type == FW_T_F64) v = f64_bits(as_f64(w0) / (double)(int64_t)cnt);
+                else {
+                    int64_t q = (int64_t)w0 / (int64_t)cnt;
+                    if (type == FW_T_I32) q = (int32_t)q;
+                    v = (uint64_t)q;
+                }
+                break;
+            }
+        }
+        a.out_val[g][i] = ((nm >> g) & 1u) ? 0ull : v;  // a NULL's value word is 0
+    }
+    a.out_null[i] = nm;
+}
+
+// LOCAL phase output (LocalAggCombiner.combine :69-97 -> output(key, window, acc)): one row per
+// (key, sliceEnd) of the flush holding the local accumulator fields of every aggregate in order
+// (COUNT(*) / COUNT: count; SUM, MIN, MAX: value, NULL-able; AVG: sum, count), window_end =
+// window_start = sliceEnd.  The GLOBAL phase ingests exactly these columns.
+template <int NW, bool Q>
+__device__ void emit_partial(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t se, const uint64_t* acc) {
+    const int64_t i = claim_out_row(a, sb, s_emit);
+    if (i < 0) return;
+    a.out_key[i] = key;
+    a.out_ws[i] = se;
+    a.out_we[i] = se;
+    uint32_t nm = 0;
+    int j = 0;
+    for (int g = 0; g < a.ad.n; g++) {
+        const int32_t kind = a.ad.kind[g], type = a.ad.type[g];
+        const uint64_t w0 = acc[a.ad.w0[g]];
+        const bool no_rows = a.ad.nn[g] >= 0 && acc[a.ad.nn[g]] == 0;
+        uint64_t v = w0;
+        bool isnull = false;
+        switch (kind) {
+            case FW_AGG_SUM:
+                v = type == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)w0 : w0;
+                isnull = no_rows;
+                break;
+            case FW_AGG_MIN:
+            case FW_AGG_MAX:
+                if (Q && a.ad.qf[g] >= 0) {
+                    v = q_result(a.ad, g, acc, &isnull);
+                    break;
+                }
+                v = type == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
+                isnull = no_rows;
+                break;
+            case FW_AGG_AVG:  // (sum, count); the sum of AVG(INT) is a BIGINT (IntAvgAggFunction)
+                a.out_val[j][i] = w0;
+                j++;
+                v = acc[a.ad.w1[g]];
+                break;
+            default: break;  // counts
+        }
+        if (isnull) nm |= 1u << j;
+        a.out_val[j][i] = isnull ? 0ull : v;
+        j++;
+    }
+    a.out_null[i] = nm;
+}
+
+// flags that live only inside one k_merge_fire launch (dropped at write-back)
+constexpr uint32_t F_FIRED = 4u;    // HOP: window (key, this slice end) fired in this advance (chain claim)
+constexpr uint32_t F_NOTHEAD = 8u;  // CUMULATE: an earlier due step of the same window chains to this one
+constexpr uint32_t F_EXPIRE = 16u;  // HOP: slice expired by a window fired in this advance (cleared at write-back)
+
+template <int NW>
+__device__ __forceinline__ void acc_identity(const WordDesc& wd, uint64_t* acc) {
+#pragma unroll
+    for (int i = 0; i < NW; i++) acc[i] = i < wd.nw ? word_identity(wd.op[i]) : 0;
+}
+
+// acc = merge(acc, state of entry e) when the entry holds an accumulator (windowState.value != null)
+template <int NW, int E, bool Q>
+__device__ __forceinline__ void merge_entry(const MergeArgs& a, StateLds<NW, E>& S, int e, uint64_t* acc) {
+    if (e < 0 || !(S.flag[e] & F_ACC)) return;
+    uint64_t o[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) o[i] = S.acc[i][e];
+    merge_slice<NW, Q>(a.wd, a.ad, acc, o);
+}
+
+// TUMBLE: SliceUnsharedSyncStateWindowAggProcessor.fireWindow (:54-66) + clearWindow
+// (expiredSlices(we) = [we]); DataStream tumbling: WindowOperator.onEventTime + clearAllState.
+// Windows of different keys and of one key are independent: every due entry fires once.
+template <int NW, int E, bool Q>
+__device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+    uint64_t acc[NW];
+    const uint32_t f = atomicAnd(&S.flag[e], ~(F_TIMER | F_ACC));
+    if (f & F_ACC) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
+    } else {
+        acc_identity<NW>(a.wd, acc);
+    }
+    if (a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0) emit_row<NW, Q>(a, sb, s_emit, S.key[e], S.slice[e], acc);
+    return 1;
+}
+
+// HOP: the timer chain of one key starting at due entry e, fired without timestamp rounds.
+// SliceSharedSyncStateWindowAggProcessor.fireWindow (:65-86): merge the n slices ending at we
+// newest first into a fresh accumulator, emit unless empty (hidden COUNT(*)), and while the window
+// is non-empty register we + slice (nextTriggerWindow); a registered timer that is already due
+// fires in this same advance (InternalTimerServiceImpl.tryAdvanceWatermark :328-348), so the
+// chain continues.  clearWindow expires windowStart + slice: that slice also belongs to the
+// earlier windows of the key that are due in this advance, so the expiry is deferred to the
+// write-back (F_EXPIRE), after every window of the advance has read its slices.  With that, the
+// chains of one key may run concurrently in any order; the F_FIRED claim makes every window fire
+// exactly once.
+template <int NW, int E, bool Q>
+__device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+    const WinDesc& w = a.win;
+    const WordDesc& wd = a.wd;
+    constexpr int HB = NW <= 2 ? 8 : NW <= 4 ? 4 : 2;
+    const int64_t k = S.key[e];
+    int64_t we = S.slice[e];
+    int ew = e;
+    uint32_t nf = 0;
+    for (;;) {
+        const uint32_t old = atomicOr(&S.flag[ew], F_FIRED);
+        if (old & F_FIRED) break;  // fired by another chain of this key
+        atomicAnd(&S.flag[ew], ~F_TIMER);
+        nf++;
+        uint64_t acc[NW];
+        acc_identity<NW>(wd, acc);
+        const int n = w.n_slices;
+        const int64_t s_exp = wadd(wsub(we, w.size), w.interval);  // clearWindow's expired slice
+        int e_exp = -3;
+        int64_t s = we;
+        for (int j0 = 0; j0 < n; j0 += HB) {
+            int64_t kk[HB], ss[HB];
+            int eb[HB];
+#pragma unroll
+            for (int j = 0; j < HB; j++) {
+                kk[j] = k;
+                ss[j] = s;
+                s = wsub(s, w.interval);  // wrapping, like the reference's long arithmetic
+            }
+            probe_batch<NW, E, HB>(S, kk, ss, eb, min(HB, n - j0));
+#pragma unroll
+            for (int j = 0; j < HB; j++) {
+                if (j0 + j >= n) break;
+                int e2 = eb[j];
+                if (e2 == -2) e2 = find_entry(S, k, ss[j]);
+                merge_entry<NW, E, Q>(a, S, e2, acc);
+                if (ss[j] == s_exp) e_exp = e2;
+            }
+        }
+        const bool nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
+        if (nonempty) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
+        const int e2 = e_exp != -3 ? e_exp : find_entry(S, k, s_exp);
+        if (e2 >= 0) atomicOr(&S.flag[e2], F_EXPIRE);
+        if (!nonempty) break;
+        const int64_t nx = wadd(we, w.interval);
+        const int en = find_or_insert(S, k, nx, wd);
+        if (en < 0) break;  // state overflow (flagged)
+        if (!win_fired(w, nx, a.wm)) {
+            atomicOr(&S.flag[en], F_TIMER);
+            break;
+        }
+        we = nx;
+        ew = en;
+    }
+    return nf;
+}
+
+// CUMULATE: the steps of one cumulative window of one key, from its earliest due step, in order:
+// mergeSlices merges step we's slice into the first-slice state (CumulativeSliceAssigner
+// .mergeSlices, SliceSharedSyncStateWindowAggProcessor.merge :89-118), the window is emitted
+// unless empty, the next step is registered up to the window's last step (nextTriggerWindow), and
+// clearWindow expires we (and the first slice at the last step).  The merged accumulator stays in
+// registers across the chain and is written back to the first slice once.
+template <int NW, int E, bool Q>
+__device__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+    const WinDesc& w = a.win;
+    const WordDesc& wd = a.wd;
+    const int64_t k = S.key[e];
+    int64_t we = S.slice[e];
+    const int64_t ws = window_start_of(w, we);
+    const int64_t first = wadd(ws, w.interval);
+    const int64_t last = wadd(ws, w.size);
+    const int ef = find_or_insert(S, k, first, wd);
+    uint64_t acc[NW];
+    if (ef >= 0 && (S.flag[ef] & F_ACC)) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) acc[i] = S.acc[i][ef];
+    } else {
+        acc_identity<NW>(wd, acc);
+    }
+    uint32_t nf = 0;
+    bool done = false;
+    int ewe = e;
+    for (;;) {
+        if (ewe >= 0) atomicAnd(&S.flag[ewe], ~F_TIMER);
+        if (we != first) merge_entry<NW, E, Q>(a, S, ewe, acc);
+        nf++;
+        if (a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
+        if (we != first && ewe >= 0) atomicAnd(&S.flag[ewe], ~F_ACC);
+        if (we == last) {  // expiredSlices(last) = [last, first]
+            if (ef >= 0) atomicAnd(&S.flag[ef], ~F_ACC);
+            done = true;
+            break;
+        }
+        const int64_t nx = wadd(we, w.interval);
+        if (!win_fired(w, nx, a.wm)) {
+            const int en = find_or_insert(S, k, nx, wd);
+            if (en >= 0) atomicOr(&S.flag[en], F_TIMER);
+            break;
+        }
+        we = nx;
+        ewe = we == first ? ef : find_entry(S, k, we);
+    }
+    if (!done && ef >= 0) {  // windowState.update(firstSlice, acc)
+#pragma unroll
+        for (int i = 0; i < NW; i++) S.acc[i][ef] = acc[i];
+        atomicOr(&S.flag[ef], F_ACC);
+    }
+    return nf;
+}
+
+// CUMULATE pre-pass: a due step whose window has an earlier due step is reached by that step's
+// chain (CUMULATE chains never stop before the window's last step), so it starts no chain of its
+// own.  Each due step marks the next due step of its window.
+template <int NW, int E>
+__device__ __forceinline__ void mark_cumulate_successor(const MergeArgs& a, StateLds<NW, E>& S, int e) {
+    const WinDesc& w = a.win;
+    const int64_t k = S.key[e];
+    const int64_t we = S.slice[e];
+    const int64_t last = wadd(window_start_of(w, we), w.size);
+    for (int64_t s = we; s != last;) {
+        s = wadd(s, w.interval);
+        if (!win_fired(w, s, a.wm)) break;
+        const int e2 = find_entry(S, k, s);
+        if (e2 >= 0 && (S.flag[e2] & F_TIMER)) {
+            atomicOr(&S.flag[e2], F_NOTHEAD);
+            break;
+        }
+    }
+}
+
+// ---- DataStream windows (KIND_DSWIN): one entry per (key, window end), as WindowOperator keeps
+// one state per (key, window).  A pane partial (key, pane end) is added to every window of the
+// pane that is not late (HeapReducingState.add per window, WindowOperator.java:405-433); a window
+// gets its maxTimestamp timer (EventTimeTrigger.onElement) and its cleanup timer
+// (registerCleanupTimer).  Windows the watermark already fired are not reached here: their rows
+// took the late-fire path.
+template <int NW, int E>
+__device__ void ds_add_to_windows(const MergeArgs& a, StateLds<NW, E>& S, int64_t k, int64_t pe, const uint64_t* v,
+                                  int64_t w_old, bool late_rows) {
+    const WinDesc& w = a.win;
+    const int64_t e0 = ds_first_window_end(w, pe);
+    for (int i = 0; i < w.n_win; i++) {
+        const int64_t e = wsub(e0, (int64_t)i * w.slide);
+        const int64_t ct = ds_cleanup_time(w, e);
+        if (ct <= w_old) continue;  // isWindowLate
+        const bool fired_already = is_fired(e, w_old);
+        if (fired_already && !late_rows) continue;
+        const uint32_t fl = F_ACC | (ct != INT64_MAX ? F_CLEAN : 0u) | (fired_already ? 0u : F_TIMER);
+        bool ins = false;
+        const int en = find_or_insert(S, k, e, a.wd, v, fl, &ins);
+        if (en < 0 || ins) continue;
+#pragma unroll
+        for (int q = 0; q < NW; q++)
+            if (q < a.wd.nw) lds_fold(a.wd.op[q], &S.acc[q][en], v[q]);
+        atomicOr(&S.flag[en], fl);
+    }
+}
+
+// is window `e` one of pane `pe`'s windows
+__device__ __forceinline__ bool ds_pane_in_window(const WinDesc& w, int64_t pe, int64_t e) {
+    const int64_t e0 = ds_first_window_end(w, pe);
+    const uint64_t d = (uint64_t)wsub(e0, e);
+    if ((int64_t)d < 0) return false;
+    const uint64_t q = udiv(d, w.slide_div);
+    return q * (uint64_t)w.slide == d && q < (uint64_t)w.n_win;
+}
+
+// DataStream timers of one entry at watermark W (WindowOperator.onEventTime :450-494): the
+// maxTimestamp timer FIREs (emitWindowContents), the cleanup timer clears the window state; with
+// allowedLateness 0 they are the same timer (fire, then clear)
+template <int NW, int E>
+__device__ __forceinline__ uint32_t fire_ds(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+    const int64_t we = S.slice[e];
+    const uint32_t f = S.flag[e];
+    const bool fire = (f & F_TIMER) && is_fired(we, a.wm);
+    const bool clean = (f & F_CLEAN) && ds_cleanup_time(a.win, we) <= a.wm;
+    if (fire && (f & F_ACC)) {
+        uint64_t acc[NW];
+#pragma unroll
+        for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
+        emit_row<NW, false>(a, sb, s_emit, S.key[e], we, acc);
+    }
+    S.flag[e] = f & ~((fire ? F_TIMER : 0u) | (clean ? (F_ACC | F_TIMER | F_CLEAN) : 0u));
+    return fire ? 1u : 0u;
+}
+
+// diagnostic phase stamps (FW_ABLATE & AB_STAMPS): lane 0 sums cycles per phase
+struct Stamps {
+    bool on;
+    uint64_t t;
+    uint64_t acc[N_STAMPS];
+    __device__ void init(bool enable) {
+        on = enable;
+        for (int i = 0; i < N_STAMPS; i++) acc[i] = 0;
+        if (on) t = __builtin_amdgcn_s_memtime();
+    }
+    __device__ void mark(int phase) {  // call right after a __syncthreads()
+        if (!on) return;
+        const uint64_t n = __builtin_amdgcn_s_memtime();
+        acc[phase] += n - t;
+        t = n;
+    }
+    __device__ void flush(unsigned long long* dst) {
+        if (!on || threadIdx.x != 0 || !dst) return;
+        for (int i = 0; i < N_STAMPS; i++)
+            if (acc[i]) atomicAdd(&dst[i], (unsigned long long)acc[i]);
+    }
+};
+
+// XCD-aware superbucket order: blocks b, b+8, b+16, ... are dealt to one XCD (round robin,
+// speed only), so they get consecutive superbuckets, whose cells sit next to each other in
+// every chunk region -> the boundary lines two cells share are read from the same L2.
+__device__ __forceinline__ int sb_of_block(int b, int n_sb) {
+    if (n_sb % 8 != 0) return b;
+    return (b % 8) * (n_sb / 8) + b / 8;
+}
+
+// the last workgroup of a k_merge_fire launch applies the launch's control decisions (every
+// workgroup read the old values at its start): advanceProgress bookkeeping of the processor
+// (AbstractSliceSyncStateWindowAggProcessor.java:139-153), the buffer reset after a flush, the
+// consumed timer requests, and the overflow-counter switch of a result reset.
+__device__ void merge_finalize(const MergeArgs& a) {
+    Ctrl* c = a.ctrl;
+    const int64_t W = a.wm;
+    const int64_t cur = c->cur, pend = c->pending_pushes, ntp = c->ntp;
+    const bool adv = !a.force_flush && W > cur;
+    const bool do_flush = pend > 0 && (a.force_flush || (adv && (a.always_flush || (W >= ntp && win_fired(a.win, c->min_pending, W)))));
+    if (adv) {
+        c->cur = W;
+        if (W >= ntp) c->ntp = tz_next_trigger_watermark(a.win.tz, W, a.win.slice_div);
+    }
+    if (do_flush) {
+        c->pending_pushes = 0;
+        c->min_pending = INT64_MAX;
+        c->pending_rows = 0;
+        c->n_lfire = 0;
+    }
+    c->n_treq = 0;
+    const int sel = (c->ovf_sel ^ a.reset_out) & 1;
+    c->ovf_sel = sel;
+    __hip_atomic_store(&c->out_count[sel ^ 1], 0ull, __ATOMIC_RELAXED, DEV_SCOPE);
+}
+
+__device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
+    if (threadIdx.x != 0) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (grid_last_wg(a.tickets->c[1])) merge_finalize(a);
+}
+
+// rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
+constexpr int mg_rows_in_flight(int nw) { return nw <= 1 ? 4 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1; }
+
+template <int NW, int E, bool Q, int KIND>
+__global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
+    constexpr int PW = 2 + NW;
+    constexpr int PWE = 3 + NW;
+    const int64_t CH = a.chunk_rows;  // chunk rows of the ingest kernel that wrote the cells
+    constexpr int GU = mg_rows_in_flight(NW);
+    __shared__ StateLds<NW, E> S;
+    __shared__ int32_t s_work;
+    __shared__ int32_t s_nlive;
+    __shared__ int64_t s_newmin;
+    __shared__ uint32_t s_fired;
+    __shared__ int32_t s_emit;
+
+    const int tid = threadIdx.x;
+    const int sb = sb_of_block(blockIdx.x, a.n_sb);
+    Ctrl* c = a.ctrl;
+    const int64_t W = a.wm;
+    // control decisions; the launch's last workgroup applies them to the control block (merge_finalize)
+    const int64_t cur = __hip_atomic_load(&c->cur, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t pend = __hip_atomic_load(&c->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t ntreq = min(__hip_atomic_load(&c->n_treq, __ATOMIC_RELAXED, DEV_SCOPE), (int64_t)0x7fffffff);
+    const int64_t nlf = KIND == KIND_DSWIN ? min(__hip_atomic_load(&c->n_lfire, __ATOMIC_RELAXED, DEV_SCOPE), a.lfire_cap) : 0;
+    const int64_t ntp = __hip_atomic_load(&c->ntp, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t minp = __hip_atomic_load(&c->min_pending, __ATOMIC_RELAXED, DEV_SCOPE);
+    const bool adv = !a.force_flush && W > cur;
+    const bool do_flush = pend > 0 &&
+                          (a.force_flush || (adv && (a.always_flush || (W >= ntp && win_fired(a.win, minp, W)))));
+    const bool do_fire = adv;
+    const int64_t w_old = cur;
+    const int32_t n0 = a.state_count[sb];
+
+    Stamps stm;
+    stm.init((a.ablate & AB_STAMPS) != 0);
+    if (tid == 0) {
+        s_work = (ntreq > 0) || do_flush || (do_fire && win_fired(a.win, a.sb_min_timer[sb], W));
+        s_fired = 0;
+        s_emit = a.reset_out ? 0 : a.sb_out[sb];
+        if (!s_work && a.reset_out) a.sb_out[sb] = 0;
+    }
+    __syncthreads();
+    if (!s_work) {
+        merge_ticket(a);
+        return;
+    }
+    const bool gather = do_flush && !(a.ablate & AB_M_NO_GATHER);
+    // this thread's first cell word, loaded while the state loads (the gather below walks the
+    // cells of every pending push, one cell per thread per pass, in flat tile order f:
+    // cell_chunk(f) is the chunk, positions past the push's last chunk are padding)
+    auto cell_at = [&](int64_t pi, int f) -> uint32_t {
+        if (cell_chunk(f) >= a.slot_nch[pi]) return 0u;
+        const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
+        return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
+    };
+    // the gather splits a push's cells into groups of gather_group(ncell) <= 64 consecutive
+    // cells, one group per wave per pass (16 groups when a push has <= 1024 cells)
+    const int lane = tid & 63, wv = tid >> 6;
+    auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
+    uint32_t v_first = 0;
+    if (gather && lane < gather_group((int)cell_pad(a.slot_nch[0])))
+        v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
+    // ---- load this superbucket's entries into LDS
+    for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
+    if (tid == 0) {
+        S.n = (a.ablate & AB_M_NO_LOAD) ? 0 : n0;
+        S.overflow = 0;
+        S.ndue = 0;
+    }
+    __syncthreads();
+    const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
+    if (!(a.ablate & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
+        const uint64_t* p = st + (size_t)e * PWE;
+        const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
+        S.key[e] = k;
+        S.slice[e] = s;
+        S.flag[e] = (uint32_t)p[2];
+#pragma unroll
+        for (int w = 0; w < NW; w++) S.acc[w][e] = p[3 + w];
+        uint32_t h = index_hash(k, s) & (2 * E - 1);
+        for (;;) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 2u + (uint32_t)e, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, LDS_SCOPE))
+                break;
+            h = (h + 1) & (2 * E - 1);
+        }
+    }
+    __syncthreads();
+    stm.mark(0);
+    // ---- timers registered by late records in processElement
+    for (int64_t r = tid; r < ntreq; r += MG_BLOCK) {
+        if (a.treq[3 * r + 2] != sb) continue;
+        const int e = find_or_insert(S, a.treq[3 * r], a.treq[3 * r + 1], a.wd);
+        if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
+    }
+    // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket.
+    // A wave takes a group of cells (the rows ingest chunks wrote for this superbucket), scans
+    // their row counts and deals the rows of the whole group over its 64 lanes, GU rows per lane
+    // per pass: every lane is busy whatever the cells' sizes, and neighbouring lanes load
+    // neighbouring rows.  Rows are looked up in the LDS table (first probes batched), hits
+    // folded; the misses of a lane are then inserted one at a time.
+    // diagnostic (AB_GSTAMPS): thread 0's cycles in row loads / first probes / fold + insert
+    const bool gst = (a.ablate & AB_GSTAMPS) && stm.on && tid == 0;
+    if (gather) {
+        for (int64_t pi = 0; pi < pend; pi++) {
+            const int ncell = (int)cell_pad(a.slot_nch[pi]);
+            const int G = gather_group(ncell);
+            const int ngroups = ncell / G;
+            const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
+            for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
+                const int f = g * G + lane;
+                const uint32_t v = lane >= G ? 0u : (pi == 0 && g == wv) ? v_first : cell_at(pi, f);
+                const uint32_t cnt = v >> 16;
+                uint32_t inc = cnt;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+                    if (lane >= d) inc += t;
+                }
+                const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+                const uint32_t excl = inc - cnt;
+                // segment row of this cell's first row, less the rows of the group before it
+                const uint32_t adj = (uint32_t)(cell_chunk(f) * CH + (v & 0xFFFFu)) - excl;
+                for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
+                    uint64_t row[GU][PW];
+                    uint64_t g0 = gst ? __builtin_amdgcn_s_memtime() : 0;
+#pragma unroll
+                    for (int u = 0; u < GU; u++) {
+                        // the group's row x lives in the last cell whose first row is <= x
+                        const uint32_t x = min(r0 + (uint32_t)(u * 64 + lane), tot - 1);
+                        int lo = 0;
+#pragma unroll
+                        for (int step = 32; step > 0; step >>= 1)
+                            if ((uint32_t)__shfl((int)excl, lo + step, 64) <= x) lo += step;
+                        const uint64_t* p = seg + (size_t)((uint32_t)__shfl((int)adj, lo, 64) + x) * PW;
+#pragma unroll
+                        for (int w = 0; w < PW; w++) row[u][w] = p[w];
+                    }
+                    if (gst) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                        stm.acc[2] += g1 - g0;
+                        g0 = g1;
+                    }
+                    if (a.ablate & AB_M_NO_HASH) {  // diagnostic: loads only
+                        uint64_t x = 0;
+#pragma unroll
+                        for (int u = 0; u < GU; u++) x ^= row[u][0] ^ row[u][1] ^ row[u][PW - 1];
+                        asm volatile("" ::"v"(x));  // keeps the loads
+                        continue;
+                    }
+                    if constexpr (KIND == KIND_DSWIN) {
+                        static_for<GU>([&](auto UU) {
+                            constexpr int u = decltype(UU)::value;
+                            if (r0 + (uint32_t)(u * 64 + lane) < tot)
+                                ds_add_to_windows<NW, E>(a, S, (int64_t)row[u][0], (int64_t)row[u][1], &row[u][2], w_old, false);
+                        });
+                        continue;
+                    }
+                    int ge[GU];
+                    {
+                        int64_t gk[GU], gs[GU];
+#pragma unroll
+                        for (int u = 0; u < GU; u++) {
+                            gk[u] = (int64_t)row[u][0];
+                            gs[u] = (int64_t)row[u][1];
+                        }
+                        probe_batch<NW, E, GU>(S, gk, gs, ge);
+                    }
+                    if (gst) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                        stm.acc[4] += g1 - g0;
+                        g0 = g1;
+                    }
+                    // register the window timer unless already fired (AggCombiner.java:103-110);
+                    // the LOCAL phase keeps no timers (LocalAggCombiner.java:69-97)
+                    auto flags_of = [&](int64_t sl) -> uint32_t {
+                        return (a.local || win_fired(a.win, sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
+                    };
+                    uint32_t miss = 0;
+                    static_for<GU>([&](auto UU) {
+                        constexpr int u = decltype(UU)::value;
+                        if (r0 + (uint32_t)(u * 64 + lane) >= tot) return;
+                        const int e = ge[u];  // -1 / -2: not found by the batched first probe
+                        if (e < 0) {
+                            miss |= 1u << u;
+                            return;
+                        }
+                        if (a.ablate & AB_M_NO_FOLDOP) return;
+#pragma unroll
+                        for (int w = 0; w < NW; w++)
+                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
+                        atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
+                    });
+                    while (miss) {  // the wave loops max(popcount) times, not GU times
+                        const int um = __ffs(miss) - 1;
+                        miss &= miss - 1;
+                        uint64_t r[PW];
+                        static_for<GU>([&](auto UU) {
+                            constexpr int u = decltype(UU)::value;
+                            if (u == um) {
+#pragma unroll
+                                for (int w = 0; w < PW; w++) r[w] = row[u][w];
+                            }
+                        });
+                        const int64_t k = (int64_t)r[0], sl = (int64_t)r[1];
+                        const uint32_t fl = flags_of(sl);
+                        bool ins = false;
+                        const int e = find_or_insert(S, k, sl, a.wd, &r[2], fl, &ins);
+                        if (e < 0 || ins || (a.ablate & AB_M_NO_FOLDOP)) continue;
+#pragma unroll
+                        for (int w = 0; w < NW; w++)
+                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], r[2 + w]);
+                        atomicOr(&S.flag[e], fl);
+                    }
+                    if (gst) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        stm.acc[7] += __builtin_amdgcn_s_memtime() - g0;
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    stm.mark(1);
+    // ---- DataStream late-fire rows: an element for a fired window that is not cleaned yet fires
+    // that window at once with the element added (EventTimeTrigger.onElement -> FIRE,
+    // WindowOperator.java:418-426).  Every such element emits the window's contents as of its own
+    // arrival: the state before this flush plus the late elements of the same (key, window) up to
+    // it (arrival ordinals).  Pass 1 emits from the unchanged state, pass 2 adds the elements to
+    // all their live windows.  Quadratic in the late rows of a superbucket (bounded by lfire_cap).
+    if (KIND == KIND_DSWIN && gather && nlf > 0) {
+        const WinDesc& w = a.win;
+        for (int64_t r = tid; r < nlf; r += MG_BLOCK) {
+            const uint64_t* p = a.lfire + (size_t)r * LFW;
+            if ((uint32_t)p[2] != (uint32_t)sb) continue;
+            const int64_t k = (int64_t)p[0], pe = (int64_t)p[1];
+            const uint32_t ord = (uint32_t)(p[2] >> 32);
+            const int64_t e0 = ds_first_window_end(w, pe);
+            for (int i = 0; i < w.n_win; i++) {
+                const int64_t e = wsub(e0, (int64_t)i * w.slide);
+                if (ds_cleanup_time(w, e) <= w_old || !is_fired(e, w_old)) continue;
+                uint64_t acc[NW];
+                const int es = find_entry(S, k, e);
+                if (es >= 0 && (S.flag[es] & F_ACC)) {
+#pragma unroll
+                    for (int q = 0; q < NW; q++) acc[q] = S.acc[q][es];
+                } else {
+                    acc_identity<NW>(a.wd, acc);
+                }
+                for (int64_t q2 = 0; q2 < nlf; q2++) {
+                    const uint64_t* o = a.lfire + (size_t)q2 * LFW;
+                    if ((uint32_t)o[2] != (uint32_t)sb || (int64_t)o[0] != k || (uint32_t)(o[2] >> 32) > ord) continue;
+                    if (!ds_pane_in_window(w, (int64_t)o[1], e)) continue;
+#pragma unroll
+                    for (int q = 0; q < NW; q++)
+                        if (q < a.wd.nw) acc[q] = reg_fold(a.wd.op[q], acc[q], o[3 + q]);
+                }
+                emit_row<NW, false>(a, sb, &s_emit, k, e, acc);
+            }
+        }
+        __syncthreads();
+        for (int64_t r = tid; r < nlf; r += MG_BLOCK) {
+            const uint64_t* p = a.lfire + (size_t)r * LFW;
+            if ((uint32_t)p[2] != (uint32_t)sb) continue;
+            uint64_t v[NW];
+#pragma unroll
+            for (int q = 0; q < NW; q++) v[q] = p[3 + q];
+            ds_add_to_windows<NW, E>(a, S, (int64_t)p[0], (int64_t)p[1], v, w_old, true);
+        }
+        __syncthreads();
+    }
+    // ---- fire: InternalTimerServiceImpl.tryAdvanceWatermark (:328-348) -> WindowAggOperator
+    // .onTimer -> fireWindow + clearWindow.  One pass over the entries whose timer is due; HOP and
+    // CUMULATE follow their timer chains per key (no timestamp rounds, see fire_*_chain).
+    if (do_fire && !(a.ablate & AB_M_NO_FIRE)) {
+        const int n = min(S.n, E);
+        for (int e = tid; e < n; e += MG_BLOCK)
+            if (KIND == KIND_DSWIN ? (((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W)) ||
+                                      ((S.flag[e] & F_CLEAN) && ds_cleanup_time(a.win, S.slice[e]) <= W))
+                                   : ((S.flag[e] & F_TIMER) && win_fired(a.win, S.slice[e], W))) {
+                const int q = wave_claim(&S.ndue);
+                if (q < E) S.due[q] = (uint16_t)e;
+            }
+        __syncthreads();
+        const int nd = min(S.ndue, E);
+        if (KIND == FW_WIN_CUMULATE) {
+            for (int q = tid; q < nd; q += MG_BLOCK) mark_cumulate_successor<NW, E>(a, S, S.due[q]);
+            __syncthreads();
+        }
+        stm.mark(6);
+        uint32_t nf = 0;
+        for (int q = tid; q < nd; q += MG_BLOCK) {
+            const int e = S.due[q];
+            if (KIND == KIND_DSWIN) {
+                nf += fire_ds<NW, E>(a, S, e, sb, &s_emit);
+            } else if (KIND == FW_WIN_TUMBLE) {
+                nf += fire_tumble<NW, E, Q>(a, S, e, sb, &s_emit);
+            } else if (KIND == FW_WIN_HOP) {
+                nf += fire_hop_chain<NW, E, Q>(a, S, e, sb, &s_emit);
+            } else {
+                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_cumulate_chain<NW, E, Q>(a, S, e, sb, &s_emit);
+            }
+        }
+        nf = wave_sum_u32(nf);
+        if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
+        if (S.ndue > E && tid == 0) S.overflow = 1;
+    }
+    // ---- write back live entries (LOCAL phase: emit every partial instead, keep no state)
+    if (tid == 0) {
+        s_nlive = 0;
+        s_newmin = INT64_MAX;
+    }
+    __syncthreads();
+    stm.mark(5);
+    const int n = min(S.n, E);
+    uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
+    int64_t lnm = INT64_MAX;
+    if (a.local) {
+        if (gather)
+            for (int e = tid; e < n; e += MG_BLOCK) {
+                uint64_t v[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
+                emit_partial<NW, Q>(a, sb, &s_emit, S.key[e], S.slice[e], v);
+            }
+    } else if (!(a.ablate & AB_M_NO_WB)) {
+        for (int e = tid; e < n; e += MG_BLOCK) {
+            const uint32_t f0 = S.flag[e];
+            const uint32_t f = f0 & ((f0 & F_EXPIRE) ? F_TIMER : (F_ACC | F_TIMER | F_CLEAN));
+            if (!f) continue;
+            const int pos = wave_claim(&s_nlive);
+            uint64_t* p = so + (size_t)pos * PWE;
+            p[0] = (uint64_t)S.key[e];
+            p[1] = (uint64_t)S.slice[e];
+            p[2] = f;
+            if (Q) {
+                uint64_t v[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
+#pragma unroll
+                for (int w = 0; w < NW; w++) p[3 + w] = w < a.wd.nw ? q_normalise(a.wd, w, v) : v[w];
+            } else {
+#pragma unroll
+                for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];
+            }
+            if (f & F_TIMER) lnm = min(lnm, S.slice[e]);
+            if (KIND == KIND_DSWIN && (f & F_CLEAN)) lnm = min(lnm, wadd(ds_cleanup_time(a.win, S.slice[e]), 1));
+        }
+    }
+    lnm = wave_min_i64(lnm);
+    if ((tid & 63) == 0 && lnm != INT64_MAX) __hip_atomic_fetch_min(&s_newmin, lnm, __ATOMIC_RELAXED, LDS_SCOPE);
+    __syncthreads();
+    if (tid == 0) {
+        a.state_count[sb] = a.local ? 0 : s_nlive;
+        a.sb_min_timer[sb] = s_newmin;
+        a.sb_out[sb] = min(s_emit, a.slab_cap);
+        if (s_fired) a.sb_fired[sb] += s_fired;
+        if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
+    }
+    __syncthreads();
+    stm.mark(3);
+    stm.flush(a.stamps);
+    merge_ticket(a);
+}
+
+template <int NW, bool Q>
+static hipError_t merge_q(const MergeArgs& a, hipStream_t s) {
+    constexpr int E = mg_entries(NW);
+    if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
+        if (Q) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
+        return hipGetLastError();
+    }
+    switch (a.win.kind) {
+        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_TUMBLE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_HOP>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_CUMULATE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+template <int NW>
+hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
+    return a.wd.has_q ? merge_q<NW, true>(a, s) : merge_q<NW, false>(a, s);
+}
+
+}  // namespace fw

@@ -1,0 +1,6 @@
+// k_ingest_nv8.hip -- k_ingest instantiations for 8 loaded value column slot(s)
+#include "fw_ingest_impl.h"
+
+namespace fw {
+template hipError_t ingest_nv<8>(const IngestArgs& a, hipStream_t s, KTimer* t);
+}  // namespace fw

@@ -3,14 +3,18 @@
 WindowOperatorBuilder.buildWindowOperator (flink-runtime/.../windowing/WindowOperatorBuilder.java:432-446)
 would return this operator iff: the assigner is TumblingEventTimeWindows or
 SlidingEventTimeWindows (size % slide == 0), the trigger is EventTimeTrigger, there is no
-evictor, allowedLateness is 0, there is no late-data side output, and the function is a built-in
-field aggregation (SumAggregator / ComparableAggregator for min/max, WindowedStream.java:660-880)
-on a numeric field.  Anything else stays on the reference WindowOperator.
+evictor, and the function is a built-in field aggregation (SumAggregator / ComparableAggregator
+for min/max, WindowedStream.java:660-880) on a numeric field.  Any allowedLateness and a
+late-data side output (sideOutputLateData) are supported.  Anything else stays on the reference
+WindowOperator.
 
-Semantics (WindowOperator.java:293-494): per element, every non-late window gets the value and a
-timer at window.maxTimestamp(); a watermark fires (key, window) timers in timestamp order and emits
-(key, aggregate) with record timestamp window.maxTimestamp(), then clears the window.  Elements
-whose windows are all late are counted in numLateRecordsDropped.
+Semantics (WindowOperator.java:293-682): per element, every window that is not late (cleanupTime =
+maxTimestamp + allowedLateness > watermark) gets the value; a window the watermark has not
+reached gets a timer at window.maxTimestamp(), one it has already passed fires again at once with
+the element added (EventTimeTrigger.onElement).  A watermark fires (key, window) timers and emits
+(key, aggregate) with record timestamp window.maxTimestamp(); the window state is cleared at its
+cleanup time.  Elements late for all their windows go to the late side output when one is set,
+else they are counted in numLateRecordsDropped.
 """
 import numpy as np
 
@@ -31,8 +35,10 @@ def is_gpu_eligible(assigner, trigger, aggregation, *, evictor=None, allowed_lat
         return False, "sliding windows need size % slide == 0 to share slices"
     if not isinstance(trigger, EventTimeTrigger):
         return False, "custom trigger"
-    if evictor is not None or allowed_lateness != 0 or late_data_output_tag is not None:
-        return False, "evictor / allowed lateness / late side output"
+    if evictor is not None:
+        return False, "evictor"
+    if allowed_lateness < 0:
+        return False, "The allowed lateness cannot be negative."
     if aggregation[0] not in _AGG or aggregation[1] not in _TYPE:
         return False, "not a built-in field aggregation"
     return True, ""
@@ -41,8 +47,10 @@ def is_gpu_eligible(assigner, trigger, aggregation, *, evictor=None, allowed_lat
 class WindowOperator:
     def __init__(self, assigner, trigger, aggregation, key_type="LONG", max_parallelism=128,
                  parallelism=1, subtask_index=0, device=0, state_capacity=1 << 20,
-                 max_batch_rows=1 << 22, output_capacity=1 << 22):
-        ok, why = is_gpu_eligible(assigner, trigger, aggregation)
+                 max_batch_rows=1 << 22, output_capacity=1 << 22, allowed_lateness=0,
+                 late_data_output_tag=None):
+        ok, why = is_gpu_eligible(assigner, trigger, aggregation, allowed_lateness=allowed_lateness,
+                                  late_data_output_tag=late_data_output_tag)
         if not ok:
             raise ValueError(f"not eligible for the GPU window operator: {why}")
         fn, ftype = aggregation
@@ -57,7 +65,9 @@ class WindowOperator:
             value_col_types=[t], key_hash=_KEY[key_type], max_parallelism=max_parallelism,
             parallelism=parallelism, subtask_index=subtask_index, device=device,
             state_capacity=state_capacity, max_batch_rows=max_batch_rows,
-            output_capacity=output_capacity)
+            output_capacity=output_capacity, allowed_lateness_ms=allowed_lateness,
+            late_side_output=late_data_output_tag is not None)
+        self.late_data_output_tag = late_data_output_tag
         self.handle = None
 
     def open(self):
@@ -82,6 +92,13 @@ class WindowOperator:
         return {"key": r["key"], "value": r["values"][0], "timestamp": r["window_end"] - 1,
                 "window_start": r["window_start"], "window_end": r["window_end"],
                 "values": r["values"], "null_mask": r["null_mask"]}
+
+    def side_output(self):
+        """Records routed to the late-data side output since the last call
+        (WindowOperator.sideOutput): {key, timestamp, value, push_seq, row}."""
+        r = self.handle.late_records()
+        return {"key": r["key"], "timestamp": r["ts"], "value": r["values"][0], "push_seq": r["push_seq"],
+                "row": r["row"]}
 
     def snapshot_state(self) -> bytes:
         return self.handle.snapshot()

@@ -147,6 +147,16 @@ class WindowAggHandle:
     def reset_results(self):
         check(lib().fw_results_reset(self._h))
 
+    def late_records(self):
+        """The late side output since the last call (DataStream, late_side_output): key, ts,
+        values (per value column), push_seq, row -- consumed (WindowOperator.sideOutput)."""
+        r = abi.fw_late_rows()
+        check(lib().fw_late_records(self._h, C.byref(r)))
+        n = r.n
+        return {"key": _np_view(r.key, n, np.int64).copy(), "ts": _np_view(r.ts, n, np.int64).copy(),
+                "values": [_np_view(r.values[c], n, np.int64).copy() for c in range(self.cfg.n_value_cols)],
+                "push_seq": _np_view(r.push_seq, n, np.int64).copy(), "row": _np_view(r.row, n, np.int64).copy()}
+
     def stats(self):
         s = abi.fw_stats()
         check(lib().fw_get_stats(self._h, C.byref(s)))

@@ -2,8 +2,9 @@
 
 The assigner objects describe the window for the GPU operator and expose the reference's
 scalar slice arithmetic on the host (window_start goes through the library's host entry point,
-i.e. the exact code the kernels run).  Event time, UTC shift zone only (the GPU seam's
-eligibility rule; TIMESTAMP_LTZ / DST falls back to the reference operator).
+i.e. the exact code the kernels run).  Event time.  A TIMESTAMP_LTZ window carries its shift time
+zone (SliceAssigners.tumbling/hopping/cumulative(rowtimeIndex, shiftTimeZone, ...)): rowtimes are
+sliced on the zone's wall clock (AbstractSliceAssigner.assignSliceEnd :655-670), DST included.
 """
 import math
 
@@ -19,17 +20,29 @@ class SliceAssigner:
     kind = None
     shared = False
 
+    shift_zone = None  # flink_amd.table.time_zone.ShiftZone, None = UTC
+
     def __init__(self, rowtime_index, size, slide, offset):
         self.rowtime_index = rowtime_index
         self.size = size
         self.slide = slide
         self.offset = offset
 
+    def in_zone(self, zone):
+        """The same assigner on a TIMESTAMP_LTZ rowtime sliced in `zone` (name or ShiftZone)."""
+        import copy
+        from .time_zone import ShiftZone
+        a = copy.copy(self)
+        a.shift_zone = ShiftZone.of(zone) if isinstance(zone, str) else zone
+        return a
+
     def get_slice_end_interval(self):
         raise NotImplementedError
 
     def assign_slice_end(self, timestamp):
         iv = self.get_slice_end_interval()
+        if self.shift_zone is not None:  # toUtcTimestampMills (TimeWindowUtil.java:52-60)
+            timestamp = self.shift_zone.to_utc_timestamp_mills(timestamp)
         return _window_start(timestamp, self.offset, iv) + iv
 
     def is_event_time(self):

@@ -24,15 +24,20 @@ KEY_HASH = {"BIGINT": abi.KEYHASH_BINROW_BIGINT, "INT": abi.KEYHASH_BINROW_INT,
 
 def is_gpu_eligible(assigner, aggs, value_types, *, is_event_time=True, shift_time_zone="UTC",
                     has_distinct=False, needs_retraction=False, key_type="BIGINT"):
-    """The builder-seam eligibility rule: rowtime, UTC shift zone, built-in
-    SUM/COUNT/COUNT(*)/MIN/MAX/AVG on numeric columns, no DISTINCT / retraction / UDAF.
-    Returns (ok, reason); callers fall back to the reference processor when not ok."""
+    """The builder-seam eligibility rule: rowtime (TIMESTAMP, or TIMESTAMP_LTZ with
+    any shift time zone), built-in SUM/COUNT/COUNT(*)/MIN/MAX/AVG on numeric columns, no DISTINCT /
+    retraction / UDAF.  Returns (ok, reason); callers fall back to the reference processor when
+    not ok."""
     if not isinstance(assigner, SliceAssigner):
         return False, "not a slicing assigner"
     if not is_event_time or not assigner.is_event_time():
         return False, "processing-time windows run on the reference operator"
-    if shift_time_zone != "UTC":
-        return False, "TIMESTAMP_LTZ shift zones run on the reference operator"
+    if shift_time_zone not in (None, "UTC"):
+        try:
+            from .time_zone import ShiftZone
+            ShiftZone.of(shift_time_zone)
+        except Exception:
+            return False, f"unknown shift time zone {shift_time_zone}"
     if has_distinct or needs_retraction:
         return False, "DISTINCT / retraction aggregates run on the reference operator"
     if isinstance(key_type, (tuple, list)):  # key row of several / non-integer fields (fw_key_row_hash)
@@ -56,7 +61,11 @@ class WindowAggOperator:
                  max_parallelism=128, parallelism=1, subtask_index=0, device=0,
                  state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22,
                  nullable_cols=()):
-        ok, why = is_gpu_eligible(assigner, aggs, value_types, key_type=key_type)
+        """``assigner``: a SliceAssigner; a TIMESTAMP_LTZ window's assigner carries its shift time
+        zone (``assigner.in_zone(zone)``, SliceAssigners.*(rowtimeIndex, shiftTimeZone, ...))."""
+        zone = assigner.shift_zone
+        ok, why = is_gpu_eligible(assigner, aggs, value_types, key_type=key_type,
+                                  shift_time_zone=zone.name if zone is not None else "UTC")
         if not ok:
             raise ValueError(f"not eligible for the GPU window operator: {why}")
         if assigner.kind == abi.WIN_HOP and count_star_index < 0:
@@ -76,7 +85,7 @@ class WindowAggOperator:
             max_parallelism=max_parallelism,
             parallelism=parallelism, subtask_index=subtask_index, device=device,
             state_capacity=state_capacity, max_batch_rows=max_batch_rows,
-            output_capacity=output_capacity, nullable_cols=nullable_cols)
+            output_capacity=output_capacity, nullable_cols=nullable_cols, shift_zone=zone)
         self.handle = None
         self.current_watermark = -(1 << 63)
 

@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 3
+#define FW_ABI_VERSION 4
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -80,7 +80,8 @@ extern "C" {
 /* ---- configuration ----------------------------------------------------------------- */
 typedef enum {
     FW_API_SQL = 0,         /* Table/SQL slicing WindowAggOperator (window TVF aggregate) */
-    FW_API_DATASTREAM = 1   /* DataStream WindowOperator + EventTimeTrigger, lateness 0  */
+    FW_API_DATASTREAM = 1   /* DataStream WindowOperator + EventTimeTrigger (+ allowedLateness,
+                               late side output)                                        */
 } fw_api_kind;
 
 typedef enum {
@@ -157,6 +158,23 @@ typedef struct {
     int64_t state_capacity;   /* expected max live (key, slice) state entries (sizing hint) */
     int64_t max_batch_rows;   /* max rows per fw_commit / fw_push_device call              */
     int64_t output_capacity;  /* result rows kept between fw_results_reset calls           */
+    /* ---- v4: lateness (DataStream) and shift time zones (SQL TIMESTAMP_LTZ) ---------------- */
+    int64_t allowed_lateness_ms; /* DataStream WindowOperator allowedLateness (>= 0; SQL: 0).  A
+                                    window fires at maxTimestamp and keeps its state until
+                                    cleanupTime = maxTimestamp + lateness (WindowOperator.java
+                                    :609-682); an element for a fired, not yet cleaned window
+                                    fires it again at once (EventTimeTrigger.onElement)           */
+    int32_t late_side_output;    /* DataStream: 1 = elements late for every window go to the late
+                                    side output (fw_late_records; WindowOperator.sideOutput, the
+                                    sideOutputLateData tag) instead of numLateRecordsDropped      */
+    int32_t tz_use_dst;          /* TimeZone.getTimeZone(shiftTimeZone).useDaylightTime()          */
+    int32_t tz_n;                /* SQL TIMESTAMP_LTZ rowtime: entries of the shift time zone's
+                                    offset table (TimeWindowUtil.getShiftTimeZone); 0 = UTC       */
+    int32_t reserved1;
+    const int64_t* tz_utc;       /* tz_n ascending UTC epoch ms, tz_utc[0] = INT64_MIN: offset
+                                    tz_offset_ms[i] is in force from tz_utc[i] (ZoneRules
+                                    .getOffset(Instant)); host memory, copied by fw_create        */
+    const int64_t* tz_offset_ms;
 } fw_config;
 
 typedef struct fw_handle fw_handle;
@@ -220,6 +238,22 @@ int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t*
                    const uint8_t* const* d_nulls);
 
 /* ---- progress / output --------------------------------------------------------------- */
+/* Late side output of a DataStream operator with late_side_output (WindowOperator.sideOutput,
+   WindowOperator.java:440-446,549): the elements skipped as late for every window since the last
+   call, as columns.  push_seq counts fw_commit / fw_push_device calls from 0, row is the element's
+   index in that call (so a host shim can forward its original record); values[c] holds the value
+   columns the aggregates read (0 for the others).  Host arrays owned by the
+   handle, valid until the next call; the rows are consumed. */
+typedef struct {
+    int64_t n;
+    int64_t* key;
+    int64_t* ts;
+    int64_t* values[FW_MAX_COLS];
+    int64_t* push_seq;
+    int64_t* row;
+} fw_late_rows;
+int fw_late_records(fw_handle* h, fw_late_rows* out);
+
 int fw_advance(fw_handle* h, int64_t watermark);
 int fw_flush(fw_handle* h);
 /* copy_to_host != 0: host arrays owned by the handle, valid until the next call;
@@ -344,6 +378,14 @@ int fw_host_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n
 int64_t fw_host_window_start(int64_t ts, int64_t offset, int64_t size);
 /* TimeWindowUtil.getNextTriggerWatermark, UTC (TR/util/TimeWindowUtil.java:186). */
 int64_t fw_host_next_trigger_watermark(int64_t watermark, int64_t interval);
+/* Window / shift-zone arithmetic of an operator configuration (no device use): the plan
+   fw_create makes from cfg and the code the kernels run.  what = 0 toUtcTimestampMills(x)
+   (TimeWindowUtil.java:52), 1 toEpochMillsForTimer(x) (:69), 2 getNextTriggerWatermark(x, slice
+   interval, useDaylightTime) (:186), 3 the slice end assigned to rowtime x
+   (AbstractSliceAssigner.assignSliceEnd, SliceAssigners.java:655-670), 4 the window start of
+   slice end x (SliceAssigner.getWindowStart).  *out receives the value; returns FW_E_INVALID for a
+   configuration fw_create would reject. */
+int fw_host_time_op(const fw_config* cfg, int32_t what, int64_t x, int64_t* out);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,8 @@
 //                         + BinaryRowData.java:69-124,459 (hashByWords, seed 42)
 //   * window math         FR/streaming/api/windowing/windows/TimeWindow.java:84,264-272
 //                         TR/operators/window/tvf/slicing/SliceAssigners.java:140-757
-//                         TR/util/TimeWindowUtil.java:52-211 (UTC shift zone only)
+//                         TR/util/TimeWindowUtil.java:52-211 (shift zones over java.time
+//                           ZoneRules semantics: ZonedDateTime.ofLocal gap / overlap rules)
 //   * SQL operator        TR/operators/window/tvf/common/WindowAggOperator.java:216-265
 //                         TR/operators/aggregate/window/processors/
 //                           AbstractSliceSyncStateWindowAggProcessor.java:96-167
@@ -27,6 +28,7 @@
 //   * SQL aggregates      flink-table-planner/.../functions/aggfunctions/
 //                           {Count1,Count,Sum,Max,Min,Avg}AggFunction.java
 //   * DataStream operator FR/streaming/runtime/operators/windowing/WindowOperator.java:293-682
+//                           (allowedLateness, cleanup timers, late side output :440-446,549,609-682)
 //                         FR/streaming/api/windowing/triggers/EventTimeTrigger.java:37-52
 //                         FR/streaming/api/windowing/assigners/{Tumbling,Sliding}EventTimeWindows.java
 //                         FR/streaming/api/functions/aggregation/{SumAggregator,ComparableAggregator,
@@ -185,12 +187,6 @@ int64_t window_start_with_offset(int64_t ts, int64_t offset, int64_t size) {
     return jsub64(ts, remainder);
 }
 
-// TimeWindowUtil.isWindowFired (TimeWindowUtil.java:175-183), UTC shift zone.
-bool is_window_fired(int64_t window_end, int64_t progress) {
-    if (window_end == INT64_MAX) return false;
-    return progress >= jsub64(window_end, 1);
-}
-
 // TimeWindowUtil.getNextTriggerWatermark (TimeWindowUtil.java:186-211), no DST.
 int64_t next_trigger_watermark(int64_t wm, int64_t interval) {
     if (wm == INT64_MAX) return wm;
@@ -240,10 +236,78 @@ int java_double_compare(double a, double b) {
     return x == y ? 0 : (x < y ? -1 : 1);
 }
 
+// A shift time zone as java.time ZoneRules sees it: offset off[i] from UTC instant utc[i]
+// (utc[0] = Long.MIN_VALUE).  Empty = UTC (no shift).
+struct Zone {
+    std::vector<int64_t> utc, off;
+    bool dst = false;  // TimeZone.getTimeZone(zone).useDaylightTime()
+    bool utc_zone() const { return utc.empty(); }
+    // ZoneRules.getOffset(Instant)
+    int64_t offset_of_instant(int64_t epoch) const {
+        size_t i = (size_t)(std::upper_bound(utc.begin(), utc.end(), epoch) - utc.begin());
+        return off[i - 1];
+    }
+    // LocalDateTime.atZone(zone).toInstant().toEpochMilli(): ZonedDateTime.ofLocal(ldt, zone,
+    // null) walks the transitions: before a transition's local range the old offset holds; inside
+    // a gap (offset grows) the local time moves later by the gap and takes the new offset; inside
+    // an overlap (offset shrinks) the earlier (old) offset wins
+    int64_t local_to_epoch(int64_t local) const {
+        for (size_t i = 1; i < utc.size(); i++) {
+            const int64_t before = off[i - 1], after = off[i];
+            const int64_t lb = jadd64(utc[i], before), la = jadd64(utc[i], after);
+            if (local < std::min(lb, la)) return jsub64(local, before);
+            if (local < std::max(lb, la)) {
+                if (after > before) return jsub64(jadd64(local, after - before), after);  // gap
+                return jsub64(local, before);                                            // overlap
+            }
+        }
+        return jsub64(local, off.back());
+    }
+};
+
+// TimeWindowUtil.toUtcTimestampMills (:52-60)
+int64_t to_utc_timestamp_mills(int64_t epoch, const Zone& z) {
+    if (z.utc_zone() || epoch == INT64_MAX) return epoch;
+    return jadd64(epoch, z.offset_of_instant(epoch));
+}
+// TimeWindowUtil.toEpochMillsForTimer (:69-140)
+int64_t to_epoch_mills_for_timer(int64_t utc_ts, const Zone& z) {
+    if (z.utc_zone() || utc_ts == INT64_MAX) return utc_ts;
+    if (z.dst) {
+        const int64_t hour = 3600LL * 1000;
+        const int64_t t1 = z.local_to_epoch(utc_ts);
+        const int64_t t2 = z.local_to_epoch(jadd64(utc_ts, hour));  // plusSeconds(SECONDS_PER_HOUR)
+        const bool no_epoch = t1 == t2, two_epochs = jsub64(t2, t1) > hour;
+        if (no_epoch) return jsub64(t1, t1 % hour);
+        if (two_epochs) return jadd64(t1, hour);
+        return t1;
+    }
+    return z.local_to_epoch(utc_ts);
+}
+// TimeWindowUtil.isWindowFired (:175-183)
+bool is_window_fired_tz(int64_t window_end, int64_t progress, const Zone& z) {
+    if (window_end == INT64_MAX) return false;
+    return progress >= to_epoch_mills_for_timer(jsub64(window_end, 1), z);
+}
+// TimeWindowUtil.getNextTriggerWatermark (:186-211)
+int64_t next_trigger_watermark_tz(int64_t wm, int64_t interval, const Zone& z) {
+    if (wm == INT64_MAX) return wm;
+    int64_t trig;
+    if (z.dst) {
+        const int64_t utc_start = window_start_with_offset(to_utc_timestamp_mills(wm, z), 0, interval);
+        trig = to_epoch_mills_for_timer(jadd64(utc_start, interval) - 1, z);
+    } else {
+        trig = jsub64(jadd64(window_start_with_offset(wm, 0, interval), interval), 1);
+    }
+    return trig > wm ? trig : jadd64(trig, interval);
+}
+
 struct Config {
     fw_config c;
     int64_t interval;  // slice size (SliceAssigner.getSliceEndInterval)
     int n_slices;      // HOP slices per window
+    Zone zone;         // SQL shift time zone (TimeWindowUtil.getShiftTimeZone)
+    int64_t lateness = 0;  // DataStream allowedLateness
 };
 
 struct Oracle {
@@ -271,6 +335,10 @@ struct Oracle {
     std::set<std::tuple<int64_t, int64_t, int64_t>> timers;
 
     std::vector<OutRow> out;
+    // DataStream late side output (WindowOperator.sideOutput): (key, ts, values, push, row)
+    struct SideRow { int64_t key, ts; uint64_t v[FW_MAX_COLS]; int64_t push, row; };
+    std::vector<SideRow> side;
+    int64_t push_seq = 0;
 
     // -------------------------------------------------------------------------------
     // aggregate function expressions
@@ -460,11 +528,14 @@ struct Oracle {
     // -------------------------------------------------------------------------------
     // SliceAssigner (SliceAssigners.java)
     // -------------------------------------------------------------------------------
+    // AbstractSliceAssigner.assignSliceEnd(element, clock) (SliceAssigners.java:655-670): the
+    // rowtime goes through toUtcTimestampMills first
     int64_t assign_slice_end(int64_t ts) const {
         const fw_config& c = cfg.c;
         const int64_t step = cfg.interval;
-        return jadd64(window_start_with_offset(ts, c.offset_ms, step), step);
+        return jadd64(window_start_with_offset(to_utc_timestamp_mills(ts, cfg.zone), c.offset_ms, step), step);
     }
+    bool wfired(int64_t window_end, int64_t progress) const { return is_window_fired_tz(window_end, progress, cfg.zone); }
     int64_t get_window_start(int64_t we) const {
         const fw_config& c = cfg.c;
         if (c.window_kind == FW_WIN_CUMULATE)
@@ -487,8 +558,9 @@ struct Oracle {
     }
 
     void register_timer(int64_t key, int64_t window) {
-        // SlicingWindowTimerServiceImpl.registerEventTimeWindowTimer: ts = window - 1 (UTC)
-        timers.insert(std::make_tuple(jsub64(window, 1), key, window));
+        // SlicingWindowTimerServiceImpl.registerEventTimeWindowTimer (:43-46):
+        // ts = toEpochMillsForTimer(window - 1, shiftTimeZone)
+        timers.insert(std::make_tuple(to_epoch_mills_for_timer(jsub64(window, 1), cfg.zone), key, window));
     }
 
     // -------------------------------------------------------------------------------
@@ -501,12 +573,12 @@ struct Oracle {
         }
         // GLOBAL: SliceAssigners.sliced -> the row's slice-end field (here: the ts column)
         const int64_t slice_end = phase == FW_PHASE_GLOBAL ? ts : assign_slice_end(ts);
-        if (is_window_fired(slice_end, current_progress)) {
+        if (wfired(slice_end, current_progress)) {
             const int64_t last = get_last_window_end(slice_end);
-            if (is_window_fired(last, current_progress)) return true;  // dropped
+            if (wfired(last, current_progress)) return true;  // dropped
             buffer_add(key, merge_target(slice_end), vals, nul);
             int64_t unfired = slice_end;
-            while (is_window_fired(unfired, current_progress)) unfired = jadd64(unfired, cfg.interval);
+            while (wfired(unfired, current_progress)) unfired = jadd64(unfired, cfg.interval);
             register_timer(key, unfired);
             return false;
         }
@@ -560,7 +632,7 @@ struct Oracle {
                 for (auto& rec : g.second) accumulate(acc, rec.vals, rec.nul);
             }
             state[sk] = acc;
-            if (!is_window_fired(slice, timer_watermark)) register_timer(key, slice);
+            if (!wfired(slice, timer_watermark)) register_timer(key, slice);
         }
         buffer.clear();
         buffer_index.clear();
@@ -668,8 +740,8 @@ struct Oracle {
         if (wm > current_watermark) {
             current_watermark = wm;
             if (current_watermark >= next_trigger_progress) {
-                if (is_window_fired(min_slice_end, current_watermark)) flush();
-                next_trigger_progress = next_trigger_watermark(current_watermark, cfg.interval);
+                if (wfired(min_slice_end, current_watermark)) flush();
+                next_trigger_progress = next_trigger_watermark_tz(current_watermark, cfg.interval, cfg.zone);
             }
         }
     }
@@ -682,8 +754,8 @@ struct Oracle {
                 current_progress = wm;
                 if (current_progress >= next_trigger_progress) {
                     // RecordsWindowBuffer.advanceProgress (:107-112)
-                    if (is_window_fired(min_slice_end, current_progress)) flush();
-                    next_trigger_progress = next_trigger_watermark(current_progress, cfg.interval);
+                    if (wfired(min_slice_end, current_progress)) flush();
+                    next_trigger_progress = next_trigger_watermark_tz(current_progress, cfg.interval, cfg.zone);
                 }
             }
             current_watermark = wm;
@@ -693,9 +765,14 @@ struct Oracle {
 
     // -------------------------------------------------------------------------------
     // DataStream: WindowOperator.processElement (non-merging branch :405-446) with
-    // EventTimeTrigger, allowedLateness = 0, no late side output.
+    // EventTimeTrigger, allowedLateness >= 0 and an optional late side output.
     // -------------------------------------------------------------------------------
-    bool ds_process_element(int64_t key, int64_t ts, const uint64_t* vals) {
+    // WindowOperator.cleanupTime (:670-677): maxTimestamp + allowedLateness, Long.MAX_VALUE on overflow
+    int64_t cleanup_time(int64_t max_ts) const {
+        const int64_t t = jadd64(max_ts, cfg.lateness);
+        return t >= max_ts ? t : INT64_MAX;
+    }
+    bool ds_process_element(int64_t key, int64_t ts, const uint64_t* vals, int64_t row) {
         static const uint8_t no_nulls[FW_MAX_COLS] = {0};
         const fw_config& c = cfg.c;
         std::vector<int64_t> starts;
@@ -711,29 +788,42 @@ struct Oracle {
         for (int64_t s : starts) {
             const int64_t end = jadd64(s, c.size_ms);
             const int64_t max_ts = jsub64(end, 1);
-            if (max_ts <= timer_watermark) continue;  // isWindowLate: cleanupTime <= currentWatermark
+            if (cleanup_time(max_ts) <= timer_watermark) continue;  // isWindowLate (:609-612)
             skipped = false;
             auto sk = std::make_pair(key, end);
             auto it = state.find(sk);
             Row acc = it == state.end() ? create_accumulators() : it->second;
             accumulate(acc, vals, no_nulls);  // HeapReducingState.add / HeapAggregatingState.add
             state[sk] = acc;
-            // EventTimeTrigger.onElement: maxTs > watermark -> registerEventTimeTimer(maxTs);
-            // registerCleanupTimer(window) registers the same (key, window, maxTs) timer.
-            timers.insert(std::make_tuple(max_ts, key, end));
+            // EventTimeTrigger.onElement (:37-45): a window whose maxTimestamp the watermark has
+            // passed FIRES at once (emitWindowContents), else its timer is registered
+            if (max_ts <= timer_watermark) emit(key, end, acc);
+            else timers.insert(std::make_tuple(max_ts, key, end));
+            // registerCleanupTimer (:616-628): no timer for a cleanup time of Long.MAX_VALUE
+            const int64_t ct = cleanup_time(max_ts);
+            if (ct != INT64_MAX) timers.insert(std::make_tuple(ct, key, end));
         }
-        if (skipped && ts <= timer_watermark) return true;  // isElementLate -> numLateRecordsDropped
+        // isSkippedElement && isElementLate (:438-446, :640-644)
+        if (skipped && jadd64(ts, cfg.lateness) <= timer_watermark) {
+            if (c.late_side_output) {
+                SideRow r{key, ts, {0}, push_seq, row};
+                std::memcpy(r.v, vals, sizeof(r.v));
+                side.push_back(r);
+                return false;
+            }
+            return true;  // numLateRecordsDropped
+        }
         return false;
     }
 
     // WindowOperator.onEventTime (:450-494)
     void ds_on_event_time(int64_t key, int64_t end, int64_t time) {
         const int64_t max_ts = jsub64(end, 1);
+        auto it = state.find({key, end});
         if (time == max_ts) {  // EventTimeTrigger.onEventTime -> FIRE
-            auto it = state.find({key, end});
             if (it != state.end()) emit(key, end, it->second);  // emitWindowContents, ts = maxTimestamp
         }
-        if (time == max_ts) state.erase({key, end});  // isCleanupTime -> clearAllState
+        if (time == cleanup_time(max_ts)) state.erase({key, end});  // isCleanupTime -> clearAllState
     }
 
     void ds_process_watermark(int64_t wm) {
@@ -787,6 +877,14 @@ void* or_create(const fw_config* c) {
         o->cfg.interval = gcd64(c->size_ms, c->slide_ms);
         o->cfg.n_slices = (int)(c->size_ms / o->cfg.interval);
     } else { o->cfg.interval = c->slide_ms; o->cfg.n_slices = (int)(c->size_ms / c->slide_ms); }
+    o->cfg.lateness = o->ds ? c->allowed_lateness_ms : 0;
+    if (c->tz_n > 0 && c->tz_utc && c->tz_offset_ms) {
+        o->cfg.zone.utc.assign(c->tz_utc, c->tz_utc + c->tz_n);
+        o->cfg.zone.off.assign(c->tz_offset_ms, c->tz_offset_ms + c->tz_n);
+        o->cfg.zone.dst = c->tz_use_dst != 0;
+    }
+    o->cfg.c.tz_utc = nullptr;  // the table lives in cfg.zone
+    o->cfg.c.tz_offset_ms = nullptr;
     return o;
 }
 
@@ -812,10 +910,11 @@ int64_t or_process_batch(void* h, int64_t n, const int64_t* key, const int64_t* 
             row[c] = vals[(int64_t)c * n + i];
             nul[c] = nulls ? nulls[(int64_t)c * n + i] : 0;
         }
-        bool d = o->ds ? o->ds_process_element(key[i], ts[i], row) : o->sql_process_element(key[i], ts[i], row, nul);
+        bool d = o->ds ? o->ds_process_element(key[i], ts[i], row, i) : o->sql_process_element(key[i], ts[i], row, nul);
         if (d) dropped++;
     }
     o->late_dropped += dropped;
+    o->push_seq++;
     return dropped;
 }
 
@@ -851,6 +950,33 @@ void or_get_results(void* h, int64_t* key, int64_t* ws, int64_t* we, uint64_t* v
     }
 }
 void or_clear_results(void* h) { ((Oracle*)h)->out.clear(); }
+// late side output rows since the last call (consumed): SoA, vals[c * n + i]
+int64_t or_num_side_rows(void* h) { return (int64_t)((Oracle*)h)->side.size(); }
+void or_take_side_rows(void* h, int64_t* key, int64_t* ts, uint64_t* vals, int64_t* push, int64_t* row) {
+    Oracle* o = (Oracle*)h;
+    const int64_t n = (int64_t)o->side.size();
+    for (int64_t i = 0; i < n; i++) {
+        const Oracle::SideRow& r = o->side[i];
+        key[i] = r.key;
+        ts[i] = r.ts;
+        push[i] = r.push;
+        row[i] = r.row;
+        for (int c = 0; c < o->cfg.c.n_value_cols; c++) vals[(int64_t)c * n + i] = r.v[c];
+    }
+    o->side.clear();
+}
+// shift-zone arithmetic of an operator (what: 0 toUtcTimestampMills, 1 toEpochMillsForTimer,
+// 2 getNextTriggerWatermark, 3 assignSliceEnd, 4 getWindowStart)
+int64_t or_time_op(void* h, int32_t what, int64_t x) {
+    Oracle* o = (Oracle*)h;
+    switch (what) {
+        case 0: return to_utc_timestamp_mills(x, o->cfg.zone);
+        case 1: return to_epoch_mills_for_timer(x, o->cfg.zone);
+        case 2: return next_trigger_watermark_tz(x, o->cfg.interval, o->cfg.zone);
+        case 3: return o->assign_slice_end(x);
+        default: return o->get_window_start(x);
+    }
+}
 
 // Hash / key-group restatements.
 int32_t or_murmur_hash(int32_t code) { return murmur_hash(code); }

@@ -45,6 +45,11 @@ def lib():
             getattr(L, f).argtypes = [vp]
         L.or_get_results.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.or_clear_results.argtypes = [vp]
+        L.or_num_side_rows.restype = i64
+        L.or_num_side_rows.argtypes = [vp]
+        L.or_take_side_rows.argtypes = [vp, vp, vp, vp, vp, vp]
+        L.or_time_op.restype = i64
+        L.or_time_op.argtypes = [vp, i32, i64]
         L.or_murmur_hash.restype = i32
         L.or_murmur_hash.argtypes = [i32]
         L.or_java_key_hash.restype = i32
@@ -139,6 +144,22 @@ class OracleOperator:
             L.or_clear_results(self.h)
         return {"key": key, "window_start": ws, "window_end": we,
                 "values": [vals[a].view(np.int64) for a in range(na)], "null_mask": nm, "epoch": ep}
+
+
+    def side_output(self):
+        """Late side-output rows since the last call (consumed): key, ts, values, push, row."""
+        L = lib()
+        n = L.or_num_side_rows(self.h)
+        nv = max(self.cfg.n_value_cols, 1)
+        key, ts, push, row = (np.empty(n, np.int64) for _ in range(4))
+        vals = np.zeros((nv, n), np.uint64)
+        if n:
+            L.or_take_side_rows(self.h, _ptr(key), _ptr(ts), _ptr(vals), _ptr(push), _ptr(row))
+        return {"key": key, "ts": ts, "values": [vals[c].view(np.int64) for c in range(self.cfg.n_value_cols)],
+                "push_seq": push, "row": row}
+
+    def time_op(self, what, x):
+        return lib().or_time_op(self.h, int(what), int(x))
 
 
 def murmur_hash(code):

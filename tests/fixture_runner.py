@@ -40,6 +40,9 @@ def fixture_config(fx, **overrides):
         key_hash=getattr(abi, "KEYHASH_" + kh),
         state_capacity=1 << 14, max_batch_rows=1 << 12, output_capacity=1 << 12,
         nullable_cols=c.get("nullable_cols", []),
+        allowed_lateness_ms=c.get("allowed_lateness_ms", 0),
+        late_side_output=c.get("late_side_output", False),
+        shift_zone=c.get("shift_zone"),
     )
     kw.update(overrides)
     return abi.make_config(**kw)
@@ -113,6 +116,12 @@ def replay(fx, op, check_late=True):
         assert got == want, f"{fx['name']}: watermark {st['wm']} (step {step_no}): got {got} want {want}"
     drain()
     assert not collected, f"{fx['name']}: unchecked rows {collected}"
+    if "side_output" in fx:  # late side output: multiset of (key, ts, values)
+        so = op.side_output()
+        got = sorted((int(so["key"][i]), int(so["ts"][i])) + tuple(int(v[i]) for v in so["values"])
+                     for i in range(len(so["key"])))
+        want = sorted((keys[r["key"]]["id"], r["ts"]) + tuple(_bits(v) for v in r["values"]) for r in fx["side_output"])
+        assert got == want, f"{fx['name']}: side output {got} != {want}"
     if check_late and fx["late_dropped"] is not None:
         assert op.late_dropped == fx["late_dropped"], \
             f"{fx['name']}: late dropped {op.late_dropped} != {fx['late_dropped']}"
@@ -147,6 +156,9 @@ class OracleAdapter:
     def snapshot_restore(self):
         self.op.snapshot_restore()
 
+    def side_output(self):
+        return self.op.side_output()
+
     @property
     def late_dropped(self):
         return self.op.late_dropped
@@ -161,6 +173,7 @@ class GpuAdapter:
         self.cfg = fixture_config(fx, **overrides)
         self.h = WindowAggHandle(self.cfg)
         self.dropped_before = 0
+        self._side = []
 
     def process_batch(self, k, t, h, vals, nulls=None):
         self.h.push_host(k, t, vals, key_hashes=h, nulls=nulls)
@@ -170,10 +183,20 @@ class GpuAdapter:
         return self.h.results(reset=True)
 
     def snapshot_restore(self):
+        side = self.h.late_records() if self.cfg.late_side_output else None
         blob = self.h.snapshot()
         self.h.close()
         self.h = self._cls(self.cfg)
         self.h.restore(blob)
+        if side is not None:
+            self._side.append(side)
+
+    _side = None
+
+    def side_output(self):
+        parts = (self._side or []) + [self.h.late_records()]
+        return {"key": np.concatenate([p["key"] for p in parts]), "ts": np.concatenate([p["ts"] for p in parts]),
+                "values": [np.concatenate([p["values"][c] for p in parts]) for c in range(len(parts[0]["values"]))]}
 
     @property
     def late_dropped(self):

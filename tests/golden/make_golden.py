@@ -35,7 +35,20 @@ the reference test asserts after each watermark (plus the late-drop counter).  S
        aggregates.
   KATS flink-table/flink-table-runtime/src/test/java/org/apache/flink/table/runtime/operators/
        window/tvf/slicing/{Tumbling,Hopping,Cumulative}SliceAssignerTest.java (UTC): slice end,
-       window start, expired slices, slices to merge, next trigger window.
+       window start, expired slices, slices to merge, next trigger window; testDstSaving (:63-96,
+       :66-100, :66-100) under America/Los_Angeles: slice start / end across the 2021 DST changes.
+  LTZ  SlicingWindowAggOperatorTest runs every event-time test under UTC *and* Asia/Shanghai
+       (:53-59).  With Asia/Shanghai the expected window_start / window_end are
+       localMills(epoch) = toUtcTimestampMills(epoch, zone) = epoch + 8 h
+       (WindowAggOperatorTestBase.java:79-81) while elements and watermarks stay epoch millis:
+       the *_shanghai fixtures.
+  LATE WindowOperatorTest.java allowed lateness / late side output (SumReducer, EventTimeTrigger):
+       - testCleanupTimeOverflow                              :2139-2245 (lateness 2000 ms,
+         cleanup time past Long.MAX_VALUE)
+       - testSideOutputDueToLatenessTumbling                  :2249-2344
+       - testSideOutputDueToLatenessSliding                   :2348-2462
+       - testCleanupTimerWithEmptyReduceStateForTumblingWindows :3248-3321 (lateness 1 ms)
+       "side_output" lists the elements the test expects on the late side output.
 
 Keys that are strings in the reference tests are mapped to integer ids; their Java
 String.hashCode is recorded so key-group assignment matches the reference.  "snapshot_restore"
@@ -191,6 +204,48 @@ FIXTURES.append({
         wm(3999), wm(4999),
         wm(5999, ds_row("key2", 2, 5999)),
         wm(6999), wm(7999)],
+    "late_dropped": 0,
+})
+
+# ---------------------------------------------------------------- DataStream lateness
+_LMAX = INT64_MAX - 1750                       # testCleanupTimeOverflow's element timestamp
+_LWIN_END = _LMAX - (_LMAX % 1000) + 1000      # its 1 s tumbling window [start, end)
+FIXTURES.append({
+    "name": "ds_lateness_cleanup_overflow",
+    "source": "WindowOperatorTest.java:2139-2245 testCleanupTimeOverflow (lateness 2000 ms)",
+    "config": dict(DS_CFG_BASE, window="TUMBLE", size_ms=1000, slide_ms=0, allowed_lateness_ms=2000),
+    "steps": [el("key2", _LMAX), wm(INT64_MAX - 1500), wm(_LWIN_END - 1, ds_row("key2", 1, _LWIN_END - 1))],
+    "late_dropped": 0,
+})
+FIXTURES.append({
+    "name": "ds_side_output_tumbling_2s",
+    "source": "WindowOperatorTest.java:2249-2344 testSideOutputDueToLatenessTumbling",
+    "config": dict(DS_CFG_BASE, window="TUMBLE", size_ms=2000, slide_ms=0, allowed_lateness_ms=0, late_side_output=True),
+    "steps": [el("key2", 1000), wm(1985),
+              el("key2", 1980), wm(1999, ds_row("key2", 2, 1999)),
+              el("key2", 1998), el("key2", 2001), wm(2999),
+              wm(3999, ds_row("key2", 1, 3999))],
+    "side_output": [{"key": "key2", "ts": 1998, "values": [1]}],
+    "late_dropped": 0,
+})
+FIXTURES.append({
+    "name": "ds_side_output_sliding_3s_1s",
+    "source": "WindowOperatorTest.java:2348-2462 testSideOutputDueToLatenessSliding",
+    "config": dict(DS_CFG_BASE, window="HOP", size_ms=3000, slide_ms=1000, allowed_lateness_ms=0, late_side_output=True),
+    "steps": [el("key2", 1000), wm(1999, ds_row("key2", 1, 1999)),
+              el("key2", 2000), wm(3000, ds_row("key2", 2, 2999)),
+              el("key1", 3001), el("key2", 2400), el("key2", 2400), el("key1", 3001), el("key2", 3900),
+              wm(6000, ds_row("key2", 5, 3999), ds_row("key1", 2, 3999), ds_row("key2", 4, 4999),
+                 ds_row("key1", 2, 4999), ds_row("key2", 1, 5999), ds_row("key1", 2, 5999)),
+              el("key1", 3001), wm(25000)],
+    "side_output": [{"key": "key1", "ts": 3001, "values": [1]}],
+    "late_dropped": 0,
+})
+FIXTURES.append({
+    "name": "ds_lateness_cleanup_timer_tumbling_2s",
+    "source": "WindowOperatorTest.java:3248-3321 testCleanupTimerWithEmptyReduceStateForTumblingWindows (lateness 1 ms)",
+    "config": dict(DS_CFG_BASE, window="TUMBLE", size_ms=2000, slide_ms=0, allowed_lateness_ms=1),
+    "steps": [el("key2", 1000), wm(1599), wm(1999, ds_row("key2", 1, 1999)), wm(2000), wm(5000)],
     "late_dropped": 0,
 })
 
@@ -464,6 +519,57 @@ KATS = [
     {"src": _SAT + "CumulativeSliceAssignerTest.java testNextTriggerWindow", "assigner": ["CUMULATE", 5 * H, 1 * H, 0], "op": "next_trigger",
      "cases": [[[_u("1970-01-01T0%d:00:00" % h, ), empty], (None if h in (0, 5) else _u("1970-01-01T0%d:00:00" % (h + 1)))]
                for empty in (False, True) for h in range(7)]},
+]
+
+
+# ---------------------------------------------------------------- TIMESTAMP_LTZ: Asia/Shanghai
+_SH = 8 * H
+
+
+def _shanghai(name):
+    import copy
+    f = copy.deepcopy(next(x for x in FIXTURES if x["name"] == name))
+    f["name"] = name + "_shanghai"
+    f["source"] += " [TimeZone = Asia/Shanghai: window props = localMills(epoch)]"
+    f["config"]["shift_zone"] = "Asia/Shanghai"
+    for st in f["steps"]:
+        for r in st.get("expect", []):
+            r["window_start"] += _SH
+            r["window_end"] += _SH
+    return f
+
+
+FIXTURES += [_shanghai(n) for n in ("sql_hop_3s_1s", "sql_hop_expired_slice_restore", "sql_hop_expired_slice_norestore",
+                                    "sql_cumulate_3s_1s", "sql_tumble_3s")]
+
+# ---------------------------------------------------------------- DST KATs (America/Los_Angeles)
+_LA_EPOCHS = [1615708800000, 1615712400000, 1615716000000, 1615719600000,
+              1636268400000, 1636272000000, 1636275600000, 1636279200000, 1636282800000, 1636286400000]
+
+
+def _dst(src, kind, size, slide, pairs):
+    # assertSliceStartEnd(start, end, epochMills, assigner): the local wall-clock strings of
+    # getWindowStart(assignSliceEnd(epoch)) and assignSliceEnd(epoch)
+    return {"src": _SAT + src, "assigner": [kind, size, slide, 0], "zone": "America/Los_Angeles", "op": "dst_slice",
+            "cases": [[e, [_u(a + ":00"), _u(b + ":00")]] for e, (a, b) in zip(_LA_EPOCHS, pairs)]}
+
+
+KATS += [
+    _dst("TumblingSliceAssignerTest.java:63-96 testDstSaving", "TUMBLE", 4 * H, 0,
+         [("2021-03-14T00:00", "2021-03-14T04:00")] * 3 + [("2021-03-14T04:00", "2021-03-14T08:00")] +
+         [("2021-11-07T00:00", "2021-11-07T04:00")] * 5 + [("2021-11-07T04:00", "2021-11-07T08:00")]),
+    _dst("HoppingSliceAssignerTest.java:66-100 testDstSaving", "HOP", 4 * H, 1 * H,
+         [("2021-03-13T21:00", "2021-03-14T01:00"), ("2021-03-13T22:00", "2021-03-14T02:00"),
+          ("2021-03-14T00:00", "2021-03-14T04:00"), ("2021-03-14T01:00", "2021-03-14T05:00"),
+          ("2021-11-06T21:00", "2021-11-07T01:00"), ("2021-11-06T22:00", "2021-11-07T02:00"),
+          ("2021-11-06T22:00", "2021-11-07T02:00"), ("2021-11-06T23:00", "2021-11-07T03:00"),
+          ("2021-11-07T00:00", "2021-11-07T04:00"), ("2021-11-07T01:00", "2021-11-07T05:00")]),
+    _dst("CumulativeSliceAssignerTest.java:66-100 testDstSaving", "CUMULATE", 4 * H, 1 * H,
+         [("2021-03-14T00:00", "2021-03-14T01:00"), ("2021-03-14T00:00", "2021-03-14T02:00"),
+          ("2021-03-14T00:00", "2021-03-14T04:00"), ("2021-03-14T04:00", "2021-03-14T05:00"),
+          ("2021-11-07T00:00", "2021-11-07T01:00"), ("2021-11-07T00:00", "2021-11-07T02:00"),
+          ("2021-11-07T00:00", "2021-11-07T02:00"), ("2021-11-07T00:00", "2021-11-07T03:00"),
+          ("2021-11-07T00:00", "2021-11-07T04:00"), ("2021-11-07T04:00", "2021-11-07T05:00")]),
 ]
 
 

@@ -28,8 +28,13 @@ def _assigner(kind, size, slide, offset):
 @pytest.mark.parametrize("kat", KATS, ids=[f"{k['op']}:{k['src'].split('/')[-1]}" for k in KATS])
 def test_slice_assigner_known_answers(kat):
     a = _assigner(*kat["assigner"])
+    if "zone" in kat:
+        a = a.in_zone(kat["zone"])
     for arg, want in kat["cases"]:
-        if kat["op"] == "slice_end":
+        if kat["op"] == "dst_slice":  # assertSliceStartEnd(start, end, epoch, assigner)
+            se = a.assign_slice_end(arg)
+            assert [a.get_window_start(se), se] == want
+        elif kat["op"] == "slice_end":
             assert a.assign_slice_end(arg) == want
             iv = a.get_slice_end_interval()  # the oracle's restatement agrees
             assert O.window_start_with_offset(arg, a.offset, iv) + iv == want
@@ -75,7 +80,7 @@ def test_sql_eligible_builtin_aggregates():
 @pytest.mark.parametrize("change,reason", [
     (dict(has_distinct=True), "DISTINCT"),
     (dict(needs_retraction=True), "retraction"),
-    (dict(shift_time_zone="Asia/Shanghai"), "TIMESTAMP_LTZ"),
+    (dict(shift_time_zone="Mars/Olympus_Mons"), "shift time zone"),
     (dict(is_event_time=False), "processing-time"),
     (dict(aggs=[("FIRST_VALUE", 0, "BIGINT")]), "not a built-in GPU aggregate"),
     (dict(aggs=[("MIN", 0, "FLOAT")], value_types=["FLOAT"]), "FLOAT"),
@@ -87,6 +92,11 @@ def test_sql_fallback_reasons(change, reason):
     kw.update(change)
     ok, why = sqlo.is_gpu_eligible(**kw)
     assert not ok and reason in why
+
+
+def test_sql_timestamp_ltz_windows_are_eligible():
+    for zone in ("Asia/Shanghai", "America/Los_Angeles", "UTC"):
+        assert sqlo.is_gpu_eligible(**dict(SQL_OK, shift_time_zone=zone)) == (True, "")
 
 
 def test_sql_processing_time_assigner_is_not_eligible():
@@ -104,6 +114,8 @@ DS_OK = dict(assigner=TumblingEventTimeWindows.of(5000), trigger=EventTimeTrigge
 
 def test_datastream_eligible():
     assert dso.is_gpu_eligible(**DS_OK) == (True, "")
+    # allowedLateness and sideOutputLateData (WindowOperator.java:609-682, :440-446)
+    assert dso.is_gpu_eligible(**dict(DS_OK, allowed_lateness=1000, late_data_output_tag="late")) == (True, "")
     assert dso.is_gpu_eligible(SlidingEventTimeWindows.of(6000, 2000), EventTimeTrigger(), ("max", "DOUBLE"))[0]
 
 
@@ -116,8 +128,7 @@ class _Sessions:  # a merging assigner (EventTimeSessionWindows)
 
 
 @pytest.mark.parametrize("change,reason", [
-    (dict(allowed_lateness=1000), "lateness"),
-    (dict(late_data_output_tag="late"), "side output"),
+    (dict(allowed_lateness=-1), "lateness cannot be negative"),
     (dict(evictor=object()), "evictor"),
     (dict(trigger=_CountTrigger()), "custom trigger"),
     (dict(assigner=_Sessions()), "assigner"),

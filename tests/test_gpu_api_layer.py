@@ -33,7 +33,8 @@ def _slice_assigner(c):
         a = SliceAssigners.hopping(0, c["size_ms"], c["slide_ms"])
     else:
         a = SliceAssigners.cumulative(0, c["size_ms"], c["slide_ms"])
-    return a.with_offset(c.get("offset_ms", 0)) if c.get("offset_ms") else a
+    a = a.with_offset(c.get("offset_ms", 0)) if c.get("offset_ms") else a
+    return a.in_zone(c["shift_zone"]) if c.get("shift_zone") else a
 
 
 class SqlOperatorAdapter:
@@ -75,8 +76,11 @@ class DataStreamOperatorAdapter:
         kind, _, typ = c["aggs"][0]
         self.kw = dict(assigner=assigner, trigger=EventTimeTrigger.create(),
                        aggregation=(kind.lower(), {"BIGINT": "LONG", "INT": "INT", "DOUBLE": "DOUBLE"}[typ]),
-                       key_type="HOST_HASHED", state_capacity=1 << 14, max_batch_rows=1 << 12, output_capacity=1 << 12)
+                       key_type="HOST_HASHED", state_capacity=1 << 14, max_batch_rows=1 << 12, output_capacity=1 << 12,
+                       allowed_lateness=c.get("allowed_lateness_ms", 0),
+                       late_data_output_tag="late" if c.get("late_side_output") else None)
         self.op = WindowOperator(**self.kw).open()
+        self._side = []
 
     def process_batch(self, k, t, h, vals, nulls=None):
         self.op.process_batch(k, t, vals[0], key_hashes=h)
@@ -87,8 +91,15 @@ class DataStreamOperatorAdapter:
         assert np.array_equal(r["timestamp"], r["window_end"] - 1)
         return r
 
+    def side_output(self):
+        parts = self._side + [self.op.side_output()]
+        return {"key": np.concatenate([p["key"] for p in parts]), "ts": np.concatenate([p["timestamp"] for p in parts]),
+                "values": [np.concatenate([p["value"] for p in parts])]}
+
     def snapshot_restore(self):
         from flink_amd.datastream.window_operator import WindowOperator
+        if self.kw["late_data_output_tag"] is not None:
+            self._side.append(self.op.side_output())
         blob = self.op.snapshot_state()
         self.op.close()
         self.op = WindowOperator(**self.kw).open()

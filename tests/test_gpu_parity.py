@@ -88,13 +88,7 @@ def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None):
     from oracle.oracle import OracleOperator
     o = OracleOperator(cfg)
     g = WindowAggHandle(cfg)
-    sliding_ds = cfg.api == abi.API_DATASTREAM and cfg.window_kind == abi.WIN_HOP
-    restored_at = None
     for bi, (k, t, iv, dv, wm) in enumerate(batches):
-        if sliding_ds and restored_at is not None and bi == restored_at + 1:
-            # the sliding-window restore deviation (test_rescale_restore_by_key_group docstring)
-            keep = t > batches[restored_at][4]
-            k, t, iv, dv = k[keep], t[keep], iv[keep], dv[keep]
         vals = [iv, dv.view(np.int64)]
         nb = nulls[bi] if nulls is not None else None
         o.process_batch(k, t, vals, nb)
@@ -107,12 +101,19 @@ def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None):
         got = _rows(g.results(reset=True), cfg, double_cols)
         _compare(got, want, double_cols, f"batch {bi} wm {wm}")
         if snapshot_at is not None and bi == snapshot_at:
-            restored_at = bi
             o.snapshot_restore()
             blob = g.snapshot()
             g.close()
             g = WindowAggHandle(cfg)
             g.restore(blob)
+        if cfg.late_side_output:  # late side output: the same elements, as a multiset
+            # (values: the columns the operator reads; the shim forwards the element by push/row)
+            sg, so = g.late_records(), o.side_output()
+            used = sorted({cfg.aggs[a].input_col for a in range(cfg.n_aggs) if cfg.aggs[a].kind != abi.AGG_COUNT_STAR})
+            side_rows = lambda d: sorted(zip(d["key"].tolist(), d["ts"].tolist(), *[d["values"][c].tolist() for c in used]))
+            assert side_rows(sg) == side_rows(so), f"batch {bi}: late side output differs"
+            assert sorted(zip(sg["push_seq"].tolist(), sg["row"].tolist())) == \
+                sorted(zip(so["push_seq"].tolist(), so["row"].tolist())) or split > 1
     assert g.stats()["num_late_records_dropped"] == o.late_dropped
     assert g.stats()["error_flags"] == 0
     return o.late_dropped
@@ -141,6 +142,16 @@ CASES = {
                            aggs=[(abi.AGG_MAX, 0, I64)]),
     "ds_sliding_min_double": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=4000, slide_ms=1000,
                                   aggs=[(abi.AGG_MIN, 1, F64)]),
+    # DataStream allowedLateness (WindowOperator.java:609-682): fired windows keep their state until
+    # maxTimestamp + lateness and fire again per late element (EventTimeTrigger.onElement)
+    "ds_tumble_lateness": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_TUMBLE, size_ms=4000, allowed_lateness_ms=3000,
+                               aggs=[(abi.AGG_SUM, 0, I64)]),
+    "ds_tumble_lateness_double_sum": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_TUMBLE, size_ms=3000,
+                                          allowed_lateness_ms=1500, aggs=[(abi.AGG_SUM, 1, F64)]),
+    "ds_sliding_lateness_side_output": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000,
+                                            allowed_lateness_ms=2500, late_side_output=True, aggs=[(abi.AGG_MAX, 0, I64)]),
+    "ds_sliding_side_output": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=4000, slide_ms=1000,
+                                   late_side_output=True, aggs=[(abi.AGG_MIN, 1, F64)]),
 }
 
 
@@ -165,10 +176,45 @@ def test_random_stream_matches_oracle(name):
     kw = CASES[name]
     late = _run_both(_cfg(kw), _stream(zlib.crc32(name.encode()) % 1000, 60000, 700, ooo=2 * kw["size_ms"] + 1500,
                                        step_ms=1500, n_wm=30), _double_cols(kw))
-    assert late > 0  # the stream exercises the late-record paths
+    assert late > 0 or kw.get("late_side_output")  # the stream exercises the late-record paths
 
 
-@pytest.mark.parametrize("name", ["sql_hop", "sql_cumulate_countstar", "ds_sliding_max"])
+# TIMESTAMP_LTZ windows across daylight-saving changes: slices on the zone's wall clock, timers at
+# toEpochMillsForTimer (gap -> first skipped hour, overlap -> the later instant), next trigger
+# watermarks through the zone (TimeWindowUtil.java:52-211); bit-exact against the oracle.
+LTZ_CASES = {
+    "tumble_1h": dict(window_kind=abi.WIN_TUMBLE, size_ms=3600000,
+                      aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MAX, 0, I64)]),
+    "hop_2h_30min": dict(window_kind=abi.WIN_HOP, size_ms=7200000, slide_ms=1800000, count_star_index=0,
+                         aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64)]),
+    "cumulate_4h_1h": dict(window_kind=abi.WIN_CUMULATE, size_ms=4 * 3600000, slide_ms=3600000, count_star_index=0,
+                           aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_MIN, 0, I64), (abi.AGG_MAX, 0, I64)]),
+}
+
+
+def _ltz_stream(seed, t_mid, n_wm=80, per=1500, n_keys=200, step_ms=600000, ooo=3 * 3600000):
+    rng = np.random.default_rng(seed)
+    t0 = t_mid - n_wm // 2 * step_ms
+    out = []
+    for b in range(n_wm):
+        base = t0 + b * step_ms
+        ts = base + rng.integers(0, step_ms, per) - rng.integers(0, ooo, per)
+        keys = rng.integers(0, n_keys, per).astype(np.int64) * 31 + 7
+        iv = rng.integers(-1000, 1000, per).astype(np.int64)
+        out.append((keys, ts.astype(np.int64), iv, rng.random(per) * 100.0, base + step_ms - ooo // 4))
+    return out
+
+
+@pytest.mark.parametrize("zone,t_mid", [("America/Los_Angeles", 1615716000000), ("America/Los_Angeles", 1636275600000),
+                                        ("Asia/Shanghai", 1600000000000), ("Australia/Lord_Howe", 1617460200000)])
+@pytest.mark.parametrize("case", sorted(LTZ_CASES))
+def test_ltz_windows_across_dst_match_oracle(case, zone, t_mid):
+    kw = dict(LTZ_CASES[case], shift_zone=zone)
+    _run_both(_cfg(kw), _ltz_stream(zlib.crc32((case + zone).encode()) % 1000, t_mid), set(), snapshot_at=37)
+
+
+@pytest.mark.parametrize("name", ["sql_hop", "sql_cumulate_countstar", "ds_sliding_max", "ds_tumble_lateness",
+                                  "ds_sliding_lateness_side_output"])
 def test_split_pushes_snapshot_and_stale_watermarks(name):
     kw = CASES[name]
     _run_both(_cfg(kw), _stream(5, 40000, 300, ooo=2500, step_ms=1000, n_wm=24, dup_wm=True),
@@ -372,8 +418,6 @@ def test_rescale_restore_by_key_group(p_from, p_to, case):
     cfgs, hs = handles(p_from)
     ex = KeyByExchange(kh, 128)
     cut = 9
-    last_wm = None
-    sliding_ds = kw.get("api") == abi.API_DATASTREAM and kw["window_kind"] == abi.WIN_HOP
     for bi, (k, t, iv, dv, wm) in enumerate(_stream(33, 48000, 1500, ooo=2500, step_ms=1200, n_wm=20)):
         if bi == cut:  # checkpoint (flush + per-key-group state), then restart at p_to
             blobs, wms = {}, []
@@ -387,10 +431,6 @@ def test_rescale_restore_by_key_group(p_from, p_to, case):
             for h in hs:
                 h.restore_key_groups(blobs, wms)
             o.snapshot_restore()
-            if sliding_ds:
-                keep = t > last_wm
-                k, t, iv, dv = k[keep], t[keep], iv[keep], dv[keep]
-        last_wm = wm
         vals = [iv, dv.view(np.int64)]
         o.process_batch(k, t, vals)
         ex.world = len(hs)  # route for the current parallelism (slicing replaces the all-to-all)

@@ -26,9 +26,10 @@ def test_library_loads_and_exports_header_symbols():
 def test_config_struct_layout_matches_header():
     import ctypes as C
     # fw_config: 4 ints, 3 int64, 2 ints, 8 agg descs (16 B), int, 8 ints, nullable mask + phase,
-    # 4 ints + reserved, 3 int64
-    assert C.sizeof(abi.fw_config) == 16 + 24 + 8 + 128 + 4 + 32 + 8 + 16 + 4 + 24
+    # 4 ints + reserved, 3 int64; v4: lateness, side output / dst / tz_n / reserved, 2 pointers
+    assert C.sizeof(abi.fw_config) == 16 + 24 + 8 + 128 + 4 + 32 + 8 + 16 + 4 + 24 + 8 + 16 + 16
     assert abi.fw_config.state_capacity.offset == 240
+    assert abi.fw_config.tz_utc.offset == 288
     # fw_host_cols: key, ts, key_hash, 8 value and 8 null-flag pointers
     assert C.sizeof(abi.fw_host_cols) == 8 * (3 + 2 * abi.FW_MAX_COLS)
 

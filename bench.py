@@ -9,9 +9,11 @@ CFG2 (Nexmark Q7-style TUMBLE 10 s MAX(price) GROUP BY auction, 10^6 auctions) f
 = 100.7 M events, the configuration BASELINE.json quotes the metric on (configs[1]).
 
 N > 1 (torchrun, one rank per GPU, RCCL): every rank generates its slice of each global batch,
-routes rows to the key-group owner with fw_partition_by_dest + an all-to-all over xGMI (the
-keyBy exchange), min-reduces the watermark, then runs its own operator subtask.  Weak scaling:
-per-GPU events, keys and event rate stay fixed as N grows.
+routes rows to the key-group owner with fw_partition_by_dest + padded all-to-alls over xGMI (the
+keyBy exchange; the row counts stay on the device and the operator skips the padding itself),
+min-reduces the watermark on the host (gloo), then runs its own operator subtask -- no host
+synchronisation inside a step.  Weak scaling: per-GPU events, keys and event rate stay fixed as
+N grows.
 """
 import argparse
 import ctypes as C
@@ -176,10 +178,22 @@ def main():
     ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
 
     def exchange(b):
+        """Untimed helper (G_b count): the plain exchange, exact row counts."""
         if world == 1:
             return gk[b], gt[b], gv[b]
         k, t, v = ex.exchange(gk[b], gt[b], [gv[b]] if nv else [])
         return k, t, (v[0] if nv else None)
+
+    # the timed keyBy exchange is the padded one (no host round trip per step); its per-destination
+    # capacity comes from the untimed pass below (the largest share any subtask gets, + 5 %)
+    seg_cap = [0]
+
+    def push_step(b, handle):
+        if world == 1:
+            handle.push_device(gk[b], gt[b], [gv[b]] if nv else [])
+            return
+        k, t, v, rc = ex.exchange_padded(gk[b], gt[b], [gv[b]] if nv else [], seg_cap[0])
+        handle.push_device_segments(rc, k, t, v)
 
     def global_watermark(b):
         return ex.global_watermark(watermark(b, wl["rate"]))
@@ -191,9 +205,8 @@ def main():
 
     def run(first, nsteps, handle):
         for b in range(first, first + nsteps):
-            k, t, v = exchange(b)
+            push_step(b, handle)
             wm = global_watermark(b)
-            handle.push_device(k, t, [v] if nv else [])
             handle.reset_results()       # blackhole sink: results of the previous watermark consumed
             handle.advance(wm)
 
@@ -215,6 +228,13 @@ def main():
         import math
         interval = math.gcd(wl["window"][1], wl["window"][2])
     groups = []
+    if world > 1:
+        mx = 0
+        for b in range(total_steps):
+            _, _, _, cnt = ex.partition(gk[b], gt[b], [])
+            mx = max(mx, int(cnt.max()))
+        mx = ex.global_max(mx)  # every subtask sizes its segments alike
+        seg_cap[0] = mx + mx // 20 + 256
     for b in range(args.warmup, total_steps):
         k, t, _ = exchange(b)
         sl = torch.div(t, interval, rounding_mode="floor")
@@ -248,6 +268,7 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    ex.check_capacity()
     st = h.stats()
     kt = h.kernel_times()
     if st["error_flags"]:

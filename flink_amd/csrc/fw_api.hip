@@ -192,6 +192,12 @@ struct fw_handle {
     std::vector<uint32_t> r_null;
 
     int64_t pushes_ub = 0;  // upper bound of device pending_pushes
+    // pending-push mirror: host-mapped word written by each merge launch (MergeArgs::host_mirror)
+    volatile unsigned long long* mirror = nullptr;
+    unsigned long long* d_mirror = nullptr;
+    uint64_t merge_seq = 0;         // merge launches so far
+    uint64_t pushes_total = 0;      // ingest launches so far
+    uint64_t pushes_at_merge[64] = {};  // pushes_total when merge launch (seq % 64) was issued
     bool reset_pending = false;  // fw_results_reset called: the next merge launch empties the results
     int64_t host_cur = INT64_MIN;
     KTimer* timer = nullptr;  // non-null while fw_set_profiling is on
@@ -527,6 +533,9 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->chunk_stats, 4 * h->max_nch + 4))) return rc;
     if ((rc = dalloc(&h->stamps, N_STAMPS))) return rc;
     if ((rc = dalloc(&h->tickets, 1))) return rc;
+    HIP_TRY(hipHostMalloc((void**)&h->mirror, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent));
+    *h->mirror = ~0ull;
+    HIP_TRY(hipHostGetDevicePointer((void**)&h->d_mirror, (void*)h->mirror, 0));
     HIP_TRY(hipMemsetAsync(h->tickets, 0, sizeof(Tickets), h->stream));
     HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(unsigned long long) * N_STAMPS, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
@@ -632,6 +641,8 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
 
 int launch_merge(fw_handle* h, int64_t wm, int force) {
     HIP_TRY(launch_merge_fire(merge_args(h, wm, force), h->stream, h->timer));
+    h->pushes_at_merge[h->merge_seq % 64] = h->pushes_total;
+    h->merge_seq++;
     h->reset_pending = false;  // the launch started every output slab (and the overflow) afresh
     return FW_OK;
 }
@@ -644,9 +655,17 @@ int force_flush(fw_handle* h) {
 }
 
 int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int32_t* kh, const void* const* vals,
-         const uint8_t* const* nulls) {
+         const uint8_t* const* nulls, const int64_t* seg_counts = nullptr, int64_t seg_len = 1) {
     for (int64_t o = 0; o < n; o += h->cap_rows) {
         const int64_t m = std::min(h->cap_rows, n - o);
+        if (h->pushes_ub >= FW_MAX_PENDING) {
+            // what the last completed merge launch left pending, plus the pushes issued after it
+            const unsigned long long v = *h->mirror;
+            const uint64_t seq = v >> 8;
+            if (v != ~0ull && seq < h->merge_seq && h->merge_seq - seq <= 64)
+                h->pushes_ub = std::min<int64_t>(h->pushes_ub,
+                                                 (int64_t)(v & 0xff) + (int64_t)(h->pushes_total - h->pushes_at_merge[seq % 64]));
+        }
         if (h->pushes_ub >= FW_MAX_PENDING) {
             Ctrl c;
             int rc = read_ctrl(h, &c);
@@ -675,6 +694,8 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.side_output = h->cfg.late_side_output ? 1 : 0;
         a.push_seq = h->push_seq;
         a.row0 = o;
+        a.seg_counts = seg_counts;
+        a.seg_div = make_udiv((uint64_t)std::max<int64_t>(seg_len, 1));
         a.ks = h->ks;
         a.wd = h->wd;
         a.nv = h->nv;
@@ -695,6 +716,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.ablate = h->ablate;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
+        h->pushes_total++;
     }
     h->push_seq++;
     return FW_OK;
@@ -744,6 +766,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->cells);
     hipFree(h->slot_nch);
     hipFree(h->treq);
+    if (h->mirror) hipHostFree((void*)h->mirror);
     hipFree(h->lfire);
     hipFree(h->side);
     hipFree(h->d_tz);
@@ -867,6 +890,25 @@ int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t*
             return fail(FW_E_INVALID, "nullable value column %d needs its null-flag column", v);
     }
     return push(h, n, d_key, d_ts, d_key_hash, d_values, d_nulls);
+}
+
+int fw_push_device_segments(fw_handle* h, int32_t n_segs, int64_t seg_len, const int64_t* d_seg_counts,
+                            const int64_t* d_key, const int64_t* d_ts, const int32_t* d_key_hash,
+                            const void* const* d_values, const uint8_t* const* d_nulls) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    if (n_segs < 0 || seg_len < 1 || (n_segs > 0 && !d_seg_counts)) return fail(FW_E_INVALID, "bad segments");
+    const int64_t n = (int64_t)n_segs * seg_len;
+    if (n == 0) return FW_OK;
+    if (!d_key || !d_ts) return fail(FW_E_INVALID, "null key/ts column");
+    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED && !d_key_hash) return fail(FW_E_INVALID, "key_hash column required");
+    if (h->nv > 0 && !d_values) return fail(FW_E_INVALID, "value columns required");
+    for (int s = 0; s < h->nv; s++) {
+        const int v = h->slot_col[s];
+        if (!d_values[v]) return fail(FW_E_INVALID, "value column %d is NULL", v);
+        if (((h->cfg.nullable_cols >> v) & 1u) && (!d_nulls || !d_nulls[v]))
+            return fail(FW_E_INVALID, "nullable value column %d needs its null-flag column", v);
+    }
+    return push(h, n, d_key, d_ts, d_key_hash, d_values, d_nulls, d_seg_counts, seg_len);
 }
 
 int fw_advance(fw_handle* h, int64_t watermark) {
@@ -1049,7 +1091,8 @@ int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     for (int k = 0; k < N_STAMPS && k < FW_KT_N; k++) out->merge_phase_cycles[k] = (int64_t)st[k];
     if (h->ablate & AB_FSTAMPS)  // diagnostic builds only: per-lane cycles of fire_one's parts
-        fprintf(stderr, "fire_parts lookup+merge=%llu emit=%llu next=%llu calls=%llu\n", st[8], st[9], st[10], st[11]);
+        fprintf(stderr, "fire_parts probe+merge=%llu emit=%llu expire+next=%llu claim=%llu windows=%llu\n", st[8], st[9],
+                st[10], st[11], st[12]);
     if (!h->timer) return FW_OK;
     EvTimer* t = static_cast<EvTimer*>(h->timer);
     HIP_TRY(t->resolve());

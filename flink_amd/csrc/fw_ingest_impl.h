@@ -110,7 +110,13 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         rnul[j] = 0;
 #pragma unroll
         for (int q = 0; q < NVR; q++) rv[j][q] = 0;
-        if (i < a.n) {
+        bool live = i < a.n;
+        if (live && a.seg_counts) {  // padded all-to-all buffer: skip each segment's padding
+            const uint64_t g = (uint64_t)(i + a.row0);
+            const uint64_t sg = udiv(g, a.seg_div);
+            live = (int64_t)(g - sg * a.seg_div.d) < a.seg_counts[sg];
+        }
+        if (live) {
             rk[j] = a.key[i];
             rs[j] = a.ts[i];
             if (a.khash) pre[j] = a.khash[i];

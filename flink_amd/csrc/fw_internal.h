@@ -296,6 +296,8 @@ struct IngestArgs {
     int32_t side_output;   // late side output instead of numLateRecordsDropped
     int32_t push_seq;      // fw_commit / fw_push_device call number (side-output rows)
     int64_t row0;          // row offset of this launch within its call
+    const int64_t* seg_counts;  // padded exchange buffer: valid rows per segment (nullptr: all valid)
+    UDiv seg_div;          // divisor = segment length
 };
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
 constexpr int AB_NO_SORT = 2;    // skip rank/scan/cells; store partials at their row position
@@ -348,6 +350,10 @@ struct MergeArgs {
     unsigned long long* stamps;  // [N_STAMPS] phase cycles summed over workgroups (AB_STAMPS)
     const uint64_t* lfire;   // DataStream late-fire rows (IngestArgs::lfire)
     int64_t lfire_cap;
+    // host-mapped word the launch's last workgroup sets to merge_seq << 8 | pending pushes after
+    // the launch: the host learns how full the partial buffer is without a stream sync
+    unsigned long long* host_mirror;
+    uint64_t merge_seq;
 };
 constexpr int LFW = 3 + MAX_WORDS;  // words per late-fire row
 constexpr int SOW = 3 + MAX_KCOLS;  // words per late side-output row

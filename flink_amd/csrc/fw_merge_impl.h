@@ -300,7 +300,8 @@ __device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW,
 // chains of one key may run concurrently in any order; the F_FIRED claim makes every window fire
 // exactly once.
 template <int NW, int E, bool Q>
-__device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+__device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit,
+                                   uint64_t* fst = nullptr) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
     constexpr int HB = NW <= 2 ? 8 : NW <= 4 ? 4 : 2;
@@ -308,11 +309,20 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
     int64_t we = S.slice[e];
     int ew = e;
     uint32_t nf = 0;
+    uint64_t t0 = fst ? __builtin_amdgcn_s_memtime() : 0;
+    auto lap = [&](int i) {  // diagnostic (AB_FSTAMPS): per-lane cycles of the chain's parts
+        if (!fst) return;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        fst[i] += t1 - t0;
+        t0 = t1;
+    };
     for (;;) {
         const uint32_t old = atomicOr(&S.flag[ew], F_FIRED);
         if (old & F_FIRED) break;  // fired by another chain of this key
         atomicAnd(&S.flag[ew], ~F_TIMER);
         nf++;
+        lap(3);
         uint64_t acc[NW];
         acc_identity<NW>(wd, acc);
         const int n = w.n_slices;
@@ -338,13 +348,16 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
                 if (ss[j] == s_exp) e_exp = e2;
             }
         }
+        lap(0);
         const bool nonempty = a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0;
         if (nonempty) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
+        lap(1);
         const int e2 = e_exp != -3 ? e_exp : find_entry(S, k, s_exp);
         if (e2 >= 0) atomicOr(&S.flag[e2], F_EXPIRE);
         if (!nonempty) break;
         const int64_t nx = wadd(we, w.interval);
         const int en = find_or_insert(S, k, nx, wd);
+        lap(2);
         if (en < 0) break;  // state overflow (flagged)
         if (!win_fired(w, nx, a.wm)) {
             atomicOr(&S.flag[en], F_TIMER);
@@ -541,6 +554,9 @@ __device__ void merge_finalize(const MergeArgs& a) {
     const int sel = (c->ovf_sel ^ a.reset_out) & 1;
     c->ovf_sel = sel;
     __hip_atomic_store(&c->out_count[sel ^ 1], 0ull, __ATOMIC_RELAXED, DEV_SCOPE);
+    if (a.host_mirror)  // vector store to host-mapped memory (system scope)
+        __hip_atomic_store(a.host_mirror, (unsigned long long)((a.merge_seq << 8) | (uint64_t)(do_flush ? 0 : pend)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
@@ -844,6 +860,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         }
         stm.mark(6);
         uint32_t nf = 0;
+        uint64_t fst[4] = {0, 0, 0, 0};
+        const bool fs = (a.ablate & AB_FSTAMPS) != 0;
         for (int q = tid; q < nd; q += MG_BLOCK) {
             const int e = S.due[q];
             if (KIND == KIND_DSWIN) {
@@ -851,10 +869,20 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             } else if (KIND == FW_WIN_TUMBLE) {
                 nf += fire_tumble<NW, E, Q>(a, S, e, sb, &s_emit);
             } else if (KIND == FW_WIN_HOP) {
-                nf += fire_hop_chain<NW, E, Q>(a, S, e, sb, &s_emit);
+                nf += fire_hop_chain<NW, E, Q>(a, S, e, sb, &s_emit, fs ? fst : nullptr);
             } else {
                 if (!(S.flag[e] & F_NOTHEAD)) nf += fire_cumulate_chain<NW, E, Q>(a, S, e, sb, &s_emit);
             }
+        }
+        if (fs && a.stamps) {
+            const uint32_t nfw = wave_sum_u32(nf);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                uint64_t x = fst[i];
+                for (int d = 32; d > 0; d >>= 1) x += (uint64_t)__shfl_xor((long long)x, d, 64);
+                if ((tid & 63) == 0) atomicAdd(&a.stamps[8 + i], (unsigned long long)x);
+            }
+            if ((tid & 63) == 0) atomicAdd(&a.stamps[12], (unsigned long long)nfw);
         }
         nf = wave_sum_u32(nf);
         if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);

@@ -8,11 +8,18 @@ ChannelSelectorRecordWriter.emit (flink-runtime/.../io/network/api/writer/
 ChannelSelectorRecordWriter.java:54) over Netty, and the receiving side's
 StatusWatermarkValve.inputWatermark (min over input channels, StatusWatermarkValve.java:153).
 
-Here a columnar batch is counting-sorted by destination subtask, then moved with one
-all-to-all per column (RCCL over xGMI for device batches; gloo for host batches).  Partitioning
-runs where the batch lives: device batches on the GPU (fw_partition_by_dest), host-staged
-batches with the library's host routine (fw_host_assign_key_groups) - the reference routes
-records on the sending task's CPU too.  Both use the same key-group code the kernels run.
+Here a columnar batch is counting-sorted by destination subtask, then moved with an all-to-all
+(RCCL over xGMI for device batches; gloo for host batches).  Partitioning runs where the batch
+lives: device batches on the GPU (fw_partition_by_dest), host-staged batches with the library's
+host routine (fw_host_assign_key_groups) - the reference routes records on the sending task's CPU
+too.  Both use the same key-group code the kernels run.
+
+exchange_padded is the per-step device path: the rows travel as ONE packed all-to-all of
+fixed-size per-destination segments (every row's columns side by side), the row counts as a
+second small all-to-all that stays on the device, and the receiving operator skips each
+segment's padding itself (fw_push_device_segments) -- no host synchronisation per step.  The
+watermark valve runs on the host (a gloo group over CPU tensors), as Flink's
+StatusWatermarkValve does on the receiving task, so it never waits on the GPU stream.
 """
 import ctypes as C
 
@@ -32,12 +39,18 @@ class KeyByExchange:
         self.kind = key_hash_kind
         self.max_p = max_parallelism
         self._ws = None
+        self._cpu_group = None
+        if self.world > 1 and dist.get_backend(group) != "gloo":
+            # the watermark valve's host-side group (collective creation: every rank builds the
+            # exchange at the same point)
+            self._cpu_group = dist.new_group(backend="gloo")
 
     # ---- routing ------------------------------------------------------------------------
     def partition(self, key, ts, values, key_hash=None):
         """Rows grouped by destination subtask (ascending).  Returns (key, ts, values, counts)
-        with counts[d] = rows for subtask d; stable within a destination.  ``key_hash`` (int32
-        per row) routes FW_KEYHASH_PRECOMPUTED keys, e.g. VARCHAR keys hashed by fw_key_row_hash."""
+        with counts[d] = rows for subtask d; rows keep their input order within a destination
+        (fw_partition_by_dest's scatter is stable).  ``key_hash`` (int32 per row) routes
+        FW_KEYHASH_PRECOMPUTED keys, e.g. VARCHAR keys hashed by fw_key_row_hash."""
         p = self.world
         if self.kind == abi.KEYHASH_PRECOMPUTED and key_hash is None:
             raise ValueError("precomputed-hash keys need their key_hash column")
@@ -105,11 +118,59 @@ class KeyByExchange:
             out.append(r.to(key.device) if stage else r)
         return out[0], out[1], out[2:]
 
+    def exchange_padded(self, key, ts, values, capacity):
+        """Device batches, no host round trip: every destination's rows travel in a fixed-size
+        segment of ``capacity`` rows (one equal-split all-to-all per column), the row counts in
+        one small all-to-all that stays on the device.  Returns (key, ts, values, recv_counts):
+        columns of p segments of ``capacity`` rows, segment s holding the first recv_counts[s]
+        rows subtask s sent here -- the layout fw_push_device_segments ingests.  A destination
+        with more rows than ``capacity`` is detected by check_capacity()."""
+        p, n, dev = self.world, key.numel(), key.device
+        pk, pt, pv, counts = self.partition(key, ts, values)
+        if p == 1:
+            return pk, pt, pv, counts
+        cap = int(capacity)
+        starts = torch.cumsum(counts, 0) - counts
+        j = torch.arange(cap, device=dev)
+        src = (starts[:, None] + j[None, :]).clamp_(max=max(n - 1, 0)).reshape(-1)
+        # gloo moves host tensors only (the one-GPU rehearsal stages through host memory)
+        stage = key.is_cuda and dist.get_backend(self.group) != "nccl"
+        mv = (lambda x: x.cpu()) if stage else (lambda x: x)
+        back = (lambda x: x.to(dev)) if stage else (lambda x: x)
+        rc = torch.empty_like(mv(counts))
+        dist.all_to_all_single(rc, mv(counts), group=self.group)
+        out = []
+        for col in [pk, pt] + list(pv):
+            send = mv(col.index_select(0, src))  # segment d = the rows for subtask d, padded to cap
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=self.group)
+            out.append(back(recv))
+        rc = back(rc)
+        self._check_cap = (counts.max(), cap)  # validated lazily, off the hot path
+        return out[0], out[1], out[2:], rc
+
+    def check_capacity(self):
+        """Raises if a padded exchange dropped rows (a destination got more than its capacity)."""
+        if getattr(self, "_check_cap", None) is not None:
+            m, cap = self._check_cap
+            if int(m) > cap:
+                raise RuntimeError(f"padded exchange: {int(m)} rows for one subtask > capacity {cap}")
+
+    def global_max(self, x):
+        """Max of a host integer over all subtasks (e.g. the padded exchange's capacity, which
+        every subtask must agree on)."""
+        if self.world == 1:
+            return int(x)
+        t = torch.tensor([int(x)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group if self._cpu_group is None else self._cpu_group)
+        return int(t.item())
+
     def global_watermark(self, w):
-        """StatusWatermarkValve: the combined watermark is the min over all input channels."""
+        """StatusWatermarkValve: the combined watermark is the min over all input channels.  Runs
+        on the host (gloo over CPU tensors): the watermark is a host value, like the valve's."""
         if self.world == 1:
             return int(w)
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
-        t = torch.tensor([int(w)], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        g = self.group if self._cpu_group is None else self._cpu_group
+        t = torch.tensor([int(w)], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=g)
         return int(t.item())

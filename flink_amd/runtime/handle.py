@@ -97,6 +97,27 @@ class WindowAggHandle:
         # stream dies with the handle, before torch frees the tensors)
         torch.cuda.current_stream(keys.device).wait_stream(ext)
 
+    def push_device_segments(self, seg_counts, keys, ts, values=(), key_hashes=None, nulls=None):
+        """A padded exchange receive buffer (KeyByExchange.exchange_padded): len(seg_counts)
+        segments of keys.numel() // len(seg_counts) rows; segment s holds seg_counts[s] valid rows
+        (a device int64 tensor -- no host round trip)."""
+        import torch
+        p = seg_counts.numel()
+        n = keys.numel()
+        if p == 0 or n == 0:
+            return
+        ext = torch.cuda.ExternalStream(self.stream_ptr, device=keys.device)
+        ext.wait_stream(torch.cuda.current_stream(keys.device))
+        arr = (C.c_void_p * abi.FW_MAX_COLS)()
+        for c, v in enumerate(values):
+            arr[c] = v.data_ptr()
+        nul = (C.c_void_p * abi.FW_MAX_COLS)()
+        for c, v in (nulls or {}).items():
+            nul[c] = v.data_ptr()
+        check(lib().fw_push_device_segments(self._h, p, n // p, seg_counts.data_ptr(), keys.data_ptr(), ts.data_ptr(),
+                                            key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
+        torch.cuda.current_stream(keys.device).wait_stream(ext)
+
     # ---- progress / output
     def advance(self, wm):
         check(lib().fw_advance(self._h, int(wm)))

@@ -237,6 +237,14 @@ int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t*
                    const int32_t* d_key_hash, const void* const* d_values,
                    const uint8_t* const* d_nulls);
 
+/* The receive buffer of a padded all-to-all (the keyBy exchange without a host round trip for
+   the row counts): n_segs segments of seg_len rows, one per sending subtask; segment s holds
+   d_seg_counts[s] valid rows (device int64, e.g. the counts all-to-all's result), the rest is
+   padding and is never read.  Otherwise as fw_push_device. */
+int fw_push_device_segments(fw_handle* h, int32_t n_segs, int64_t seg_len, const int64_t* d_seg_counts,
+                            const int64_t* d_key, const int64_t* d_ts, const int32_t* d_key_hash,
+                            const void* const* d_values, const uint8_t* const* d_nulls);
+
 /* ---- progress / output --------------------------------------------------------------- */
 /* Late side output of a DataStream operator with late_side_output (WindowOperator.sideOutput,
    WindowOperator.java:440-446,549): the elements skipped as late for every window since the last

@@ -2,8 +2,9 @@
 
 Each rank is one operator subtask (parallelism 2, maxParallelism 128).  It generates its slice
 of every global batch (the bench's layout), routes rows to the owner of their key group through
-KeyByExchange (host partitioner + all_to_all_single), min-reduces the watermark
-(StatusWatermarkValve), and feeds a per-subtask operator.  Every batch is routed through the
+KeyByExchange (host partitioner + all_to_all_single; every other batch through the padded
+exchange the bench times: fixed-size segments per destination, counts exchanged separately),
+min-reduces the watermark (StatusWatermarkValve), and feeds a per-subtask operator.  Every batch is routed through the
 exchange, so the test checks three things:
   * every received row belongs to this subtask's key-group range
     (KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex, :93-106);
@@ -61,7 +62,15 @@ def _worker(rank, port, n_batches, n, out_q):
         rows, received = [], 0
         for b in range(n_batches):
             k, t, v = _stream(rank, b, n)
-            rk, rt, rv = ex.exchange(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)])
+            if b % 2 == 0:
+                rk, rt, rv = ex.exchange(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)])
+            else:  # the bench's padded exchange: fixed segments + device-side counts
+                cap = n  # a subtask never gets more than all of one sender's rows
+                pk, pt, pv, rc = ex.exchange_padded(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)], cap)
+                assert pk.numel() == WORLD * cap
+                keep = (torch.arange(WORLD * cap) % cap) < rc.repeat_interleave(cap)
+                rk, rt, rv = pk[keep], pt[keep], [pv[0][keep]]
+                ex.check_capacity()
             received += rk.numel()
             kgs = {key_group(abi.KEYHASH_BINROW_BIGINT, int(x), 128) for x in np.unique(rk.numpy())}
             assert all(lo <= g <= hi for g in kgs), f"rank {rank}: foreign key group"

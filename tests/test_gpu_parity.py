@@ -705,3 +705,42 @@ def test_two_phase_sharded_subtasks_match_one_phase(p):
     for op in ops:
         assert op.glob.stats()["error_flags"] == 0
         op.close()
+
+
+@pytest.mark.parametrize("name", ["sql_hop", "sql_tumble_int_aggs", "ds_tumble_lateness"])
+def test_padded_segments_ingest_matches_oracle(name):
+    """fw_push_device_segments (the padded all-to-all receive buffer of the bench's exchange):
+    segments of a fixed capacity whose tails hold garbage rows (keys of foreign key groups, wild
+    timestamps) that must never be read; results equal the oracle fed only the valid rows."""
+    torch = _torch_cuda()
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = CASES[name]
+    cfg = _cfg(kw, parallelism=2, subtask_index=1, key_hash=abi.KEYHASH_LONG)
+    g, o = WindowAggHandle(cfg), OracleOperator(cfg)
+    from flink_amd._native import lib
+    rng = np.random.default_rng(3)
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(9, 30000, 400, ooo=2500, step_ms=1000, n_wm=12)):
+        mine = np.array([lib().fw_host_key_group(abi.KEYHASH_LONG, int(x), 0, 128) >= 64 for x in k])
+        k, t, iv, dv = k[mine], t[mine], iv[mine], dv[mine]
+        nseg, cap = 3, len(k) + 50
+        cuts = np.sort(rng.integers(0, len(k) + 1, nseg - 1))
+        parts = np.split(np.arange(len(k)), cuts)
+        counts = np.array([len(p) for p in parts], np.int64)
+        assert counts.max() <= cap
+        cols = {c: np.zeros(nseg * cap, np.int64) for c in ("k", "t", "i", "d")}
+        for c in cols:  # garbage everywhere first: foreign keys, timestamps far in the past / future
+            cols[c][:] = rng.integers(-(1 << 62), 1 << 62, nseg * cap)
+        for s_, p_ in enumerate(parts):
+            sl = slice(s_ * cap, s_ * cap + len(p_))
+            cols["k"][sl], cols["t"][sl], cols["i"][sl], cols["d"][sl] = k[p_], t[p_], iv[p_], dv[p_].view(np.int64)
+        dvc = lambda a: torch.tensor(a, device="cuda")
+        g.push_device_segments(dvc(counts), dvc(cols["k"]), dvc(cols["t"]), [dvc(cols["i"]), dvc(cols["d"])])
+        o.process_batch(k, t, [iv, dv.view(np.int64)])
+        g.advance(wm)
+        o.process_watermark(wm)
+        _compare(_rows(g.results(reset=True), cfg, _double_cols(kw)), _rows(o.results(clear=True), cfg, _double_cols(kw)),
+                 _double_cols(kw), f"{name} batch {bi}")
+    assert g.stats()["error_flags"] == 0
+    assert g.stats()["num_late_records_dropped"] == o.late_dropped
+    g.close()

@@ -34,6 +34,9 @@ HBM_PEAK_GBPS = 8000.0         # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 WORKLOADS = {
     # name: (description, window, aggs, keys per GPU, rate per GPU, value kind, key dist, input B/event)
+    # state_per_key: the operator's capacity hint, (key, slice) entries per key at the PEAK of a
+    # flush (live entries plus the batch's new slices before firing expires the old ones; live after
+    # a step: CFG2 0.94, CFG3 5.3, CFG4 0.90, CFG5 1.24); a step that outgrows it fails loudly
     "cfg2": dict(desc="Nexmark Q7-style TUMBLE(10 s) MAX(price) GROUP BY auction",
                  window=("TUMBLE", 10_000, 0), aggs=[("MAX", 0, "BIGINT")], count_star=-1,
                  keys=1_000_000, key_base=1000, rate=1_000_000, value_kind=0, dist=0, w_in=24,

@@ -202,6 +202,8 @@ struct fw_handle {
     int64_t host_cur = INT64_MIN;
     KTimer* timer = nullptr;  // non-null while fw_set_profiling is on
     int ablate = 0;           // FW_ABLATE (development timing builds only; results are wrong)
+    int fold_always = 0;      // FW_FOLD=1 (development A/B): no adaptive fold skip
+    int fill_pct = 75;        // superbucket LDS fill target (FW_FILL_PCT: development A/B)
     unsigned long long* stamps = nullptr;  // [N_STAMPS] merge phase cycles (FW_ABLATE & AB_STAMPS)
 };
 
@@ -451,9 +453,11 @@ int validate_and_plan(fw_handle* h) {
     const int kg_end = ((c.subtask_index + 1) * c.max_parallelism - 1) / c.parallelism;
     ks.n_kg = kg_end - ks.kg_start + 1;
     const int64_t cap_target = std::max<int64_t>(c.state_capacity, 1024);
-    // aim for <= ~55% occupancy of the per-superbucket LDS table (hash skew headroom)
+    // aim for <= ~75% occupancy of the per-superbucket LDS entry table at the hinted capacity (the
+    // index has 2E slots, so its load factor stays <= 38%); fewer, fuller superbuckets amortise the
+    // merge kernel's per-workgroup costs (CFG5: 4096 -> 2048 superbuckets, merge -27%)
     h->cap_e = mg_entries(h->nw_t);
-    const int64_t fill = h->cap_e * 55 / 100;
+    const int64_t fill = h->cap_e * h->fill_pct / 100;
     int64_t per_kg = (cap_target + ks.n_kg - 1) / ks.n_kg;
     int64_t sbk = next_pow2((per_kg + fill - 1) / fill);
     const int64_t max_sb = IG_MAX_SB;
@@ -695,6 +699,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.push_seq = h->push_seq;
         a.row0 = o;
         a.seg_counts = seg_counts;
+        a.fold_always = h->fold_always;
         a.seg_div = make_udiv((uint64_t)std::max<int64_t>(seg_len, 1));
         a.ks = h->ks;
         a.wd = h->wd;
@@ -744,6 +749,8 @@ int fw_create(const fw_config* cfg, fw_handle** out) {
     fw_handle* h = new fw_handle();
     h->cfg = *cfg;
     if (const char* ab = getenv("FW_ABLATE")) h->ablate = atoi(ab);
+    if (const char* fo = getenv("FW_FOLD")) h->fold_always = atoi(fo);
+    if (const char* fp = getenv("FW_FILL_PCT")) h->fill_pct = std::min(95, std::max(10, atoi(fp)));
     int rc = validate_and_plan(h);
     h->cfg.tz_utc = nullptr;  // the shift-zone table was copied (h->tz_*); never read the caller's
     h->cfg.tz_offset_ms = nullptr;

@@ -86,6 +86,11 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         return;
     }
     const int64_t cur_wm = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
+    // adaptive fold: when the LDS fold of the previous push merged < 2 % of its rows (uniform keys
+    // spread over many more groups than a chunk holds), skip it -- the merge kernel folds those
+    // rows anyway; every 8th push folds again to notice a skewed stream
+    const bool fold = a.fold_always || !(__hip_atomic_load(&ctrl->fold_skip, __ATOMIC_RELAXED, DEV_SCOPE) &&
+                        (__hip_atomic_load(&ctrl->push_count, __ATOMIC_RELAXED, DEV_SCOPE) & 7u) != 0);
     if (tid == 0) {
         *s_min = INT64_MAX;
         *s_drop = 0;
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         lrows++;
     });
     // ---- K3: fold equal (key, slice) rows, one 1024-row sub-tile at a time
-    if (!(a.ablate & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
+    if (fold && !(a.ablate & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
         constexpr int s = decltype(S)::value;
         uint32_t rh[IG_SRPT];
         __syncthreads();  // previous sub-tile's owners are done with claim/cacc
@@ -423,6 +428,8 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         ctrl->min_pending = min(ctrl->min_pending, m);
         ctrl->pending_rows += (uint64_t)r;
         ctrl->partials += (uint64_t)q;
+        if (fold) ctrl->fold_skip = q * 50 > r * 49;  // folded away fewer than 2 % of the rows
+        ctrl->push_count += 1;
         ctrl->late_dropped += (uint64_t)d;
     }
 }

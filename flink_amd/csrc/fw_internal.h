@@ -137,7 +137,8 @@ struct Ctrl {
     uint32_t error;
     int32_t push_slot;       // partial-buffer slot of the push being ingested
     uint64_t partials;       // partials written by the ingest kernels (cumulative)
-    uint32_t pad1[2];
+    uint32_t fold_skip;      // k_ingest: the last pushes' LDS fold merged (almost) nothing -> skip it
+    uint32_t push_count;     // pushes ingested (every 8th one folds regardless, to re-measure)
     int32_t ovf_sel;         // live out_count
     int32_t pad0;
     int64_t n_lfire;         // DataStream late-fire rows pending (EventTimeTrigger.onElement FIRE)
@@ -296,6 +297,7 @@ struct IngestArgs {
     int32_t side_output;   // late side output instead of numLateRecordsDropped
     int32_t push_seq;      // fw_commit / fw_push_device call number (side-output rows)
     int64_t row0;          // row offset of this launch within its call
+    int32_t fold_always;   // development (FW_FOLD=1): fold every push (no adaptive skip)
     const int64_t* seg_counts;  // padded exchange buffer: valid rows per segment (nullptr: all valid)
     UDiv seg_div;          // divisor = segment length
 };

@@ -109,6 +109,8 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->live_entries = 0;
         c->error = 0;
         c->partials = 0;
+        c->fold_skip = 0;
+        c->push_count = 0;
     }
 }
 

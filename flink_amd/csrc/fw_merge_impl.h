@@ -22,6 +22,56 @@ struct StateLds {
 
 constexpr uint32_t IDX_DEAD = 0xFFFFFFFFu;
 
+// W consecutive 8-byte words at p with 16-byte accesses: a partial row or state entry is one
+// lane's scattered record, so every load instruction touches up to 64 cache lines -- halving the
+// instruction count halves that traffic through the texture path.  Even W: p is 16-B aligned (an
+// even word offset from an aligned base).  Odd W: the lane's parity picks where the lone 8-byte
+// word sits; every lane runs the same instructions.
+template <int W>
+__device__ __forceinline__ void load_words(const uint64_t* p, uint64_t (&o)[W]) {
+    if constexpr (W % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < W / 2; k++) {
+            const ulonglong2 v = *(const ulonglong2*)(p + 2 * k);
+            o[2 * k] = v.x;
+            o[2 * k + 1] = v.y;
+        }
+    } else {
+        const bool odd = ((uintptr_t)p & 8) != 0;
+        const uint64_t one = *(odd ? p : p + (W - 1));
+        const uint64_t* q = p + (odd ? 1 : 0);
+        uint64_t pr[W - 1 > 0 ? W - 1 : 1];
+#pragma unroll
+        for (int k = 0; k < (W - 1) / 2; k++) {
+            const ulonglong2 v = *(const ulonglong2*)(q + 2 * k);
+            pr[2 * k] = v.x;
+            pr[2 * k + 1] = v.y;
+        }
+        if constexpr (W == 1) {
+            o[0] = one;
+        } else {
+            o[0] = odd ? one : pr[0];
+#pragma unroll
+            for (int w = 1; w < W - 1; w++) o[w] = odd ? pr[w - 1] : pr[w];
+            o[W - 1] = odd ? pr[W - 2] : one;
+        }
+    }
+}
+template <int W>
+__device__ __forceinline__ void store_words(uint64_t* p, const uint64_t (&v)[W]) {
+    if constexpr (W % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < W / 2; k++) *(ulonglong2*)(p + 2 * k) = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+    } else {
+        const bool odd = ((uintptr_t)p & 8) != 0;
+        *(odd ? p : p + (W - 1)) = odd ? v[0] : v[W - 1];
+        uint64_t* q = p + (odd ? 1 : 0);
+#pragma unroll
+        for (int k = 0; k < (W - 1) / 2; k++)
+            *(ulonglong2*)(q + 2 * k) = make_ulonglong2(odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
+    }
+}
+
 template <int NW, int E>
 __device__ __forceinline__ void init_entry_acc(StateLds<NW, E>& S, int e, const WordDesc& wd) {
 #pragma unroll
@@ -638,7 +688,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     __syncthreads();
     const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
     if (!(a.ablate & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
-        const uint64_t* p = st + (size_t)e * PWE;
+        uint64_t p[PWE];
+        load_words<PWE>(st + (size_t)e * PWE, p);
         const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
         S.key[e] = k;
         S.slice[e] = s;
@@ -703,7 +754,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                             if ((uint32_t)__shfl((int)excl, lo + step, 64) <= x) lo += step;
                         const uint64_t* p = seg + (size_t)((uint32_t)__shfl((int)adj, lo, 64) + x) * PW;
 #pragma unroll
-                        for (int w = 0; w < PW; w++) row[u][w] = p[w];
+                        load_words<PW>(p, row[u]);
                     }
                     if (gst) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -912,7 +963,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             const uint32_t f = f0 & ((f0 & F_EXPIRE) ? F_TIMER : (F_ACC | F_TIMER | F_CLEAN));
             if (!f) continue;
             const int pos = wave_claim(&s_nlive);
-            uint64_t* p = so + (size_t)pos * PWE;
+            uint64_t p[PWE];
             p[0] = (uint64_t)S.key[e];
             p[1] = (uint64_t)S.slice[e];
             p[2] = f;
@@ -926,6 +977,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
 #pragma unroll
                 for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];
             }
+            store_words<PWE>(so + (size_t)pos * PWE, p);
             if (f & F_TIMER) lnm = min(lnm, S.slice[e]);
             if (KIND == KIND_DSWIN && (f & F_CLEAN)) lnm = min(lnm, wadd(ds_cleanup_time(a.win, S.slice[e]), 1));
         }

@@ -905,15 +905,19 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             }
         __syncthreads();
         const int nd = min(S.ndue, E);
+        // due entries are dealt lane-major over the waves (lane l of wave w takes l * 16 + w):
+        // fewer due entries than threads then still keep every wave busy, so each SIMD has four
+        // waves of dependent LDS chains to interleave instead of two
+        const int qlane = (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
         if (KIND == FW_WIN_CUMULATE) {
-            for (int q = tid; q < nd; q += MG_BLOCK) mark_cumulate_successor<NW, E>(a, S, S.due[q]);
+            for (int q = qlane; q < nd; q += MG_BLOCK) mark_cumulate_successor<NW, E>(a, S, S.due[q]);
             __syncthreads();
         }
         stm.mark(6);
         uint32_t nf = 0;
         uint64_t fst[4] = {0, 0, 0, 0};
         const bool fs = (a.ablate & AB_FSTAMPS) != 0;
-        for (int q = tid; q < nd; q += MG_BLOCK) {
+        for (int q = qlane; q < nd; q += MG_BLOCK) {
             const int e = S.due[q];
             if (KIND == KIND_DSWIN) {
                 nf += fire_ds<NW, E>(a, S, e, sb, &s_emit);

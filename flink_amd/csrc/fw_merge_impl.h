@@ -753,7 +753,6 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         for (int step = 32; step > 0; step >>= 1)
                             if ((uint32_t)__shfl((int)excl, lo + step, 64) <= x) lo += step;
                         const uint64_t* p = seg + (size_t)((uint32_t)__shfl((int)adj, lo, 64) + x) * PW;
-#pragma unroll
                         load_words<PW>(p, row[u]);
                     }
                     if (gst) {

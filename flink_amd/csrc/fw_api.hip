@@ -1097,6 +1097,9 @@ int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
     HIP_TRY(hipMemcpyAsync(st, h->stamps, sizeof st, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     for (int k = 0; k < N_STAMPS && k < FW_KT_N; k++) out->merge_phase_cycles[k] = (int64_t)st[k];
+    if (h->ablate & AB_GSTAMPS)  // diagnostic builds only: thread 0's gather parts
+        fprintf(stderr, "gather_parts cells=%llu scan=%llu loads=%llu probe=%llu fold+insert=%llu seq_miss=%llu\n", st[13],
+                st[14], st[2], st[4], st[7], st[15]);
     if (h->ablate & AB_FSTAMPS)  // diagnostic builds only: per-lane cycles of fire_one's parts
         fprintf(stderr, "fire_parts probe+merge=%llu emit=%llu expire+next=%llu claim=%llu windows=%llu\n", st[8], st[9],
                 st[10], st[11], st[12]);

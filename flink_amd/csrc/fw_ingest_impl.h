@@ -106,34 +106,50 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     int32_t pre[RPT];
     uint32_t rnul[RPT];  // bit q: value slot q is NULL in this row
     uint32_t valid = 0;
+    // Loads are unconditional (a partial last chunk clamps its row index to the last row), so
+    // every column load of the chunk is in flight at once; liveness is a bit mask computed beside
+    // them.  Optional inputs (precomputed hashes, NULL flags, padded-segment counts) are switched
+    // per launch, outside the per-row code.
+    // Column pointers are rebased to the chunk (scalar) and rows addressed by a 32-bit offset, so
+    // all columns of a row share one offset register (saddr + voffset loads).
+    const uint32_t last = (uint32_t)min((int64_t)CH - 1, a.n - 1 - base);  // last row of the chunk
+    const int64_t* kp = a.key + base;
+    const int64_t* tp = a.ts + base;
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        const int64_t i = base + (int64_t)j * IG_BLOCK + tid;
-        rk[j] = 0;
-        rs[j] = 0;
+        const uint32_t o = (uint32_t)(j * IG_BLOCK + tid);
+        const uint32_t oc = min(o, last);
+        rk[j] = kp[oc];
+        rs[j] = tp[oc];
+#pragma unroll
+        for (int q = 0; q < NVR; q++) rv[j][q] = (q < NV && !(NV > 2 && q >= a.nv)) ? (a.vals[q] + base)[oc] : 0;
         pre[j] = 0;
         rnul[j] = 0;
-#pragma unroll
-        for (int q = 0; q < NVR; q++) rv[j][q] = 0;
-        bool live = i < a.n;
-        if (live && a.seg_counts) {  // padded all-to-all buffer: skip each segment's padding
-            const uint64_t g = (uint64_t)(i + a.row0);
-            const uint64_t sg = udiv(g, a.seg_div);
-            live = (int64_t)(g - sg * a.seg_div.d) < a.seg_counts[sg];
-        }
-        if (live) {
-            rk[j] = a.key[i];
-            rs[j] = a.ts[i];
-            if (a.khash) pre[j] = a.khash[i];
-#pragma unroll
-            for (int q = 0; q < NV; q++) {
-                if (NV > 2 && q >= a.nv) break;  // the NV = 4 / 8 variants also serve 3 / 5-7 columns
-                rv[j][q] = a.vals[q][i];
-                if (X && a.nulls[q] && a.nulls[q][i]) rnul[j] |= 1u << q;
-            }
-            valid |= 1u << j;
-        }
+        valid |= (uint32_t)(o <= last) << j;
     });
+    if (a.khash)
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            pre[j] = (a.khash + base)[min((uint32_t)(j * IG_BLOCK + tid), last)];
+        });
+    if (X)
+#pragma unroll
+        for (int q = 0; q < NV; q++) {
+            if (NV > 2 && q >= a.nv) break;
+            if (!a.nulls[q]) continue;
+            static_for<RPT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                rnul[j] |= ((a.nulls[q] + base)[min((uint32_t)(j * IG_BLOCK + tid), last)] ? 1u : 0u) << q;
+            });
+        }
+    if (a.seg_counts)  // padded all-to-all buffer: each segment's padding rows are not live
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint64_t g = (uint64_t)(base + (int64_t)j * IG_BLOCK + tid + a.row0);
+            const uint64_t sg = udiv(g, a.seg_div);
+            const int64_t cnt = a.seg_counts[sg];
+            valid &= ~((uint32_t)((int64_t)(g - sg * a.seg_div.d) >= cnt) << j);
+        });
     // arrival ordinal base of this chunk within the flush (W_Q* words; >= 1, see record_word)
     const uint32_t ord0 = (uint32_t)(slot * a.cap_rows + base) + 1u;
     // TIMESTAMP_LTZ: slices live on the shift zone's wall clock (AbstractSliceAssigner
@@ -158,18 +174,70 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     uint64_t racc[RPT][NW];
     int64_t lmin = INT64_MAX;
     uint32_t ldrop = 0, lrows = 0;
+    // Common path, branch free: a UTC SQL slice assignment of a row within 2^31 ms of the chunk
+    // base whose window is not fired and whose key group this subtask owns.  Every other row
+    // (DataStream, LTZ, GLOBAL phase, late, far-off timestamps, foreign key groups) is marked
+    // `slow` and takes the general path below, entered only by waves that have such a row: the
+    // per-row divergent branches of the general path cost as many scalar instructions as the
+    // vector work itself.
+    const bool simple = fast && !a.win.ds && !a.global && a.win.tz.n == 0;
+    uint32_t slow = simple ? 0u : valid;
+    // record words: the word op is uniform, so it is resolved once per launch into a mode and
+    // the rows only select (no per-row switch over the op)
+    int32_t wmode[NW];  // 0: the value, 1: a count of 1, 2: dkey(value), 3: general (X only)
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const int32_t op = w < a.wd.nw ? a.wd.op[w] : W_SUM_I;
+        wmode[w] = X ? 3 : op == W_CNT ? 1 : (op == W_MIN_D || op == W_MAX_D) ? 2 : 0;
+    }
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        rsb[j] = 0;
-        rm[j] = 0;
 #pragma unroll
-        for (int w = 0; w < NW; w++)
-            racc[j][w] = w >= a.wd.nw ? 0
-                         : X ? gated_word(a.wd, w, pick_col(rv[j], a.wd.col[w]), rnul[j],
-                                          ord0 + (uint32_t)(j * IG_BLOCK + tid))
-                             : record_word(a.wd.op[w], pick_col(rv[j], a.wd.col[w]), 0);
-        if (!(valid & (1u << j))) return;
-        rsb[j] = route_key(a.ks, rk[j], pre[j], &rm[j]);
+        for (int w = 0; w < NW; w++) {
+            if (w >= a.wd.nw) {
+                racc[j][w] = 0;
+                continue;
+            }
+            const uint64_t v = pick_col(rv[j], a.wd.col[w]);
+            if (X) {
+                racc[j][w] = gated_word(a.wd, w, v, rnul[j], ord0 + (uint32_t)(j * IG_BLOCK + tid));
+            } else {
+                const uint64_t dk = (uint64_t)dkey(v);
+                racc[j][w] = wmode[w] == 1 ? 1ull : wmode[w] == 2 ? dk : v;
+            }
+        }
+    });
+    // key routing with the key-hash kind resolved per launch
+    auto route_rows = [&](auto HK) {
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            rsb[j] = route_key(a.ks, rk[j], pre[j], &rm[j], decltype(HK)::value);
+        });
+    };
+    switch (a.ks.hash_kind) {
+        case KH_LONG: route_rows(std::integral_constant<int, KH_LONG>{}); break;
+        case KH_INT: route_rows(std::integral_constant<int, KH_INT>{}); break;
+        case KH_BINROW_BIGINT: route_rows(std::integral_constant<int, KH_BINROW_BIGINT>{}); break;
+        case KH_BINROW_INT: route_rows(std::integral_constant<int, KH_BINROW_INT>{}); break;
+        default: route_rows(std::integral_constant<int, KH_PRE>{}); break;
+    }
+    if (simple) static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const int32_t sb = rsb[j];
+        const uint64_t d = (uint64_t)rs[j] - (uint64_t)tbase;
+        const uint32_t d32 = (uint32_t)d;
+        const uint32_t r = d32 - udiv32(d32, a.win.slice_div32) * (uint32_t)a.win.interval;
+        const int64_t se = rs[j] - (int64_t)r + a.win.interval;
+        const bool live = (valid >> j) & 1u;
+        const bool ok = live && d < (1ull << 31) && (uint32_t)sb < (uint32_t)n_sb && (a.local || cur_wm < se - 1);
+        slow |= (uint32_t)(live && !ok) << j;
+        rs[j] = ok ? se : rs[j];
+        lmin = ok ? min(lmin, se) : lmin;
+        lrows += ok ? 1u : 0u;
+    });
+    if (__ballot(slow != 0)) static_for<RPT>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        if (!((slow >> j) & 1u)) return;
         if ((uint32_t)rsb[j] >= (uint32_t)n_sb) {  // key group not owned by this subtask
             __hip_atomic_fetch_or(&ctrl->error, ERR_KEYGROUP, __ATOMIC_RELAXED, DEV_SCOPE);
             valid &= ~(1u << j);
@@ -206,7 +274,8 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                             p[1] = rs[j];
                             p[2] = ((int64_t)a.push_seq << 32) | (int64_t)(i + a.row0);
 #pragma unroll
-                            for (int q = 0; q < NVR; q++) p[3 + q] = (int64_t)rv[j][q];
+                            for (int q = 0; q < NV; q++)  // reloaded: rv is dead after the record words
+                                p[3 + q] = (NV > 2 && q >= a.nv) ? 0 : (int64_t)a.vals[q][i];
                         } else {
                             __hip_atomic_fetch_or(&ctrl->error, ERR_LATE, __ATOMIC_RELAXED, DEV_SCOPE);
                         }

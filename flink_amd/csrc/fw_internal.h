@@ -225,8 +225,9 @@ struct KeySpace {
 // Routing of one key: m = MathUtils.murmurHash(key.hashCode()) (>= 0), key group = m % maxP
 // (KeyGroupRangeAssignment.computeKeyGroupForKeyHash), and the build's own sub-bucket inside
 // the key group from the quotient bits m / maxP (uniform, since m is a murmur hash).
-FW_HD int32_t route_key(const KeySpace& ks, int64_t key, int32_t pre, uint32_t* m_out) {
-    const uint32_t m = (uint32_t)flink_murmur_hash(java_key_hash(ks.hash_kind, key, pre));
+// `kind` overrides ks.hash_kind with a compile-time constant where the caller resolved it.
+FW_HD int32_t route_key(const KeySpace& ks, int64_t key, int32_t pre, uint32_t* m_out, int32_t kind = -1) {
+    const uint32_t m = (uint32_t)flink_murmur_hash(java_key_hash(kind >= 0 ? kind : ks.hash_kind, key, pre));
     const uint32_t q = udiv32(m, ks.maxp_div);
     const int32_t kg = (int32_t)(m - q * (uint32_t)ks.max_p);
     const uint32_t sub = q & ((1u << ks.sb_per_kg_log2) - 1u);

@@ -729,7 +729,14 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
             for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                 const int f = g * G + lane;
+                uint64_t gc0 = gst ? __builtin_amdgcn_s_memtime() : 0;
                 const uint32_t v = lane >= G ? 0u : (pi == 0 && g == wv) ? v_first : cell_at(pi, f);
+                if (gst) {  // diagnostic: cell word wait
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                    stm.acc[13] += g1 - gc0;
+                    gc0 = g1;
+                }
                 const uint32_t cnt = v >> 16;
                 uint32_t inc = cnt;
 #pragma unroll
@@ -741,6 +748,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                 const uint32_t excl = inc - cnt;
                 // segment row of this cell's first row, less the rows of the group before it
                 const uint32_t adj = (uint32_t)(cell_chunk(f) * CH + (v & 0xFFFFu)) - excl;
+                if (gst) stm.acc[14] += __builtin_amdgcn_s_memtime() - gc0;  // diagnostic: scan
                 for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
                     uint64_t row[GU][PW];
                     uint64_t g0 = gst ? __builtin_amdgcn_s_memtime() : 0;
@@ -812,6 +820,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                             if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
                         atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
                     });
+                    const uint64_t gm0 = gst ? __builtin_amdgcn_s_memtime() : 0;
                     while (miss) {  // the wave loops max(popcount) times, not GU times
                         const int um = __ffs(miss) - 1;
                         miss &= miss - 1;
@@ -835,7 +844,9 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     }
                     if (gst) {
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        stm.acc[7] += __builtin_amdgcn_s_memtime() - g0;
+                        const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                        stm.acc[7] += g1 - g0;
+                        stm.acc[15] += g1 - gm0;
                     }
                 }
             }

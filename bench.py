@@ -126,6 +126,8 @@ def main():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: time the steps without the per-launch hipEvents (no roofline)")
     ap.add_argument("--e2e-steps", type=int, default=6)
+    ap.add_argument("--kernel-timing", default="device", choices=["device", "events"],
+                    help="per-launch kernel timing: in-kernel device-clock stamps (default) or hipEvents")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
                          "one-GPU box: ranks share the GPUs round robin and the exchange is staged "
@@ -258,7 +260,10 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    h.set_profiling(not args.no_kernel_events)  # hipEvents around the launches on the operator's stream
+    # per-launch kernel times over the timed region: in-kernel device-clock stamps (block 0's start
+    # -> the grid's last workgroup's end) by default; --kernel-timing events puts hipEvents around
+    # every launch on the operator's stream instead (they idle the stream ~7 us per launch)
+    h.set_profiling(not args.no_kernel_events, mode=args.kernel_timing)
     t0 = time.perf_counter()
     run(args.warmup, args.steps, h)
     h.sync()
@@ -380,6 +385,9 @@ def main():
                          "kernel": "fw::k_ingest (K1 key group + K2 slice assign + K3 LDS segmented reduce, "
                                    "chunk-local superbucket sort)",
                          "algorithmic_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_reduce_s * 1e6,
+                         "launch_timing": ("in-kernel device clock (block 0 start -> last workgroup end), "
+                                           "every launch of the timed region" if args.kernel_timing == "device"
+                                           else "hipEvents around every launch of the timed region"),
                          "launches": red_n, "distinct_groups_per_launch": g_per_launch,
                          "partials_written_per_launch": st["partials_emitted"] / red_n,
                          "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None},

@@ -75,8 +75,10 @@ struct EvTimer final : KTimer {
             pool.pop_back();
             return e;
         }
+        // timing-only events: no system-scope fence (cache write-back + invalidate) at each
+        // record, which would otherwise add ~10 us of idle stream time around every launch
         hipEvent_t e = nullptr;
-        (void)hipEventCreate(&e);
+        (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
         return e;
     }
     bool all = false;  // also the small bookkeeping launches (FW_KT_OTHER)
@@ -205,6 +207,8 @@ struct fw_handle {
     int fold_always = 0;      // FW_FOLD=1 (development A/B): no adaptive fold skip
     int fill_pct = 75;        // superbucket LDS fill target (FW_FILL_PCT: development A/B)
     unsigned long long* stamps = nullptr;  // [N_STAMPS] merge phase cycles (FW_ABLATE & AB_STAMPS)
+    unsigned long long* kt_dev = nullptr;  // [FW_KT_N][KT_WORDS] in-kernel launch timing
+    int kt_device = 0;                     // fw_set_profiling(FW_PROF_DEVICE) is on
 };
 
 namespace {
@@ -536,12 +540,14 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->coff, h->ks.n_sb + 2))) return rc;
     if ((rc = dalloc(&h->chunk_stats, 4 * h->max_nch + 4))) return rc;
     if ((rc = dalloc(&h->stamps, N_STAMPS))) return rc;
+    if ((rc = dalloc(&h->kt_dev, FW_KT_N * KT_WORDS))) return rc;
     if ((rc = dalloc(&h->tickets, 1))) return rc;
     HIP_TRY(hipHostMalloc((void**)&h->mirror, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent));
     *h->mirror = ~0ull;
     HIP_TRY(hipHostGetDevicePointer((void**)&h->d_mirror, (void*)h->mirror, 0));
     HIP_TRY(hipMemsetAsync(h->tickets, 0, sizeof(Tickets), h->stream));
     HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(unsigned long long) * N_STAMPS, h->stream));
+    HIP_TRY(hipMemsetAsync(h->kt_dev, 0, sizeof(unsigned long long) * FW_KT_N * KT_WORDS, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_fired, 0, sizeof(uint32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->state_count, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
@@ -640,6 +646,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.reset_out = h->reset_pending;
     a.ablate = h->ablate;
     a.stamps = h->stamps;
+    a.kt = h->kt_device ? h->kt_dev + FW_KT_MERGE * KT_WORDS : nullptr;
     return a;
 }
 
@@ -719,6 +726,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.local = h->cfg.agg_phase == FW_PHASE_LOCAL;
         a.global = h->cfg.agg_phase == FW_PHASE_GLOBAL;
         a.ablate = h->ablate;
+        a.kt = h->kt_device ? h->kt_dev + FW_KT_REDUCE * KT_WORDS : nullptr;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
         h->pushes_total++;
@@ -796,6 +804,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->chunk_stats);
     hipFree(h->tickets);
     hipFree(h->stamps);
+    hipFree(h->kt_dev);
     for (int b = 0; b < 2; b++) {
         hipHostFree(h->h_key[b]);
         hipHostFree(h->h_ts[b]);
@@ -1082,10 +1091,15 @@ int fw_set_profiling(fw_handle* h, int enable) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     delete h->timer;
     h->timer = nullptr;
-    if (enable) {
+    h->kt_device = enable == FW_PROF_DEVICE;
+    HIP_TRY(hipMemsetAsync(h->kt_dev, 0, sizeof(unsigned long long) * FW_KT_N * KT_WORDS, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (enable == FW_PROF_EVENTS || enable == FW_PROF_EVENTS_ALL) {
         EvTimer* t = new EvTimer();
-        t->all = enable >= 2;
+        t->all = enable == FW_PROF_EVENTS_ALL;
         h->timer = t;
+    } else if (enable && enable != FW_PROF_DEVICE) {
+        return fail(FW_E_INVALID, "bad profiling mode %d", enable);
     }
     return FW_OK;
 }
@@ -1103,6 +1117,18 @@ int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
     if (h->ablate & AB_FSTAMPS)  // diagnostic builds only: per-lane cycles of fire_one's parts
         fprintf(stderr, "fire_parts probe+merge=%llu emit=%llu expire+next=%llu claim=%llu windows=%llu\n", st[8], st[9],
                 st[10], st[11], st[12]);
+    if (h->kt_device) {
+        unsigned long long kt[FW_KT_N * KT_WORDS];
+        HIP_TRY(hipMemcpyAsync(kt, h->kt_dev, sizeof kt, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        int khz = 0;  // rate of the constant device clock wall_clock64() counts
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->cfg.device));
+        for (int k = 0; k < FW_KT_N; k++) {
+            out->ms[k] = khz > 0 ? (double)kt[k * KT_WORDS + 1] / (double)khz : 0.0;
+            out->launches[k] = (int64_t)kt[k * KT_WORDS + 2];
+        }
+        return FW_OK;
+    }
     if (!h->timer) return FW_OK;
     EvTimer* t = static_cast<EvTimer*>(h->timer);
     HIP_TRY(t->resolve());

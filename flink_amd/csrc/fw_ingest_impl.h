@@ -79,6 +79,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     const int tid = threadIdx.x;
     Ctrl* ctrl = a.ctrl;
     const int64_t c = blockIdx.x;
+    kt_start(a.kt);
     // the push's slot in the partial buffer; k_push_stats (next launch) advances pending_pushes
     const int64_t slot = __hip_atomic_load(&ctrl->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
     if (slot >= FW_MAX_PENDING) {
@@ -500,6 +501,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         if (fold) ctrl->fold_skip = q * 50 > r * 49;  // folded away fewer than 2 % of the rows
         ctrl->push_count += 1;
         ctrl->late_dropped += (uint64_t)d;
+        kt_end(a.kt);
     }
 }
 

@@ -301,6 +301,7 @@ struct IngestArgs {
     int32_t fold_always;   // development (FW_FOLD=1): fold every push (no adaptive skip)
     const int64_t* seg_counts;  // padded exchange buffer: valid rows per segment (nullptr: all valid)
     UDiv seg_div;          // divisor = segment length
+    unsigned long long* kt;  // launch timing (fw_set_profiling FW_PROF_DEVICE): KtSlot of this kernel class
 };
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
 constexpr int AB_NO_SORT = 2;    // skip rank/scan/cells; store partials at their row position
@@ -357,6 +358,7 @@ struct MergeArgs {
     // the launch: the host learns how full the partial buffer is without a stream sync
     unsigned long long* host_mirror;
     uint64_t merge_seq;
+    unsigned long long* kt;  // launch timing (fw_set_profiling FW_PROF_DEVICE): KtSlot of this kernel class
 };
 constexpr int LFW = 3 + MAX_WORDS;  // words per late-fire row
 constexpr int SOW = 3 + MAX_KCOLS;  // words per late side-output row
@@ -381,7 +383,14 @@ struct CompactArgs {
     int64_t res_cap;
 };
 
-// Optional per-launch timing hook (fw_set_profiling): records hipEvents around launches.
+// In-kernel launch timing (fw_set_profiling FW_PROF_DEVICE): per kernel class 4 words -- the
+// constant-rate device clock (s_memrealtime) when block 0 started the current launch, the summed
+// launch durations, the launch count, spare.  Block 0 stamps the start; the last workgroup of the
+// grid (the one the launch's ticket election picks, after every other workgroup has finished)
+// adds now - start.  Unlike stream events this adds no work between launches.
+constexpr int KT_WORDS = 4;
+
+// Optional per-launch timing hook (fw_set_profiling FW_PROF_EVENTS): records hipEvents around launches.
 struct KTimer {
     virtual void mark(int kind, bool end, hipStream_t s) = 0;
     virtual ~KTimer() = default;

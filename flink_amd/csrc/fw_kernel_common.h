@@ -249,4 +249,16 @@ static __device__ bool grid_last_wg(uint32_t (*t)[32]) {
     return true;
 }
 
+// launch timing (KT_WORDS): block 0 stamps the start, the grid's last workgroup the duration
+__device__ __forceinline__ void kt_start(unsigned long long* kt) {
+    if (kt && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&kt[0], (unsigned long long)wall_clock64(), __ATOMIC_RELAXED, DEV_SCOPE);
+}
+__device__ __forceinline__ void kt_end(unsigned long long* kt) {  // one thread of the last workgroup
+    if (!kt) return;
+    const unsigned long long t0 = __hip_atomic_load(&kt[0], __ATOMIC_RELAXED, DEV_SCOPE);
+    __hip_atomic_fetch_add(&kt[1], (unsigned long long)wall_clock64() - t0, __ATOMIC_RELAXED, DEV_SCOPE);
+    __hip_atomic_fetch_add(&kt[2], 1ull, __ATOMIC_RELAXED, DEV_SCOPE);
+}
+
 }  // namespace fw

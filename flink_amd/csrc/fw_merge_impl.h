@@ -612,7 +612,10 @@ __device__ void merge_finalize(const MergeArgs& a) {
 __device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
     if (threadIdx.x != 0) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (grid_last_wg(a.tickets->c[1])) merge_finalize(a);
+    if (grid_last_wg(a.tickets->c[1])) {
+        merge_finalize(a);
+        kt_end(a.kt);
+    }
 }
 
 // rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
@@ -633,6 +636,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
 
     const int tid = threadIdx.x;
     const int sb = sb_of_block(blockIdx.x, a.n_sb);
+    kt_start(a.kt);
     Ctrl* c = a.ctrl;
     const int64_t W = a.wm;
     // control decisions; the launch's last workgroup applies them to the control block (merge_finalize)

@@ -184,8 +184,11 @@ class WindowAggHandle:
         return {f: getattr(s, f) for f, _ in abi.fw_stats._fields_}
 
     # ---- device timing (hipEvents around each launch on the handle stream)
-    def set_profiling(self, enable=True):
-        check(lib().fw_set_profiling(self._h, 1 if enable else 0))
+    def set_profiling(self, enable=True, mode="device"):
+        """Per-launch timing of the ingest and merge/fire kernels: mode "device" (in-kernel clock
+        stamps, nothing added to the stream) or "events" (hipEvents around each launch)."""
+        m = {"device": 1, "events": 2, "events_all": 3}[mode]
+        check(lib().fw_set_profiling(self._h, m if enable else 0))
 
     def kernel_times(self):
         """{kind: (ms, launches)} accumulated since set_profiling(True)."""

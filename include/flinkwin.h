@@ -270,7 +270,7 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host);
 int fw_results_reset(fw_handle* h);
 int fw_get_stats(fw_handle* h, fw_stats* out);
 
-/* ---- per-kernel device timing (hipEvents on the handle stream, around each launch) ------- */
+/* ---- per-kernel device timing (in-kernel clock stamps, or hipEvents around each launch) --- */
 /* The reference has no per-kernel profiler for this path (flame graphs and latency
    markers only); this is the MI355X-side equivalent used by bench.py for the roofline figure. */
 #define FW_KT_PARTITION 0   /* K1: key group -> superbucket row histogram per chunk            */
@@ -285,9 +285,15 @@ typedef struct {
     int64_t merge_phase_cycles[FW_KT_N];  /* diagnostic builds only (FW_ABLATE stamps): shader
                                              cycles per merge phase, summed over workgroups     */
 } fw_kernel_times;
-/* enable = 1 times the ingest and merge/fire launches, 2 also the small bookkeeping launches
-   (FW_KT_OTHER; each timed launch costs the stream two event records); 0 stops timing.  Enabling
-   resets the accumulators. */
+/* FW_PROF_DEVICE times the ingest (FW_KT_REDUCE) and merge/fire (FW_KT_MERGE) launches inside the
+   kernels: block 0 stamps the device's constant-rate clock at its start and the grid's last
+   workgroup adds the launch's duration, so nothing is inserted into the stream between launches.
+   FW_PROF_EVENTS times the same launches with hipEvents around them (each record costs the stream a
+   few microseconds of idle time); FW_PROF_EVENTS_ALL also the small bookkeeping launches
+   (FW_KT_OTHER).  0 stops timing.  Enabling resets the accumulators. */
+#define FW_PROF_DEVICE 1
+#define FW_PROF_EVENTS 2
+#define FW_PROF_EVENTS_ALL 3
 int fw_set_profiling(fw_handle* h, int enable);
 /* synchronises the handle stream, then returns the accumulated times */
 int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out);

@@ -460,7 +460,7 @@ int validate_and_plan(fw_handle* h) {
     // aim for <= ~75% occupancy of the per-superbucket LDS entry table at the hinted capacity (the
     // index has 2E slots, so its load factor stays <= 38%); fewer, fuller superbuckets amortise the
     // merge kernel's per-workgroup costs (CFG5: 4096 -> 2048 superbuckets, merge -27%)
-    h->cap_e = mg_entries(h->nw_t);
+    h->cap_e = mg_entries(h->nw_t, c.api == FW_API_DATASTREAM ? KIND_DSWIN : c.window_kind);
     const int64_t fill = h->cap_e * h->fill_pct / 100;
     int64_t per_kg = (cap_target + ks.n_kg - 1) / ks.n_kg;
     int64_t sbk = next_pow2((per_kg + fill - 1) / fill);

@@ -35,7 +35,23 @@ constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw)
 constexpr int MG_BLOCK = 1024;
 constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a time per pending push (one per thread)
 // LDS slice-state capacity (entries) per superbucket by accumulator words
-constexpr int mg_entries(int nw) { return nw <= 1 ? 4096 : nw <= 4 ? 2048 : 1024; }
+// (kind: FW_WIN_* of a SQL operator, KIND_DSWIN (3) for DataStream windows).  One accumulator word
+// and TUMBLE: 3072 entries, which leaves room for an index of 4x the entries (short probes); the
+// window kinds that keep several slices per key (HOP, CUMULATE, DataStream panes) keep 4096 entries
+// of capacity with a 2x index.
+constexpr int mg_entries(int nw, int kind) {
+    return nw <= 1 ? (kind == FW_WIN_TUMBLE ? 3072 : 4096) : nw <= 4 ? 2048 : 1024;
+}
+// LDS index slots of a table of E entries with NW accumulator words: a power of two, 4E when it
+// fits beside the entries in a workgroup's LDS, else the largest that does
+constexpr int mg_idx_slots(int nw, int e) {
+    const int entry_bytes = 8 + 8 + 4 + 8 * nw + 2;  // key, slice, flag, acc, due
+    const int room = (158 * 1024 - e * entry_bytes) / 4;
+    int n = 1;
+    while (n < 4 * e) n <<= 1;
+    while (n > room) n >>= 1;
+    return n;
+}
 
 // ---- cell table tiling.  A cell word (start | count << 16) is written once per (chunk,
 // superbucket) by the ingest workgroup of that chunk.  16 cells share one 64-B line, and the 16

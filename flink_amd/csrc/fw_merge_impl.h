@@ -9,7 +9,8 @@ namespace fw {
 // ======================================================================================
 template <int NW, int E>
 struct StateLds {
-    uint32_t idx[2 * E];   // open-addressing index: 0 empty, 1 claiming, 2+e entry e
+    static constexpr int NI = mg_idx_slots(NW, E);  // 4E slots where they fit (mg_idx_slots)
+    uint32_t idx[NI];      // open-addressing index: 0 empty, 1 claiming, 2+e entry e
     int64_t key[E];
     int64_t slice[E];
     uint32_t flag[E];
@@ -87,9 +88,9 @@ __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory")
 
 template <int NW, int E>
 __device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
-    constexpr uint32_t MASK = 2 * E - 1;
+    constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
     uint32_t h = index_hash(k, s) & MASK;
-    for (int probes = 0; probes < 2 * E;) {
+    for (int probes = 0; probes < StateLds<NW, E>::NI;) {
         const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_RELAXED, LDS_SCOPE);
         if (st == 0) return -1;
         if (st == 1) continue;  // being inserted by another lane: re-read
@@ -106,9 +107,9 @@ __device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
 template <int NW, int E>
 __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd,
                               const uint64_t* v = nullptr, uint32_t flag0 = 0, bool* inserted = nullptr) {
-    constexpr uint32_t MASK = 2 * E - 1;
+    constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
     uint32_t h = index_hash(k, s) & MASK;
-    for (int probes = 0; probes < 2 * E;) {
+    for (int probes = 0; probes < StateLds<NW, E>::NI;) {
         const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_RELAXED, LDS_SCOPE);
         if (st == 1) continue;
         if (st == 0) {
@@ -153,7 +154,7 @@ template <int NW, int E, int M>
 __device__ __forceinline__ void probe_batch(StateLds<NW, E>& S, const int64_t* k, const int64_t* s, int* e,
                                             int m = M) {
     // only the first m (<= M, uniform) lookups are needed; the others issue no LDS reads
-    constexpr uint32_t MASK = 2 * E - 1;
+    constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
     uint32_t st[M];
 #pragma unroll
     for (int j = 0; j < M; j++)
@@ -683,7 +684,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     if (gather && lane < gather_group((int)cell_pad(a.slot_nch[0])))
         v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
     // ---- load this superbucket's entries into LDS
-    for (int i = tid; i < 2 * E; i += MG_BLOCK) S.idx[i] = 0;
+    for (int i = tid; i < StateLds<NW, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
     if (tid == 0) {
         S.n = (a.ablate & AB_M_NO_LOAD) ? 0 : n0;
         S.overflow = 0;
@@ -700,13 +701,13 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         S.flag[e] = (uint32_t)p[2];
 #pragma unroll
         for (int w = 0; w < NW; w++) S.acc[w][e] = p[3 + w];
-        uint32_t h = index_hash(k, s) & (2 * E - 1);
+        uint32_t h = index_hash(k, s) & (StateLds<NW, E>::NI - 1);
         for (;;) {
             uint32_t expect = 0;
             if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 2u + (uint32_t)e, __ATOMIC_RELAXED,
                                                      __ATOMIC_RELAXED, LDS_SCOPE))
                 break;
-            h = (h + 1) & (2 * E - 1);
+            h = (h + 1) & (StateLds<NW, E>::NI - 1);
         }
     }
     __syncthreads();
@@ -1018,16 +1019,19 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
 
 template <int NW, bool Q>
 static hipError_t merge_q(const MergeArgs& a, hipStream_t s) {
-    constexpr int E = mg_entries(NW);
     if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
         if (Q) return hipErrorInvalidValue;
+        constexpr int E = mg_entries(NW, KIND_DSWIN);
         hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
         return hipGetLastError();
     }
+    // the planner sized the superbuckets for mg_entries(nw, kind) entries (fw_api.hip)
+    constexpr int ET = mg_entries(NW, FW_WIN_TUMBLE), EH = mg_entries(NW, FW_WIN_HOP), EC = mg_entries(NW, FW_WIN_CUMULATE);
+    if (a.cap_e != (a.win.kind == FW_WIN_TUMBLE ? ET : a.win.kind == FW_WIN_HOP ? EH : EC)) return hipErrorInvalidValue;
     switch (a.win.kind) {
-        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_TUMBLE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
-        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_HOP>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_merge_fire<NW, E, Q, FW_WIN_CUMULATE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
     }
     return hipGetLastError();
 }

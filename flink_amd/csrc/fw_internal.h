@@ -135,6 +135,7 @@ constexpr uint32_t ERR_LATE = 32u;      // late-fire rows or late side-output ro
 constexpr int TK_GROUPS = 16;
 struct Tickets {
     uint32_t c[2][TK_GROUPS + 1][32];
+    uint32_t work[8][32];  // k_merge_fire: next superbucket of each XCD's share (reset by the last workgroup)
 };
 
 struct Ctrl {

@@ -602,6 +602,7 @@ __device__ void merge_finalize(const MergeArgs& a) {
         c->n_lfire = 0;
     }
     c->n_treq = 0;
+    for (int q = 0; q < 8; q++) __hip_atomic_store(&a.tickets->work[q][0], 0u, __ATOMIC_RELAXED, DEV_SCOPE);
     const int sel = (c->ovf_sel ^ a.reset_out) & 1;
     c->ovf_sel = sel;
     __hip_atomic_store(&c->out_count[sel ^ 1], 0ull, __ATOMIC_RELAXED, DEV_SCOPE);
@@ -636,7 +637,6 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     __shared__ int32_t s_emit;
 
     const int tid = threadIdx.x;
-    const int sb = sb_of_block(blockIdx.x, a.n_sb);
     kt_start(a.kt);
     Ctrl* c = a.ctrl;
     const int64_t W = a.wm;
@@ -652,21 +652,35 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                           (a.force_flush || (adv && (a.always_flush || (W >= ntp && win_fired(a.win, minp, W)))));
     const bool do_fire = adv;
     const int64_t w_old = cur;
-    const int32_t n0 = a.state_count[sb];
 
     Stamps stm;
     stm.init((a.ablate & AB_STAMPS) != 0);
+    // Persistent workgroups (one per CU: the LDS table fills it) pull superbuckets from a work
+    // counter per XCD (the dispatcher deals blocks to XCDs round robin, block b to XCD b % 8), each
+    // XCD owning a contiguous eighth of the superbuckets so their cells share its L2.  A launch
+    // pays one round of workgroup start-up instead of n_sb / CUs rounds, a watermark with nothing
+    // to flush or fire costs one short pass, and skewed superbuckets balance within an XCD.  The
+    // next ticket is fetched while the current superbucket is processed.
+    const bool xq = a.n_sb % 8 == 0 && gridDim.x % 8 == 0;
+    const int nq = xq ? a.n_sb / 8 : a.n_sb;
+    uint32_t* const wq = &a.tickets->work[xq ? blockIdx.x % 8 : 0][0];
+    const int qbase = xq ? (int)(blockIdx.x % 8) * nq : 0;
+    __shared__ int32_t s_tk;
+    if (tid == 0) s_tk = (int32_t)__hip_atomic_fetch_add(wq, 1u, __ATOMIC_RELAXED, DEV_SCOPE);
+    __syncthreads();
+    for (int tk = s_tk; tk < nq; tk = s_tk) {
+    const int sb = qbase + tk;
+    const int32_t n0 = a.state_count[sb];
+    __syncthreads();  // every thread has read s_tk; the previous superbucket is done with the LDS
     if (tid == 0) {
+        s_tk = (int32_t)__hip_atomic_fetch_add(wq, 1u, __ATOMIC_RELAXED, DEV_SCOPE);  // the next one
         s_work = (ntreq > 0) || do_flush || (do_fire && win_fired(a.win, a.sb_min_timer[sb], W));
         s_fired = 0;
         s_emit = a.reset_out ? 0 : a.sb_out[sb];
         if (!s_work && a.reset_out) a.sb_out[sb] = 0;
     }
     __syncthreads();
-    if (!s_work) {
-        merge_ticket(a);
-        return;
-    }
+    if (!s_work) continue;
     const bool gather = do_flush && !(a.ablate & AB_M_NO_GATHER);
     // this thread's first cell word, loaded while the state loads (the gather below walks the
     // cells of every pending push, one cell per thread per pass, in flat tile order f:
@@ -1013,8 +1027,21 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     }
     __syncthreads();
     stm.mark(3);
+    }  // superbuckets of this workgroup (s_tk was published before the last barrier)
     stm.flush(a.stamps);
     merge_ticket(a);
+}
+
+// persistent grid of the merge kernel: one workgroup per CU, at most one per superbucket
+static unsigned merge_grid(int n_sb) {
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            n_cu = 256;
+    }
+    return (unsigned)(n_sb < n_cu ? n_sb : n_cu);
 }
 
 template <int NW, bool Q>
@@ -1022,16 +1049,16 @@ static hipError_t merge_q(const MergeArgs& a, hipStream_t s) {
     if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
         if (Q) return hipErrorInvalidValue;
         constexpr int E = mg_entries(NW, KIND_DSWIN);
-        hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
         return hipGetLastError();
     }
     // the planner sized the superbuckets for mg_entries(nw, kind) entries (fw_api.hip)
     constexpr int ET = mg_entries(NW, FW_WIN_TUMBLE), EH = mg_entries(NW, FW_WIN_HOP), EC = mg_entries(NW, FW_WIN_CUMULATE);
     if (a.cap_e != (a.win.kind == FW_WIN_TUMBLE ? ET : a.win.kind == FW_WIN_HOP ? EH : EC)) return hipErrorInvalidValue;
     switch (a.win.kind) {
-        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
-        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE>), dim3(a.n_sb), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
     }
     return hipGetLastError();
 }

@@ -667,6 +667,18 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     const int qbase = xq ? (int)(blockIdx.x % 8) * nq : 0;
     __shared__ int32_t s_tk;
     if (tid == 0) s_tk = (int32_t)__hip_atomic_fetch_add(wq, 1u, __ATOMIC_RELAXED, DEV_SCOPE);
+    // Without a flush or timer requests, a superbucket has work only if one of its timers is due:
+    // every workgroup checks its XCD's whole share in one parallel pass, and when nothing is due
+    // (a watermark that crosses no window end) the launch ends here -- results reset aside.
+    if (!do_flush && ntreq == 0) {
+        bool due = false;
+        for (int i = tid; i < nq; i += MG_BLOCK) due |= do_fire && win_fired(a.win, a.sb_min_timer[qbase + i], W);
+        if (!__syncthreads_or(due)) {
+            if (a.reset_out)
+                for (int i = tid; i < nq; i += MG_BLOCK) a.sb_out[qbase + i] = 0;
+            s_tk = nq;  // written by every thread: no superbucket for this workgroup
+        }
+    }
     __syncthreads();
     for (int tk = s_tk; tk < nq; tk = s_tk) {
     const int sb = qbase + tk;

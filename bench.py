@@ -9,8 +9,9 @@ CFG2 (Nexmark Q7-style TUMBLE 10 s MAX(price) GROUP BY auction, 10^6 auctions) f
 = 100.7 M events, the configuration BASELINE.json quotes the metric on (configs[1]).
 
 N > 1 (torchrun, one rank per GPU, RCCL): every rank generates its slice of each global batch,
-routes rows to the key-group owner with fw_partition_by_dest + padded all-to-alls over xGMI (the
-keyBy exchange; the row counts stay on the device and the operator skips the padding itself),
+routes rows to the key-group owner with fw_partition_packed + one packed padded all-to-all over
+xGMI (the keyBy exchange; the row counts stay on the device and the operator reads the packed rows
+in place, skipping the padding itself),
 min-reduces the watermark on the host (gloo), then runs its own operator subtask -- no host
 synchronisation inside a step.  Weak scaling: per-GPU events, keys and event rate stay fixed as
 N grows.
@@ -189,7 +190,7 @@ def main():
         k, t, v = ex.exchange(gk[b], gt[b], [gv[b]] if nv else [])
         return k, t, (v[0] if nv else None)
 
-    # the timed keyBy exchange is the padded one (no host round trip per step); its per-destination
+    # the timed keyBy exchange is the packed padded one (no host round trip per step); its per-destination
     # capacity comes from the untimed pass below (the largest share any subtask gets, + 5 %)
     seg_cap = [0]
 
@@ -197,8 +198,8 @@ def main():
         if world == 1:
             handle.push_device(gk[b], gt[b], [gv[b]] if nv else [])
             return
-        k, t, v, rc = ex.exchange_padded(gk[b], gt[b], [gv[b]] if nv else [], seg_cap[0])
-        handle.push_device_segments(rc, k, t, v)
+        rows, rc, w = ex.exchange_packed(gk[b], gt[b], [gv[b]] if nv else [], seg_cap[0])
+        handle.push_device_packed_segments(rc, rows, w)
 
     def global_watermark(b):
         return ex.global_watermark(watermark(b, wl["rate"]))

@@ -45,6 +45,8 @@ def lib():
         "fw_commit": (i32, [vp, i64]),
         "fw_push_device": (i32, [vp, i64, vp, vp, vp, vp, vp]),
         "fw_push_device_segments": (i32, [vp, i32, i64, vp, vp, vp, vp, vp, vp]),
+        "fw_push_device_packed_segments": (i32, [vp, i32, i64, vp, vp, i32]),
+        "fw_partition_packed": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, i64, vp]),
         "fw_advance": (i32, [vp, i64]),
         "fw_flush": (i32, [vp]),
         "fw_results": (i32, [vp, P(abi.fw_result), i32]),
@@ -81,11 +83,11 @@ def lib():
 
 # every symbol the public header declares (tests check they are exported)
 EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
-            "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_advance",
+            "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance",
             "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_key_row_hash", "fw_host_key_row_hash",
-            "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_workspace_bytes",
+            "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
             "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records"]
 

@@ -666,7 +666,7 @@ int force_flush(fw_handle* h) {
 }
 
 int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int32_t* kh, const void* const* vals,
-         const uint8_t* const* nulls, const int64_t* seg_counts = nullptr, int64_t seg_len = 1) {
+         const uint8_t* const* nulls, const int64_t* seg_counts = nullptr, int64_t seg_len = 1, int64_t stride = 1) {
     for (int64_t o = 0; o < n; o += h->cap_rows) {
         const int64_t m = std::min(h->cap_rows, n - o);
         if (h->pushes_ub >= FW_MAX_PENDING) {
@@ -688,12 +688,13 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
             }
         }
         IngestArgs a{};
-        a.key = key + o;
-        a.ts = ts + o;
+        a.stride = stride;
+        a.key = key + o * stride;
+        a.ts = ts + o * stride;
         a.khash = kh ? kh + o : nullptr;
         for (int s = 0; s < MAX_KCOLS; s++) {
             const bool live = s < h->nv;
-            a.vals[s] = live ? (const uint64_t*)vals[h->slot_col[s]] + o : nullptr;
+            a.vals[s] = live ? (const uint64_t*)vals[h->slot_col[s]] + o * stride : nullptr;
             a.nulls[s] = live && ((h->cfg.nullable_cols >> h->slot_col[s]) & 1u) ? nulls[h->slot_col[s]] + o : nullptr;
         }
         a.n = m;
@@ -925,6 +926,21 @@ int fw_push_device_segments(fw_handle* h, int32_t n_segs, int64_t seg_len, const
             return fail(FW_E_INVALID, "nullable value column %d needs its null-flag column", v);
     }
     return push(h, n, d_key, d_ts, d_key_hash, d_values, d_nulls, d_seg_counts, seg_len);
+}
+
+int fw_push_device_packed_segments(fw_handle* h, int32_t n_segs, int64_t seg_len, const int64_t* d_seg_counts,
+                                   const int64_t* d_rows, int32_t row_words) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    if (n_segs < 0 || seg_len < 1 || (n_segs > 0 && !d_seg_counts)) return fail(FW_E_INVALID, "bad segments");
+    if (row_words != 2 + h->cfg.n_value_cols) return fail(FW_E_INVALID, "row_words %d != 2 + value columns", row_words);
+    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED || h->cfg.nullable_cols)
+        return fail(FW_E_INVALID, "packed rows carry no key-hash or null-flag columns");
+    const int64_t n = (int64_t)n_segs * seg_len;
+    if (n == 0) return FW_OK;
+    if (!d_rows) return fail(FW_E_INVALID, "null rows");
+    const void* vals[FW_MAX_COLS] = {nullptr};
+    for (int c = 0; c < h->cfg.n_value_cols; c++) vals[c] = d_rows + 2 + c;
+    return push(h, n, d_rows, d_rows + 1, nullptr, vals, nullptr, d_seg_counts, seg_len, row_words);
 }
 
 int fw_advance(fw_handle* h, int64_t watermark) {

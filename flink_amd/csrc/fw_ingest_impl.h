@@ -101,7 +101,8 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
 
     // ---- coalesced column loads of the whole chunk (all in flight before the first use)
     const int64_t base = c * CH;
-    const int64_t ts0 = a.ts[base];  // chunk base for the 32-bit slice arithmetic
+    const int64_t st = a.stride;  // words per row of a column (1 unless packed rows)
+    const int64_t ts0 = a.ts[base * st];  // chunk base for the 32-bit slice arithmetic
     int64_t rk[RPT], rs[RPT];
     uint64_t rv[RPT][NVR];
     int32_t pre[RPT];
@@ -114,16 +115,16 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     // Column pointers are rebased to the chunk (scalar) and rows addressed by a 32-bit offset, so
     // all columns of a row share one offset register (saddr + voffset loads).
     const uint32_t last = (uint32_t)min((int64_t)CH - 1, a.n - 1 - base);  // last row of the chunk
-    const int64_t* kp = a.key + base;
-    const int64_t* tp = a.ts + base;
+    const int64_t* kp = a.key + base * st;
+    const int64_t* tp = a.ts + base * st;
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
         const uint32_t o = (uint32_t)(j * IG_BLOCK + tid);
-        const uint32_t oc = min(o, last);
+        const size_t oc = (size_t)min(o, last) * (size_t)st;
         rk[j] = kp[oc];
         rs[j] = tp[oc];
 #pragma unroll
-        for (int q = 0; q < NVR; q++) rv[j][q] = (q < NV && !(NV > 2 && q >= a.nv)) ? (a.vals[q] + base)[oc] : 0;
+        for (int q = 0; q < NVR; q++) rv[j][q] = (q < NV && !(NV > 2 && q >= a.nv)) ? (a.vals[q] + base * st)[oc] : 0;
         pre[j] = 0;
         rnul[j] = 0;
         valid |= (uint32_t)(o <= last) << j;
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                             p[2] = ((int64_t)a.push_seq << 32) | (int64_t)(i + a.row0);
 #pragma unroll
                             for (int q = 0; q < NV; q++)  // reloaded: rv is dead after the record words
-                                p[3 + q] = (NV > 2 && q >= a.nv) ? 0 : (int64_t)a.vals[q][i];
+                                p[3 + q] = (NV > 2 && q >= a.nv) ? 0 : (int64_t)a.vals[q][i * st];
                         } else {
                             __hip_atomic_fetch_or(&ctrl->error, ERR_LATE, __ATOMIC_RELAXED, DEV_SCOPE);
                         }

@@ -319,6 +319,8 @@ struct IngestArgs {
     const int64_t* seg_counts;  // padded exchange buffer: valid rows per segment (nullptr: all valid)
     UDiv seg_div;          // divisor = segment length
     unsigned long long* kt;  // launch timing (fw_set_profiling FW_PROF_DEVICE): KtSlot of this kernel class
+    int64_t stride;        // words between consecutive rows of a key / ts / value column (1: plain
+                           // columns; 2 + value columns: the packed rows of fw_push_device_packed_segments)
 };
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
 constexpr int AB_NO_SORT = 2;    // skip rank/scan/cells; store partials at their row position

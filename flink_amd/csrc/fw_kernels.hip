@@ -214,7 +214,8 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
                                                         const uint64_t* const* vals,
                                                         int32_t ncols, int64_t n, int32_t kind, int32_t max_p,
                                                         int32_t p, const uint32_t* offsets, int64_t* okey, int64_t* ots,
-                                                        uint64_t* const* ovals) {
+                                                        uint64_t* const* ovals, int64_t* orows = nullptr,
+                                                        int64_t seg_len = 0, const int64_t* totals = nullptr) {
     // Stable: rows keep their input order within a destination (the order a Netty channel
     // delivers them in, ChannelSelectorRecordWriter.emit :54), so a DOUBLE SUM downstream adds in
     // the same order on every run.  Each wave ranks its 64 rows per destination with ballots;
@@ -222,8 +223,14 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
     constexpr int NWV = BLOCK / 64;
     __shared__ uint32_t h[PART_MAXP];         // next output position per destination
     __shared__ uint32_t wc[NWV][PART_MAXP];   // rows per (wave, destination) of the current pass
+    __shared__ int64_t dbase[PART_MAXP];     // packed mode: first output position of each destination
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid < p) h[tid] = offsets[(size_t)blockIdx.x * p + tid];
+    if (orows && tid < p) {
+        int64_t b0 = 0;
+        for (int d = 0; d < tid; d++) b0 += totals[d];
+        dbase[tid] = b0;
+    }
     const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t b = (int64_t)blockIdx.x * PART_TILE;
     for (int j0 = 0; j0 < PART_TILE; j0 += BLOCK) {
@@ -252,7 +259,15 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
             for (int v = 0; v < NWV; v++) t += wc[v][tid];
             h[tid] += t;
         }
-        if (d >= 0) {
+        if (d >= 0 && orows) {  // packed padded segments: row (rank in d) of segment d
+            const int64_t r = (int64_t)pos - dbase[d];
+            if (r < seg_len) {
+                int64_t* o = orows + ((size_t)d * seg_len + r) * (2 + ncols);
+                o[0] = k;
+                o[1] = ts[i];
+                for (int c = 0; c < ncols; c++) o[2 + c] = (int64_t)vals[c][i];
+            }
+        } else if (d >= 0) {
             okey[pos] = k;
             ots[pos] = ts[i];
             for (int c = 0; c < ncols; c++) ovals[c][pos] = vals[c][i];
@@ -390,6 +405,35 @@ extern "C" int fw_partition_by_dest(const int64_t* d_key, const int32_t* d_key_h
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, d_ts,
                        (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
                        d_out_key, d_out_ts, (uint64_t* const*)dov);
+    return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
+}
+
+extern "C" int fw_partition_packed(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                                   const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
+                                   int32_t max_parallelism, int32_t parallelism, int64_t seg_len, int64_t* d_out_rows,
+                                   int64_t* d_counts, void* d_workspace, int64_t workspace_bytes, void* stream) {
+    if (parallelism <= 0 || parallelism > PART_MAXP || n_cols < 0 || n_cols > FW_MAX_COLS || seg_len < 1) return FW_E_INVALID;
+    if (key_hash_kind == FW_KEYHASH_PRECOMPUTED && n > 0 && !d_key_hash) return FW_E_INVALID;
+    if (key_hash_kind != FW_KEYHASH_PRECOMPUTED) d_key_hash = nullptr;
+    if (workspace_bytes < fw_partition_workspace_bytes(n, parallelism)) return FW_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (n <= 0) {
+        return hipMemsetAsync(d_counts, 0, sizeof(int64_t) * parallelism, s) == hipSuccess ? FW_OK : FW_E_DEVICE;
+    }
+    const int64_t nblk = (n + PART_TILE - 1) / PART_TILE;
+    uint32_t* counts = (uint32_t*)d_workspace;
+    const uint64_t** dv = (const uint64_t**)((char*)d_workspace + nblk * parallelism * 4);
+    dv = (const uint64_t**)(((uintptr_t)dv + 15) & ~(uintptr_t)15);
+    const void* hv[2 * FW_MAX_COLS] = {nullptr};
+    for (int c = 0; c < n_cols; c++) hv[c] = d_values[c];
+    if (hipMemcpyAsync(dv, hv, sizeof(hv), hipMemcpyHostToDevice, s) != hipSuccess) return FW_E_DEVICE;
+    hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, n, key_hash_kind,
+                       max_parallelism, parallelism, counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(BLOCK), 0, s, counts, nblk, parallelism, d_counts);
+    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, d_ts,
+                       (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
+                       (int64_t*)nullptr, (int64_t*)nullptr, (uint64_t* const*)nullptr, d_out_rows, seg_len,
+                       (const int64_t*)d_counts);
     return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
 }
 

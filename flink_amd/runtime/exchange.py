@@ -14,12 +14,15 @@ lives: device batches on the GPU (fw_partition_by_dest), host-staged batches wit
 host routine (fw_host_assign_key_groups) - the reference routes records on the sending task's CPU
 too.  Both use the same key-group code the kernels run.
 
-exchange_padded is the per-step device path: the rows travel as ONE packed all-to-all of
-fixed-size per-destination segments (every row's columns side by side), the row counts as a
-second small all-to-all that stays on the device, and the receiving operator skips each
-segment's padding itself (fw_push_device_segments) -- no host synchronisation per step.  The
-watermark valve runs on the host (a gloo group over CPU tensors), as Flink's
-StatusWatermarkValve does on the receiving task, so it never waits on the GPU stream.
+exchange_packed is the per-step device path: the partition kernel writes every row's columns
+side by side (key, ts, values) straight into fixed-size per-destination segments
+(fw_partition_packed), the rows travel as ONE all-to-all of that buffer, the row counts as a
+second small all-to-all that stays on the device, and the receiving operator reads the packed
+rows in place and skips each segment's padding itself (fw_push_device_packed_segments) -- no host
+synchronisation per step.  exchange_padded does the same with one all-to-all per column (for
+configurations whose key-hash or NULL-flag columns do not fit the packed rows).  The watermark
+valve runs on the host (a gloo group over CPU tensors), as Flink's StatusWatermarkValve does on
+the receiving task, so it never waits on the GPU stream.
 """
 import ctypes as C
 
@@ -148,6 +151,52 @@ class KeyByExchange:
         rc = back(rc)
         self._check_cap = (counts.max(), cap)  # validated lazily, off the hot path
         return out[0], out[1], out[2:], rc
+
+    def exchange_packed(self, key, ts, values, capacity):
+        """Like exchange_padded, with the rows packed: returns (rows, recv_counts, row_words) where
+        rows is p segments of ``capacity`` rows of row_words = 2 + len(values) int64 words (key,
+        ts, value bits), segment s holding the first recv_counts[s] rows subtask s sent here --
+        the buffer fw_push_device_packed_segments ingests.  One all-to-all for the rows, one for
+        the counts."""
+        p, n, dev = self.world, key.numel(), key.device
+        w = 2 + len(values)
+        cap = int(capacity)
+        vals64 = [v.view(torch.int64) if v.dtype == torch.float64 else v for v in values]
+        if key.is_cuda:
+            L = lib()
+            ws = L.fw_partition_workspace_bytes(n, p)
+            if self._ws is None or self._ws.numel() < ws or self._ws.device != dev:
+                self._ws = torch.empty(max(ws, 256), dtype=torch.uint8, device=dev)
+            send = torch.empty(p * cap * w, dtype=torch.int64, device=dev)
+            counts = torch.empty(p, dtype=torch.int64, device=dev)
+            vin = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in vals64])
+            check(L.fw_partition_packed(key.data_ptr(), None, ts.data_ptr(), vin, len(values), n, self.kind,
+                                        self.max_p, p, cap, send.data_ptr(), counts.data_ptr(),
+                                        self._ws.data_ptr(), self._ws.numel(),
+                                        torch.cuda.current_stream(dev).cuda_stream))
+        else:  # host batch: the host partition, then the same padded layout
+            pk, pt, pv, counts = self.partition(key, ts, vals64)
+            send = torch.zeros(p * cap * w, dtype=torch.int64)
+            rows = torch.stack([pk, pt] + list(pv), dim=1) if n else torch.zeros((0, w), dtype=torch.int64)
+            seg = send.view(p, cap, w)
+            o = 0
+            for d, c in enumerate(counts.tolist()):
+                m = min(c, cap)
+                seg[d, :m] = rows[o:o + m]
+                o += c
+        if p == 1:
+            self._check_cap = (counts.max(), cap)
+            return send, counts, w
+        stage = key.is_cuda and dist.get_backend(self.group) != "nccl"
+        mv = (lambda x: x.cpu()) if stage else (lambda x: x)
+        back = (lambda x: x.to(dev)) if stage else (lambda x: x)
+        rc = torch.empty_like(mv(counts))
+        dist.all_to_all_single(rc, mv(counts), group=self.group)
+        s_ = mv(send)
+        recv = torch.empty_like(s_)
+        dist.all_to_all_single(recv, s_, group=self.group)
+        self._check_cap = (counts.max(), cap)  # validated lazily, off the hot path
+        return back(recv), back(rc), w
 
     def check_capacity(self):
         """Raises if a padded exchange dropped rows (a destination got more than its capacity)."""

@@ -118,6 +118,20 @@ class WindowAggHandle:
                                             key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
         torch.cuda.current_stream(keys.device).wait_stream(ext)
 
+    def push_device_packed_segments(self, seg_counts, rows, row_words):
+        """A packed padded exchange receive buffer (KeyByExchange.exchange_packed): len(seg_counts)
+        segments of rows.numel() // (len(seg_counts) * row_words) packed rows (key, ts, value
+        words); segment s holds seg_counts[s] valid rows (a device int64 tensor)."""
+        import torch
+        p = seg_counts.numel()
+        if p == 0 or rows.numel() == 0:
+            return
+        ext = torch.cuda.ExternalStream(self.stream_ptr, device=rows.device)
+        ext.wait_stream(torch.cuda.current_stream(rows.device))
+        check(lib().fw_push_device_packed_segments(self._h, p, rows.numel() // (p * row_words), seg_counts.data_ptr(),
+                                                   rows.data_ptr(), int(row_words)))
+        torch.cuda.current_stream(rows.device).wait_stream(ext)
+
     # ---- progress / output
     def advance(self, wm):
         check(lib().fw_advance(self._h, int(wm)))

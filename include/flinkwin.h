@@ -245,6 +245,14 @@ int fw_push_device_segments(fw_handle* h, int32_t n_segs, int64_t seg_len, const
                             const int64_t* d_key, const int64_t* d_ts, const int32_t* d_key_hash,
                             const void* const* d_values, const uint8_t* const* d_nulls);
 
+/* The receive buffer of the packed padded all-to-all (fw_partition_packed): n_segs segments of
+   seg_len rows of row_words = 2 + n_value_cols int64 words each (key, ts, value columns in
+   config order); segment s holds d_seg_counts[s] valid rows.  One buffer, one all-to-all per
+   batch instead of one per column.  Not for FW_KEYHASH_PRECOMPUTED or NULL-able configurations
+   (their extra columns travel with fw_push_device_segments). */
+int fw_push_device_packed_segments(fw_handle* h, int32_t n_segs, int64_t seg_len, const int64_t* d_seg_counts,
+                                   const int64_t* d_rows, int32_t row_words);
+
 /* ---- progress / output --------------------------------------------------------------- */
 /* Late side output of a DataStream operator with late_side_output (WindowOperator.sideOutput,
    WindowOperator.java:440-446,549): the elements skipped as late for every window since the last
@@ -362,6 +370,14 @@ int fw_partition_by_dest(const int64_t* d_key, const int32_t* d_key_hash, const 
                          int64_t* d_counts, void* d_workspace, int64_t workspace_bytes,
                          void* stream);
 int64_t fw_partition_workspace_bytes(int64_t n, int32_t parallelism);
+/* fw_partition_by_dest into the send buffer of a packed padded all-to-all: destination d's rows
+   go to segment d of d_out_rows (seg_len rows of 2 + n_cols int64 words: key, ts, values), in
+   input order, at most seg_len of them (d_counts[d] still counts all: the caller checks
+   d_counts <= seg_len).  The segment padding is not written. */
+int fw_partition_packed(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                        const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
+                        int32_t max_parallelism, int32_t parallelism, int64_t seg_len, int64_t* d_out_rows,
+                        int64_t* d_counts, void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* Synthetic Nexmark-shaped generator: event i in [i0, i0+n). */
 typedef struct {

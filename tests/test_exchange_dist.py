@@ -2,8 +2,9 @@
 
 Each rank is one operator subtask (parallelism 2, maxParallelism 128).  It generates its slice
 of every global batch (the bench's layout), routes rows to the owner of their key group through
-KeyByExchange (host partitioner + all_to_all_single; every other batch through the padded
-exchange the bench times: fixed-size segments per destination, counts exchanged separately),
+KeyByExchange (host partitioner + all_to_all_single; a third of the batches through the padded
+exchange -- fixed-size segments per destination, counts exchanged separately -- and a third
+through the packed padded exchange the bench times, one buffer of (key, ts, value) rows),
 min-reduces the watermark (StatusWatermarkValve), and feeds a per-subtask operator.  Every batch is routed through the
 exchange, so the test checks three things:
   * every received row belongs to this subtask's key-group range
@@ -62,9 +63,17 @@ def _worker(rank, port, n_batches, n, out_q):
         rows, received = [], 0
         for b in range(n_batches):
             k, t, v = _stream(rank, b, n)
-            if b % 2 == 0:
+            if b % 3 == 0:
                 rk, rt, rv = ex.exchange(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)])
-            else:  # the bench's padded exchange: fixed segments + device-side counts
+            elif b % 3 == 2:  # the bench's packed padded exchange: one buffer of (key, ts, value) rows
+                cap = n
+                packed, rc, w = ex.exchange_packed(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)], cap)
+                assert w == 3 and packed.numel() == WORLD * cap * w
+                seg = packed.view(WORLD, cap, w)
+                keep = torch.arange(cap)[None, :] < rc[:, None]
+                rk, rt, rv = seg[..., 0][keep], seg[..., 1][keep], [seg[..., 2][keep]]
+                ex.check_capacity()
+            else:  # the padded exchange: fixed segments + device-side counts, one all-to-all per column
                 cap = n  # a subtask never gets more than all of one sender's rows
                 pk, pt, pv, rc = ex.exchange_padded(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)], cap)
                 assert pk.numel() == WORLD * cap

@@ -744,3 +744,80 @@ def test_padded_segments_ingest_matches_oracle(name):
     assert g.stats()["error_flags"] == 0
     assert g.stats()["num_late_records_dropped"] == o.late_dropped
     g.close()
+
+
+@pytest.mark.parametrize("name", ["sql_tumble_int_aggs", "sql_tumble_double", "sql_hop", "sql_cumulate_countstar", "ds_sliding_max"])
+def test_packed_segments_ingest_matches_oracle(name):
+    """fw_push_device_packed_segments (the packed padded all-to-all receive buffer the bench's
+    exchange ingests): (key, ts, values) rows side by side, segments of a fixed capacity whose
+    tails hold garbage rows; results equal the oracle fed only the valid rows."""
+    torch = _torch_cuda()
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = CASES[name]
+    cfg = _cfg(kw, parallelism=2, subtask_index=1, key_hash=abi.KEYHASH_LONG)
+    g, o = WindowAggHandle(cfg), OracleOperator(cfg)
+    from flink_amd._native import lib
+    rng = np.random.default_rng(5)
+    w = 2 + cfg.n_value_cols
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(11, 30000, 400, ooo=2500, step_ms=1000, n_wm=12)):
+        mine = np.array([lib().fw_host_key_group(abi.KEYHASH_LONG, int(x), 0, 128) >= 64 for x in k])
+        k, t, iv, dv = k[mine], t[mine], iv[mine], dv[mine]
+        nseg, cap = 3, len(k) + 37
+        cuts = np.sort(rng.integers(0, len(k) + 1, nseg - 1))
+        parts = np.split(np.arange(len(k)), cuts)
+        counts = np.array([len(p) for p in parts], np.int64)
+        rows = rng.integers(-(1 << 62), 1 << 62, (nseg, cap, w)).astype(np.int64)  # garbage padding
+        vals = [iv, dv.view(np.int64)][:cfg.n_value_cols]
+        for s_, p_ in enumerate(parts):
+            rows[s_, :len(p_), 0], rows[s_, :len(p_), 1] = k[p_], t[p_]
+            for c, v in enumerate(vals):
+                rows[s_, :len(p_), 2 + c] = v[p_]
+        dvc = lambda a: torch.tensor(a, device="cuda")
+        g.push_device_packed_segments(dvc(counts), dvc(rows.reshape(-1)), w)
+        o.process_batch(k, t, vals)
+        g.advance(wm)
+        o.process_watermark(wm)
+        _compare(_rows(g.results(reset=True), cfg, _double_cols(kw)), _rows(o.results(clear=True), cfg, _double_cols(kw)),
+                 _double_cols(kw), f"{name} batch {bi}")
+    assert g.stats()["error_flags"] == 0
+    assert g.stats()["num_late_records_dropped"] == o.late_dropped
+    g.close()
+
+
+def test_partition_packed_equals_partition_by_dest():
+    """fw_partition_packed writes exactly fw_partition_by_dest's per-destination row order into
+    padded packed segments (and counts every row, also past the capacity)."""
+    torch = _torch_cuda()
+    import ctypes as C
+    from flink_amd._native import check, lib
+    L = lib()
+    n, p = 50000, 4
+    rng = np.random.default_rng(8)
+    k = torch.tensor(rng.integers(0, 10**6, n), device="cuda")
+    t = torch.tensor(rng.integers(0, 10**9, n), device="cuda")
+    v = torch.tensor(rng.integers(-10**9, 10**9, n), device="cuda")
+    ws = torch.empty(L.fw_partition_workspace_bytes(n, p), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    pk, pt, pv = torch.empty_like(k), torch.empty_like(t), torch.empty_like(v)
+    c1 = torch.empty(p, dtype=torch.int64, device="cuda")
+    vin = (C.c_void_p * abi.FW_MAX_COLS)(v.data_ptr())
+    vout = (C.c_void_p * abi.FW_MAX_COLS)(pv.data_ptr())
+    check(L.fw_partition_by_dest(k.data_ptr(), None, t.data_ptr(), vin, 1, n, abi.KEYHASH_BINROW_BIGINT, 128, p,
+                                 pk.data_ptr(), pt.data_ptr(), vout, c1.data_ptr(), ws.data_ptr(), ws.numel(), s))
+    cnt = c1.cpu().numpy()
+    cap = int(cnt.max()) - 100  # the largest destination overflows its segment: its tail is dropped
+    rows = torch.full((p * cap * 3,), -7, dtype=torch.int64, device="cuda")
+    c2 = torch.empty(p, dtype=torch.int64, device="cuda")
+    check(L.fw_partition_packed(k.data_ptr(), None, t.data_ptr(), vin, 1, n, abi.KEYHASH_BINROW_BIGINT, 128, p, cap,
+                                rows.data_ptr(), c2.data_ptr(), ws.data_ptr(), ws.numel(), s))
+    torch.cuda.synchronize()
+    assert (c2.cpu().numpy() == cnt).all()
+    seg = rows.view(p, cap, 3).cpu().numpy()
+    ref = np.stack([pk.cpu().numpy(), pt.cpu().numpy(), pv.cpu().numpy()], axis=1)
+    o = 0
+    for d in range(p):
+        m = min(int(cnt[d]), cap)
+        assert (seg[d, :m] == ref[o:o + m]).all(), d
+        assert (seg[d, m:] == -7).all(), d  # padding untouched
+        o += int(cnt[d])

@@ -472,7 +472,7 @@ int validate_and_plan(fw_handle* h) {
     ks.n_sb = ks.n_kg << ks.sb_per_kg_log2;
     if (c.max_batch_rows <= 0) return fail(FW_E_INVALID, "max_batch_rows must be > 0");
     if (c.output_capacity <= 0) return fail(FW_E_INVALID, "output_capacity must be > 0");
-    h->chunk_rows = (int64_t)IG_BLOCK * ig_rpt(h->nw_t, ig_nv(h->nv));
+    h->chunk_rows = (int64_t)ig_block(h->nw_t, ig_nv(h->nv)) * ig_rpt(h->nw_t, ig_nv(h->nv));
     h->cap_rows = ((c.max_batch_rows + h->chunk_rows - 1) / h->chunk_rows) * h->chunk_rows;
     h->max_nch = h->cap_rows / h->chunk_rows;
     if (wd.has_q && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
@@ -723,7 +723,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.n_chunks = (m + h->chunk_rows - 1) / h->chunk_rows;
         a.treq = h->treq;
         a.treq_cap = h->treq_cap;
-        a.lds_bytes = IG_LDS;
+        a.lds_bytes = ig_lds(ig_block(h->nw_t, ig_nv(h->nv)));
         a.local = h->cfg.agg_phase == FW_PHASE_LOCAL;
         a.global = h->cfg.agg_phase == FW_PHASE_GLOBAL;
         a.ablate = h->ablate;

@@ -52,7 +52,7 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, 
 }
 
 // X: the configuration has nullable columns or SQL MIN/MAX(DOUBLE) words (gates, ordinals)
-template <int NV, int NW, int RPT, bool X>
+template <int NV, int NW, int RPT, bool X, int IG_BLOCK>
 __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int CH = IG_BLOCK * RPT;
     constexpr int NSUB = RPT / IG_SRPT;
@@ -509,19 +509,21 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
 template <int NV, int NW, bool X>
 static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
     constexpr int RPT = ig_rpt(NW, NV);
+    constexpr int BLK = ig_block(NW, NV);
     const int64_t nch = a.n_chunks;
     if (nch == 0) return hipSuccess;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT, X>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, IG_LDS);
+        hipError_t e = hipFuncSetAttribute((const void*)k_ingest<NV, NW, RPT, X, BLK>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, ig_lds(BLK));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     // the fold table and the histogram must fit the dynamic LDS
     if ((int64_t)(IG_HDR_WORDS + ig_hist_words(a.ks.n_sb)) * 8 + ig_fold_bytes(NW) > a.lds_bytes) return hipErrorInvalidValue;
     kt_mark(t, FW_KT_REDUCE, false, s);
-    hipLaunchKernelGGL((k_ingest<NV, NW, RPT, X>), dim3((unsigned)nch), dim3(IG_BLOCK), a.lds_bytes, s, a);
+    if (a.lds_bytes != ig_lds(BLK)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_ingest<NV, NW, RPT, X, BLK>), dim3((unsigned)nch), dim3(BLK), a.lds_bytes, s, a);
     kt_mark(t, FW_KT_REDUCE, true, s);
     return hipGetLastError();
 }

@@ -13,9 +13,12 @@ constexpr int MAX_WORDS = 8;        // accumulator words per (key, slice)
 constexpr int MAX_KCOLS = 8;        // value columns a kernel loads per record
 constexpr int FW_MAX_PENDING = 8;   // pushes buffered between two flushes
 
-// ---- ingest (K1+K2+K3): one 512-thread workgroup per chunk of IG_BLOCK * RPT rows, two
-// workgroups per CU (one loads while the other folds / sorts / stores)
-constexpr int IG_BLOCK = 512;
+// ---- ingest (K1+K2+K3): one workgroup per chunk of ig_block * RPT rows: 512 threads, two
+// workgroups per CU (one loads while the other folds / sorts / stores) while 8 rows per thread fit
+// the registers (<= 2 accumulator words); 1024 threads, one workgroup per CU, for the wider
+// accumulators, so a chunk still holds 4096 rows (half the cells, half the per-chunk histogram
+// and scan work of 2048-row chunks)
+constexpr int IG_BLOCK = 512;  // the 512-thread variant (and the default LDS budget below)
 constexpr int IG_SRPT = 2;                      // rows per thread per fold sub-tile
 constexpr int IG_SUB = IG_BLOCK * IG_SRPT;      // rows per fold sub-tile (1024)
 constexpr int IG_LDS = 78 * 1024;               // dynamic LDS per workgroup: histogram + fold/stage area
@@ -25,6 +28,8 @@ constexpr int ig_hist_words(int n_sb) { return ((n_sb + 3) >> 2) << 1; }  // 16-
 // rows per thread by accumulator words and loaded value columns (template NV): the chunk's rows
 // and partials stay in registers (<= 128 VGPRs)
 constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
+constexpr int ig_block(int nw, int nv) { return (nv > 4 || nw > 2) ? 1024 : 512; }
+constexpr int ig_lds(int block) { return block == 1024 ? 156 * 1024 : 78 * 1024; }
 // the template NV of a count of loaded value columns
 constexpr int ig_nv(int nv) { return nv <= 2 ? nv : nv <= 4 ? 4 : 8; }
 // LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)

@@ -343,7 +343,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         lrows++;
     });
     // ---- K3: fold equal (key, slice) rows, one 1024-row sub-tile at a time
-    if (fold && !(a.ablate & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
+    if (fold && !(FW_ABL(a) & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
         constexpr int s = decltype(S)::value;
         uint32_t rh[IG_SRPT];
         __syncthreads();  // previous sub-tile's owners are done with claim/cacc
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     });
     // ---- rank the partials per superbucket, scan, publish the cells
     uint32_t rdst[RPT];
-    const bool sort = !(a.ablate & AB_NO_SORT);
+    const bool sort = !(FW_ABL(a) & AB_NO_SORT);
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
         rdst[j] = (sort && (valid & (1u << j))) ? atomicAdd(&hist[rsb[j]], 1u) : (uint32_t)(j * IG_BLOCK + tid);
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     // ---- store the partials through an LDS stage so every global store is a full line
     uint64_t* out = a.parts + ((size_t)slot * a.cap_rows + (size_t)base) * PW;
     const uint32_t wrows = (uint32_t)(area_words / PW) & ~1u;
-    if (!(a.ablate & AB_NO_STORE))
+    if (!(FW_ABL(a) & AB_NO_STORE))
         for (uint32_t w0 = 0; w0 < total; w0 += wrows) {
             __syncthreads();  // fold table / previous window no longer read
             static_for<RPT>([&](auto J) {

@@ -327,6 +327,13 @@ struct IngestArgs {
     int64_t stride;        // words between consecutive rows of a key / ts / value column (1: plain
                            // columns; 2 + value columns: the packed rows of fw_push_device_packed_segments)
 };
+// Development ablations and phase stamps (FW_ABLATE) are compiled into the kernels only in a
+// diagnostic build (make DIAG=1): in the production build their checks fold away, so the hot loops
+// carry no scalar branches for them.
+#ifndef FW_DIAG
+#define FW_DIAG 0
+#endif
+#define FW_ABL(a) (FW_DIAG ? (a).ablate : 0)
 constexpr int AB_NO_FOLD = 1;    // skip the LDS fold
 constexpr int AB_NO_SORT = 2;    // skip rank/scan/cells; store partials at their row position
 constexpr int AB_NO_STORE = 4;   // skip the partial stores

@@ -207,7 +207,7 @@ __device__ __forceinline__ int64_t claim_out_row(const MergeArgs& a, int sb, int
 
 template <int NW, bool Q>
 __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
-    if (a.ablate & AB_M_NO_EMIT) return;
+    if (FW_ABL(a) & AB_M_NO_EMIT) return;
     const int64_t i = claim_out_row(a, sb, s_emit);
     if (i < 0) return;
     a.out_key[i] = key;
@@ -654,7 +654,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     const int64_t w_old = cur;
 
     Stamps stm;
-    stm.init((a.ablate & AB_STAMPS) != 0);
+    stm.init((FW_ABL(a) & AB_STAMPS) != 0);
     // Persistent workgroups (one per CU: the LDS table fills it) pull superbuckets from a work
     // counter per XCD (the dispatcher deals blocks to XCDs round robin, block b to XCD b % 8), each
     // XCD owning a contiguous eighth of the superbuckets so their cells share its L2.  A launch
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     }
     __syncthreads();
     if (!s_work) continue;
-    const bool gather = do_flush && !(a.ablate & AB_M_NO_GATHER);
+    const bool gather = do_flush && !(FW_ABL(a) & AB_M_NO_GATHER);
     // this thread's first cell word, loaded while the state loads (the gather below walks the
     // cells of every pending push, one cell per thread per pass, in flat tile order f:
     // cell_chunk(f) is the chunk, positions past the push's last chunk are padding)
@@ -712,13 +712,13 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // ---- load this superbucket's entries into LDS
     for (int i = tid; i < StateLds<NW, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
     if (tid == 0) {
-        S.n = (a.ablate & AB_M_NO_LOAD) ? 0 : n0;
+        S.n = (FW_ABL(a) & AB_M_NO_LOAD) ? 0 : n0;
         S.overflow = 0;
         S.ndue = 0;
     }
     __syncthreads();
     const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
-    if (!(a.ablate & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
+    if (!(FW_ABL(a) & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
         uint64_t p[PWE];
         load_words<PWE>(st + (size_t)e * PWE, p);
         const int64_t k = (int64_t)p[0], s = (int64_t)p[1];
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // neighbouring rows.  Rows are looked up in the LDS table (first probes batched), hits
     // folded; the misses of a lane are then inserted one at a time.
     // diagnostic (AB_GSTAMPS): thread 0's cycles in row loads / first probes / fold + insert
-    const bool gst = (a.ablate & AB_GSTAMPS) && stm.on && tid == 0;
+    const bool gst = (FW_ABL(a) & AB_GSTAMPS) && stm.on && tid == 0;
     if (gather) {
         for (int64_t pi = 0; pi < pend; pi++) {
             const int ncell = (int)cell_pad(a.slot_nch[pi]);
@@ -800,7 +800,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         stm.acc[2] += g1 - g0;
                         g0 = g1;
                     }
-                    if (a.ablate & AB_M_NO_HASH) {  // diagnostic: loads only
+                    if (FW_ABL(a) & AB_M_NO_HASH) {  // diagnostic: loads only
                         uint64_t x = 0;
 #pragma unroll
                         for (int u = 0; u < GU; u++) x ^= row[u][0] ^ row[u][1] ^ row[u][PW - 1];
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                             miss |= 1u << u;
                             return;
                         }
-                        if (a.ablate & AB_M_NO_FOLDOP) return;
+                        if (FW_ABL(a) & AB_M_NO_FOLDOP) return;
 #pragma unroll
                         for (int w = 0; w < NW; w++)
                             if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
@@ -867,7 +867,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         const uint32_t fl = flags_of(sl);
                         bool ins = false;
                         const int e = find_or_insert(S, k, sl, a.wd, &r[2], fl, &ins);
-                        if (e < 0 || ins || (a.ablate & AB_M_NO_FOLDOP)) continue;
+                        if (e < 0 || ins || (FW_ABL(a) & AB_M_NO_FOLDOP)) continue;
 #pragma unroll
                         for (int w = 0; w < NW; w++)
                             if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], r[2 + w]);
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // ---- fire: InternalTimerServiceImpl.tryAdvanceWatermark (:328-348) -> WindowAggOperator
     // .onTimer -> fireWindow + clearWindow.  One pass over the entries whose timer is due; HOP and
     // CUMULATE follow their timer chains per key (no timestamp rounds, see fire_*_chain).
-    if (do_fire && !(a.ablate & AB_M_NO_FIRE)) {
+    if (do_fire && !(FW_ABL(a) & AB_M_NO_FIRE)) {
         const int n = min(S.n, E);
         for (int e = tid; e < n; e += MG_BLOCK)
             if (KIND == KIND_DSWIN ? (((S.flag[e] & F_TIMER) && is_fired(S.slice[e], W)) ||
@@ -957,7 +957,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         stm.mark(6);
         uint32_t nf = 0;
         uint64_t fst[4] = {0, 0, 0, 0};
-        const bool fs = (a.ablate & AB_FSTAMPS) != 0;
+        const bool fs = (FW_ABL(a) & AB_FSTAMPS) != 0;
         for (int q = qlane; q < nd; q += MG_BLOCK) {
             const int e = S.due[q];
             if (KIND == KIND_DSWIN) {
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                 for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
                 emit_partial<NW, Q>(a, sb, &s_emit, S.key[e], S.slice[e], v);
             }
-    } else if (!(a.ablate & AB_M_NO_WB)) {
+    } else if (!(FW_ABL(a) & AB_M_NO_WB)) {
         for (int e = tid; e < n; e += MG_BLOCK) {
             const uint32_t f0 = S.flag[e];
             const uint32_t f = f0 & ((f0 & F_EXPIRE) ? F_TIMER : (F_ACC | F_TIMER | F_CLEAN));

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Development timing tool: times fw::k_ingest with phases switched off (FW_ABLATE bits, see
-fw_internal.h AB_*).  Only pushes (<= 6 per handle, so no merge ever reads the ablated
+fw_internal.h AB_*).  The ablations and phase stamps exist only in a diagnostic build of the
+library (make -C flink_amd/csrc DIAG=1); the production build compiles them out.  Only pushes (<= 6 per handle, so no merge ever reads the ablated
 partials); results are meaningless, only the per-kernel device times matter."""
 import ctypes as C
 import json

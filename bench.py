@@ -267,6 +267,7 @@ def main():
     h.set_profiling(not args.no_kernel_events, mode=args.kernel_timing)
     t0 = time.perf_counter()
     run(args.warmup, args.steps, h)
+    t_issued = time.perf_counter() - t0  # host time to enqueue the K steps
     h.sync()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -405,6 +406,7 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "device_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
+            "host_issue_ms_per_step": t_issued / args.steps * 1e3,
         }
         print(json.dumps(line), flush=True)
     h.close()

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <initializer_list>
+
 #include "../../include/flinkwin.h"
 #include "fw_device.h"
 
@@ -269,6 +271,44 @@ struct WordDesc {
     int32_t qfirst[MAX_WORDS];  // W_QNANLO / W_QMIN / W_QMAX: the W_QFIRST word of its group
     int32_t has_q;            // any W_Q* word (write-back normalisation, fire-time merges)
 };
+
+// Compile-time accumulator layout of a k_merge_fire variant: 4 bits per word (word 0 lowest),
+// the word's merge class -- W_SUM_I (integer add: also COUNT words), W_SUM_F, W_MIN_I (also
+// MIN_D), W_MAX_I (also MAX_D) -- or OPS_NONE past the last word.  Inside the merge a word is
+// only ever folded, merged and reset to its identity, and those agree within a class, so a
+// variant with the layout as a constant folds the per-word op switches away.  OPS_ANY: the
+// layout is read from the WordDesc at run time.
+constexpr uint32_t OPS_ANY = 0xFFFFFFFFu;
+constexpr uint32_t OPS_NONE = 15u;
+constexpr uint32_t ops_pack(std::initializer_list<int32_t> ops) {
+    uint32_t l = 0xFFFFFFFFu;
+    int w = 0;
+    for (int32_t o : ops) {
+        l &= ~(15u << (4 * w));
+        l |= (uint32_t)o << (4 * w);
+        w++;
+    }
+    return l;
+}
+// the layout of a WordDesc, OPS_ANY when a word is outside the four classes (SQL DOUBLE MIN/MAX)
+inline uint32_t ops_layout(const WordDesc& wd) {
+    if (wd.has_q || wd.nw > MAX_WORDS) return OPS_ANY;
+    uint32_t l = 0;
+    for (int w = 0; w < MAX_WORDS; w++) {
+        uint32_t c = OPS_NONE;
+        if (w < wd.nw) {
+            switch (wd.op[w]) {
+                case W_CNT: case W_CNTV: case W_SUM_I: c = W_SUM_I; break;
+                case W_SUM_F: c = W_SUM_F; break;
+                case W_MIN_I: case W_MIN_D: c = W_MIN_I; break;
+                case W_MAX_I: case W_MAX_D: c = W_MAX_I; break;
+                default: return OPS_ANY;
+            }
+        }
+        l |= c << (4 * w);
+    }
+    return l;
+}
 
 struct AggDesc {
     int32_t n;

@@ -174,7 +174,19 @@ static __device__ __noinline__ void merge_q_groups(const WordDesc& wd, const Agg
     }
 }
 
-template <int NW, bool Q>
+// word w of a merge-kernel variant with layout OPS: present?  its op (class representative)?
+template <uint32_t OPS>
+__device__ __forceinline__ bool word_on(const WordDesc& wd, int w) {
+    if constexpr (OPS == OPS_ANY) return w < wd.nw;
+    else return ((OPS >> (4 * w)) & 15u) != OPS_NONE;
+}
+template <uint32_t OPS>
+__device__ __forceinline__ int32_t word_op(const WordDesc& wd, int w) {
+    if constexpr (OPS == OPS_ANY) return wd.op[w];
+    else return (int32_t)((OPS >> (4 * w)) & 15u);
+}
+
+template <int NW, bool Q, uint32_t OPS = OPS_ANY>
 __device__ __forceinline__ void merge_slice(const WordDesc& wd, const AggDesc& ad, uint64_t* acc, const uint64_t* other) {
     if constexpr (Q) {
         // acc/other travel through memory for the out-of-line group merge
@@ -191,7 +203,7 @@ __device__ __forceinline__ void merge_slice(const WordDesc& wd, const AggDesc& a
     } else {
 #pragma unroll
         for (int w = 0; w < NW; w++)
-            if (w < wd.nw) acc[w] = reg_fold(wd.op[w], acc[w], other[w]);
+            if (word_on<OPS>(wd, w)) acc[w] = reg_fold(word_op<OPS>(wd, w), acc[w], other[w]);
     }
 }
 

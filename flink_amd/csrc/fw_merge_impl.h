@@ -73,12 +73,6 @@ __device__ __forceinline__ void store_words(uint64_t* p, const uint64_t (&v)[W])
     }
 }
 
-template <int NW, int E>
-__device__ __forceinline__ void init_entry_acc(StateLds<NW, E>& S, int e, const WordDesc& wd) {
-#pragma unroll
-    for (int w = 0; w < NW; w++) S.acc[w][e] = w < wd.nw ? word_identity(wd.op[w]) : 0;
-}
-
 // LDS publication protocol of the index: the inserting lane writes the entry's fields, then
 // (after a compiler barrier) the index word with a relaxed store.  LDS executes one wave's
 // requests in issue order and a reader's field loads depend on the index value it read, so a
@@ -104,7 +98,7 @@ __device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
 
 // Finds (k, s) or inserts it.  A new entry starts from `v` folded into the identity (or the
 // identity when v is null) with flags `flag0`; *inserted tells the caller it must not fold v again.
-template <int NW, int E>
+template <int NW, int E, uint32_t OPS = OPS_ANY>
 __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd,
                               const uint64_t* v = nullptr, uint32_t flag0 = 0, bool* inserted = nullptr) {
     constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
@@ -127,9 +121,9 @@ __device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const Wo
                 S.flag[e] = flag0;
 #pragma unroll
                 for (int w = 0; w < NW; w++)
-                    S.acc[w][e] = w < wd.nw ? (v ? reg_fold(wd.op[w], word_identity(wd.op[w]), v[w])
-                                                 : word_identity(wd.op[w]))
-                                            : 0;
+                    S.acc[w][e] = word_on<OPS>(wd, w) ? (v ? reg_fold(word_op<OPS>(wd, w), word_identity(word_op<OPS>(wd, w)), v[w])
+                                                           : word_identity(word_op<OPS>(wd, w)))
+                                                      : 0;
                 compiler_fence();
                 __hip_atomic_store(&S.idx[h], 2u + (uint32_t)e, __ATOMIC_RELAXED, LDS_SCOPE);
                 if (inserted) *inserted = true;
@@ -304,29 +298,29 @@ __device__ void emit_partial(const MergeArgs& a, int sb, int32_t* s_emit, int64_
 
 // flags that live only inside one k_merge_fire launch (dropped at write-back)
 constexpr uint32_t F_FIRED = 4u;    // HOP: window (key, this slice end) fired in this advance (chain claim)
-constexpr uint32_t F_NOTHEAD = 8u;  // CUMULATE: an earlier due step of the same window chains to this one
+constexpr uint32_t F_NOTHEAD = 8u;  // CUMULATE / HOP: an earlier due window's chain reaches this one
 constexpr uint32_t F_EXPIRE = 16u;  // HOP: slice expired by a window fired in this advance (cleared at write-back)
 
-template <int NW>
+template <int NW, uint32_t OPS = OPS_ANY>
 __device__ __forceinline__ void acc_identity(const WordDesc& wd, uint64_t* acc) {
 #pragma unroll
-    for (int i = 0; i < NW; i++) acc[i] = i < wd.nw ? word_identity(wd.op[i]) : 0;
+    for (int i = 0; i < NW; i++) acc[i] = word_on<OPS>(wd, i) ? word_identity(word_op<OPS>(wd, i)) : 0;
 }
 
 // acc = merge(acc, state of entry e) when the entry holds an accumulator (windowState.value != null)
-template <int NW, int E, bool Q>
+template <int NW, int E, bool Q, uint32_t OPS>
 __device__ __forceinline__ void merge_entry(const MergeArgs& a, StateLds<NW, E>& S, int e, uint64_t* acc) {
     if (e < 0 || !(S.flag[e] & F_ACC)) return;
     uint64_t o[NW];
 #pragma unroll
     for (int i = 0; i < NW; i++) o[i] = S.acc[i][e];
-    merge_slice<NW, Q>(a.wd, a.ad, acc, o);
+    merge_slice<NW, Q, OPS>(a.wd, a.ad, acc, o);
 }
 
 // TUMBLE: SliceUnsharedSyncStateWindowAggProcessor.fireWindow (:54-66) + clearWindow
 // (expiredSlices(we) = [we]); DataStream tumbling: WindowOperator.onEventTime + clearAllState.
 // Windows of different keys and of one key are independent: every due entry fires once.
-template <int NW, int E, bool Q>
+template <int NW, int E, bool Q, uint32_t OPS>
 __device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
     uint64_t acc[NW];
     const uint32_t f = atomicAnd(&S.flag[e], ~(F_TIMER | F_ACC));
@@ -334,7 +328,7 @@ __device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW,
 #pragma unroll
         for (int i = 0; i < NW; i++) acc[i] = S.acc[i][e];
     } else {
-        acc_identity<NW>(a.wd, acc);
+        acc_identity<NW, OPS>(a.wd, acc);
     }
     if (a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0) emit_row<NW, Q>(a, sb, s_emit, S.key[e], S.slice[e], acc);
     return 1;
@@ -349,8 +343,12 @@ __device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW,
 // earlier windows of the key that are due in this advance, so the expiry is deferred to the
 // write-back (F_EXPIRE), after every window of the advance has read its slices.  With that, the
 // chains of one key may run concurrently in any order; the F_FIRED claim makes every window fire
-// exactly once.
-template <int NW, int E, bool Q>
+// exactly once.  A chain step reuses the entries of the window it just fired: the next window's
+// slices are the new slice (the entry nextTriggerWindow found or inserted) plus all but the oldest
+// of the previous window's, so with n <= HB slices per window only the chain's first window probes.
+// (An entry absent when cached may since have been inserted by another chain of the key, but only
+// empty -- without F_ACC -- which merges like an absent one.)
+template <int NW, int E, bool Q, uint32_t OPS>
 __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit,
                                    uint64_t* fst = nullptr) {
     const WinDesc& w = a.win;
@@ -360,6 +358,9 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
     int64_t we = S.slice[e];
     int ew = e;
     uint32_t nf = 0;
+    const int n = w.n_slices;
+    int ring[HB];  // entries of window we's slices, newest first (n <= HB), -1 absent
+    bool have_ring = false;
     uint64_t t0 = fst ? __builtin_amdgcn_s_memtime() : 0;
     auto lap = [&](int i) {  // diagnostic (AB_FSTAMPS): per-lane cycles of the chain's parts
         if (!fst) return;
@@ -375,12 +376,18 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
         nf++;
         lap(3);
         uint64_t acc[NW];
-        acc_identity<NW>(wd, acc);
-        const int n = w.n_slices;
+        acc_identity<NW, OPS>(wd, acc);
         const int64_t s_exp = wadd(wsub(we, w.size), w.interval);  // clearWindow's expired slice
         int e_exp = -3;
         int64_t s = we;
-        for (int j0 = 0; j0 < n; j0 += HB) {
+        if (have_ring) {
+#pragma unroll
+            for (int j = 0; j < HB; j++) {
+                if (j >= n) break;
+                merge_entry<NW, E, Q, OPS>(a, S, ring[j], acc);
+                if (j == n - 1) e_exp = ring[j];  // the oldest slice is clearWindow's
+            }
+        } else for (int j0 = 0; j0 < n; j0 += HB) {
             int64_t kk[HB], ss[HB];
             int eb[HB];
 #pragma unroll
@@ -395,8 +402,9 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
                 if (j0 + j >= n) break;
                 int e2 = eb[j];
                 if (e2 == -2) e2 = find_entry(S, k, ss[j]);
-                merge_entry<NW, E, Q>(a, S, e2, acc);
+                merge_entry<NW, E, Q, OPS>(a, S, e2, acc);
                 if (ss[j] == s_exp) e_exp = e2;
+                ring[j] = e2;  // j0 == 0 whenever the ring is used (n <= HB)
             }
         }
         lap(0);
@@ -407,12 +415,18 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
         if (e2 >= 0) atomicOr(&S.flag[e2], F_EXPIRE);
         if (!nonempty) break;
         const int64_t nx = wadd(we, w.interval);
-        const int en = find_or_insert(S, k, nx, wd);
+        const int en = find_or_insert<NW, E, OPS>(S, k, nx, wd);
         lap(2);
         if (en < 0) break;  // state overflow (flagged)
         if (!win_fired(w, nx, a.wm)) {
             atomicOr(&S.flag[en], F_TIMER);
             break;
+        }
+        if (n <= HB) {  // window nx: slice nx, then window we's slices but its oldest
+#pragma unroll
+            for (int j = HB - 1; j > 0; j--) ring[j] = ring[j - 1];
+            ring[0] = en;
+            have_ring = true;
         }
         we = nx;
         ew = en;
@@ -426,7 +440,7 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
 // unless empty, the next step is registered up to the window's last step (nextTriggerWindow), and
 // clearWindow expires we (and the first slice at the last step).  The merged accumulator stays in
 // registers across the chain and is written back to the first slice once.
-template <int NW, int E, bool Q>
+template <int NW, int E, bool Q, uint32_t OPS>
 __device__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
@@ -435,20 +449,20 @@ __device__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, 
     const int64_t ws = window_start_of(w, we);
     const int64_t first = wadd(ws, w.interval);
     const int64_t last = wadd(ws, w.size);
-    const int ef = find_or_insert(S, k, first, wd);
+    const int ef = find_or_insert<NW, E, OPS>(S, k, first, wd);
     uint64_t acc[NW];
     if (ef >= 0 && (S.flag[ef] & F_ACC)) {
 #pragma unroll
         for (int i = 0; i < NW; i++) acc[i] = S.acc[i][ef];
     } else {
-        acc_identity<NW>(wd, acc);
+        acc_identity<NW, OPS>(wd, acc);
     }
     uint32_t nf = 0;
     bool done = false;
     int ewe = e;
     for (;;) {
         if (ewe >= 0) atomicAnd(&S.flag[ewe], ~F_TIMER);
-        if (we != first) merge_entry<NW, E, Q>(a, S, ewe, acc);
+        if (we != first) merge_entry<NW, E, Q, OPS>(a, S, ewe, acc);
         nf++;
         if (a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0) emit_row<NW, Q>(a, sb, s_emit, k, we, acc);
         if (we != first && ewe >= 0) atomicAnd(&S.flag[ewe], ~F_ACC);
@@ -459,7 +473,7 @@ __device__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, 
         }
         const int64_t nx = wadd(we, w.interval);
         if (!win_fired(w, nx, a.wm)) {
-            const int en = find_or_insert(S, k, nx, wd);
+            const int en = find_or_insert<NW, E, OPS>(S, k, nx, wd);
             if (en >= 0) atomicOr(&S.flag[en], F_TIMER);
             break;
         }
@@ -492,6 +506,21 @@ __device__ __forceinline__ void mark_cumulate_successor(const MergeArgs& a, Stat
             break;
         }
     }
+}
+
+// HOP pre-pass: a due window whose predecessor window (we - slide) is due and non-empty is
+// reached by the chain that fires the predecessor (which continues while its windows are
+// non-empty), so it starts no chain of its own.  Conservative: the predecessor's own slice holding
+// an accumulator (with its COUNT(*) > 0) proves the predecessor window non-empty; a window whose
+// predecessor cannot be proven so starts a chain, and the F_FIRED claim settles any overlap.
+template <int NW, int E>
+__device__ __forceinline__ void mark_hop_successor(const MergeArgs& a, StateLds<NW, E>& S, int e) {
+    const int64_t k = S.key[e];
+    const int64_t pe = wsub(S.slice[e], a.win.interval);
+    const int p = find_entry(S, k, pe);
+    if (p >= 0 && (S.flag[p] & (F_TIMER | F_ACC)) == (F_TIMER | F_ACC) && win_fired(a.win, pe, a.wm) &&
+        (a.ad.count_star_word < 0 || S.acc[a.ad.count_star_word][p] != 0))
+        atomicOr(&S.flag[e], F_NOTHEAD);
 }
 
 // ---- DataStream windows (KIND_DSWIN): one entry per (key, window end), as WindowOperator keeps
@@ -623,7 +652,7 @@ __device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
 // rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
 constexpr int mg_rows_in_flight(int nw) { return nw <= 1 ? 4 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1; }
 
-template <int NW, int E, bool Q, int KIND>
+template <int NW, int E, bool Q, int KIND, uint32_t OPS>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
@@ -741,7 +770,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // ---- timers registered by late records in processElement
     for (int64_t r = tid; r < ntreq; r += MG_BLOCK) {
         if (a.treq[3 * r + 2] != sb) continue;
-        const int e = find_or_insert(S, a.treq[3 * r], a.treq[3 * r + 1], a.wd);
+        const int e = find_or_insert<NW, E, OPS>(S, a.treq[3 * r], a.treq[3 * r + 1], a.wd);
         if (e >= 0) atomicOr(&S.flag[e], F_TIMER);
     }
     // ---- flush: AggCombiner.combine for every pending (key, slice) partial of this bucket.
@@ -848,7 +877,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         if (FW_ABL(a) & AB_M_NO_FOLDOP) return;
 #pragma unroll
                         for (int w = 0; w < NW; w++)
-                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], row[u][2 + w]);
+                            if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
                         atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
                     });
                     const uint64_t gm0 = gst ? __builtin_amdgcn_s_memtime() : 0;
@@ -866,11 +895,11 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         const int64_t k = (int64_t)r[0], sl = (int64_t)r[1];
                         const uint32_t fl = flags_of(sl);
                         bool ins = false;
-                        const int e = find_or_insert(S, k, sl, a.wd, &r[2], fl, &ins);
+                        const int e = find_or_insert<NW, E, OPS>(S, k, sl, a.wd, &r[2], fl, &ins);
                         if (e < 0 || ins || (FW_ABL(a) & AB_M_NO_FOLDOP)) continue;
 #pragma unroll
                         for (int w = 0; w < NW; w++)
-                            if (w < a.wd.nw) lds_fold(a.wd.op[w], &S.acc[w][e], r[2 + w]);
+                            if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], r[2 + w]);
                         atomicOr(&S.flag[e], fl);
                     }
                     if (gst) {
@@ -950,8 +979,11 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         // fewer due entries than threads then still keep every wave busy, so each SIMD has four
         // waves of dependent LDS chains to interleave instead of two
         const int qlane = (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
-        if (KIND == FW_WIN_CUMULATE) {
-            for (int q = qlane; q < nd; q += MG_BLOCK) mark_cumulate_successor<NW, E>(a, S, S.due[q]);
+        if (KIND == FW_WIN_CUMULATE || KIND == FW_WIN_HOP) {
+            for (int q = qlane; q < nd; q += MG_BLOCK) {
+                if (KIND == FW_WIN_CUMULATE) mark_cumulate_successor<NW, E>(a, S, S.due[q]);
+                else mark_hop_successor<NW, E>(a, S, S.due[q]);
+            }
             __syncthreads();
         }
         stm.mark(6);
@@ -963,11 +995,11 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             if (KIND == KIND_DSWIN) {
                 nf += fire_ds<NW, E>(a, S, e, sb, &s_emit);
             } else if (KIND == FW_WIN_TUMBLE) {
-                nf += fire_tumble<NW, E, Q>(a, S, e, sb, &s_emit);
+                nf += fire_tumble<NW, E, Q, OPS>(a, S, e, sb, &s_emit);
             } else if (KIND == FW_WIN_HOP) {
-                nf += fire_hop_chain<NW, E, Q>(a, S, e, sb, &s_emit, fs ? fst : nullptr);
+                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_hop_chain<NW, E, Q, OPS>(a, S, e, sb, &s_emit, fs ? fst : nullptr);
             } else {
-                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_cumulate_chain<NW, E, Q>(a, S, e, sb, &s_emit);
+                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_cumulate_chain<NW, E, Q, OPS>(a, S, e, sb, &s_emit);
             }
         }
         if (fs && a.stamps) {
@@ -1056,28 +1088,61 @@ static unsigned merge_grid(int n_sb) {
     return (unsigned)(n_sb < n_cu ? n_sb : n_cu);
 }
 
-template <int NW, bool Q>
-static hipError_t merge_q(const MergeArgs& a, hipStream_t s) {
-    if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
-        if (Q) return hipErrorInvalidValue;
-        constexpr int E = mg_entries(NW, KIND_DSWIN);
-        hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
-        return hipGetLastError();
-    }
-    // the planner sized the superbuckets for mg_entries(nw, kind) entries (fw_api.hip)
+// the accumulator layouts with a compiled variant per accumulator width (the others, and every SQL
+// MIN/MAX(DOUBLE) query, run the OPS_ANY variant): the built-in aggregates' common combinations
+template <int NW> struct MergeLayouts;
+template <> struct MergeLayouts<1> {  // COUNT(*) / SUM, MAX, MIN, SUM(DOUBLE)
+    static constexpr uint32_t L[] = {ops_pack({W_SUM_I}), ops_pack({W_MAX_I}), ops_pack({W_MIN_I}), ops_pack({W_SUM_F})};
+};
+template <> struct MergeLayouts<2> {  // AVG / SUM+AVG (DOUBLE, BIGINT), COUNT(*) + SUM / MAX / MIN
+    static constexpr uint32_t L[] = {ops_pack({W_SUM_F, W_SUM_I}), ops_pack({W_SUM_I, W_SUM_I}),
+                                     ops_pack({W_SUM_I, W_MAX_I}), ops_pack({W_SUM_I, W_MIN_I})};
+};
+template <> struct MergeLayouts<4> {  // COUNT(*), SUM, MIN, MAX
+    static constexpr uint32_t L[] = {ops_pack({W_SUM_I, W_SUM_I, W_MIN_I, W_MAX_I})};
+};
+template <> struct MergeLayouts<8> {
+    static constexpr uint32_t L[] = {OPS_ANY};
+};
+
+template <int NW, bool Q, uint32_t OPS>
+static void merge_launch(const MergeArgs& a, hipStream_t s) {
     constexpr int ET = mg_entries(NW, FW_WIN_TUMBLE), EH = mg_entries(NW, FW_WIN_HOP), EC = mg_entries(NW, FW_WIN_CUMULATE);
-    if (a.cap_e != (a.win.kind == FW_WIN_TUMBLE ? ET : a.win.kind == FW_WIN_HOP ? EH : EC)) return hipErrorInvalidValue;
     switch (a.win.kind) {
-        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
-        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE, OPS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP, OPS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE, OPS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
     }
-    return hipGetLastError();
+}
+
+template <int NW, int I>
+static bool merge_layout_launch(const MergeArgs& a, uint32_t lay, hipStream_t s) {
+    constexpr int N = (int)(sizeof(MergeLayouts<NW>::L) / sizeof(uint32_t));
+    if constexpr (I >= N) {
+        return false;
+    } else {
+        constexpr uint32_t L = MergeLayouts<NW>::L[I];
+        if (L != OPS_ANY && lay == L) {
+            merge_launch<NW, false, L>(a, s);
+            return true;
+        }
+        return merge_layout_launch<NW, I + 1>(a, lay, s);
+    }
 }
 
 template <int NW>
 hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
-    return a.wd.has_q ? merge_q<NW, true>(a, s) : merge_q<NW, false>(a, s);
+    if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
+        if (a.wd.has_q) return hipErrorInvalidValue;
+        constexpr int E = mg_entries(NW, KIND_DSWIN);
+        hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+        return hipGetLastError();
+    }
+    // the planner sized the superbuckets for mg_entries(nw, kind) entries (fw_api.hip)
+    if (a.cap_e != mg_entries(NW, a.win.kind)) return hipErrorInvalidValue;
+    if (a.wd.has_q) merge_launch<NW, true, OPS_ANY>(a, s);
+    else if (!merge_layout_launch<NW, 0>(a, ops_layout(a.wd), s)) merge_launch<NW, false, OPS_ANY>(a, s);
+    return hipGetLastError();
 }
 
 }  // namespace fw

@@ -23,9 +23,30 @@ class WindowAggHandle:
         self._h = C.c_void_p()
         check(lib().fw_create(C.byref(cfg), C.byref(self._h)))
         self.n_aggs = abi.result_columns(cfg)  # result value columns
+        self._ext = None  # torch view of the handle's stream + two reusable ordering events
+
+    # ---- stream ordering of device-resident inputs: the handle's stream waits for the producer's
+    # current stream before the ingest reads the columns, and the producer's later work waits for
+    # the ingest (no record_stream: the handle's stream dies with the handle, before torch frees the
+    # tensors).  The stream view and events are created once per handle: a push is on the per-step
+    # hot path, where creating them every time costs more host time than the launch itself.
+    def _begin_read(self, device):
+        import torch
+        if self._ext is None or self._ext[0] != device:
+            self._ext = (device, torch.cuda.ExternalStream(self.stream_ptr, device=device),
+                         torch.cuda.Event(), torch.cuda.Event())
+        cur = torch.cuda.current_stream(device)
+        self._ext[2].record(cur)
+        self._ext[1].wait_event(self._ext[2])
+        return cur
+
+    def _end_read(self, cur):
+        self._ext[3].record(self._ext[1])
+        cur.wait_event(self._ext[3])
 
     # ---- lifecycle
     def close(self):
+        self._ext = None
         if self._h:
             lib().fw_destroy(self._h)
             self._h = C.c_void_p()
@@ -78,12 +99,10 @@ class WindowAggHandle:
         """Device-resident columns (torch cuda tensors, int64 / float64; ``nulls``: {column:
         uint8 tensor}).  The handle's stream waits for the producer's current stream before
         reading them."""
-        import torch
         n = keys.numel()
         if n == 0:
             return
-        ext = torch.cuda.ExternalStream(self.stream_ptr, device=keys.device)
-        ext.wait_stream(torch.cuda.current_stream(keys.device))
+        cur = self._begin_read(keys.device)
         arr = (C.c_void_p * abi.FW_MAX_COLS)()
         for c, v in enumerate(values):
             arr[c] = v.data_ptr()
@@ -92,22 +111,17 @@ class WindowAggHandle:
             nul[c] = v.data_ptr()
         check(lib().fw_push_device(self._h, n, keys.data_ptr(), ts.data_ptr(),
                                    key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
-        # the producer stream must not reuse the input memory before the ingest kernel has read
-        # it: order the producer's later work after this push (no record_stream: the handle's
-        # stream dies with the handle, before torch frees the tensors)
-        torch.cuda.current_stream(keys.device).wait_stream(ext)
+        self._end_read(cur)
 
     def push_device_segments(self, seg_counts, keys, ts, values=(), key_hashes=None, nulls=None):
         """A padded exchange receive buffer (KeyByExchange.exchange_padded): len(seg_counts)
         segments of keys.numel() // len(seg_counts) rows; segment s holds seg_counts[s] valid rows
         (a device int64 tensor -- no host round trip)."""
-        import torch
         p = seg_counts.numel()
         n = keys.numel()
         if p == 0 or n == 0:
             return
-        ext = torch.cuda.ExternalStream(self.stream_ptr, device=keys.device)
-        ext.wait_stream(torch.cuda.current_stream(keys.device))
+        cur = self._begin_read(keys.device)
         arr = (C.c_void_p * abi.FW_MAX_COLS)()
         for c, v in enumerate(values):
             arr[c] = v.data_ptr()
@@ -116,21 +130,19 @@ class WindowAggHandle:
             nul[c] = v.data_ptr()
         check(lib().fw_push_device_segments(self._h, p, n // p, seg_counts.data_ptr(), keys.data_ptr(), ts.data_ptr(),
                                             key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
-        torch.cuda.current_stream(keys.device).wait_stream(ext)
+        self._end_read(cur)
 
     def push_device_packed_segments(self, seg_counts, rows, row_words):
         """A packed padded exchange receive buffer (KeyByExchange.exchange_packed): len(seg_counts)
         segments of rows.numel() // (len(seg_counts) * row_words) packed rows (key, ts, value
         words); segment s holds seg_counts[s] valid rows (a device int64 tensor)."""
-        import torch
         p = seg_counts.numel()
         if p == 0 or rows.numel() == 0:
             return
-        ext = torch.cuda.ExternalStream(self.stream_ptr, device=rows.device)
-        ext.wait_stream(torch.cuda.current_stream(rows.device))
+        cur = self._begin_read(rows.device)
         check(lib().fw_push_device_packed_segments(self._h, p, rows.numel() // (p * row_words), seg_counts.data_ptr(),
                                                    rows.data_ptr(), int(row_words)))
-        torch.cuda.current_stream(rows.device).wait_stream(ext)
+        self._end_read(cur)
 
     # ---- progress / output
     def advance(self, wm):

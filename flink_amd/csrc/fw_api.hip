@@ -9,11 +9,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fw_internal.h"
@@ -647,6 +649,8 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.ablate = h->ablate;
     a.stamps = h->stamps;
     a.kt = h->kt_device ? h->kt_dev + FW_KT_MERGE * KT_WORDS : nullptr;
+    a.host_mirror = h->d_mirror;  // the launch's last workgroup reports merge_seq << 8 | pending pushes
+    a.merge_seq = h->merge_seq;
     return a;
 }
 
@@ -670,12 +674,21 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
     for (int64_t o = 0; o < n; o += h->cap_rows) {
         const int64_t m = std::min(h->cap_rows, n - o);
         if (h->pushes_ub >= FW_MAX_PENDING) {
-            // what the last completed merge launch left pending, plus the pushes issued after it
-            const unsigned long long v = *h->mirror;
-            const uint64_t seq = v >> 8;
-            if (v != ~0ull && seq < h->merge_seq && h->merge_seq - seq <= 64)
-                h->pushes_ub = std::min<int64_t>(h->pushes_ub,
-                                                 (int64_t)(v & 0xff) + (int64_t)(h->pushes_total - h->pushes_at_merge[seq % 64]));
+            // what the last completed merge launch left pending, plus the pushes issued after it.
+            // While merge launches issued since are still running, wait for them to report
+            // instead of draining the stream: the queue stays busy while the host waits.
+            const auto t0 = std::chrono::steady_clock::now();
+            for (;;) {
+                const unsigned long long v = *h->mirror;
+                const uint64_t seq = v >> 8;
+                const bool valid = v != ~0ull && seq < h->merge_seq && h->merge_seq - seq <= 64;
+                if (valid)
+                    h->pushes_ub = std::min<int64_t>(h->pushes_ub,
+                                                     (int64_t)(v & 0xff) + (int64_t)(h->pushes_total - h->pushes_at_merge[seq % 64]));
+                if (h->pushes_ub < FW_MAX_PENDING || !valid || seq + 1 >= h->merge_seq) break;
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;  // read_ctrl below
+                std::this_thread::yield();
+            }
         }
         if (h->pushes_ub >= FW_MAX_PENDING) {
             Ctrl c;

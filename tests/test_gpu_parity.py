@@ -179,6 +179,39 @@ def test_random_stream_matches_oracle(name):
     assert late > 0 or kw.get("late_side_output")  # the stream exercises the late-record paths
 
 
+# Every accumulator layout with its own k_merge_fire variant (fw_merge_impl.h MergeLayouts: the
+# word ops as compile-time constants), under each SQL window kind, against the oracle.  HOP needs
+# a COUNT(*), so it runs the layouts that have one.
+LAYOUT_AGGS = {
+    "cnt": [(abi.AGG_COUNT_STAR, 0, I64)],
+    "max": [(abi.AGG_MAX, 0, I64)],
+    "min": [(abi.AGG_MIN, 0, I64)],
+    "sum_f": [(abi.AGG_SUM, 1, F64)],
+    "avg_f": [(abi.AGG_AVG, 1, F64)],
+    "sum_avg_i": [(abi.AGG_SUM, 0, I64), (abi.AGG_AVG, 0, I64)],
+    "cnt_max": [(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_MAX, 0, I64)],
+    "cnt_min": [(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_MIN, 0, I64)],
+    "cnt_sum_min_max": [(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MIN, 0, I64),
+                        (abi.AGG_MAX, 0, I64)],
+}
+LAYOUT_WINDOWS = {
+    "tumble": dict(window_kind=abi.WIN_TUMBLE, size_ms=6000),
+    "hop": dict(window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000),
+    "cumulate": dict(window_kind=abi.WIN_CUMULATE, size_ms=8000, slide_ms=2000),
+}
+LAYOUT_CASES = [(w, a) for w in LAYOUT_WINDOWS for a in LAYOUT_AGGS
+                if w != "hop" or LAYOUT_AGGS[a][0][0] == abi.AGG_COUNT_STAR]
+
+
+@pytest.mark.parametrize("win,aggs", LAYOUT_CASES, ids=[f"{w}-{a}" for w, a in LAYOUT_CASES])
+def test_compiled_accumulator_layouts_match_oracle(win, aggs):
+    kw = dict(LAYOUT_WINDOWS[win], aggs=LAYOUT_AGGS[aggs])
+    if kw["aggs"][0][0] == abi.AGG_COUNT_STAR:
+        kw["count_star_index"] = 0
+    _run_both(_cfg(kw), _stream(zlib.crc32(f"{win}{aggs}".encode()) % 1000, 20000, 300, ooo=2 * kw["size_ms"],
+                                step_ms=4500, n_wm=20), _double_cols(kw))  # 2-3 slides per watermark: HOP chains
+
+
 # TIMESTAMP_LTZ windows across daylight-saving changes: slices on the zone's wall clock, timers at
 # toEpochMillsForTimer (gap -> first skipped hour, overlap -> the later instant), next trigger
 # watermarks through the zone (TimeWindowUtil.java:52-211); bit-exact against the oracle.

@@ -232,7 +232,11 @@ int fw_commit(fw_handle* h, int64_t n);
 /* Device-resident columns (caller-owned device memory, ordered on the handle stream).
    d_values[c] points at n 8-byte words of value column c; d_key_hash may be NULL unless
    key_hash == FW_KEYHASH_PRECOMPUTED; d_nulls may be NULL unless nullable_cols != 0, and then
-   d_nulls[c] points at n null-flag bytes of each nullable column c. */
+   d_nulls[c] points at n null-flag bytes of each nullable column c.
+   Every push is asynchronous until 8 pushes may be buffered and unflushed (the device buffer):
+   the call then waits for the merge launches already issued to report (a host-mapped word),
+   and only when none is outstanding reads the control block and flushes (the reference's
+   RecordsWindowBuffer full path). */
 int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t* d_ts,
                    const int32_t* d_key_hash, const void* const* d_values,
                    const uint8_t* const* d_nulls);

@@ -303,13 +303,23 @@ def main():
     bytes_per_launch = rows_per_launch * wl["w_in"] + g_per_launch * w_partial
     avg_reduce_s = red_ms / red_n / 1e3
     achieved = bytes_per_launch / avg_reduce_s / 1e9
-    # ---------------- the flush + fire kernel: G_b * w_partial + 2 L w_entry + F w_out ---------
+    # ---------------- the flush + fire kernel -------------------------------------------------
+    # algorithmic bytes over the timed region, from device counters (fw_stats): the distinct groups
+    # of the batches those flushes merged (G_b * w_partial), the state entries the launches loaded
+    # and wrote back (counted per superbucket on the device: only launches that flush or fire move
+    # state), and the fired windows' output rows; per launch = total / launches.  Beside it, what
+    # the flushes really read: every partial row the ingest wrote (partials_merged * w_partial).
     mg_ms, mg_n = kt["merge"]
     w_entry = 8 * (3 + wl["nw"])
     w_out = 8 * (3 + len(wl["aggs"])) + 4
-    live = st["live_state_entries"]                       # entries after the last step (~ per step)
-    fired_per_step = st["num_fired_windows"] / args.steps
-    merge_bytes = g_per_launch * w_partial + 2 * live * w_entry + fired_per_step * w_out
+    live = st["live_state_entries"]
+    fired_total = st["num_fired_windows"]
+    merged_share = st["partials_merged"] / max(st["partials_emitted"], 1)  # batches flushed by the end
+    merge_total = (sum(groups) * merged_share * w_partial + st["state_entries_moved"] * w_entry
+                   + fired_total * w_out)
+    merge_bytes = merge_total / max(mg_n, 1)
+    merge_read_total = (st["partials_merged"] * w_partial + st["state_entries_moved"] * w_entry
+                        + fired_total * w_out)
     avg_merge_s = mg_ms / max(mg_n, 1) / 1e3
     traffic = traffic_m = None
     tpath = args.traffic_json
@@ -392,6 +402,7 @@ def main():
                                            else "hipEvents around every launch of the timed region"),
                          "launches": red_n, "distinct_groups_per_launch": g_per_launch,
                          "partials_written_per_launch": st["partials_emitted"] / red_n,
+                         "counter_rate_GBps": (traffic / avg_reduce_s / 1e9) if traffic else None,
                          "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None},
             "roofline_merge": {"bound": "hbm", "kernel": "fw::k_merge_fire (K4 flush into the HBM slice table + "
                                                          "K5 timers / fire / emit)",
@@ -399,9 +410,15 @@ def main():
                                "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                "frac": merge_bytes / avg_merge_s / 1e9 / HBM_PEAK_GBPS if mg_n else None,
                                "algorithmic_bytes_per_launch": merge_bytes,
-                               "terms": {"G_b_w_partial": g_per_launch * w_partial, "two_L_w_entry": 2 * live * w_entry,
-                                         "F_w_out": fired_per_step * w_out},
+                               "terms_per_launch": {
+                                   "G_b_w_partial": sum(groups) * merged_share * w_partial / max(mg_n, 1),
+                                   "state_entries_moved_w_entry": st["state_entries_moved"] * w_entry / max(mg_n, 1),
+                                   "F_w_out": fired_total * w_out / max(mg_n, 1)},
+                               "flush_launches": st["flush_launches"], "live_state_entries_end": live,
+                               "partial_bytes_read_per_launch": st["partials_merged"] * w_partial / max(mg_n, 1),
+                               "design_bytes_per_launch": merge_read_total / max(mg_n, 1),
                                "avg_launch_us": avg_merge_s * 1e6, "launches": mg_n, "traffic": traffic_m,
+                               "counter_rate_GBps": (traffic_m / avg_merge_s / 1e9) if traffic_m else None,
                                "traffic_over_algorithmic": (traffic_m / merge_bytes) if traffic_m else None},
             "cpu_baseline": cpu,
             "end_to_end": e2e,

@@ -70,6 +70,7 @@ def lib():
         "fw_host_next_trigger_watermark": (i64, [i64, i64]),
         "fw_host_time_op": (i32, [P(abi.fw_config), i32, i64, P(i64)]),
         "fw_late_records": (i32, [vp, P(abi.fw_late_rows)]),
+        "fw_first_element_events": (i32, [vp, P(abi.fw_ordinal_events)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -89,7 +90,7 @@ EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_ge
             "fw_key_row_hash", "fw_host_key_row_hash",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
-            "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records"]
+            "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records", "fw_first_element_events"]
 
 
 def check(rc):

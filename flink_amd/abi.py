@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 4
+FW_ABI_VERSION = 5
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -85,7 +85,7 @@ class fw_config(C.Structure):
         ("parallelism", C.c_int32),
         ("subtask_index", C.c_int32),
         ("device", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("ds_first_ordinals", C.c_int32),
         ("state_capacity", C.c_int64),
         ("max_batch_rows", C.c_int64),
         ("output_capacity", C.c_int64),
@@ -115,7 +115,12 @@ class fw_result(C.Structure):
     _fields_ = [("n", C.c_int64), ("key", C.POINTER(C.c_int64)),
                 ("window_start", C.POINTER(C.c_int64)), ("window_end", C.POINTER(C.c_int64)),
                 ("values", C.POINTER(C.c_int64) * FW_MAX_AGGS),
-                ("null_mask", C.POINTER(C.c_uint32))]
+                ("null_mask", C.POINTER(C.c_uint32)), ("first_ord", C.POINTER(C.c_int64))]
+
+
+class fw_ordinal_events(C.Structure):
+    _fields_ = [("n_retain", C.c_int64), ("retain", C.POINTER(C.c_int64)),
+                ("n_release", C.c_int64), ("release", C.POINTER(C.c_int64))]
 
 
 class fw_late_rows(C.Structure):
@@ -130,7 +135,9 @@ class fw_stats(C.Structure):
                 ("pending_rows", C.c_int64), ("results_available", C.c_int64),
                 ("num_fired_windows", C.c_int64), ("partials_emitted", C.c_int64),
                 ("error_flags", C.c_int32),
-                ("num_superbuckets", C.c_int32)]
+                ("num_superbuckets", C.c_int32),
+                ("flush_launches", C.c_int64), ("partials_merged", C.c_int64),
+                ("state_entries_moved", C.c_int64)]
 
 
 KT_PARTITION, KT_SCAN, KT_REDUCE, KT_MERGE, KT_OTHER = 0, 1, 2, 3, 4
@@ -154,7 +161,7 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
                 max_parallelism=128, parallelism=1, subtask_index=0, device=0,
                 state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22,
                 nullable_cols=(), agg_phase=PHASE_ONE, allowed_lateness_ms=0, late_side_output=False,
-                shift_zone=None):
+                shift_zone=None, ds_first_ordinals=False):
     """Build an fw_config.  ``aggs`` is a sequence of (kind, input_col, type); ``nullable_cols``
     the value columns that may hold SQL NULLs; ``shift_zone`` a TIMESTAMP_LTZ window's time zone
     (a zone name, or a ShiftZone from flink_amd.table.time_zone; None / "UTC": no shift)."""
@@ -188,6 +195,7 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
     c.output_capacity = output_capacity
     c.allowed_lateness_ms = allowed_lateness_ms
     c.late_side_output = 1 if late_side_output else 0
+    c.ds_first_ordinals = 1 if ds_first_ordinals else 0
     set_shift_zone(c, shift_zone)
     return c
 

@@ -149,6 +149,9 @@ struct fw_handle {
     int64_t lfire_cap = 0;
     int64_t* side = nullptr;     // DataStream late side-output rows
     int64_t side_cap = 0;
+    int64_t* ordev = nullptr;    // DataStream first-element retain / release events
+    int64_t ordev_cap = 0;
+    std::vector<int64_t> ev_retain, ev_release;  // fw_first_element_events copies
     int32_t push_seq = 0;        // fw_commit / fw_push_device calls (side-output row ids)
     std::vector<int64_t> tz_utc, tz_off, tz_bound;  // shift-zone table (host copy)
     int64_t* d_tz = nullptr;     // device copy: [utc | off | bound]
@@ -318,6 +321,10 @@ int validate_and_plan(fw_handle* h) {
     };
     ad.n = c.n_aggs;
     ad.count_star_word = -1;
+    ad.first_word = -1;
+    for (int g = 0; g < FW_MAX_AGGS; g++) ad.dn_hi[g] = ad.dn_lo[g] = -1;
+    if (c.ds_first_ordinals && c.api != FW_API_DATASTREAM)
+        return fail(FW_E_INVALID, "ds_first_ordinals is a DataStream option (SQL output rows carry no input fields)");
     bool nn_star[FW_MAX_AGGS] = {};
     for (int g = 0; g < c.n_aggs; g++) {
         const fw_agg_desc& d = c.aggs[g];
@@ -404,6 +411,11 @@ int validate_and_plan(fw_handle* h) {
                 w0 = word_of(f ? (mx ? W_MAX_D : W_MIN_D) : (mx ? W_MAX_I : W_MIN_I), slot, gate);
                 if (gate >= 0) ad.nn[g] = word_of(cnt_op, slot, gate);
                 else nn_star[g] = true;
+                if (f && c.api == FW_API_DATASTREAM) {  // the last NaN's bits (Comparator ties)
+                    ad.dn_hi[g] = word_of(W_DNHI, slot, gate);
+                    ad.dn_lo[g] = word_of(W_DNLO, slot, gate);
+                    if (ad.dn_hi[g] < 0 || ad.dn_lo[g] < 0) return fail(FW_E_INVALID, "too many accumulator words");
+                }
                 break;
             }
             case FW_AGG_AVG:
@@ -428,6 +440,12 @@ int validate_and_plan(fw_handle* h) {
         ad.count_star_word = word_of(W_CNT, 0, -1);
         if (ad.count_star_word < 0) return fail(FW_E_INVALID, "too many accumulator words");
     }
+    if (c.ds_first_ordinals) {
+        ad.first_word = word_of(W_FIRST, 0, -1);
+        if (ad.first_word < 0) return fail(FW_E_INVALID, "too many accumulator words");
+    }
+    wd.has_ord = wd.has_q;
+    for (int i = 0; i < wd.nw; i++) wd.has_ord |= wd.op[i] == W_FIRST || is_dnword(wd.op[i]);
     // NOT NULL inputs: SUM / MIN / MAX are NULL only for an entry without rows (COUNT(*) == 0),
     // which needs a COUNT(*) word to be observable; without one such an entry never fires
     int star = -1;
@@ -437,7 +455,7 @@ int validate_and_plan(fw_handle* h) {
         if (nn_star[g]) ad.nn[g] = star;
     h->nv = nslot;
     h->nw_t = round_nw(wd.nw);
-    h->n_out = c.n_aggs;
+    h->n_out = c.n_aggs + (ad.first_word >= 0 ? 1 : 0);  // + value1's ordinal (fw_result.first_ord)
     if (c.agg_phase == FW_PHASE_LOCAL) {  // output = local accumulator fields (AVG: sum, count)
         h->n_out = 0;
         for (int g = 0; g < c.n_aggs; g++) h->n_out += c.aggs[g].kind == FW_AGG_AVG ? 2 : 1;
@@ -477,8 +495,8 @@ int validate_and_plan(fw_handle* h) {
     h->chunk_rows = (int64_t)ig_block(h->nw_t, ig_nv(h->nv)) * ig_rpt(h->nw_t, ig_nv(h->nv));
     h->cap_rows = ((c.max_batch_rows + h->chunk_rows - 1) / h->chunk_rows) * h->chunk_rows;
     h->max_nch = h->cap_rows / h->chunk_rows;
-    if (wd.has_q && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
-        return fail(FW_E_INVALID, "max_batch_rows too large for SQL MIN/MAX(DOUBLE) arrival ordinals");
+    if (wd.has_ord && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
+        return fail(FW_E_INVALID, "max_batch_rows too large for MIN/MAX(DOUBLE) / first-element arrival ordinals");
     h->cell_cols = cell_pad(h->max_nch);
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     if (c.api == FW_API_DATASTREAM) {
@@ -486,6 +504,10 @@ int validate_and_plan(fw_handle* h) {
             return fail(FW_E_INVALID, "max_batch_rows too large for late-element arrival ordinals");
         h->lfire_cap = c.allowed_lateness_ms > 0 ? h->treq_cap : 0;
         h->side_cap = c.late_side_output ? h->treq_cap : 0;
+        // retains per flush <= new windows of its rows; releases <= live windows
+        h->ordev_cap = ad.first_word >= 0
+                           ? ((int64_t)FW_MAX_PENDING * h->cap_rows + std::max<int64_t>(c.state_capacity, 0)) * w.n_win + (1 << 16)
+                           : 0;
     }
     h->out_cap = c.output_capacity;
     h->slab_cap = std::max<int64_t>(64, (2 * c.output_capacity + ks.n_sb - 1) / ks.n_sb);
@@ -514,6 +536,7 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
     if (h->lfire_cap && (rc = dalloc(&h->lfire, (size_t)h->lfire_cap * LFW))) return rc;
     if (h->side_cap && (rc = dalloc(&h->side, (size_t)h->side_cap * SOW))) return rc;
+    if (h->ordev_cap && (rc = dalloc(&h->ordev, (size_t)h->ordev_cap))) return rc;
     if (!h->tz_utc.empty()) {  // shift-zone table on the device; the kernels' WinDesc points at it
         const size_t n = h->tz_utc.size();
         if ((rc = dalloc(&h->d_tz, 3 * n))) return rc;
@@ -590,11 +613,12 @@ int read_ctrl(fw_handle* h, Ctrl* out) {
     HIP_TRY(hipMemcpyAsync(out, h->ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (out->error) {
-        return fail(FW_E_CAPACITY, "device error (bits 0x%x:%s%s%s%s%s%s)", out->error,
+        return fail(FW_E_CAPACITY, "device error (bits 0x%x:%s%s%s%s%s%s%s)", out->error,
                     out->error & ERR_CHUNKS ? " partial-buffer" : "", out->error & ERR_STATE ? " state-table" : "",
                     out->error & ERR_OUTPUT ? " result-buffer" : "", out->error & ERR_TREQ ? " timer-requests" : "",
                     out->error & ERR_KEYGROUP ? " key-group-not-owned" : "",
-                    out->error & ERR_LATE ? " late-rows (call fw_late_records more often)" : "");
+                    out->error & ERR_LATE ? " late-rows (call fw_late_records more often)" : "",
+                    out->error & ERR_ORDEV ? " first-element-events (call fw_first_element_events after each advance)" : "");
     }
     return FW_OK;
 }
@@ -651,6 +675,8 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.kt = h->kt_device ? h->kt_dev + FW_KT_MERGE * KT_WORDS : nullptr;
     a.host_mirror = h->d_mirror;  // the launch's last workgroup reports merge_seq << 8 | pending pushes
     a.merge_seq = h->merge_seq;
+    a.ordev = h->ordev;
+    a.ordev_cap = h->ordev_cap;
     return a;
 }
 
@@ -671,6 +697,8 @@ int force_flush(fw_handle* h) {
 
 int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int32_t* kh, const void* const* vals,
          const uint8_t* const* nulls, const int64_t* seg_counts = nullptr, int64_t seg_len = 1, int64_t stride = 1) {
+    if (h->ad.first_word >= 0 && (n >= (1ll << 32) || h->push_seq >= (1 << 30)))
+        return fail(FW_E_INVALID, "arrival ordinals need < 2^32 rows per call and < 2^30 calls");
     for (int64_t o = 0; o < n; o += h->cap_rows) {
         const int64_t m = std::min(h->cap_rows, n - o);
         if (h->pushes_ub >= FW_MAX_PENDING) {
@@ -798,6 +826,7 @@ int fw_destroy(fw_handle* h) {
     if (h->mirror) hipHostFree((void*)h->mirror);
     hipFree(h->lfire);
     hipFree(h->side);
+    hipFree(h->ordev);
     hipFree(h->d_tz);
     hipFree(h->state);
     hipFree(h->state_count);
@@ -1011,11 +1040,13 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     memset(out, 0, sizeof *out);
     out->n = n;
     const int na = h->n_out;
+    const int nv = h->ad.first_word >= 0 ? na - 1 : na;  // the last column is value1's ordinal
     if (!copy_to_host) {
         out->key = h->res_key;
         out->window_start = h->res_ws;
         out->window_end = h->res_we;
-        for (int g = 0; g < na; g++) out->values[g] = (int64_t*)h->res_val[g];
+        for (int g = 0; g < nv; g++) out->values[g] = (int64_t*)h->res_val[g];
+        if (nv < na) out->first_ord = (int64_t*)h->res_val[nv];
         out->null_mask = h->res_null;
         return FW_OK;
     }
@@ -1037,8 +1068,34 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     out->key = h->r_key.data();
     out->window_start = h->r_ws.data();
     out->window_end = h->r_we.data();
-    for (int g = 0; g < na; g++) out->values[g] = (int64_t*)h->r_val[g].data();
+    for (int g = 0; g < nv; g++) out->values[g] = (int64_t*)h->r_val[g].data();
+    if (nv < na) out->first_ord = (int64_t*)h->r_val[nv].data();
     out->null_mask = h->r_null.data();
+    return FW_OK;
+}
+
+int fw_first_element_events(fw_handle* h, fw_ordinal_events* out) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    memset(out, 0, sizeof *out);
+    if (!h->ordev_cap) return fail(FW_E_STATE, "the operator does not track first elements (ds_first_ordinals = 0)");
+    Ctrl c;
+    int rc = read_ctrl(h, &c);
+    if (rc) return rc;
+    const int64_t n = std::min<int64_t>(c.n_ordev, h->ordev_cap);
+    std::vector<int64_t> raw((size_t)n);
+    if (n) HIP_TRY(hipMemcpy(raw.data(), h->ordev, (size_t)n * 8, hipMemcpyDeviceToHost));
+    const int64_t zero = 0;
+    HIP_TRY(hipMemcpy(&h->ctrl->n_ordev, &zero, 8, hipMemcpyHostToDevice));
+    h->ev_retain.clear();
+    h->ev_release.clear();
+    for (int64_t e : raw) {
+        if (e & ORDEV_RELEASE) h->ev_release.push_back(e & ~ORDEV_RELEASE);
+        else h->ev_retain.push_back(e);
+    }
+    out->n_retain = (int64_t)h->ev_retain.size();
+    out->retain = h->ev_retain.data();
+    out->n_release = (int64_t)h->ev_release.size();
+    out->release = h->ev_release.data();
     return FW_OK;
 }
 
@@ -1112,6 +1169,9 @@ int fw_get_stats(fw_handle* h, fw_stats* out) {
     out->partials_emitted = (int64_t)c.partials;
     out->error_flags = (int32_t)c.error;
     out->num_superbuckets = h->ks.n_sb;
+    out->flush_launches = (int64_t)c.flush_launches;
+    out->partials_merged = (int64_t)c.parts_merged;
+    out->state_entries_moved = (int64_t)c.state_moved;
     return FW_OK;
 }
 
@@ -1209,8 +1269,9 @@ struct SnapHeader {
     int32_t version, n_sb, cap_e, pwe;
     int64_t cur, late_dropped, fired, live;
     uint64_t semantics;
+    int64_t push_seq;  // arrival ordinals continue after the restore (W_FIRST words stay ordered)
 };
-static const uint64_t SNAP_MAGIC = 0x464c4b57494e3032ull;  // "FLKWIN02"
+static const uint64_t SNAP_MAGIC = 0x464c4b57494e3033ull;  // "FLKWIN03"
 
 int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     if (!h || !size) return fail(FW_E_INVALID, "null argument");
@@ -1227,7 +1288,8 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    SnapHeader hd{SNAP_MAGIC, 2, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, 0, total, semantics_fingerprint(h)};
+    SnapHeader hd{SNAP_MAGIC, 3, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, 0, total, semantics_fingerprint(h),
+                  (int64_t)h->push_seq};
     char* p = (char*)buf;
     memcpy(p, &hd, sizeof hd);
     p += sizeof hd;
@@ -1284,6 +1346,7 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
     h->pushes_ub = 0;
     h->host_cur = c.cur;
+    h->push_seq = std::max<int64_t>(h->push_seq, hd.push_seq);
     return FW_OK;
 }
 
@@ -1300,8 +1363,9 @@ struct KgHeader {
     int32_t version, key_group, pwe, nw, sb_log2, hash_kind;
     int64_t win_size, win_interval, cur, n;
     uint64_t semantics;
+    int64_t push_seq;  // arrival ordinals of the restoring handle continue after every restored blob's
 };
-static const uint64_t KG_MAGIC = 0x464c4b574b473032ull;  // "FLKWKG02"
+static const uint64_t KG_MAGIC = 0x464c4b574b473033ull;  // "FLKWKG03"
 
 int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t capacity, int64_t* size) {
     if (!h || !size) return fail(FW_E_INVALID, "null argument");
@@ -1321,8 +1385,8 @@ int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t ca
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    KgHeader hd{KG_MAGIC, 2, key_group, pwe, h->wd.nw, L, ks.hash_kind, h->win.size, h->win.interval, c.cur, total,
-                semantics_fingerprint(h)};
+    KgHeader hd{KG_MAGIC, 3, key_group, pwe, h->wd.nw, L, ks.hash_kind, h->win.size, h->win.interval, c.cur, total,
+                semantics_fingerprint(h), (int64_t)h->push_seq};
     memcpy(buf, &hd, sizeof hd);
     uint64_t* e = (uint64_t*)((char*)buf + sizeof hd);
     for (int q = 0; q < nsub; q++) {
@@ -1342,7 +1406,7 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
     memcpy(&hd, buf, sizeof hd);
     const KeySpace& ks = h->ks;
     const int pwe = 3 + h->nw_t, L = ks.sb_per_kg_log2;
-    if (hd.magic != KG_MAGIC || hd.version != 2) return fail(FW_E_INVALID, "not a key-group snapshot");
+    if (hd.magic != KG_MAGIC || hd.version != 3) return fail(FW_E_INVALID, "not a key-group snapshot");
     if (hd.pwe != pwe || hd.nw != h->wd.nw || hd.hash_kind != ks.hash_kind || hd.win_size != h->win.size ||
         hd.win_interval != h->win.interval || hd.semantics != semantics_fingerprint(h))
         return fail(FW_E_INVALID, "key-group snapshot of a different operator configuration");
@@ -1401,6 +1465,7 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
     c.live_entries += added;
     c.ntp = INT64_MIN;  // next trigger recomputed at the next advance
     HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
+    h->push_seq = std::max<int64_t>(h->push_seq, hd.push_seq);
     return FW_OK;
 }
 

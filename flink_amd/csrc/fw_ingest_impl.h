@@ -51,7 +51,7 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, 
     return v;
 }
 
-// X: the configuration has nullable columns or SQL MIN/MAX(DOUBLE) words (gates, ordinals)
+// X: the configuration has nullable columns or words that read arrival ordinals (gates, ordinals)
 template <int NV, int NW, int RPT, bool X, int IG_BLOCK>
 __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int CH = IG_BLOCK * RPT;
@@ -202,7 +202,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             }
             const uint64_t v = pick_col(rv[j], a.wd.col[w]);
             if (X) {
-                racc[j][w] = gated_word(a.wd, w, v, rnul[j], ord0 + (uint32_t)(j * IG_BLOCK + tid));
+                const uint64_t gord = ((uint64_t)(uint32_t)a.push_seq << 32) |
+                                      (uint64_t)(base + (int64_t)j * IG_BLOCK + tid + a.row0);
+                racc[j][w] = gated_word(a.wd, w, v, rnul[j], ord0 + (uint32_t)(j * IG_BLOCK + tid), gord);
             } else {
                 const uint64_t dk = (uint64_t)dkey(v);
                 racc[j][w] = wmode[w] == 1 ? 1ull : wmode[w] == 2 ? dk : v;
@@ -530,7 +532,7 @@ static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
 
 template <int NV, int NW>
 static hipError_t ingest_nw(const IngestArgs& a, hipStream_t s, KTimer* t) {
-    bool x = a.wd.has_q != 0;
+    bool x = a.wd.has_ord != 0;
     for (int q = 0; q < MAX_KCOLS; q++) x = x || a.nulls[q] != nullptr;
     return x ? ingest_x<NV, NW, true>(a, s, t) : ingest_x<NV, NW, false>(a, s, t);
 }

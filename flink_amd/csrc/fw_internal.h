@@ -100,7 +100,17 @@ enum WordOp : int32_t {
                    //   (the high half of a NaN is never 0: its exponent bits are all ones)
     W_QNANLO = 10, // unsigned min of ord << 32 | (bits & 0xffffffff) over NaN values
     W_QZERO = 11,  // unsigned min of ord << 1 | sign over +-0.0 values
-    W_CNTV = 12    // += v                      GLOBAL phase: a local COUNT / AVG count column
+    W_CNTV = 12,   // += v                      GLOBAL phase: a local COUNT / AVG count column
+    // DataStream (ComparableAggregator / SumAggregator return value1, the window's FIRST element,
+    // with the aggregated field set: SumAggregator.java:66-76, ComparableAggregator.java:83-104)
+    W_FIRST = 13,  // unsigned min of the global arrival ordinal push_seq << 32 | row: the first element
+    // DataStream MIN/MAX(DOUBLE): MaxComparator/MinComparator (Comparator.java:48-101) replace the
+    // field unless the accumulator is strictly extremal by Double.compareTo, so among equal values
+    // the LAST arrival wins; only NaNs (all equal under compareTo) differ in their bits.  The NaN
+    // that arrived last, split in halves, each with the 32-bit arrival ordinal within the flush
+    // (state from earlier flushes keeps ordinal 0):
+    W_DNHI = 14,   // unsigned max of ord << 32 | (isNaN ? bits >> 32 : 0) over NaN values (0: none)
+    W_DNLO = 15    // unsigned max of ord << 32 | (bits & 0xffffffff) over NaN values
 };
 
 FW_HD uint64_t word_identity(int32_t op) {
@@ -113,11 +123,13 @@ FW_HD uint64_t word_identity(int32_t op) {
         case W_QMAX: return (uint64_t)INT64_MIN;
         case W_QFIRST:
         case W_QNANLO:
-        case W_QZERO: return ~0ull;
-        default: return 0;  // counts, integer sums, and +0.0 for double sums
+        case W_QZERO:
+        case W_FIRST: return ~0ull;
+        default: return 0;  // counts, integer sums, +0.0 for double sums; W_DNHI / W_DNLO: no NaN yet
     }
 }
 FW_HD bool is_qword(int32_t op) { return op >= W_QMIN && op <= W_QZERO; }
+FW_HD bool is_dnword(int32_t op) { return op == W_DNHI || op == W_DNLO; }
 constexpr uint64_t Q_EMPTY = ~0ull;
 
 // Entry flags of the HBM slice-state table.
@@ -134,6 +146,7 @@ constexpr uint32_t ERR_OUTPUT = 4u;
 constexpr uint32_t ERR_TREQ = 8u;
 constexpr uint32_t ERR_KEYGROUP = 16u;  // a record's key group is outside this subtask's range
 constexpr uint32_t ERR_LATE = 32u;      // late-fire rows or late side-output rows over capacity
+constexpr uint32_t ERR_ORDEV = 64u;     // first-element retain / release events over capacity
 
 // Device-resident operator control block (one per handle).  Only kernels write it, so a
 // watermark cycle needs no host round trip.
@@ -167,6 +180,10 @@ struct Ctrl {
     int32_t pad0;
     int64_t n_lfire;         // DataStream late-fire rows pending (EventTimeTrigger.onElement FIRE)
     int64_t n_side;          // DataStream late side-output rows since the last fw_late_records
+    int64_t n_ordev;         // DataStream first-element retain / release events since the last read
+    uint64_t flush_launches; // merge launches that flushed pending partials (cumulative)
+    uint64_t parts_merged;   // partial rows those flushes read (cumulative)
+    uint64_t state_moved;    // state entries the merge launches loaded + wrote back (cumulative)
 };
 
 // Window / slice description shared by both kernels (SliceAssigners.java).
@@ -270,6 +287,7 @@ struct WordDesc {
     int32_t gate[MAX_WORDS];  // value slot whose NULL rows the word skips, -1: none (COUNT(*))
     int32_t qfirst[MAX_WORDS];  // W_QNANLO / W_QMIN / W_QMAX: the W_QFIRST word of its group
     int32_t has_q;            // any W_Q* word (write-back normalisation, fire-time merges)
+    int32_t has_ord;          // any word that reads an arrival ordinal (W_Q*, W_FIRST, W_DN*)
 };
 
 // Compile-time accumulator layout of a k_merge_fire variant: 4 bits per word (word 0 lowest),
@@ -321,6 +339,9 @@ struct AggDesc {
     int32_t qn[FW_MAX_AGGS];
     int32_t qz[FW_MAX_AGGS];
     int32_t count_star_word;  // word of the SQL indexOfCountStar aggregate, -1 if none
+    int32_t dn_hi[FW_MAX_AGGS];  // DataStream MIN/MAX(DOUBLE): the W_DNHI / W_DNLO words (else -1)
+    int32_t dn_lo[FW_MAX_AGGS];
+    int32_t first_word;       // DataStream: the W_FIRST word (-1: the first element is not tracked)
 };
 
 struct IngestArgs {
@@ -430,7 +451,13 @@ struct MergeArgs {
     unsigned long long* host_mirror;
     uint64_t merge_seq;
     unsigned long long* kt;  // launch timing (fw_set_profiling FW_PROF_DEVICE): KtSlot of this kernel class
+    // DataStream first-element tracking (AggDesc::first_word >= 0): retain events (the ordinal of a
+    // new window state's first element) and release events (ORDEV_RELEASE | ordinal of a cleaned
+    // window's first element), for the host shim that keeps those records (value1 of the reduce)
+    int64_t* ordev;
+    int64_t ordev_cap;
 };
+constexpr int64_t ORDEV_RELEASE = (int64_t)1 << 62;
 constexpr int LFW = 3 + MAX_WORDS;  // words per late-fire row
 constexpr int SOW = 3 + MAX_KCOLS;  // words per late side-output row
 

@@ -46,8 +46,9 @@ __device__ __forceinline__ bool f64_isnan(uint64_t b) { return (b & 0x7FFFFFFFFF
 __device__ __forceinline__ bool f64_iszero(uint64_t b) { return (b & 0x7FFFFFFFFFFFFFFFull) == 0; }
 
 // value of one accumulator word for a single non-NULL record (accumulate on the identity);
-// `ord` >= 1 is the record's arrival ordinal within the flush (W_Q* words only)
-__device__ __forceinline__ uint64_t record_word(int32_t op, uint64_t v, uint32_t ord) {
+// `ord` >= 1 is the record's arrival ordinal within the flush (W_Q*, W_DN* words), `gord` its
+// global arrival ordinal push_seq << 32 | row (W_FIRST)
+__device__ __forceinline__ uint64_t record_word(int32_t op, uint64_t v, uint32_t ord, uint64_t gord = 0) {
     switch (op) {
         case W_CNT: return 1;
         case W_MIN_D:
@@ -57,14 +58,18 @@ __device__ __forceinline__ uint64_t record_word(int32_t op, uint64_t v, uint32_t
         case W_QFIRST: return ((uint64_t)ord << 32) | (f64_isnan(v) ? (v >> 32) : 0ull);
         case W_QNANLO: return f64_isnan(v) ? (((uint64_t)ord << 32) | (v & 0xFFFFFFFFull)) : Q_EMPTY;
         case W_QZERO: return f64_iszero(v) ? (((uint64_t)ord << 1) | (v >> 63)) : Q_EMPTY;
+        case W_FIRST: return gord;
+        case W_DNHI: return f64_isnan(v) ? (((uint64_t)ord << 32) | (v >> 32)) : 0ull;
+        case W_DNLO: return f64_isnan(v) ? (((uint64_t)ord << 32) | (v & 0xFFFFFFFFull)) : 0ull;
         default: return v;  // SUM_I, SUM_F (bits), MIN_I, MAX_I, CNTV
     }
 }
 // a record's word, honouring the word's NULL gate (null_slots: bit s = value slot s is NULL)
-__device__ __forceinline__ uint64_t gated_word(const WordDesc& wd, int w, uint64_t v, uint32_t null_slots, uint32_t ord) {
+__device__ __forceinline__ uint64_t gated_word(const WordDesc& wd, int w, uint64_t v, uint32_t null_slots, uint32_t ord,
+                                               uint64_t gord = 0) {
     const int32_t g = wd.gate[w];
     if (g >= 0 && ((null_slots >> g) & 1u)) return word_identity(wd.op[w]);
-    return record_word(wd.op[w], v, ord);
+    return record_word(wd.op[w], v, ord, gord);
 }
 
 // atomically fold `v` into an LDS accumulator word (element-level combine: commutative)
@@ -79,7 +84,10 @@ __device__ __forceinline__ void lds_fold(int32_t op, uint64_t* slot, uint64_t v)
         case W_QMIN: __hip_atomic_fetch_min((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
         case W_QFIRST:
         case W_QNANLO:
-        case W_QZERO: __hip_atomic_fetch_min(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+        case W_QZERO:
+        case W_FIRST: __hip_atomic_fetch_min(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+        case W_DNHI:
+        case W_DNLO: __hip_atomic_fetch_max(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
         default: __hip_atomic_fetch_max((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
     }
 }
@@ -96,7 +104,10 @@ __device__ __forceinline__ uint64_t reg_fold(int32_t op, uint64_t a, uint64_t b)
         case W_QMIN: return (int64_t)a < (int64_t)b ? a : b;
         case W_QFIRST:
         case W_QNANLO:
-        case W_QZERO: return a < b ? a : b;
+        case W_QZERO:
+        case W_FIRST: return a < b ? a : b;
+        case W_DNHI:
+        case W_DNLO: return a > b ? a : b;
         default: return (int64_t)a > (int64_t)b ? a : b;
     }
 }
@@ -122,6 +133,8 @@ __device__ __forceinline__ uint64_t q_normalise(const WordDesc& wd, int w, const
     switch (wd.op[w]) {
         case W_QFIRST: return v != Q_EMPTY ? (v & 0xFFFFFFFFull) : v;
         case W_QZERO: return v != Q_EMPTY ? (v & 1ull) : v;
+        case W_DNHI:
+        case W_DNLO: return v & 0xFFFFFFFFull;  // ordinal 0: earlier than any later flush's NaN
         case W_QNANLO: {
             const uint64_t f = acc[wd.qfirst[w]];
             return (f != Q_EMPTY && (uint32_t)f) ? (v & 0xFFFFFFFFull) : Q_EMPTY;
@@ -242,6 +255,18 @@ __device__ __forceinline__ int32_t wave_claim(int32_t* ctr) {
     int32_t base = 0;
     if (lane == leader) base = atomicAdd(ctr, (int32_t)__popcll(act));
     return __shfl(base, leader, 64) + rank;
+}
+
+// slot claim on a device-scope counter for the active lanes of a wave (one atomic per wave)
+__device__ __forceinline__ int64_t wave_claim_dev(int64_t* ctr) {
+    const uint64_t act = __ballot(1);
+    const int lane = __lane_id();
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const int rank = __popcll(act & ((1ull << lane) - 1ull));
+    long long base = 0;
+    if (lane == leader)
+        base = (long long)__hip_atomic_fetch_add(ctr, (int64_t)__popcll(act), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (int64_t)__shfl(base, leader, 64) + rank;
 }
 
 // Last-workgroup election, called by one thread per workgroup once the workgroup's published

@@ -111,6 +111,12 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->partials = 0;
         c->fold_skip = 0;
         c->push_count = 0;
+        c->n_lfire = 0;
+        c->n_side = 0;
+        c->n_ordev = 0;
+        c->flush_launches = 0;
+        c->parts_merged = 0;
+        c->state_moved = 0;
     }
 }
 

@@ -230,6 +230,9 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
                     break;
                 }
                 v = type == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
+                // DataStream: a NaN result is the NaN that arrived last, with its own bits
+                if (a.ad.dn_hi[g] >= 0 && f64_isnan(v))
+                    v = (acc[a.ad.dn_hi[g]] << 32) | (acc[a.ad.dn_lo[g]] & 0xFFFFFFFFull);
                 if (no_rows) nm |= 1u << g;
                 break;
             case FW_AGG_AVG: {
@@ -246,6 +249,7 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
         }
         a.out_val[g][i] = ((nm >> g) & 1u) ? 0ull : v;  // a NULL's value word is 0
     }
+    if (a.ad.first_word >= 0) a.out_val[a.ad.n][i] = acc[a.ad.first_word];  // value1's arrival ordinal
     a.out_null[i] = nm;
 }
 
@@ -300,6 +304,14 @@ __device__ void emit_partial(const MergeArgs& a, int sb, int32_t* s_emit, int64_
 constexpr uint32_t F_FIRED = 4u;    // HOP: window (key, this slice end) fired in this advance (chain claim)
 constexpr uint32_t F_NOTHEAD = 8u;  // CUMULATE / HOP: an earlier due window's chain reaches this one
 constexpr uint32_t F_EXPIRE = 16u;  // HOP: slice expired by a window fired in this advance (cleared at write-back)
+constexpr uint32_t F_NEW = 64u;     // DataStream: window state created in this launch (first element retained)
+
+// DataStream first-element events (MergeArgs::ordev), called by the lanes that have one
+__device__ __forceinline__ void push_ordev(const MergeArgs& a, int64_t ev) {
+    const int64_t r = wave_claim_dev(&a.ctrl->n_ordev);
+    if (r < a.ordev_cap) a.ordev[r] = ev;
+    else __hip_atomic_fetch_or(&a.ctrl->error, ERR_ORDEV, __ATOMIC_RELAXED, DEV_SCOPE);
+}
 
 template <int NW, uint32_t OPS = OPS_ANY>
 __device__ __forceinline__ void acc_identity(const WordDesc& wd, uint64_t* acc) {
@@ -542,7 +554,7 @@ __device__ void ds_add_to_windows(const MergeArgs& a, StateLds<NW, E>& S, int64_
         if (fired_already && !late_rows) continue;
         const uint32_t fl = F_ACC | (ct != INT64_MAX ? F_CLEAN : 0u) | (fired_already ? 0u : F_TIMER);
         bool ins = false;
-        const int en = find_or_insert(S, k, e, a.wd, v, fl, &ins);
+        const int en = find_or_insert(S, k, e, a.wd, v, fl | F_NEW, &ins);
         if (en < 0 || ins) continue;
 #pragma unroll
         for (int q = 0; q < NW; q++)
@@ -576,6 +588,9 @@ __device__ __forceinline__ uint32_t fire_ds(const MergeArgs& a, StateLds<NW, E>&
         emit_row<NW, false>(a, sb, s_emit, S.key[e], we, acc);
     }
     S.flag[e] = f & ~((fire ? F_TIMER : 0u) | (clean ? (F_ACC | F_TIMER | F_CLEAN) : 0u));
+    // clearAllState: a window state retained by an earlier launch releases its first element
+    if (clean && (f & F_ACC) && !(f & F_NEW) && a.ad.first_word >= 0)
+        push_ordev(a, ORDEV_RELEASE | (int64_t)S.acc[a.ad.first_word][e]);
     return fire ? 1u : 0u;
 }
 
@@ -629,6 +644,8 @@ __device__ void merge_finalize(const MergeArgs& a) {
         c->min_pending = INT64_MAX;
         c->pending_rows = 0;
         c->n_lfire = 0;
+        c->flush_launches += 1;
+        c->parts_merged = c->partials;  // a flush reads every partial written so far
     }
     c->n_treq = 0;
     for (int q = 0; q < 8; q++) __hip_atomic_store(&a.tickets->work[q][0], 0u, __ATOMIC_RELAXED, DEV_SCOPE);
@@ -1044,12 +1061,15 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             p[0] = (uint64_t)S.key[e];
             p[1] = (uint64_t)S.slice[e];
             p[2] = f;
-            if (Q) {
+            if (Q || (KIND == KIND_DSWIN && a.wd.has_ord)) {
                 uint64_t v[NW];
 #pragma unroll
                 for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
 #pragma unroll
                 for (int w = 0; w < NW; w++) p[3 + w] = w < a.wd.nw ? q_normalise(a.wd, w, v) : v[w];
+                // a new DataStream window state: its first element is retained by the host shim
+                if (KIND == KIND_DSWIN && (f0 & F_NEW) && (f & F_ACC) && a.ad.first_word >= 0)
+                    push_ordev(a, (int64_t)v[a.ad.first_word]);
             } else {
 #pragma unroll
                 for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];
@@ -1067,6 +1087,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         a.sb_min_timer[sb] = s_newmin;
         a.sb_out[sb] = min(s_emit, a.slab_cap);
         if (s_fired) a.sb_fired[sb] += s_fired;
+        // state traffic of this superbucket: entries loaded + entries written back
+        __hip_atomic_fetch_add(&c->state_moved, (uint64_t)(n0 + (a.local ? 0 : s_nlive)), __ATOMIC_RELAXED, DEV_SCOPE);
         if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
     }
     __syncthreads();

@@ -15,7 +15,18 @@ the element added (EventTimeTrigger.onElement).  A watermark fires (key, window)
 (key, aggregate) with record timestamp window.maxTimestamp(); the window state is cleared at its
 cleanup time.  Elements late for all their windows go to the late side output when one is set,
 else they are counted in numLateRecordsDropped.
+
+Output records.  SumAggregator.reduce (SumAggregator.java:66-76) and ComparableAggregator.reduce
+(ComparableAggregator.java:83-104) return value1 -- the window's FIRST element, copied -- with the
+aggregated field set, so every non-aggregated field of an output record comes from the first
+element.  With ``field`` set the operator is record-shaped: ``process_batch(..., records=...)``
+takes the elements themselves, the device tracks each window's first arrival ordinal
+(ds_first_ordinals) and tells the operator which elements to keep (fw_first_element_events);
+``process_watermark`` then returns the reference's records.
 """
+import json
+import struct
+
 import numpy as np
 
 from .. import abi
@@ -48,7 +59,9 @@ class WindowOperator:
     def __init__(self, assigner, trigger, aggregation, key_type="LONG", max_parallelism=128,
                  parallelism=1, subtask_index=0, device=0, state_capacity=1 << 20,
                  max_batch_rows=1 << 22, output_capacity=1 << 22, allowed_lateness=0,
-                 late_data_output_tag=None):
+                 late_data_output_tag=None, field=None):
+        """``field``: position of the aggregated field in the records (``sum(field)``, ...); given,
+        the operator emits whole records (value1.copy() with the field set), else (key, agg)."""
         ok, why = is_gpu_eligible(assigner, trigger, aggregation, allowed_lateness=allowed_lateness,
                                   late_data_output_tag=late_data_output_tag)
         if not ok:
@@ -66,9 +79,13 @@ class WindowOperator:
             parallelism=parallelism, subtask_index=subtask_index, device=device,
             state_capacity=state_capacity, max_batch_rows=max_batch_rows,
             output_capacity=output_capacity, allowed_lateness_ms=allowed_lateness,
-            late_side_output=late_data_output_tag is not None)
+            late_side_output=late_data_output_tag is not None, ds_first_ordinals=field is not None)
         self.late_data_output_tag = late_data_output_tag
+        self.field = field
         self.handle = None
+        self._pending = {}   # push_seq -> records of that push (not yet flushed into state)
+        self._retained = {}  # arrival ordinal -> [record, windows whose first element it is]
+        self._wm = -(1 << 63)
 
     def open(self):
         self.handle = WindowAggHandle(self.cfg)
@@ -79,19 +96,76 @@ class WindowOperator:
             self.handle.close()
             self.handle = None
 
-    def process_batch(self, keys, timestamps, values, key_hashes=None):
+    def process_batch(self, keys, timestamps, values, key_hashes=None, records=None):
+        """processElement for a batch; ``records``: the elements themselves (record-shaped
+        operator), kept until the device says which ones are first elements of a window."""
+        seq0 = self.handle.push_seq
         self.handle.push_host(keys, timestamps, [values], key_hashes)
+        self._keep(seq0, records, len(keys))
 
-    def process_batch_device(self, keys, timestamps, values, key_hashes=None):
+    def process_batch_device(self, keys, timestamps, values, key_hashes=None, records=None):
+        seq0 = self.handle.push_seq
         self.handle.push_device(keys, timestamps, [values], key_hashes)
+        self._keep(seq0, records, keys.numel())
+
+    def _keep(self, seq0, records, n):
+        if self.field is None:
+            return
+        if records is None or len(records) != n:
+            raise ValueError("a record-shaped operator needs the batch's records")
+        cap = self.cfg.max_batch_rows
+        for i, seq in enumerate(range(seq0, self.handle.push_seq)):  # one push per max_batch_rows rows
+            self._pending[seq] = records[i * cap:(i + 1) * cap] if self.handle.push_seq - seq0 > 1 else records
+
+    def _element(self, ord_):
+        rec = self._retained.get(int(ord_))
+        if rec is not None:
+            return rec[0]
+        return self._pending[int(ord_) >> 32][int(ord_) & 0xFFFFFFFF]
+
+    def _first_elements(self, first_ord, flushed):
+        """The retain events (records -> kept), the results' first elements, then the releases."""
+        retain, release = self.handle.first_element_events()
+        for o in retain.tolist():
+            ent = self._retained.get(o)
+            if ent is None:
+                self._retained[o] = [self._element(o), 1]
+            else:
+                ent[1] += 1
+        firsts = [self._element(o) for o in first_ord.tolist()]
+        for o in release.tolist():
+            ent = self._retained[o]
+            ent[1] -= 1
+            if ent[1] == 0:
+                del self._retained[o]
+        if flushed:  # every pushed row is in the state now: the batches are no longer needed
+            self._pending.clear()
+        return firsts
 
     def process_watermark(self, watermark):
-        """Fires all (key, window) timers <= watermark; returns {key, value, timestamp}."""
+        """Fires all (key, window) timers <= watermark; returns {key, value, timestamp} (and, for
+        a record-shaped operator, "records": value1.copy() with the aggregated field set)."""
         self.handle.advance(watermark)
         r = self.handle.results(reset=True)
-        return {"key": r["key"], "value": r["values"][0], "timestamp": r["window_end"] - 1,
-                "window_start": r["window_start"], "window_end": r["window_end"],
-                "values": r["values"], "null_mask": r["null_mask"]}
+        out = {"key": r["key"], "value": r["values"][0], "timestamp": r["window_end"] - 1,
+               "window_start": r["window_start"], "window_end": r["window_end"],
+               "values": r["values"], "null_mask": r["null_mask"]}
+        if self.field is not None:
+            flushed = watermark > self._wm
+            out["first_ord"] = r["first_ord"]
+            firsts = self._first_elements(r["first_ord"], flushed)
+            vals = self._field_values(r["values"][0])
+            out["records"] = [tuple(f[:self.field]) + (v,) + tuple(f[self.field + 1:]) for f, v in zip(firsts, vals)]
+        self._wm = max(self._wm, watermark)
+        return out
+
+    def _field_values(self, words):
+        fn, ftype = self.aggregation
+        if ftype == "DOUBLE" and fn != "count":
+            return [struct.unpack("<d", struct.pack("<q", int(w)))[0] for w in words]
+        if ftype == "INT" and fn != "count":
+            return [int(np.int32(np.int64(w))) for w in words]
+        return [int(w) for w in words]
 
     def side_output(self):
         """Records routed to the late-data side output since the last call
@@ -101,10 +175,24 @@ class WindowOperator:
                 "row": r["row"]}
 
     def snapshot_state(self) -> bytes:
-        return self.handle.snapshot()
+        """The device blob; a record-shaped operator appends the first elements it keeps (the
+        reference's window state holds them: HeapReducingState's value is value1)."""
+        if self.field is None:
+            return self.handle.snapshot()
+        self.handle.flush()                          # prepareSnapshotPreBarrier
+        self._first_elements(np.empty(0, np.int64), True)  # the flush's retains; batches flushed
+        blob = self.handle.snapshot()
+        side = json.dumps([[o, list(r), c] for o, (r, c) in self._retained.items()]).encode()
+        return struct.pack("<q", len(blob)) + blob + side
 
     def initialize_state(self, blob: bytes):
-        self.handle.restore(blob)
+        if self.field is None:
+            self.handle.restore(blob)
+            return
+        n = struct.unpack_from("<q", blob, 0)[0]
+        self.handle.restore(blob[8:8 + n])
+        self._retained = {o: [tuple(r), c] for o, r, c in json.loads(blob[8 + n:].decode())}
+        self._pending.clear()
 
     @property
     def num_late_records_dropped(self):

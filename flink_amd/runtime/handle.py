@@ -23,6 +23,7 @@ class WindowAggHandle:
         self._h = C.c_void_p()
         check(lib().fw_create(C.byref(cfg), C.byref(self._h)))
         self.n_aggs = abi.result_columns(cfg)  # result value columns
+        self.push_seq = 0  # fw_commit / fw_push_device* calls so far (arrival ordinals: push_seq << 32 | row)
         self._ext = None  # torch view of the handle's stream + two reusable ordering events
 
     # ---- stream ordering of device-resident inputs: the handle's stream waits for the producer's
@@ -94,6 +95,7 @@ class WindowAggHandle:
                             np.asarray(nulls[c]).astype(np.uint8, copy=False)
                         _np_view(cols.nulls[c], m, np.uint8)[:] = nf[o:o + m]
             check(lib().fw_commit(self._h, m))
+            self.push_seq += 1
 
     def push_device(self, keys, ts, values=(), key_hashes=None, nulls=None):
         """Device-resident columns (torch cuda tensors, int64 / float64; ``nulls``: {column:
@@ -111,6 +113,7 @@ class WindowAggHandle:
             nul[c] = v.data_ptr()
         check(lib().fw_push_device(self._h, n, keys.data_ptr(), ts.data_ptr(),
                                    key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
+        self.push_seq += 1
         self._end_read(cur)
 
     def push_device_segments(self, seg_counts, keys, ts, values=(), key_hashes=None, nulls=None):
@@ -130,6 +133,7 @@ class WindowAggHandle:
             nul[c] = v.data_ptr()
         check(lib().fw_push_device_segments(self._h, p, n // p, seg_counts.data_ptr(), keys.data_ptr(), ts.data_ptr(),
                                             key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
+        self.push_seq += 1
         self._end_read(cur)
 
     def push_device_packed_segments(self, seg_counts, rows, row_words):
@@ -142,6 +146,7 @@ class WindowAggHandle:
         cur = self._begin_read(rows.device)
         check(lib().fw_push_device_packed_segments(self._h, p, rows.numel() // (p * row_words), seg_counts.data_ptr(),
                                                    rows.data_ptr(), int(row_words)))
+        self.push_seq += 1
         self._end_read(cur)
 
     # ---- progress / output
@@ -162,6 +167,8 @@ class WindowAggHandle:
             "values": [_np_view(r.values[a], n, np.int64).copy() for a in range(self.n_aggs)],
             "null_mask": _np_view(r.null_mask, n, np.uint32).copy(),
         }
+        if self.cfg.ds_first_ordinals:  # DataStream: arrival ordinal of each window's first element
+            out["first_ord"] = _np_view(r.first_ord, n, np.int64).copy()
         if reset:
             self.reset_results()
         return out
@@ -203,6 +210,13 @@ class WindowAggHandle:
         return {"key": _np_view(r.key, n, np.int64).copy(), "ts": _np_view(r.ts, n, np.int64).copy(),
                 "values": [_np_view(r.values[c], n, np.int64).copy() for c in range(self.cfg.n_value_cols)],
                 "push_seq": _np_view(r.push_seq, n, np.int64).copy(), "row": _np_view(r.row, n, np.int64).copy()}
+
+    def first_element_events(self):
+        """DataStream with ds_first_ordinals: (retain, release) arrival ordinals since the last call
+        (fw_first_element_events) -- the first elements a shim must keep / may drop."""
+        r = abi.fw_ordinal_events()
+        check(lib().fw_first_element_events(self._h, C.byref(r)))
+        return (_np_view(r.retain, r.n_retain, np.int64).copy(), _np_view(r.release, r.n_release, np.int64).copy())
 
     def stats(self):
         s = abi.fw_stats()
@@ -271,7 +285,16 @@ class WindowAggHandle:
         """One key group's blob; raises if this subtask does not own it or the layout differs."""
         buf = C.create_string_buffer(blob, len(blob))
         check(lib().fw_restore_key_group(self._h, buf, len(blob)))
+        self.push_seq = max(self.push_seq, _snapshot_push_seq(blob))
 
     def restore(self, blob: bytes):
         buf = C.create_string_buffer(blob, len(blob))
         check(lib().fw_restore(self._h, buf, len(blob)))
+        self.push_seq = max(self.push_seq, _snapshot_push_seq(blob))
+
+
+def _snapshot_push_seq(blob):
+    """The push counter a snapshot blob carries (SnapHeader / KgHeader .push_seq, the last field)."""
+    import struct
+    off = {0x464c4b57494e3033: 8 + 16 + 32 + 8, 0x464c4b574b473033: 8 + 24 + 32 + 8}.get(struct.unpack_from("<Q", blob, 0)[0])
+    return struct.unpack_from("<q", blob, off)[0] if off is not None else 0

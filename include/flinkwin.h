@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 4
+#define FW_ABI_VERSION 5
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -154,7 +154,11 @@ typedef struct {
     int32_t parallelism;      /* operator parallelism p                                    */
     int32_t subtask_index;    /* this subtask: owns computeKeyGroupRangeForOperatorIndex   */
     int32_t device;           /* HIP device ordinal                                        */
-    int32_t reserved0;
+    int32_t ds_first_ordinals;/* v5, DataStream: 1 = track each window's first element, the value1
+                                 SumAggregator / ComparableAggregator copy into every output record
+                                 (SumAggregator.java:66-76, ComparableAggregator.java:83-104): results
+                                 carry its arrival ordinal (fw_result.first_ord) and
+                                 fw_first_element_events tells the shim which records to keep    */
     int64_t state_capacity;   /* expected max live (key, slice) state entries (sizing hint) */
     int64_t max_batch_rows;   /* max rows per fw_commit / fw_push_device call              */
     int64_t output_capacity;  /* result rows kept between fw_results_reset calls           */
@@ -192,7 +196,10 @@ typedef struct {
 } fw_host_cols;
 
 /* Window results: SQL rows are key ++ aggs ++ (window_start, window_end); DataStream
-   records are (key, agg) with record timestamp window.maxTimestamp() = window_end - 1. */
+   records are the window's first element with the aggregated field set to values[0], record
+   timestamp window.maxTimestamp() = window_end - 1.
+   Arrival ordinal of an element: push_seq << 32 | row, push_seq counting fw_commit /
+   fw_push_device* calls from 0 (continued across fw_restore*), row its index in that call. */
 typedef struct {
     int64_t n;
     int64_t* key;
@@ -200,6 +207,8 @@ typedef struct {
     int64_t* window_end;
     int64_t* values[FW_MAX_AGGS];      /* per agg: int64, or double bits for DOUBLE results */
     uint32_t* null_mask;               /* bit a set => agg a is SQL NULL                */
+    int64_t* first_ord;                /* v5, DataStream with ds_first_ordinals: arrival ordinal of
+                                          the window's first element (value1), else NULL */
 } fw_result;
 
 typedef struct {
@@ -213,6 +222,10 @@ typedef struct {
     int64_t partials_emitted;          /* partial (key, slice) aggregates written by ingest */
     int32_t error_flags;
     int32_t num_superbuckets;
+    /* v5: merge traffic counters (cumulative, device-side): measurement of the flush kernel */
+    int64_t flush_launches;            /* fw_advance / flush launches that merged pending partials */
+    int64_t partials_merged;           /* partial rows those flushes read                */
+    int64_t state_entries_moved;       /* state entries loaded + written back by merge launches */
 } fw_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------- */
@@ -273,6 +286,26 @@ typedef struct {
     int64_t* row;
 } fw_late_rows;
 int fw_late_records(fw_handle* h, fw_late_rows* out);
+
+/* DataStream with ds_first_ordinals: which first elements the host shim must keep.  The reference
+   keeps value1 inside the window state (HeapReducingState holds the reduced record); here the state
+   holds only the aggregate and the first element's arrival ordinal, and the shim keeps the record.
+   retain: ordinals of elements that became the first element of a window state that outlives the
+   advance that created it (one event per window: an element of n sliding windows may be retained
+   n times).  release: ordinals whose window state was cleared (cleanupTime, WindowOperator
+   .clearAllState :494).  A window created and cleared within one advance is neither: its records
+   are still the caller's pending batch.  Ordering for the shim, per advance: fw_results, then the
+   retains (copy the records out of the pushed batches), resolve the results' first_ord, then the
+   releases.  After fw_advance moves the watermark forward every pushed row has been flushed, so the
+   pushed batches may be dropped once the events are read.  Host arrays owned by the handle, valid
+   until the next call; the events are consumed. */
+typedef struct {
+    int64_t n_retain;
+    int64_t* retain;
+    int64_t n_release;
+    int64_t* release;
+} fw_ordinal_events;
+int fw_first_element_events(fw_handle* h, fw_ordinal_events* out);
 
 int fw_advance(fw_handle* h, int64_t watermark);
 int fw_flush(fw_handle* h);

@@ -213,6 +213,8 @@ struct AggState {
 
 struct Row {
     AggState a[FW_MAX_AGGS];
+    int64_t first = -1;  // DataStream: arrival ordinal (push << 32 | row) of the state's first element,
+                         // the value1 every later reduce copies (SumAggregator.java:66-76)
 };
 
 struct OutRow {
@@ -220,6 +222,7 @@ struct OutRow {
     uint64_t v[FW_MAX_AGGS];
     uint32_t null_mask;
     int64_t epoch;  // index of the watermark call that produced it
+    int64_t first;  // DataStream: Row::first of the emitted window
 };
 constexpr int MAX_FIELDS = FW_MAX_AGGS;
 
@@ -374,9 +377,13 @@ struct Oracle {
                     if (s.is_null) {
                         if (isf) s.d = dv; else s.i = iv;
                     } else if (isf) {
-                        if (ds) {  // ComparableAggregator + Comparator: Double.compareTo
-                            int c = java_double_compare(dv, s.d);
-                            if (mx ? c > 0 : c < 0) s.d = dv;
+                        if (ds) {
+                            // ComparableAggregator.reduce (:83-104): c = isExtremal(acc, new);
+                            // MaxComparator is 1 iff acc.compareTo(new) > 0 (Comparator.java:73-80),
+                            // and c == 0 sets the field to the new value: ties (equal under
+                            // Double.compareTo -- only NaNs differ in bits) go to the LATER element
+                            const int c = java_double_compare(s.d, dv);
+                            if (!(mx ? c > 0 : c < 0)) s.d = dv;
                         } else {   // MaxAggFunction: operand > max ; MinAggFunction: operand < min
                             if (mx ? dv > s.d : dv < s.d) s.d = dv;
                         }
@@ -644,6 +651,7 @@ struct Oracle {
         o.key = key;
         o.we = we;
         o.ws = ds ? jsub64(we, cfg.c.size_ms) : get_window_start(we);
+        o.first = acc.first;
         get_value(acc, o.v, &o.null_mask);
         o.epoch = epoch;
         out.push_back(o);
@@ -793,6 +801,7 @@ struct Oracle {
             auto sk = std::make_pair(key, end);
             auto it = state.find(sk);
             Row acc = it == state.end() ? create_accumulators() : it->second;
+            if (it == state.end()) acc.first = (int64_t)(((uint64_t)push_seq << 32) | (uint64_t)row);
             accumulate(acc, vals, no_nulls);  // HeapReducingState.add / HeapAggregatingState.add
             state[sk] = acc;
             // EventTimeTrigger.onElement (:37-45): a window whose maxTimestamp the watermark has
@@ -950,6 +959,11 @@ void or_get_results(void* h, int64_t* key, int64_t* ws, int64_t* we, uint64_t* v
     }
 }
 void or_clear_results(void* h) { ((Oracle*)h)->out.clear(); }
+// DataStream: the first-element arrival ordinal of each result (Row::first), same order as or_get_results
+void or_get_first(void* h, int64_t* first) {
+    Oracle* o = (Oracle*)h;
+    for (size_t i = 0; i < o->out.size(); i++) first[i] = o->out[i].first;
+}
 // late side output rows since the last call (consumed): SoA, vals[c * n + i]
 int64_t or_num_side_rows(void* h) { return (int64_t)((Oracle*)h)->side.size(); }
 void or_take_side_rows(void* h, int64_t* key, int64_t* ts, uint64_t* vals, int64_t* push, int64_t* row) {

@@ -45,6 +45,7 @@ def lib():
             getattr(L, f).argtypes = [vp]
         L.or_get_results.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.or_clear_results.argtypes = [vp]
+        L.or_get_first.argtypes = [vp, vp]
         L.or_num_side_rows.restype = i64
         L.or_num_side_rows.argtypes = [vp]
         L.or_take_side_rows.argtypes = [vp, vp, vp, vp, vp, vp]
@@ -138,12 +139,15 @@ class OracleOperator:
         vals = np.empty((max(na, 1), n), np.uint64)
         nm = np.empty(n, np.uint32)
         ep = np.empty(n, np.int64)
+        first = np.empty(n, np.int64)
         if n:
             L.or_get_results(self.h, _ptr(key), _ptr(ws), _ptr(we), _ptr(vals), _ptr(nm), _ptr(ep))
+            L.or_get_first(self.h, _ptr(first))
         if clear:
             L.or_clear_results(self.h)
         return {"key": key, "window_start": ws, "window_end": we,
-                "values": [vals[a].view(np.int64) for a in range(na)], "null_mask": nm, "epoch": ep}
+                "values": [vals[a].view(np.int64) for a in range(na)], "null_mask": nm, "epoch": ep,
+                "first_ord": first}
 
 
     def side_output(self):

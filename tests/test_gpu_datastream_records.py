@@ -1,0 +1,121 @@
+"""DataStream output records on the GPU, record for record.
+
+SumAggregator.reduce (SumAggregator.java:66-76) and ComparableAggregator.reduce
+(ComparableAggregator.java:83-104) return value1 -- the window's first element -- copied, with the
+aggregated field set; MaxComparator / MinComparator (Comparator.java:48-101) leave the field to
+the later element on a Double.compareTo tie (NaN payloads).  The device tracks each window's first
+arrival ordinal and the NaN that arrived last; the record-shaped WindowOperator keeps only the
+first elements the device names (fw_first_element_events).  Checked against the oracle: value bits,
+the first element's ordinal, and the reconstructed records (elements with an extra non-key,
+non-aggregated field), including allowed lateness, side output and a snapshot/restore; at the end
+every window is cleaned and no element may remain retained."""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from flink_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_600_000_000_000
+_SPECIAL = np.array([0x7FF8000000000000, 0xFFF8000000000001, 0x7FF0000000000001, 0x7FF00000DEADBEEF,
+                     0x8000000000000000, 0, np.float64(1.0).view(np.int64), np.float64(-1.0).view(np.int64)],
+                    dtype=np.uint64).view(np.int64)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _batches(seed, n_wm=20, per=2500, n_keys=150, step_ms=1000, ooo=2500, special=True):
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in range(n_wm):
+        base = T0 + b * step_ms
+        ts = (base + rng.integers(0, step_ms, per) - rng.integers(0, ooo, per)).astype(np.int64)
+        keys = rng.integers(0, n_keys, per).astype(np.int64) * 977 - 3000
+        iv = rng.integers(-10**6, 10**6, per).astype(np.int64)
+        dv = (rng.random(per) * 100.0).view(np.int64).copy()
+        if special:
+            sp = rng.random(per) < 0.4
+            dv[sp] = _SPECIAL[rng.integers(0, len(_SPECIAL), int(sp.sum()))]
+        out.append((keys, ts, iv, dv, base + step_ms - ooo // 3))
+    return out
+
+
+CASES = {
+    # (window, lateness, side output, aggregation, value column)
+    "tumble_sum_long": (("tumble", 3000, 0), 0, False, ("sum", "LONG"), 2),
+    "tumble_max_double_nan": (("tumble", 2000, 0), 0, False, ("max", "DOUBLE"), 3),
+    "sliding_min_double_nan": (("sliding", 4000, 1000), 0, False, ("min", "DOUBLE"), 3),
+    "sliding_max_double_lateness": (("sliding", 3000, 1000), 2000, False, ("max", "DOUBLE"), 3),
+    "tumble_min_long_lateness_side": (("tumble", 2000, 0), 1500, True, ("min", "LONG"), 2),
+}
+
+
+def _operator(case):
+    from flink_amd.datastream.window_operator import WindowOperator
+    from flink_amd.datastream.windowing import EventTimeTrigger, SlidingEventTimeWindows, TumblingEventTimeWindows
+    (kind, size, slide), late, side, agg, _ = CASES[case]
+    assigner = TumblingEventTimeWindows.of(size) if kind == "tumble" else SlidingEventTimeWindows.of(size, slide)
+    return WindowOperator(assigner, EventTimeTrigger(), agg, key_type="LONG", state_capacity=1 << 16,
+                          max_batch_rows=1 << 14, output_capacity=1 << 18, allowed_lateness=late,
+                          late_data_output_tag="late" if side else None, field=1).open()
+
+
+def _bits(v):
+    return struct.unpack("<q", struct.pack("<d", v))[0] if isinstance(v, float) else v
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_datastream_records_match_reference_shape(case):
+    from oracle.oracle import OracleOperator
+    op = _operator(case)
+    o = OracleOperator(op.cfg)
+    vcol = CASES[case][4]
+    elements = {}  # arrival ordinal -> element (key, field, tag)
+    snap_at = 9
+    for b, (k, t, iv, dv, wm) in enumerate(_batches(zlib.crc32(case.encode()) % 1000)):
+        v = iv if vcol == 2 else dv
+        seq = op.handle.push_seq
+        recs = []
+        for i in range(len(k)):
+            fv = int(v[i]) if vcol == 2 else struct.unpack("<d", struct.pack("<q", int(v[i])))[0]
+            rec = (int(k[i]), fv, f"e{b}.{i}")  # the tag is a field neither keyed nor aggregated
+            recs.append(rec)
+            elements[(seq << 32) | i] = rec
+        op.process_batch(k, t, v, records=recs)
+        o.process_batch(k, t, [v])
+        got = op.process_watermark(wm)
+        o.process_watermark(wm)
+        want = o.results(clear=True)
+        g = sorted(zip(got["key"].tolist(), got["window_end"].tolist(), got["value"].tolist(), got["first_ord"].tolist(),
+                       [(r[0], _bits(r[1]), r[2]) for r in got["records"]]))
+        w = sorted(zip(want["key"].tolist(), want["window_end"].tolist(), want["values"][0].tolist(),
+                       want["first_ord"].tolist()))
+        assert [x[:4] for x in g] == w, f"batch {b}: value bits / first element differ from the oracle"
+        for key, we, val, fo, rec in g:  # value1.copy() with the field set
+            first = elements[fo]
+            assert rec == (first[0], val, first[2]), f"batch {b}: record of window ({key}, {we})"
+        if CASES[case][2]:
+            sg, so = op.side_output(), o.side_output()
+            assert sorted(zip(sg["push_seq"].tolist(), sg["row"].tolist())) == \
+                sorted(zip(so["push_seq"].tolist(), so["row"].tolist()))
+        if b == snap_at:  # checkpoint: device state + the retained first elements, restored fresh
+            blob = op.snapshot_state()
+            op.close()
+            op = _operator(case)
+            op.initialize_state(blob)
+            o.snapshot_restore()
+        assert len(op._retained) <= op.handle.stats()["live_state_entries"]
+    op.process_watermark(T0 + 10**9)  # every window fires and is cleaned
+    o.process_watermark(T0 + 10**9)
+    assert op.handle.stats()["live_state_entries"] == 0
+    assert not op._retained, "first elements still retained after every window was cleared"
+    assert op.num_late_records_dropped == o.late_dropped
+    op.close()

@@ -523,7 +523,9 @@ def test_bench_workload_full_size_key_subset(wl_name):
     from flink_amd.runtime.handle import WindowAggHandle
     from oracle.oracle import OracleOperator
     wl = bench.WORKLOADS[wl_name]
-    steps, B, MOD, PICK = 6, bench.B, 97, 13
+    # CFG5: 27 steps = 4077 s of event time at 27 778 ev/s, past the 1 h CUMULATE window's last step
+    # (its final slice fires and the window's first-slice state is cleared, SliceAssigners.java:398-453)
+    steps, B, MOD, PICK = (27 if wl_name == "cfg5" else 6), bench.B, 97, 13
     L = _native.lib()
     zipf_t = None
     if wl["dist"] == 1:
@@ -540,6 +542,7 @@ def test_bench_workload_full_size_key_subset(wl_name):
     total_rows = 0
     count_sum = 0
     cs = wl["count_star"]
+    live, wms, ends = [], [], set()
     for b in range(steps + 1):
         wm = bench.watermark(b, wl["rate"])
         if b == steps:  # last: fire every window (CUMULATE: a few more steps; its 1 h windows
@@ -554,6 +557,9 @@ def test_bench_workload_full_size_key_subset(wl_name):
         g.advance(wm)
         o.process_watermark(wm)
         r = g.results(reset=True)
+        live.append(g.stats()["live_state_entries"])
+        wms.append(wm)
+        ends.update(np.unique(r["window_end"]).tolist())
         total_rows += len(r["key"])
         if cs >= 0:
             count_sum += int(r["values"][cs].sum())
@@ -570,6 +576,14 @@ def test_bench_workload_full_size_key_subset(wl_name):
     kind = wl["window"][0]
     if kind == "HOP" and cs >= 0:       # every event is counted in size/slide windows
         assert count_sum == steps * B * (wl["window"][1] // wl["window"][2])
+    if kind == "CUMULATE":
+        # the first 1 h window's last step fired (window_end = its start + 1 h) ...
+        first_end = bench.T0 - bench.T0 % wl["window"][1] + wl["window"][1]
+        assert first_end in ends and wms[-1] >= first_end
+        # ... and its state (first slice + current slice per key) was cleared: the live entries after
+        # the watermark crossed the hour are far fewer than just before it
+        cross = next(i for i, w in enumerate(wms) if w >= first_end - 1)
+        assert live[cross] < 0.8 * live[cross - 1], (live[cross - 1], live[cross])
     g.close()
 
 

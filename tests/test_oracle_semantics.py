@@ -5,7 +5,11 @@ derived by hand from the reference's aggregate-function expressions:
   value and replace it only on a strict `>` / `<` (NaN compares false both ways, -0.0 == +0.0),
   and merge slices the same way on their result values (MaxAggFunction.java:82-95).
 * DataStream max/min(double): ComparableAggregator + Comparator (Comparator.java:48-101) use
-  Double.compareTo, a total order with -0.0 < +0.0 and NaN greatest.
+  Double.compareTo, a total order with -0.0 < +0.0 and NaN greatest.  MaxComparator.isExtremal is 1
+  only when the accumulator is strictly greater, and ComparableAggregator.reduce (:83-104) sets the
+  field to the new value otherwise, so ties -- all NaNs compare equal -- go to the LATER element.
+* DataStream output records: value1 (the window's first element) with the field set
+  (SumAggregator.java:66-76): the oracle reports that element's arrival ordinal.
 * NULL inputs: SumAggFunction.java:66-69 (NULL until a non-NULL operand), CountAggFunction.java:60-87
   (counts non-NULL operands), AvgAggFunction.java:79-105 (sum and count of non-NULL operands; NULL
   result when the count is 0), Max/MinAggFunction (NULL operands skipped).
@@ -102,4 +106,38 @@ def test_sql_hop_merge_uses_result_values():
     we = list(r["window_end"])
     i = we.index(T0 + 2000)
     assert math.isnan(struct.unpack("<d", struct.pack("<q", int(r["values"][0][i])))[0])
+    o.close()
+
+
+NAN3 = struct.unpack("<d", struct.pack("<Q", 0x7FF0000000000001))[0]  # signalling-NaN payload
+
+
+def test_datastream_ties_go_to_the_later_element():
+    # (inputs, DataStream max, DataStream min) -- NaN bit patterns compared exactly
+    cases = [
+        ([NAN2, math.nan], math.nan, math.nan),      # both NaN: the later one, for max and min
+        ([math.nan, NAN2], NAN2, NAN2),
+        ([NAN2, 1.0, NAN3, 2.0], NAN3, 1.0),         # max: the last NaN; min: the least non-NaN
+        ([NAN3, NAN2, -0.0, 0.0], NAN2, -0.0),
+        ([0.0, -0.0, 0.0], 0.0, -0.0),
+    ]
+    for vals, mx, mn in cases:
+        rmax = run(vals, [(abi.AGG_MAX, 0, abi.T_F64)], api=abi.API_DATASTREAM)
+        rmin = run(vals, [(abi.AGG_MIN, 0, abi.T_F64)], api=abi.API_DATASTREAM)
+        assert rmax["values"][0][0] == bits(mx), (vals, "max", hex(int(rmax["values"][0][0]) & (2**64 - 1)))
+        assert rmin["values"][0][0] == bits(mn), (vals, "min", hex(int(rmin["values"][0][0]) & (2**64 - 1)))
+
+
+def test_datastream_first_element_ordinal():
+    # one key, sliding 2 s / 1 s: rows at T0+0.., each window's first element is its earliest
+    # arrival (push << 32 | row), whatever its timestamp
+    cfg = abi.make_config(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=2000, slide_ms=1000,
+                          aggs=[(abi.AGG_SUM, 0, abi.T_I64)], value_col_types=[abi.T_I64], key_hash=abi.KEYHASH_LONG)
+    o = OracleOperator(cfg)
+    o.process_batch(np.zeros(3, np.int64), np.array([T0 + 1500, T0 + 200, T0 + 1700], np.int64), [np.arange(3, dtype=np.int64)])
+    o.process_batch(np.zeros(2, np.int64), np.array([T0 + 2500, T0 + 100], np.int64), [np.arange(2, dtype=np.int64)])
+    o.process_watermark(T0 + 10_000)
+    r = o.results()
+    got = dict(zip(r["window_end"].tolist(), r["first_ord"].tolist()))
+    assert got == {T0 + 1000: 1, T0 + 2000: 0, T0 + 3000: 0, T0 + 4000: (1 << 32) | 0}
     o.close()

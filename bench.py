@@ -190,19 +190,21 @@ def main():
         k, t, v = ex.exchange(gk[b], gt[b], [gv[b]] if nv else [])
         return k, t, (v[0] if nv else None)
 
-    # the timed keyBy exchange is the packed padded one (no host round trip per step); its per-destination
-    # capacity comes from the untimed pass below (the largest share any subtask gets, + 5 %)
-    seg_cap = [0]
-
+    # the timed keyBy exchange is the packed padded one: segments of the batch's even share + 25 %
+    # (KeyByExchange.segment_capacity, from the batch itself), rows past a segment in an overflow
+    # round; the overflow decision and the watermark valve share one host all-reduce per step
     def push_step(b, handle):
+        """Ingest step b; returns the watermark to advance to (the valve's minimum over subtasks)."""
         if world == 1:
             handle.push_device(gk[b], gt[b], [gv[b]] if nv else [])
-            return
-        rows, rc, w = ex.exchange_packed(gk[b], gt[b], [gv[b]] if nv else [], seg_cap[0])
+            return watermark(b, wl["rate"])
+        rows, rc, w, spill, wm = ex.exchange_packed(gk[b], gt[b], [gv[b]] if nv else [],
+                                                    watermark=watermark(b, wl["rate"]))
         handle.push_device_packed_segments(rc, rows, w)
-
-    def global_watermark(b):
-        return ex.global_watermark(watermark(b, wl["rate"]))
+        if spill is not None:
+            n_sp = spill.numel() // w
+            handle.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=dev), spill, w)
+        return wm
 
     out_cap = 2 * keys_total // world + (1 << 20)
     if wl["window"][0] == "CUMULATE":
@@ -211,8 +213,7 @@ def main():
 
     def run(first, nsteps, handle):
         for b in range(first, first + nsteps):
-            push_step(b, handle)
-            wm = global_watermark(b)
+            wm = push_step(b, handle)
             handle.reset_results()       # blackhole sink: results of the previous watermark consumed
             handle.advance(wm)
 
@@ -234,13 +235,6 @@ def main():
         import math
         interval = math.gcd(wl["window"][1], wl["window"][2])
     groups = []
-    if world > 1:
-        mx = 0
-        for b in range(total_steps):
-            _, _, _, cnt = ex.partition(gk[b], gt[b], [])
-            mx = max(mx, int(cnt.max()))
-        mx = ex.global_max(mx)  # every subtask sizes its segments alike
-        seg_cap[0] = mx + mx // 20 + 256
     for b in range(args.warmup, total_steps):
         k, t, _ = exchange(b)
         sl = torch.div(t, interval, rounding_mode="floor")
@@ -278,7 +272,6 @@ def main():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
-    ex.check_capacity()
     st = h.stats()
     kt = h.kernel_times()
     if st["error_flags"]:
@@ -391,7 +384,11 @@ def main():
                        "parallelism": f"key-group sharded x{world}" + (
                            "" if world == 1 else " + RCCL all-to-all" if args.dist_backend == "nccl"
                            else " + gloo all-to-all (rehearsal, shared GPU)"),
-                       "max_parallelism": 128, "superbuckets": st["num_superbuckets"]},
+                       "max_parallelism": 128, "superbuckets": st["num_superbuckets"],
+                       "exchange": None if world == 1 else {
+                           "kind": "packed padded all-to-all, segments of the batch's even share + 25 %",
+                           "segment_rows": ex.segment_capacity(B, world),
+                           "overflow_rounds": ex.spill_rounds}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                          "kernel": "fw::k_ingest (K1 key group + K2 slice assign + K3 LDS segmented reduce, "

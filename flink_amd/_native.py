@@ -47,6 +47,7 @@ def lib():
         "fw_push_device_segments": (i32, [vp, i32, i64, vp, vp, vp, vp, vp, vp]),
         "fw_push_device_packed_segments": (i32, [vp, i32, i64, vp, vp, i32]),
         "fw_partition_packed": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, i64, vp]),
+        "fw_partition_packed_spill": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, vp, i64, vp]),
         "fw_advance": (i32, [vp, i64]),
         "fw_flush": (i32, [vp]),
         "fw_results": (i32, [vp, P(abi.fw_result), i32]),
@@ -71,6 +72,11 @@ def lib():
         "fw_host_time_op": (i32, [P(abi.fw_config), i32, i64, P(i64)]),
         "fw_late_records": (i32, [vp, P(abi.fw_late_rows)]),
         "fw_first_element_events": (i32, [vp, P(abi.fw_ordinal_events)]),
+        "fw_push_device_key_rows": (i32, [vp, i64, vp, vp, vp, vp, vp]),
+        "fw_key_row_images": (i32, [P(abi.fw_key_field), i32, i64, vp, vp, vp]),
+        "fw_host_key_row_image_lengths": (i32, [P(abi.fw_key_field), i32, i64, vp]),
+        "fw_host_key_row_images": (i32, [P(abi.fw_key_field), i32, i64, vp, vp]),
+        "fw_host_key_row_image_hash": (i32, [vp, i64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -88,9 +94,11 @@ EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_ge
             "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_key_row_hash", "fw_host_key_row_hash",
-            "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_workspace_bytes",
+            "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_packed_spill", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
-            "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records", "fw_first_element_events"]
+            "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records", "fw_first_element_events",
+            "fw_push_device_key_rows", "fw_key_row_images", "fw_host_key_row_image_lengths", "fw_host_key_row_images",
+            "fw_host_key_row_image_hash"]
 
 
 def check(rc):

@@ -44,6 +44,7 @@ KEYHASH_INT = 1
 KEYHASH_BINROW_BIGINT = 2
 KEYHASH_BINROW_INT = 3
 KEYHASH_PRECOMPUTED = 4
+KEYHASH_KEYROW = 5
 
 # fw_key_field_kind (key-row fields for fw_key_row_hash)
 KF_STRING, KF_FIXED1, KF_FIXED2, KF_FIXED4, KF_FIXED8 = 0, 1, 2, 4, 8
@@ -93,7 +94,7 @@ class fw_config(C.Structure):
         ("late_side_output", C.c_int32),
         ("tz_use_dst", C.c_int32),
         ("tz_n", C.c_int32),
-        ("reserved1", C.c_int32),
+        ("key_row_max_bytes", C.c_int32),
         ("tz_utc", C.POINTER(C.c_int64)),
         ("tz_offset_ms", C.POINTER(C.c_int64)),
     ]
@@ -108,14 +109,18 @@ class fw_host_cols(C.Structure):
     _fields_ = [("key", C.POINTER(C.c_int64)), ("ts", C.POINTER(C.c_int64)),
                 ("key_hash", C.POINTER(C.c_int32)),
                 ("values", C.POINTER(C.c_int64) * FW_MAX_COLS),
-                ("nulls", C.POINTER(C.c_uint8) * FW_MAX_COLS)]
+                ("nulls", C.POINTER(C.c_uint8) * FW_MAX_COLS),
+                ("key_row_offsets", C.POINTER(C.c_int64)), ("key_row_bytes", C.POINTER(C.c_uint8)),
+                ("key_row_bytes_cap", C.c_int64)]
 
 
 class fw_result(C.Structure):
     _fields_ = [("n", C.c_int64), ("key", C.POINTER(C.c_int64)),
                 ("window_start", C.POINTER(C.c_int64)), ("window_end", C.POINTER(C.c_int64)),
                 ("values", C.POINTER(C.c_int64) * FW_MAX_AGGS),
-                ("null_mask", C.POINTER(C.c_uint32)), ("first_ord", C.POINTER(C.c_int64))]
+                ("null_mask", C.POINTER(C.c_uint32)), ("first_ord", C.POINTER(C.c_int64)),
+                ("key_row_len", C.POINTER(C.c_int32)), ("key_row_bytes", C.POINTER(C.c_uint8)),
+                ("key_row_stride", C.c_int64)]
 
 
 class fw_ordinal_events(C.Structure):
@@ -137,7 +142,8 @@ class fw_stats(C.Structure):
                 ("error_flags", C.c_int32),
                 ("num_superbuckets", C.c_int32),
                 ("flush_launches", C.c_int64), ("partials_merged", C.c_int64),
-                ("state_entries_moved", C.c_int64)]
+                ("state_entries_moved", C.c_int64), ("key_rows", C.c_int64),
+                ("key_row_collections", C.c_int64)]
 
 
 KT_PARTITION, KT_SCAN, KT_REDUCE, KT_MERGE, KT_OTHER = 0, 1, 2, 3, 4
@@ -161,7 +167,7 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
                 max_parallelism=128, parallelism=1, subtask_index=0, device=0,
                 state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22,
                 nullable_cols=(), agg_phase=PHASE_ONE, allowed_lateness_ms=0, late_side_output=False,
-                shift_zone=None, ds_first_ordinals=False):
+                shift_zone=None, ds_first_ordinals=False, key_row_max_bytes=0):
     """Build an fw_config.  ``aggs`` is a sequence of (kind, input_col, type); ``nullable_cols``
     the value columns that may hold SQL NULLs; ``shift_zone`` a TIMESTAMP_LTZ window's time zone
     (a zone name, or a ShiftZone from flink_amd.table.time_zone; None / "UTC": no shift)."""
@@ -196,6 +202,7 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
     c.allowed_lateness_ms = allowed_lateness_ms
     c.late_side_output = 1 if late_side_output else 0
     c.ds_first_ordinals = 1 if ds_first_ordinals else 0
+    c.key_row_max_bytes = key_row_max_bytes
     set_shift_zone(c, shift_zone)
     return c
 

@@ -193,6 +193,22 @@ struct fw_handle {
     uint8_t* d_nul[FW_MAX_COLS] = {};
     int64_t reserved = -1;
 
+    // FW_KEYHASH_KEYROW: the key-row intern table, per-push intern output, key-row staging
+    bool keyrow = false;
+    KeyRowTable kr{};
+    int64_t kr_scratch_n = 0;
+    int64_t* d_kid = nullptr;       // interned ids of the push being ingested
+    int32_t* d_khash = nullptr;     // their hashCodes
+    int64_t* h_kro[2] = {};         // pinned staging: key row offsets / bytes (fw_reserve)
+    uint8_t* h_krb[2] = {};
+    int64_t krb_cap = 0;            // staging bytes per batch
+    int64_t* d_kro = nullptr;
+    uint8_t* d_krb = nullptr;
+    int32_t* res_kr_len = nullptr;  // result key rows (fw_results)
+    uint64_t* res_kr_img = nullptr;
+    std::vector<int32_t> r_kr_len;
+    std::vector<uint64_t> r_kr_img;
+
     // host copies of results
     std::vector<int64_t> r_key, r_ws, r_we;
     std::vector<uint64_t> r_val[FW_MAX_AGGS];
@@ -227,7 +243,15 @@ int validate_and_plan(fw_handle* h) {
     if (c.max_parallelism < 1 || c.max_parallelism > 32768) return fail(FW_E_INVALID, "max_parallelism out of range");
     if (c.parallelism < 1 || c.parallelism > c.max_parallelism) return fail(FW_E_INVALID, "parallelism out of range");
     if (c.subtask_index < 0 || c.subtask_index >= c.parallelism) return fail(FW_E_INVALID, "subtask_index out of range");
-    if (c.key_hash < FW_KEYHASH_LONG || c.key_hash > FW_KEYHASH_PRECOMPUTED) return fail(FW_E_INVALID, "bad key_hash");
+    if (c.key_hash < FW_KEYHASH_LONG || c.key_hash > FW_KEYHASH_KEYROW) return fail(FW_E_INVALID, "bad key_hash");
+    h->keyrow = c.key_hash == FW_KEYHASH_KEYROW;
+    if (h->keyrow) {
+        if (c.api != FW_API_SQL) return fail(FW_E_INVALID, "key rows (FW_KEYHASH_KEYROW) are SQL keys");
+        const int32_t mb = c.key_row_max_bytes ? c.key_row_max_bytes : 120;  // 120: one 128-B line per id
+        if (mb < 16 || mb > 4096 || (mb & 7)) return fail(FW_E_INVALID, "key_row_max_bytes must be a multiple of 8 in [16, 4096]");
+        h->kr.stride_words = (int32_t)(((8 + mb) + 127) / 128 * 16);  // meta word + image, whole 128-B lines
+        h->kr.max_len = mb;
+    }
     if (c.size_ms <= 0) return fail(FW_E_INVALID, "window size must be > 0");
     // ---- window (SliceAssigners constructors' argument checks)
     WinDesc& w = h->win;
@@ -470,7 +494,7 @@ int validate_and_plan(fw_handle* h) {
 
     // ---- key space: this subtask's key groups, split into superbuckets
     KeySpace& ks = h->ks;
-    ks.hash_kind = c.key_hash;
+    ks.hash_kind = h->keyrow ? FW_KEYHASH_PRECOMPUTED : c.key_hash;  // key rows route by their interned hash
     ks.max_p = c.max_parallelism;
     ks.maxp_div = make_udiv32((uint32_t)c.max_parallelism);
     ks.kg_start = (c.subtask_index * c.max_parallelism + c.parallelism - 1) / c.parallelism;
@@ -512,6 +536,12 @@ int validate_and_plan(fw_handle* h) {
     h->out_cap = c.output_capacity;
     h->slab_cap = std::max<int64_t>(64, (2 * c.output_capacity + ks.n_sb - 1) / ks.n_sb);
     h->stage_cap = c.max_batch_rows;
+    if (h->keyrow) {
+        h->kr.cap_ids = std::max<int64_t>(1024, std::max<int64_t>(c.state_capacity, 0) + (int64_t)FW_MAX_PENDING * c.max_batch_rows);
+        if (h->kr.cap_ids >= (1ll << 31) - 2) return fail(FW_E_INVALID, "key-row table over 2^31 ids");
+        h->kr.n_slots = next_pow2(2 * h->kr.cap_ids);
+        h->krb_cap = c.max_batch_rows * (int64_t)h->kr.max_len;
+    }
     return FW_OK;
 }
 
@@ -537,6 +567,17 @@ int allocate(fw_handle* h) {
     if (h->lfire_cap && (rc = dalloc(&h->lfire, (size_t)h->lfire_cap * LFW))) return rc;
     if (h->side_cap && (rc = dalloc(&h->side, (size_t)h->side_cap * SOW))) return rc;
     if (h->ordev_cap && (rc = dalloc(&h->ordev, (size_t)h->ordev_cap))) return rc;
+    if (h->keyrow) {
+        KeyRowTable& t = h->kr;
+        if ((rc = dalloc(&t.slots, (size_t)t.n_slots))) return rc;
+        if ((rc = dalloc(&t.arena, (size_t)t.cap_ids * t.stride_words))) return rc;
+        if ((rc = dalloc(&t.mark, (size_t)t.cap_ids))) return rc;
+        if ((rc = dalloc(&t.free_list, (size_t)t.cap_ids))) return rc;
+        HIP_TRY(hipMemsetAsync(t.slots, 0, sizeof(uint32_t) * t.n_slots, h->stream));
+        HIP_TRY(hipMemsetAsync(t.mark, 0, sizeof(uint32_t) * t.cap_ids, h->stream));
+        if ((rc = dalloc(&h->res_kr_len, (size_t)h->out_cap))) return rc;
+        if ((rc = dalloc(&h->res_kr_img, (size_t)h->out_cap * (t.stride_words - 1)))) return rc;
+    }
     if (!h->tz_utc.empty()) {  // shift-zone table on the device; the kernels' WinDesc points at it
         const size_t n = h->tz_utc.size();
         if ((rc = dalloc(&h->d_tz, 3 * n))) return rc;
@@ -599,6 +640,14 @@ int alloc_staging(fw_handle* h) {
         HIP_TRY(hipEventRecord(h->stage_ev[b], h->stream));
     }
     int rc;
+    if (h->keyrow) {
+        for (int b = 0; b < 2; b++) {
+            HIP_TRY(hipHostMalloc((void**)&h->h_kro[b], (n + 1) * 8, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&h->h_krb[b], (size_t)std::max<int64_t>(h->krb_cap, 8), hipHostMallocDefault));
+        }
+        if ((rc = dalloc(&h->d_kro, n + 1))) return rc;
+        if ((rc = dalloc(&h->d_krb, (size_t)std::max<int64_t>(h->krb_cap, 8)))) return rc;
+    }
     if ((rc = dalloc(&h->d_key, n))) return rc;
     if ((rc = dalloc(&h->d_ts, n))) return rc;
     if ((rc = dalloc(&h->d_kh, n))) return rc;
@@ -777,6 +826,30 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
     return FW_OK;
 }
 
+// interns n key-row images (device) into the table: d_kid / d_khash hold their ids and hashCodes
+int kr_intern(fw_handle* h, int64_t n, const int64_t* d_off, const uint8_t* d_bytes) {
+    if (n > h->kr_scratch_n) {
+        hipFree(h->d_kid);
+        hipFree(h->d_khash);
+        h->d_kid = nullptr;
+        h->d_khash = nullptr;
+        h->kr_scratch_n = 0;
+        int rc;
+        if ((rc = dalloc(&h->d_kid, (size_t)n))) return rc;
+        if ((rc = dalloc(&h->d_khash, (size_t)n))) return rc;
+        h->kr_scratch_n = n;
+    }
+    HIP_TRY(launch_kr_intern(h->kr, h->ctrl, n, d_off, d_bytes, h->d_kid, h->d_khash, h->stream));
+    return FW_OK;
+}
+
+int push_key_rows(fw_handle* h, int64_t n, const int64_t* d_off, const uint8_t* d_bytes, const int64_t* ts,
+                  const void* const* vals, const uint8_t* const* nulls) {
+    int rc = kr_intern(h, n, d_off, d_bytes);
+    if (rc) return rc;
+    return push(h, n, h->d_kid, ts, h->d_khash, vals, nulls);
+}
+
 // earliest watermark-visible time of an entry's timers, as a window end (is_fired(x, W) <=> due):
 // the maxTimestamp timer at its window end, a DataStream cleanup timer at cleanupTime + 1
 int64_t entry_timer_end(const fw_handle* h, int64_t slice, uint64_t flags) {
@@ -827,6 +900,20 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->lfire);
     hipFree(h->side);
     hipFree(h->ordev);
+    hipFree(h->kr.slots);
+    hipFree(h->kr.arena);
+    hipFree(h->kr.mark);
+    hipFree(h->kr.free_list);
+    hipFree(h->d_kid);
+    hipFree(h->d_khash);
+    hipFree(h->d_kro);
+    hipFree(h->d_krb);
+    hipFree(h->res_kr_len);
+    hipFree(h->res_kr_img);
+    for (int b = 0; b < 2; b++) {
+        hipHostFree(h->h_kro[b]);
+        hipHostFree(h->h_krb[b]);
+    }
     hipFree(h->d_tz);
     hipFree(h->state);
     hipFree(h->state_count);
@@ -902,6 +989,12 @@ int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out) {
         out->values[v] = h->h_val[b][v];
         out->nulls[v] = h->h_nul[b][v];
     }
+    if (h->keyrow) {
+        out->key_row_offsets = h->h_kro[b];
+        out->key_row_bytes = h->h_krb[b];
+        out->key_row_bytes_cap = h->krb_cap;
+        h->h_kro[b][0] = 0;
+    }
     h->reserved = n;
     return FW_OK;
 }
@@ -915,7 +1008,16 @@ int fw_commit(fw_handle* h, int64_t n) {
     if (n == 0) return FW_OK;
     // device staging is reused across commits; ingest of the previous commit is ordered before
     // these copies on the same stream
-    HIP_TRY(hipMemcpyAsync(h->d_key, h->h_key[b], n * 8, hipMemcpyHostToDevice, h->stream));
+    int64_t krb_n = 0;
+    if (h->keyrow) {
+        krb_n = h->h_kro[b][n];
+        if (h->h_kro[b][0] != 0 || krb_n < 0 || krb_n > h->krb_cap)
+            return fail(FW_E_INVALID, "key row offsets must start at 0 and end within key_row_bytes_cap");
+        HIP_TRY(hipMemcpyAsync(h->d_kro, h->h_kro[b], (n + 1) * 8, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->d_krb, h->h_krb[b], (size_t)krb_n, hipMemcpyHostToDevice, h->stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(h->d_key, h->h_key[b], n * 8, hipMemcpyHostToDevice, h->stream));
+    }
     HIP_TRY(hipMemcpyAsync(h->d_ts, h->h_ts[b], n * 8, hipMemcpyHostToDevice, h->stream));
     if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED)
         HIP_TRY(hipMemcpyAsync(h->d_kh, h->h_kh[b], n * 4, hipMemcpyHostToDevice, h->stream));
@@ -931,7 +1033,25 @@ int fw_commit(fw_handle* h, int64_t n) {
         vals[v] = h->d_val[v];
         nuls[v] = h->d_nul[v];
     }
+    if (h->keyrow) return push_key_rows(h, n, h->d_kro, h->d_krb, h->d_ts, vals, nuls);
     return push(h, n, h->d_key, h->d_ts, h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED ? h->d_kh : nullptr, vals, nuls);
+}
+
+int fw_push_device_key_rows(fw_handle* h, int64_t n, const int64_t* d_key_row_offsets, const uint8_t* d_key_row_bytes,
+                            const int64_t* d_ts, const void* const* d_values, const uint8_t* const* d_nulls) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    if (!h->keyrow) return fail(FW_E_INVALID, "fw_push_device_key_rows needs a FW_KEYHASH_KEYROW operator");
+    if (n < 0) return fail(FW_E_INVALID, "negative n");
+    if (n == 0) return FW_OK;
+    if (!d_key_row_offsets || !d_key_row_bytes || !d_ts) return fail(FW_E_INVALID, "null key row / ts column");
+    if (h->nv > 0 && !d_values) return fail(FW_E_INVALID, "value columns required");
+    for (int s = 0; s < h->nv; s++) {
+        const int v = h->slot_col[s];
+        if (!d_values[v]) return fail(FW_E_INVALID, "value column %d is NULL", v);
+        if (((h->cfg.nullable_cols >> v) & 1u) && (!d_nulls || !d_nulls[v]))
+            return fail(FW_E_INVALID, "nullable value column %d needs its null-flag column", v);
+    }
+    return push_key_rows(h, n, d_key_row_offsets, d_key_row_bytes, d_ts, d_values, d_nulls);
 }
 
 int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t* d_ts, const int32_t* d_key_hash,
@@ -940,6 +1060,7 @@ int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t*
     if (n < 0) return fail(FW_E_INVALID, "negative n");
     if (n == 0) return FW_OK;
     if (!d_key || !d_ts) return fail(FW_E_INVALID, "null key/ts column");
+    if (h->keyrow) return fail(FW_E_INVALID, "a FW_KEYHASH_KEYROW operator takes key rows (fw_push_device_key_rows)");
     if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED && !d_key_hash) return fail(FW_E_INVALID, "key_hash column required");
     if (h->nv > 0 && !d_values) return fail(FW_E_INVALID, "value columns required");
     for (int s = 0; s < h->nv; s++) {
@@ -956,6 +1077,7 @@ int fw_push_device_segments(fw_handle* h, int32_t n_segs, int64_t seg_len, const
                             const void* const* d_values, const uint8_t* const* d_nulls) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     if (n_segs < 0 || seg_len < 1 || (n_segs > 0 && !d_seg_counts)) return fail(FW_E_INVALID, "bad segments");
+    if (h->keyrow) return fail(FW_E_INVALID, "a FW_KEYHASH_KEYROW operator takes key rows (fw_push_device_key_rows)");
     const int64_t n = (int64_t)n_segs * seg_len;
     if (n == 0) return FW_OK;
     if (!d_key || !d_ts) return fail(FW_E_INVALID, "null key/ts column");
@@ -975,8 +1097,8 @@ int fw_push_device_packed_segments(fw_handle* h, int32_t n_segs, int64_t seg_len
     if (!h) return fail(FW_E_INVALID, "null handle");
     if (n_segs < 0 || seg_len < 1 || (n_segs > 0 && !d_seg_counts)) return fail(FW_E_INVALID, "bad segments");
     if (row_words != 2 + h->cfg.n_value_cols) return fail(FW_E_INVALID, "row_words %d != 2 + value columns", row_words);
-    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED || h->cfg.nullable_cols)
-        return fail(FW_E_INVALID, "packed rows carry no key-hash or null-flag columns");
+    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED || h->keyrow || h->cfg.nullable_cols)
+        return fail(FW_E_INVALID, "packed rows carry no key-hash, key-row or null-flag columns");
     const int64_t n = (int64_t)n_segs * seg_len;
     if (n == 0) return FW_OK;
     if (!d_rows) return fail(FW_E_INVALID, "null rows");
@@ -989,6 +1111,10 @@ int fw_advance(fw_handle* h, int64_t watermark) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     int rc = launch_merge(h, watermark, 0);
     if (rc) return rc;
+    if (h->keyrow)  // key rows no state / partial / timer request / unread result holds any more
+        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->ks.n_sb, h->cap_e, 3 + h->nw_t,
+                                  2 + h->nw_t, h->parts, h->cap_rows, h->treq, h->out_key, h->sb_out, h->slab_cap,
+                                  h->stream));
     if (watermark > h->host_cur) h->host_cur = watermark;
     return FW_OK;
 }
@@ -1028,6 +1154,10 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     ca.res_null = h->res_null;
     ca.res_cap = h->out_cap;
     HIP_TRY(launch_compact(ca, h->stream, h->timer));
+    const int32_t krw = h->kr.stride_words - 1;  // image words per result row
+    if (h->keyrow)  // each result row's key row, gathered from the table while its id is held
+        HIP_TRY(launch_kr_result_rows(h->kr, h->res_key, h->coff + h->ks.n_sb + 1, h->out_cap, h->res_kr_len,
+                                      h->res_kr_img, krw, h->stream));
     Ctrl c;
     int rc = read_ctrl(h, &c);
     if (rc) return rc;
@@ -1048,6 +1178,11 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
         for (int g = 0; g < nv; g++) out->values[g] = (int64_t*)h->res_val[g];
         if (nv < na) out->first_ord = (int64_t*)h->res_val[nv];
         out->null_mask = h->res_null;
+        if (h->keyrow) {
+            out->key_row_len = h->res_kr_len;
+            out->key_row_bytes = (uint8_t*)h->res_kr_img;
+            out->key_row_stride = 8ll * krw;
+        }
         return FW_OK;
     }
     h->r_key.resize(n);
@@ -1064,6 +1199,14 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
         h->r_val[g].resize(n);
         if (n) HIP_TRY(hipMemcpyAsync(h->r_val[g].data(), h->res_val[g], n * 8, hipMemcpyDeviceToHost, h->stream));
     }
+    if (h->keyrow) {
+        h->r_kr_len.resize(n);
+        h->r_kr_img.resize((size_t)n * krw);
+        if (n) {
+            HIP_TRY(hipMemcpyAsync(h->r_kr_len.data(), h->res_kr_len, n * 4, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipMemcpyAsync(h->r_kr_img.data(), h->res_kr_img, (size_t)n * krw * 8, hipMemcpyDeviceToHost, h->stream));
+        }
+    }
     HIP_TRY(hipStreamSynchronize(h->stream));
     out->key = h->r_key.data();
     out->window_start = h->r_ws.data();
@@ -1071,6 +1214,11 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     for (int g = 0; g < nv; g++) out->values[g] = (int64_t*)h->r_val[g].data();
     if (nv < na) out->first_ord = (int64_t*)h->r_val[nv].data();
     out->null_mask = h->r_null.data();
+    if (h->keyrow) {
+        out->key_row_len = h->r_kr_len.data();
+        out->key_row_bytes = (uint8_t*)h->r_kr_img.data();
+        out->key_row_stride = 8ll * krw;
+    }
     return FW_OK;
 }
 
@@ -1172,6 +1320,8 @@ int fw_get_stats(fw_handle* h, fw_stats* out) {
     out->flush_launches = (int64_t)c.flush_launches;
     out->partials_merged = (int64_t)c.parts_merged;
     out->state_entries_moved = (int64_t)c.state_moved;
+    out->key_rows = h->keyrow ? c.kr_next_id - std::max<int64_t>(0, c.kr_free_count - std::min(c.kr_free_cursor, c.kr_free_count)) : 0;
+    out->key_row_collections = c.kr_collections;
     return FW_OK;
 }
 
@@ -1246,7 +1396,7 @@ static uint64_t semantics_fingerprint(const fw_handle* h) {
     mix(h->win.size);
     mix(h->win.interval);
     mix(h->win.offset);
-    mix(h->ks.hash_kind);
+    mix(h->cfg.key_hash);
     mix(h->ks.max_p);
     mix(c.allowed_lateness_ms);
     mix(c.tz_use_dst);
@@ -1273,6 +1423,91 @@ struct SnapHeader {
 };
 static const uint64_t SNAP_MAGIC = 0x464c4b57494e3033ull;  // "FLKWIN03"
 
+// ---- key rows in a blob (FW_KEYHASH_KEYROW): the entries carry table ids, which mean nothing to
+// another handle, so a blob also holds the key row of every id its entries use:
+//   [n_keys] then per key [id, hash << 32 | length, image words...]  (uint64 words)
+// and a restore interns the images into its own table and rewrites the entries' keys.
+static int kr_section(fw_handle* h, const uint64_t* entries, int64_t n, int pwe, std::vector<uint64_t>* out) {
+    out->clear();
+    if (!h->keyrow) return FW_OK;
+    Ctrl c;
+    int rc = read_ctrl(h, &c);
+    if (rc) return rc;
+    std::vector<int64_t> ids;
+    ids.reserve((size_t)n);
+    for (int64_t i = 0; i < n; i++) ids.push_back((int64_t)entries[(size_t)i * pwe]);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    const int64_t sw = h->kr.stride_words;
+    std::vector<uint64_t> rows;
+    if (!ids.empty()) {
+        if (ids.front() < 0 || ids.back() >= c.kr_next_id) return fail(FW_E_STATE, "state entry with an unknown key row id");
+        rows.resize((size_t)(ids.back() + 1) * sw);
+        HIP_TRY(hipMemcpy(rows.data(), h->kr.arena, rows.size() * 8, hipMemcpyDeviceToHost));
+    }
+    out->push_back((uint64_t)ids.size());
+    for (int64_t id : ids) {
+        const uint64_t* r = rows.data() + (size_t)id * sw;
+        out->push_back((uint64_t)id);
+        out->insert(out->end(), r, r + 1 + ((uint32_t)r[0] >> 3));
+    }
+    return FW_OK;
+}
+
+// interns a blob's key-row section: old id -> this handle's id (and its hash); *used = words read
+static int kr_restore_section(fw_handle* h, const uint64_t* sec, int64_t avail_words, std::vector<std::pair<int64_t, int64_t>>* map,
+                              std::vector<int32_t>* hashes, int64_t* used) {
+    map->clear();
+    hashes->clear();
+    if (avail_words < 1) return fail(FW_E_INVALID, "key-row section truncated");
+    const int64_t nk = (int64_t)sec[0];
+    int64_t p = 1;
+    std::vector<int64_t> off(1, 0);
+    std::vector<uint64_t> bytes;
+    std::vector<int64_t> old;
+    for (int64_t k = 0; k < nk; k++) {
+        if (p + 2 > avail_words) return fail(FW_E_INVALID, "key-row section truncated");
+        const int64_t id = (int64_t)sec[p];
+        const int64_t len = (int64_t)(uint32_t)sec[p + 1];
+        if ((len & 7) || p + 2 + len / 8 > avail_words) return fail(FW_E_INVALID, "key-row section truncated");
+        old.push_back(id);
+        bytes.insert(bytes.end(), sec + p + 2, sec + p + 2 + len / 8);
+        off.push_back(off.back() + len);
+        p += 2 + len / 8;
+    }
+    *used = p;
+    if (nk == 0) return FW_OK;
+    int64_t* d_off = nullptr;
+    uint8_t* d_bytes = nullptr;
+    int rc;
+    if ((rc = dalloc(&d_off, off.size()))) return rc;
+    if ((rc = dalloc(&d_bytes, std::max<size_t>(bytes.size() * 8, 8)))) { hipFree(d_off); return rc; }
+    HIP_TRY(hipMemcpy(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_bytes, bytes.data(), bytes.size() * 8, hipMemcpyHostToDevice));
+    rc = kr_intern(h, nk, d_off, d_bytes);
+    std::vector<int64_t> ids((size_t)nk);
+    hashes->resize((size_t)nk);
+    if (!rc) {
+        HIP_TRY(hipMemcpyAsync(ids.data(), h->d_kid, nk * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(hashes->data(), h->d_khash, nk * 4, hipMemcpyDeviceToHost, h->stream));
+        Ctrl c;
+        rc = read_ctrl(h, &c);  // syncs; a full table is a device error
+    }
+    hipFree(d_off);
+    hipFree(d_bytes);
+    if (rc) return rc;
+    for (int64_t k = 0; k < nk; k++) map->emplace_back(old[(size_t)k], ids[(size_t)k]);
+    std::sort(map->begin(), map->end());
+    return FW_OK;
+}
+
+static int64_t kr_lookup(const std::vector<std::pair<int64_t, int64_t>>& map, int64_t old, size_t* pos) {
+    auto it = std::lower_bound(map.begin(), map.end(), std::make_pair(old, INT64_MIN));
+    if (it == map.end() || it->first != old) return -1;
+    *pos = (size_t)(it - map.begin());
+    return it->second;
+}
+
 int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     if (!h || !size) return fail(FW_E_INVALID, "null argument");
     int rc = force_flush(h);  // prepareSnapshotPreBarrier -> windowBuffer.flush()
@@ -1284,7 +1519,18 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     HIP_TRY(hipMemcpy(cnt.data(), h->state_count, sizeof(int32_t) * nsb, hipMemcpyDeviceToHost));
     int64_t total = 0;
     for (int s = 0; s < nsb; s++) total += cnt[s];
-    const int64_t need = (int64_t)sizeof(SnapHeader) + 4ll * nsb + total * pwe * 8;
+    std::vector<uint64_t> ent((size_t)total * pwe);
+    {
+        uint64_t* e = ent.data();
+        for (int s = 0; s < nsb; s++) {
+            if (!cnt[s]) continue;
+            HIP_TRY(hipMemcpy(e, h->state + (size_t)s * h->cap_e * pwe, (size_t)cnt[s] * pwe * 8, hipMemcpyDeviceToHost));
+            e += (size_t)cnt[s] * pwe;
+        }
+    }
+    std::vector<uint64_t> krs;
+    if ((rc = kr_section(h, ent.data(), total, pwe, &krs))) return rc;
+    const int64_t need = (int64_t)sizeof(SnapHeader) + 4ll * nsb + total * pwe * 8 + (int64_t)krs.size() * 8;
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
@@ -1295,12 +1541,9 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     p += sizeof hd;
     memcpy(p, cnt.data(), 4ll * nsb);
     p += 4ll * nsb;
-    for (int s = 0; s < nsb; s++) {
-        if (!cnt[s]) continue;
-        const size_t bytes = (size_t)cnt[s] * pwe * 8;
-        HIP_TRY(hipMemcpy(p, h->state + (size_t)s * h->cap_e * pwe, bytes, hipMemcpyDeviceToHost));
-        p += bytes;
-    }
+    memcpy(p, ent.data(), ent.size() * 8);
+    p += ent.size() * 8;
+    if (!krs.empty()) memcpy(p, krs.data(), krs.size() * 8);
     return FW_OK;
 }
 
@@ -1313,27 +1556,46 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     if (hd.magic != SNAP_MAGIC || hd.n_sb != nsb || hd.pwe != pwe || hd.cap_e != h->cap_e ||
         hd.semantics != semantics_fingerprint(h))
         return fail(FW_E_INVALID, "snapshot layout does not match this operator configuration");
-    if (size < (int64_t)sizeof hd + 4ll * nsb + hd.live * pwe * 8) return fail(FW_E_INVALID, "snapshot truncated");
+    const int64_t ent_end = (int64_t)sizeof hd + 4ll * nsb + hd.live * pwe * 8;
+    if (size < ent_end) return fail(FW_E_INVALID, "snapshot truncated");
     const char* p = (const char*)buf + sizeof hd;
     std::vector<int32_t> cnt(nsb);
     memcpy(cnt.data(), p, 4ll * nsb);
     p += 4ll * nsb;
+    std::vector<uint64_t> ent((size_t)hd.live * pwe);
+    memcpy(ent.data(), p, ent.size() * 8);
+    int rc;
+    if (h->keyrow) {  // this handle's ids for the blob's key rows
+        std::vector<std::pair<int64_t, int64_t>> map;
+        std::vector<int32_t> hashes;
+        int64_t used = 0;
+        std::vector<uint64_t> sec((size_t)((size - ent_end) / 8));
+        memcpy(sec.data(), (const char*)buf + ent_end, sec.size() * 8);
+        if ((rc = kr_restore_section(h, sec.data(), (int64_t)sec.size(), &map, &hashes, &used))) return rc;
+        for (int64_t i = 0; i < hd.live; i++) {
+            size_t pos;
+            const int64_t id = kr_lookup(map, (int64_t)ent[(size_t)i * pwe], &pos);
+            if (id < 0) return fail(FW_E_INVALID, "snapshot entry without its key row");
+            ent[(size_t)i * pwe] = (uint64_t)id;
+        }
+    }
     HIP_TRY(hipStreamSynchronize(h->stream));
     std::vector<int64_t> mins(nsb, INT64_MAX);
+    const uint64_t* e = ent.data();
     for (int s = 0; s < nsb; s++) {
         if (!cnt[s]) continue;
-        const size_t bytes = (size_t)cnt[s] * pwe * 8;
-        const uint64_t* e = (const uint64_t*)p;
         for (int i = 0; i < cnt[s]; i++)
             mins[s] = std::min(mins[s], entry_timer_end(h, (int64_t)e[(size_t)i * pwe + 1], e[(size_t)i * pwe + 2]));
-        HIP_TRY(hipMemcpy(h->state + (size_t)s * h->cap_e * pwe, p, bytes, hipMemcpyHostToDevice));
-        p += bytes;
+        HIP_TRY(hipMemcpy(h->state + (size_t)s * h->cap_e * pwe, e, (size_t)cnt[s] * pwe * 8, hipMemcpyHostToDevice));
+        e += (size_t)cnt[s] * pwe;
     }
     HIP_TRY(hipMemcpy(h->state_count, cnt.data(), 4ll * nsb, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(h->sb_min_timer, mins.data(), 8ll * nsb, hipMemcpyHostToDevice));
+    Ctrl c;
+    HIP_TRY(hipMemcpy(&c, h->ctrl, sizeof c, hipMemcpyDeviceToHost));  // the key-row allocator survives
+    const Ctrl keep = c;
     HIP_TRY(launch_init_ctrl(h->ctrl, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    Ctrl c;
     HIP_TRY(hipMemcpy(&c, h->ctrl, sizeof c, hipMemcpyDeviceToHost));
     // SQL: union-list watermark state (WindowAggOperator.initializeState :183-206).  DataStream:
     // the WindowOperator keeps no watermark state, its timer service restarts at Long.MIN_VALUE
@@ -1343,6 +1605,11 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     c.late_dropped = (uint64_t)hd.late_dropped;
     c.fired = (uint64_t)hd.fired;
     c.live_entries = hd.live;
+    c.kr_next_id = keep.kr_next_id;
+    c.kr_free_count = keep.kr_free_count;
+    c.kr_free_cursor = keep.kr_free_cursor;
+    c.kr_epoch = keep.kr_epoch;
+    c.kr_collections = keep.kr_collections;
     HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
     h->pushes_ub = 0;
     h->host_cur = c.cur;
@@ -1381,14 +1648,8 @@ int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t ca
     HIP_TRY(hipMemcpy(cnt.data(), h->state_count + ((size_t)li << L), sizeof(int32_t) * nsub, hipMemcpyDeviceToHost));
     int64_t total = 0;
     for (int q = 0; q < nsub; q++) total += cnt[q];
-    const int64_t need = (int64_t)sizeof(KgHeader) + total * pwe * 8;
-    *size = need;
-    if (!buf) return FW_OK;
-    if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    KgHeader hd{KG_MAGIC, 3, key_group, pwe, h->wd.nw, L, ks.hash_kind, h->win.size, h->win.interval, c.cur, total,
-                semantics_fingerprint(h), (int64_t)h->push_seq};
-    memcpy(buf, &hd, sizeof hd);
-    uint64_t* e = (uint64_t*)((char*)buf + sizeof hd);
+    std::vector<uint64_t> ent((size_t)total * pwe);
+    uint64_t* e = ent.data();
     for (int q = 0; q < nsub; q++) {
         if (!cnt[q]) continue;
         const size_t sb = ((size_t)li << L) + q;
@@ -1396,6 +1657,17 @@ int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t ca
         for (int i = 0; i < cnt[q]; i++) e[(size_t)i * pwe + 2] = (uint32_t)e[(size_t)i * pwe + 2] | ((uint64_t)q << 32);
         e += (size_t)cnt[q] * pwe;
     }
+    std::vector<uint64_t> krs;
+    if ((rc = kr_section(h, ent.data(), total, pwe, &krs))) return rc;
+    const int64_t need = (int64_t)sizeof(KgHeader) + total * pwe * 8 + (int64_t)krs.size() * 8;
+    *size = need;
+    if (!buf) return FW_OK;
+    if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
+    KgHeader hd{KG_MAGIC, 3, key_group, pwe, h->wd.nw, L, h->cfg.key_hash, h->win.size, h->win.interval, c.cur, total,
+                semantics_fingerprint(h), (int64_t)h->push_seq};
+    memcpy(buf, &hd, sizeof hd);
+    memcpy((char*)buf + sizeof hd, ent.data(), ent.size() * 8);
+    if (!krs.empty()) memcpy((char*)buf + sizeof hd + ent.size() * 8, krs.data(), krs.size() * 8);
     return FW_OK;
 }
 
@@ -1407,22 +1679,48 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
     const KeySpace& ks = h->ks;
     const int pwe = 3 + h->nw_t, L = ks.sb_per_kg_log2;
     if (hd.magic != KG_MAGIC || hd.version != 3) return fail(FW_E_INVALID, "not a key-group snapshot");
-    if (hd.pwe != pwe || hd.nw != h->wd.nw || hd.hash_kind != ks.hash_kind || hd.win_size != h->win.size ||
+    if (hd.pwe != pwe || hd.nw != h->wd.nw || hd.hash_kind != h->cfg.key_hash || hd.win_size != h->win.size ||
         hd.win_interval != h->win.interval || hd.semantics != semantics_fingerprint(h))
         return fail(FW_E_INVALID, "key-group snapshot of a different operator configuration");
-    if (size < (int64_t)sizeof hd + hd.n * pwe * 8) return fail(FW_E_INVALID, "key-group snapshot truncated");
+    const int64_t ent_end = (int64_t)sizeof hd + hd.n * pwe * 8;
+    if (size < ent_end) return fail(FW_E_INVALID, "key-group snapshot truncated");
     const int li = hd.key_group - ks.kg_start;
     if (li < 0 || li >= ks.n_kg) return fail(FW_E_INVALID, "key group %d is not owned by this subtask", hd.key_group);
-    if (ks.hash_kind == KH_PRE && L > hd.sb_log2)
+    if (ks.hash_kind == KH_PRE && !h->keyrow && L > hd.sb_log2)
         return fail(FW_E_INVALID, "precomputed-hash keys cannot be split finer than the snapshot's sub-buckets");
-    const uint64_t* src = (const uint64_t*)((const char*)buf + sizeof hd);
-    // target superbucket of every entry
     const int nsub = 1 << L;
+    std::vector<int32_t> cnt(nsub);
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(cnt.data(), h->state_count + ((size_t)li << L), sizeof(int32_t) * nsub, hipMemcpyDeviceToHost));
+    for (int q = 0; q < nsub; q++)
+        if (cnt[q] != 0)  // restored twice, or restored after records of this key group arrived
+            return fail(FW_E_STATE, "key group %d already holds state in this subtask", hd.key_group);
+    std::vector<uint64_t> src((size_t)hd.n * pwe);
+    memcpy(src.data(), (const char*)buf + sizeof hd, src.size() * 8);
+    // key rows: this handle's ids, and the hash that routes each (BinaryRowData.hashCode)
+    std::vector<std::pair<int64_t, int64_t>> map;
+    std::vector<int32_t> hashes;
+    if (h->keyrow) {
+        int64_t used = 0;
+        std::vector<uint64_t> sec((size_t)((size - ent_end) / 8));
+        memcpy(sec.data(), (const char*)buf + ent_end, sec.size() * 8);
+        int rc = kr_restore_section(h, sec.data(), (int64_t)sec.size(), &map, &hashes, &used);
+        if (rc) return rc;
+    }
+    // target superbucket of every entry
     std::vector<std::vector<uint64_t>> per(nsub);
     for (int64_t i = 0; i < hd.n; i++) {
-        const uint64_t* e = src + (size_t)i * pwe;
+        uint64_t* e = src.data() + (size_t)i * pwe;
         int sb;
-        if (ks.hash_kind == KH_PRE) {
+        if (h->keyrow) {
+            size_t pos = 0;
+            const int64_t id = kr_lookup(map, (int64_t)e[0], &pos);
+            if (id < 0) return fail(FW_E_INVALID, "key-group snapshot entry without its key row");
+            e[0] = (uint64_t)id;
+            uint32_t m;
+            sb = route_key(ks, id, hashes[pos], &m);
+            if ((sb >> L) != li) return fail(FW_E_INVALID, "entry key does not belong to key group %d", hd.key_group);
+        } else if (ks.hash_kind == KH_PRE) {
             sb = (li << L) + (int)((e[2] >> 32) & (uint64_t)(nsub - 1));
         } else {
             uint32_t m;
@@ -1433,14 +1731,8 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
         v.insert(v.end(), e, e + pwe);
         v[v.size() - pwe + 2] = (uint32_t)e[2];  // flags without the source sub-bucket
     }
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    std::vector<int32_t> cnt(nsub);
     std::vector<int64_t> mins(nsub);
-    HIP_TRY(hipMemcpy(cnt.data(), h->state_count + ((size_t)li << L), sizeof(int32_t) * nsub, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(mins.data(), h->sb_min_timer + ((size_t)li << L), sizeof(int64_t) * nsub, hipMemcpyDeviceToHost));
-    for (int q = 0; q < nsub; q++)
-        if (cnt[q] != 0)  // restored twice, or restored after records of this key group arrived
-            return fail(FW_E_STATE, "key group %d already holds state in this subtask", hd.key_group);
     for (int q = 0; q < nsub; q++)
         if (cnt[q] + (int64_t)(per[q].size() / pwe) > h->cap_e)
             return fail(FW_E_CAPACITY, "restored key group %d exceeds the state table (%lld entries per superbucket)",

@@ -158,6 +158,71 @@ FW_HD int32_t key_row_hash(const KeyRowDesc& d, int64_t i) {
     return (int32_t)fmix32(h ^ cursor);
 }
 
+// ---- key row images: the bytes BinaryRowWriter writes for a key row (layout above), which the
+// SQL operator's state keys on (BinaryRowData.equals compares them byte by byte) ----------------
+// length in bytes: fixed part + each long string padded to 8 (always a multiple of 8)
+FW_HD int64_t key_row_image_len(const KeyRowDesc& d, int64_t i) {
+    int64_t len = ((d.n + 71) / 64) * 8 + 8 * (int64_t)d.n;
+    for (int f = 0; f < d.n; f++) {
+        if (d.width[f] > 0 || (d.nulls[f] && d.nulls[f][i])) continue;
+        const int64_t l = d.offs[f][i + 1] - d.offs[f][i];
+        if (l > 7) len += (l + 7) & ~(int64_t)7;
+    }
+    return len;
+}
+// row i's image as 8-byte words at out (8-byte aligned)
+FW_HD void key_row_image_write(const KeyRowDesc& d, int64_t i, uint64_t* out) {
+    uint64_t hdr = 0;
+    for (int f = 0; f < d.n; f++)
+        if (d.nulls[f] && d.nulls[f][i]) hdr |= 1ull << (8 + f);
+    int64_t w = 0;
+    out[w++] = hdr;  // n <= 8 < 56: one null-bit word
+    uint32_t cursor = (uint32_t)(8 + 8 * d.n);
+    for (int f = 0; f < d.n; f++) {
+        uint64_t slot = 0;
+        if (!((hdr >> (8 + f)) & 1u)) {
+            const int wd = d.width[f];
+            if (wd > 0) {
+                const uint64_t v = (uint64_t)d.fixed[f][i];
+                slot = wd == 8 ? v : v & ((1ull << (8 * wd)) - 1ull);
+            } else {
+                const int64_t o = d.offs[f][i];
+                const uint32_t len = (uint32_t)(d.offs[f][i + 1] - o);
+                if (len <= 7) {
+                    slot = (uint64_t)(0x80u | len) << 56;
+                    if (len) slot |= kr_load_word(d.bytes[f], o, len);
+                    if (len > 4) slot |= (uint64_t)kr_load_word(d.bytes[f], o + 4, len - 4) << 32;
+                } else {
+                    slot = ((uint64_t)cursor << 32) | len;
+                    cursor += (len + 7u) & ~7u;
+                }
+            }
+        }
+        out[w++] = slot;
+    }
+    for (int f = 0; f < d.n; f++) {
+        if (d.width[f] > 0 || ((hdr >> (8 + f)) & 1u)) continue;
+        const int64_t o = d.offs[f][i];
+        const int64_t len = d.offs[f][i + 1] - o;
+        if (len <= 7) continue;
+        for (int64_t j = 0; j < len; j += 8) {
+            const uint64_t lo = kr_load_word(d.bytes[f], o + j, len - j);
+            const uint64_t hi = j + 4 < len ? kr_load_word(d.bytes[f], o + j + 4, len - j - 4) : 0u;
+            out[w++] = lo | (hi << 32);
+        }
+    }
+}
+// BinaryRowData.hashCode of an image: MurmurHashUtils.hashBytesByWords (seed 42) over its words
+FW_HD int32_t key_row_image_hash(const uint64_t* img, int64_t len) {
+    uint32_t h = 42u;
+    for (int64_t j = 0; j < len / 8; j++) {
+        const uint64_t v = img[j];
+        h = murmur_h1(h, murmur_k1((uint32_t)v));
+        h = murmur_h1(h, murmur_k1((uint32_t)(v >> 32)));
+    }
+    return (int32_t)fmix32(h ^ (uint32_t)len);
+}
+
 // KeyGroupRangeAssignment.computeKeyGroupForKeyHash
 FW_HD int32_t key_group_for_hash(int32_t h, int32_t max_p) { return flink_murmur_hash(h) % max_p; }
 // KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup

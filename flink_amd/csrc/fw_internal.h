@@ -147,6 +147,26 @@ constexpr uint32_t ERR_TREQ = 8u;
 constexpr uint32_t ERR_KEYGROUP = 16u;  // a record's key group is outside this subtask's range
 constexpr uint32_t ERR_LATE = 32u;      // late-fire rows or late side-output rows over capacity
 constexpr uint32_t ERR_ORDEV = 64u;     // first-element retain / release events over capacity
+constexpr uint32_t ERR_KEYROW = 128u;   // key-row table full, or a key row over key_row_max_bytes / misaligned
+
+// FW_KEYHASH_KEYROW: the key-row intern table in HBM.  The window state keys on a dense int64 id per
+// distinct key row; the id's image (the key row's BinaryRowData bytes, what BinaryRowData.equals
+// compares) sits at arena[id * stride_words], its hashCode and length in meta[id].  An open-
+// addressing index over the images gives each pushed row its id (k_kr_intern); ids whose key row
+// no state entry, pending partial, timer request or unread result holds any more are collected
+// (k_kr_gc_*) when the fresh ids run low, reused through the free list, and the index is rebuilt
+// without them.
+struct KeyRowTable {
+    uint32_t* slots;        // [n_slots] 0 empty, 1 being inserted, 2 + id
+    int64_t n_slots;        // power of two, >= 2 * cap_ids
+    int64_t* meta;          // [cap_ids] hash << 32 | image length
+    uint64_t* arena;        // [cap_ids * stride_words]
+    int32_t stride_words;   // words per id: meta word + image, padded to whole 128-B lines
+    int32_t max_len;        // key_row_max_bytes: longest image accepted
+    int64_t cap_ids;
+    uint32_t* mark;         // [cap_ids] collection epoch that found the id live
+    int64_t* free_list;     // [cap_ids]
+};
 
 // Device-resident operator control block (one per handle).  Only kernels write it, so a
 // watermark cycle needs no host round trip.
@@ -184,6 +204,13 @@ struct Ctrl {
     uint64_t flush_launches; // merge launches that flushed pending partials (cumulative)
     uint64_t parts_merged;   // partial rows those flushes read (cumulative)
     uint64_t state_moved;    // state entries the merge launches loaded + wrote back (cumulative)
+    // FW_KEYHASH_KEYROW: the key-row intern table's allocator (KeyRowTable)
+    int64_t kr_next_id;      // ids handed out fresh so far (ids < kr_next_id exist)
+    int64_t kr_free_count;   // ids in the free list (rebuilt by each collection)
+    int64_t kr_free_cursor;  // free-list ids handed out since that collection
+    uint32_t kr_epoch;       // mark epoch of the current collection
+    int32_t kr_gc;           // a collection runs in the current advance (set by k_kr_gc_begin)
+    int64_t kr_collections;  // collections so far
 };
 
 // Window / slice description shared by both kernels (SliceAssigners.java).
@@ -502,5 +529,15 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_ingest(const IngestArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_merge_fire(const MergeArgs& a, hipStream_t s, KTimer* t);
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s);
+// key rows (fw_keyrows.hip)
+int key_row_desc(const fw_key_field* fields, int32_t n_fields, KeyRowDesc* d);
+hipError_t launch_kr_intern(const KeyRowTable& t, Ctrl* c, int64_t n, const int64_t* off, const uint8_t* bytes,
+                            int64_t* out_id, int32_t* out_hash, hipStream_t s);
+hipError_t launch_kr_collect(const KeyRowTable& t, Ctrl* c, const uint64_t* state, const int32_t* state_count,
+                             int32_t n_sb, int32_t cap_e, int32_t pwe, int32_t pw, const uint64_t* parts,
+                             int64_t cap_rows, const int64_t* treq, const int64_t* out_key, const int32_t* sb_out,
+                             int64_t slab_cap, hipStream_t s);
+hipError_t launch_kr_result_rows(const KeyRowTable& t, const int64_t* res_key, const int64_t* n_ptr, int64_t cap,
+                                 int32_t* len, uint64_t* img, int32_t stride_words, hipStream_t s);
 
 }  // namespace fw

@@ -117,6 +117,12 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->flush_launches = 0;
         c->parts_merged = 0;
         c->state_moved = 0;
+        c->kr_next_id = 0;
+        c->kr_free_count = 0;
+        c->kr_free_cursor = 0;
+        c->kr_epoch = 0;
+        c->kr_gc = 0;
+        c->kr_collections = 0;
     }
 }
 
@@ -221,7 +227,8 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
                                                         int32_t ncols, int64_t n, int32_t kind, int32_t max_p,
                                                         int32_t p, const uint32_t* offsets, int64_t* okey, int64_t* ots,
                                                         uint64_t* const* ovals, int64_t* orows = nullptr,
-                                                        int64_t seg_len = 0, const int64_t* totals = nullptr) {
+                                                        int64_t seg_len = 0, const int64_t* totals = nullptr,
+                                                        int64_t* spill = nullptr) {
     // Stable: rows keep their input order within a destination (the order a Netty channel
     // delivers them in, ChannelSelectorRecordWriter.emit :54), so a DOUBLE SUM downstream adds in
     // the same order on every run.  Each wave ranks its 64 rows per destination with ballots;
@@ -230,12 +237,17 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
     __shared__ uint32_t h[PART_MAXP];         // next output position per destination
     __shared__ uint32_t wc[NWV][PART_MAXP];   // rows per (wave, destination) of the current pass
     __shared__ int64_t dbase[PART_MAXP];     // packed mode: first output position of each destination
+    __shared__ int64_t sbase[PART_MAXP];     // packed mode: first spill row of each destination
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid < p) h[tid] = offsets[(size_t)blockIdx.x * p + tid];
     if (orows && tid < p) {
-        int64_t b0 = 0;
-        for (int d = 0; d < tid; d++) b0 += totals[d];
+        int64_t b0 = 0, s0 = 0;
+        for (int d = 0; d < tid; d++) {
+            b0 += totals[d];
+            s0 += max(totals[d] - seg_len, (int64_t)0);
+        }
         dbase[tid] = b0;
+        sbase[tid] = s0;
     }
     const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t b = (int64_t)blockIdx.x * PART_TILE;
@@ -267,8 +279,12 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
         }
         if (d >= 0 && orows) {  // packed padded segments: row (rank in d) of segment d
             const int64_t r = (int64_t)pos - dbase[d];
-            if (r < seg_len) {
-                int64_t* o = orows + ((size_t)d * seg_len + r) * (2 + ncols);
+            // rows past the segment go to the spill region (destination-major, in input order):
+            // the overflow round of the exchange sends them
+            int64_t* o = r < seg_len ? orows + ((size_t)d * seg_len + r) * (2 + ncols)
+                         : spill      ? spill + (size_t)(sbase[d] + r - seg_len) * (2 + ncols)
+                                      : nullptr;
+            if (o) {
                 o[0] = k;
                 o[1] = ts[i];
                 for (int c = 0; c < ncols; c++) o[2 + c] = (int64_t)vals[c][i];
@@ -334,7 +350,7 @@ extern "C" int fw_assign_key_groups(const int64_t* d_key, const int32_t* d_key_h
 }
 
 // fw_key_field[] -> KeyRowDesc (FW_E_INVALID on a bad description)
-static int key_row_desc(const fw_key_field* fields, int32_t n_fields, KeyRowDesc* d) {
+int fw::key_row_desc(const fw_key_field* fields, int32_t n_fields, KeyRowDesc* d) {
     if (!fields || n_fields <= 0 || n_fields > FW_MAX_KEY_FIELDS || n_fields > KR_MAX_FIELDS) return FW_E_INVALID;
     *d = KeyRowDesc{};
     d->n = n_fields;
@@ -418,6 +434,16 @@ extern "C" int fw_partition_packed(const int64_t* d_key, const int32_t* d_key_ha
                                    const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
                                    int32_t max_parallelism, int32_t parallelism, int64_t seg_len, int64_t* d_out_rows,
                                    int64_t* d_counts, void* d_workspace, int64_t workspace_bytes, void* stream) {
+    return fw_partition_packed_spill(d_key, d_key_hash, d_ts, d_values, n_cols, n, key_hash_kind, max_parallelism,
+                                     parallelism, seg_len, d_out_rows, nullptr, d_counts, d_workspace, workspace_bytes,
+                                     stream);
+}
+
+extern "C" int fw_partition_packed_spill(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                                         const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
+                                         int32_t max_parallelism, int32_t parallelism, int64_t seg_len,
+                                         int64_t* d_out_rows, int64_t* d_spill_rows, int64_t* d_counts,
+                                         void* d_workspace, int64_t workspace_bytes, void* stream) {
     if (parallelism <= 0 || parallelism > PART_MAXP || n_cols < 0 || n_cols > FW_MAX_COLS || seg_len < 1) return FW_E_INVALID;
     if (key_hash_kind == FW_KEYHASH_PRECOMPUTED && n > 0 && !d_key_hash) return FW_E_INVALID;
     if (key_hash_kind != FW_KEYHASH_PRECOMPUTED) d_key_hash = nullptr;
@@ -439,7 +465,7 @@ extern "C" int fw_partition_packed(const int64_t* d_key, const int32_t* d_key_ha
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, d_ts,
                        (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
                        (int64_t*)nullptr, (int64_t*)nullptr, (uint64_t* const*)nullptr, d_out_rows, seg_len,
-                       (const int64_t*)d_counts);
+                       (const int64_t*)d_counts, d_spill_rows);
     return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
 }
 

@@ -16,10 +16,13 @@ too.  Both use the same key-group code the kernels run.
 
 exchange_packed is the per-step device path: the partition kernel writes every row's columns
 side by side (key, ts, values) straight into fixed-size per-destination segments
-(fw_partition_packed), the rows travel as ONE all-to-all of that buffer, the row counts as a
+(fw_partition_packed_spill), the rows travel as ONE all-to-all of that buffer, the row counts as a
 second small all-to-all that stays on the device, and the receiving operator reads the packed
-rows in place and skips each segment's padding itself (fw_push_device_packed_segments) -- no host
-synchronisation per step.  exchange_padded does the same with one all-to-all per column (for
+rows in place and skips each segment's padding itself (fw_push_device_packed_segments).  The
+segment size comes from the batch itself (its even share plus headroom), never from later data:
+rows past a destination's segment go to a spill region, and an overflow round sends them when
+any subtask had some (the subtasks agree on it in the same host all-reduce as the watermark valve,
+after waiting only for their own partition kernel, not for the all-to-all in flight).  exchange_padded does the same with one all-to-all per column (for
 configurations whose key-hash or NULL-flag columns do not fit the packed rows).  The watermark
 valve runs on the host (a gloo group over CPU tensors), as Flink's StatusWatermarkValve does on
 the receiving task, so it never waits on the GPU stream.
@@ -44,9 +47,12 @@ class KeyByExchange:
         self._ws = None
         self._cpu_group = None
         if self.world > 1 and dist.get_backend(group) != "gloo":
-            # the watermark valve's host-side group (collective creation: every rank builds the
-            # exchange at the same point)
-            self._cpu_group = dist.new_group(backend="gloo")
+            # the watermark valve's host-side group over the same ranks (collective creation:
+            # every rank builds the exchange at the same point)
+            ranks = dist.get_process_group_ranks(group) if group is not None else None
+            self._cpu_group = dist.new_group(ranks=ranks, backend="gloo")
+        self._max_count = None  # running max of rows per destination (padded exchanges), on the device
+        self.spill_rounds = 0
 
     # ---- routing ------------------------------------------------------------------------
     def partition(self, key, ts, values, key_hash=None):
@@ -149,61 +155,118 @@ class KeyByExchange:
             dist.all_to_all_single(recv, send, group=self.group)
             out.append(back(recv))
         rc = back(rc)
-        self._check_cap = (counts.max(), cap)  # validated lazily, off the hot path
+        self._note_counts(counts, cap)  # validated lazily, off the hot path
         return out[0], out[1], out[2:], rc
 
-    def exchange_packed(self, key, ts, values, capacity):
-        """Like exchange_padded, with the rows packed: returns (rows, recv_counts, row_words) where
-        rows is p segments of ``capacity`` rows of row_words = 2 + len(values) int64 words (key,
-        ts, value bits), segment s holding the first recv_counts[s] rows subtask s sent here --
-        the buffer fw_push_device_packed_segments ingests.  One all-to-all for the rows, one for
-        the counts."""
+    @staticmethod
+    def segment_capacity(n_rows, world, headroom=0.25):
+        """The padded segment size for a batch of n_rows: its even share plus headroom (rows past
+        it take the overflow round, so this never has to bound the batch)."""
+        return int(n_rows / max(world, 1) * (1.0 + headroom)) + 1024
+
+    def exchange_packed(self, key, ts, values, capacity=None, watermark=None):
+        """Like exchange_padded, with the rows packed: returns (rows, recv_counts, row_words, spill,
+        watermark) where rows is p segments of ``capacity`` rows of row_words = 2 + len(values)
+        int64 words (key, ts, value bits), segment s holding the first recv_counts[s] rows subtask s
+        sent here -- the buffer fw_push_device_packed_segments ingests.  One all-to-all for the
+        rows, one for the counts.  Rows past a destination's segment come in ``spill`` (packed
+        rows, None when no subtask overflowed).  ``watermark``: this subtask's input watermark;
+        the returned one is the valve's minimum over all subtasks (StatusWatermarkValve)."""
         p, n, dev = self.world, key.numel(), key.device
         w = 2 + len(values)
-        cap = int(capacity)
+        cap = int(capacity) if capacity is not None else self.segment_capacity(n, p)
         vals64 = [v.view(torch.int64) if v.dtype == torch.float64 else v for v in values]
+        spill = None
         if key.is_cuda:
             L = lib()
             ws = L.fw_partition_workspace_bytes(n, p)
             if self._ws is None or self._ws.numel() < ws or self._ws.device != dev:
                 self._ws = torch.empty(max(ws, 256), dtype=torch.uint8, device=dev)
             send = torch.empty(p * cap * w, dtype=torch.int64, device=dev)
+            spill = torch.empty(max(n, 1) * w, dtype=torch.int64, device=dev)
             counts = torch.empty(p, dtype=torch.int64, device=dev)
             vin = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in vals64])
-            check(L.fw_partition_packed(key.data_ptr(), None, ts.data_ptr(), vin, len(values), n, self.kind,
-                                        self.max_p, p, cap, send.data_ptr(), counts.data_ptr(),
-                                        self._ws.data_ptr(), self._ws.numel(),
-                                        torch.cuda.current_stream(dev).cuda_stream))
+            check(L.fw_partition_packed_spill(key.data_ptr(), None, ts.data_ptr(), vin, len(values), n, self.kind,
+                                              self.max_p, p, cap, send.data_ptr(), spill.data_ptr(), counts.data_ptr(),
+                                              self._ws.data_ptr(), self._ws.numel(),
+                                              torch.cuda.current_stream(dev).cuda_stream))
+            counts_h = torch.empty(p, dtype=torch.int64, pin_memory=True)
+            counts_h.copy_(counts, non_blocking=True)
+            part_done = torch.cuda.Event()
+            part_done.record(torch.cuda.current_stream(dev))
         else:  # host batch: the host partition, then the same padded layout
             pk, pt, pv, counts = self.partition(key, ts, vals64)
             send = torch.zeros(p * cap * w, dtype=torch.int64)
             rows = torch.stack([pk, pt] + list(pv), dim=1) if n else torch.zeros((0, w), dtype=torch.int64)
             seg = send.view(p, cap, w)
+            sp = []
             o = 0
             for d, c in enumerate(counts.tolist()):
                 m = min(c, cap)
                 seg[d, :m] = rows[o:o + m]
+                sp.append(rows[o + m:o + c])
                 o += c
-        if p == 1:
-            self._check_cap = (counts.max(), cap)
-            return send, counts, w
-        stage = key.is_cuda and dist.get_backend(self.group) != "nccl"
+            spill = torch.cat(sp).reshape(-1) if sp else torch.zeros(0, dtype=torch.int64)
+            counts_h, part_done = counts, None
+        stage = key.is_cuda and p > 1 and dist.get_backend(self.group) != "nccl"
         mv = (lambda x: x.cpu()) if stage else (lambda x: x)
         back = (lambda x: x.to(dev)) if stage else (lambda x: x)
-        rc = torch.empty_like(mv(counts))
-        dist.all_to_all_single(rc, mv(counts), group=self.group)
-        s_ = mv(send)
-        recv = torch.empty_like(s_)
-        dist.all_to_all_single(recv, s_, group=self.group)
-        self._check_cap = (counts.max(), cap)  # validated lazily, off the hot path
-        return back(recv), back(rc), w
+        if p > 1:
+            rc = torch.empty_like(mv(counts))
+            dist.all_to_all_single(rc, mv(counts), group=self.group)
+            s_ = mv(send)
+            recv = torch.empty_like(s_)
+            dist.all_to_all_single(recv, s_, group=self.group)
+            recv, rc = back(recv), back(rc)
+        else:
+            recv, rc = send, counts
+        # the overflow round: wait for this subtask's partition only (the all-to-all stays in flight)
+        if part_done is not None:
+            part_done.synchronize()
+        over = [max(0, c - cap) for c in counts_h.tolist()]
+        any_over, wm = self._agree(sum(over) > 0, watermark)
+        out_spill = None
+        if any_over:
+            self.spill_rounds += 1
+            if p == 1:
+                out_spill = spill[:over[0] * w] if over[0] else None
+            else:
+                g = self._cpu_group if self._cpu_group is not None else self.group
+                sc = torch.tensor(over, dtype=torch.int64)
+                rsc = torch.empty_like(sc)
+                dist.all_to_all_single(rsc, sc, group=g)
+                rin = rsc.tolist()
+                total = sum(over)
+                src = mv(spill[:total * w] if total else spill[:0])
+                dst = torch.empty(sum(rin) * w, dtype=torch.int64, device=src.device)
+                dist.all_to_all_single(dst, src, [r * w for r in rin], [o * w for o in over], group=self.group)
+                out_spill = back(dst) if sum(rin) else None
+        return recv, rc, w, out_spill, wm
+
+    def _agree(self, overflow, watermark):
+        """One host all-reduce for the overflow decision and the watermark valve's minimum."""
+        wm = None if watermark is None else int(watermark)
+        if self.world == 1:
+            return overflow, wm
+        g = self.group if self._cpu_group is None else self._cpu_group
+        t = torch.tensor([1 if overflow else 0, -wm if wm is not None else 0], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
+        return bool(t[0].item()), (None if wm is None else -int(t[1].item()))
+
+    def _note_counts(self, counts, cap):
+        """Keep the running max of rows per destination on the device (check_capacity)."""
+        m = counts.max() if counts.numel() else torch.zeros((), dtype=torch.int64, device=counts.device)
+        self._max_count = m if self._max_count is None or self._max_count.device != m.device else torch.maximum(self._max_count, m)
+        self._cap_min = cap if getattr(self, "_cap_min", None) is None else min(self._cap_min, cap)
 
     def check_capacity(self):
-        """Raises if a padded exchange dropped rows (a destination got more than its capacity)."""
-        if getattr(self, "_check_cap", None) is not None:
-            m, cap = self._check_cap
-            if int(m) > cap:
-                raise RuntimeError(f"padded exchange: {int(m)} rows for one subtask > capacity {cap}")
+        """Raises if exchange_padded dropped rows: some destination of some batch since the first
+        exchange got more rows than its segment (running max; exchange_packed never drops -- its
+        overflow round sends them)."""
+        if self._max_count is not None:
+            m, cap = int(self._max_count), self._cap_min
+            if m > cap:
+                raise RuntimeError(f"padded exchange: {m} rows for one subtask > capacity {cap}")
 
     def global_max(self, x):
         """Max of a host integer over all subtasks (e.g. the padded exchange's capacity, which

@@ -97,6 +97,55 @@ class WindowAggHandle:
             check(lib().fw_commit(self._h, m))
             self.push_seq += 1
 
+    def push_host_key_rows(self, offsets, images, ts, values=(), nulls=None):
+        """FW_KEYHASH_KEYROW: host key-row images (row i = images[offsets[i]:offsets[i + 1]], the
+        key's BinaryRowData bytes) through the pinned staging of fw_reserve / fw_commit -- the path
+        the JNI shim takes."""
+        offsets = np.asarray(offsets, dtype=np.int64)
+        images = np.asarray(images, dtype=np.uint8)
+        n = len(offsets) - 1
+        cap = self.cfg.max_batch_rows
+        for o in range(0, n, cap):
+            m = min(cap, n - o)
+            cols = abi.fw_host_cols()
+            check(lib().fw_reserve(self._h, m, C.byref(cols)))
+            if m:
+                off = offsets[o:o + m + 1] - offsets[o]
+                if off[-1] > cols.key_row_bytes_cap:
+                    raise ValueError("key rows exceed the staging bytes (key_row_max_bytes per row)")
+                _np_view(cols.key_row_offsets, m + 1, np.int64)[:] = off
+                _np_view(cols.key_row_bytes, int(off[-1]), np.uint8)[:] = images[offsets[o]:offsets[o + m]]
+                _np_view(cols.ts, m, np.int64)[:] = np.asarray(ts, dtype=np.int64)[o:o + m]
+                for c, v in enumerate(values):
+                    v = np.asarray(v)
+                    if v.dtype == np.float64:
+                        v = v.view(np.int64)
+                    _np_view(cols.values[c], m, np.int64)[:] = v.astype(np.int64, copy=False)[o:o + m]
+                for c in range(self.cfg.n_value_cols):
+                    if self.cfg.nullable_cols >> c & 1:
+                        nf = np.zeros(n, np.uint8) if nulls is None or c not in nulls else \
+                            np.asarray(nulls[c]).astype(np.uint8, copy=False)
+                        _np_view(cols.nulls[c], m, np.uint8)[:] = nf[o:o + m]
+            check(lib().fw_commit(self._h, m))
+            self.push_seq += 1
+
+    def push_device_key_rows(self, offsets, images, ts, values=(), nulls=None):
+        """FW_KEYHASH_KEYROW: device-resident key-row images (int64 offsets tensor of n + 1, uint8
+        bytes tensor, 8-byte aligned rows)."""
+        n = ts.numel()
+        if n == 0:
+            return
+        cur = self._begin_read(ts.device)
+        arr = (C.c_void_p * abi.FW_MAX_COLS)()
+        for c, v in enumerate(values):
+            arr[c] = v.data_ptr()
+        nul = (C.c_void_p * abi.FW_MAX_COLS)()
+        for c, v in (nulls or {}).items():
+            nul[c] = v.data_ptr()
+        check(lib().fw_push_device_key_rows(self._h, n, offsets.data_ptr(), images.data_ptr(), ts.data_ptr(), arr, nul))
+        self.push_seq += 1
+        self._end_read(cur)
+
     def push_device(self, keys, ts, values=(), key_hashes=None, nulls=None):
         """Device-resident columns (torch cuda tensors, int64 / float64; ``nulls``: {column:
         uint8 tensor}).  The handle's stream waits for the producer's current stream before
@@ -169,6 +218,11 @@ class WindowAggHandle:
         }
         if self.cfg.ds_first_ordinals:  # DataStream: arrival ordinal of each window's first element
             out["first_ord"] = _np_view(r.first_ord, n, np.int64).copy()
+        if self.cfg.key_hash == abi.KEYHASH_KEYROW:  # each row's key row (BinaryRowData image)
+            lens = _np_view(r.key_row_len, n, np.int32)
+            img = _np_view(r.key_row_bytes, n * r.key_row_stride, np.uint8)
+            st = r.key_row_stride
+            out["key_rows"] = [img[i * st:i * st + int(lens[i])].tobytes() for i in range(n)]
         if reset:
             self.reset_results()
         return out

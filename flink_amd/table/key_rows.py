@@ -6,15 +6,18 @@ and routes records by that row's hashCode (BinaryRowData.java:459 -> MurmurHashU
 .hashBytesByWords, KeyGroupStreamPartitioner.java:55-65).  For keys that are not a single
 BIGINT / INT, this module turns the key rows of a batch into:
 
-  * the key's identity in the window state: a dense int64 id per distinct key row
-    (``KeyDictionary``; results come back as ids and are mapped back to the key rows), and
   * the key-row columns (``KeyRowColumns``: one 8-byte column per fixed-width field, offsets +
-    bytes per string field, NULL flags) from which ``fw_key_row_hash`` computes the Java hash
-    on the device (or ``fw_host_key_row_hash`` on the host for host-staged partitioning).
+    bytes per string field, NULL flags), and
+  * the key rows' BinaryRowData images (``images_host`` / ``images_device``: the bytes
+    BinaryRowWriter writes, what the reference's state keys on and BinaryRowData.equals compares).
 
-The handle then runs with ``FW_KEYHASH_PRECOMPUTED``: the hash decides key group, subtask and
-superbucket exactly as the reference's key group does.
+A ``FW_KEYHASH_KEYROW`` handle takes the images (fw_reserve staging or fw_push_device_key_rows),
+interns them in an HBM table (the key's identity is its bytes) and routes each by its
+BinaryRowData.hashCode; results come back with their key rows (``decode_key_row``).  The
+columnar hash (``fw_key_row_hash`` / ``fw_host_key_row_hash``) serves host-side partitioners.
 """
+import struct
+
 import ctypes as C
 
 import numpy as np
@@ -89,13 +92,43 @@ class KeyRowColumns:
         return cls(types, fixed, offsets, data, nulls, n)
 
     def to(self, device):
-        """A copy with every column as a torch tensor on `device` (for fw_key_row_hash)."""
+        """A copy with every column as a torch tensor on `device` (for fw_key_row_hash /
+        images_device); the image offsets are computed from the host columns first."""
         import torch
 
         def t(a):
             return None if a is None else torch.from_numpy(a).to(device)
-        return KeyRowColumns(self.types, [t(a) for a in self.fixed], [t(a) for a in self.offsets],
-                             [t(a) for a in self.data], [t(a) for a in self.nulls], self.n)
+        out = KeyRowColumns(self.types, [t(a) for a in self.fixed], [t(a) for a in self.offsets],
+                            [t(a) for a in self.data], [t(a) for a in self.nulls], self.n)
+        out._img_off = self.image_offsets()
+        return out
+
+    def image_offsets(self):
+        """Arrow offsets (n + 1) of the rows' BinaryRowData images (host columns)."""
+        lens = np.empty(self.n, dtype=np.int64)
+        check(lib().fw_host_key_row_image_lengths(self.fields(), len(self.kinds), self.n, lens.ctypes.data))
+        off = np.zeros(self.n + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        return off
+
+    def images_host(self):
+        """(offsets, bytes) of the rows' BinaryRowData images (fw_host_key_row_images)."""
+        off = self.image_offsets()
+        buf = np.zeros(max(int(off[-1]) // 8, 1), dtype=np.uint64).view(np.uint8)  # 8-byte aligned
+        check(lib().fw_host_key_row_images(self.fields(), len(self.kinds), self.n, off.ctypes.data, buf.ctypes.data))
+        return off, buf[:int(off[-1])]
+
+    def images_device(self, stream=None):
+        """(offsets, bytes) cuda tensors: the images written on the device (fw_key_row_images);
+        this object must come from ``to``."""
+        import torch
+        dev = next(a.device for a in self.offsets + self.fixed if a is not None)
+        off = torch.from_numpy(self._img_off).to(dev)
+        nb = int(self._img_off[-1])
+        buf = torch.zeros(max(nb // 8, 1), dtype=torch.int64, device=dev).view(torch.uint8)
+        s = torch.cuda.current_stream(dev).cuda_stream if stream is None else stream
+        check(lib().fw_key_row_images(self.fields(), len(self.kinds), self.n, off.data_ptr(), buf.data_ptr(), C.c_void_p(s)))
+        return off, buf
 
     def fields(self):
         """The fw_key_field array (pointers into this object's columns)."""
@@ -130,27 +163,35 @@ class KeyRowColumns:
         return out
 
 
-class KeyDictionary:
-    """Dense int64 ids for distinct key rows: the key's identity in the device window state."""
-
-    def __init__(self):
-        self._ids = {}
-        self._rows = []
-
-    def encode(self, rows):
-        out = np.empty(len(rows), dtype=np.int64)
-        ids, lst = self._ids, self._rows
-        for i, r in enumerate(rows):
-            r = tuple(r)
-            k = ids.get(r)
-            if k is None:
-                k = ids[r] = len(lst)
-                lst.append(r)
-            out[i] = k
-        return out
-
-    def decode(self, key_id):
-        return self._rows[int(key_id)]
-
-    def __len__(self):
-        return len(self._rows)
+def decode_key_row(image, types):
+    """A key row image (BinaryRowData bytes) back to a tuple of Python values by SQL type --
+    BinaryRowData.getLong / getInt / getString... (NULL -> None)."""
+    image = bytes(image)
+    n = len(types)
+    nb = ((n + 71) // 64) * 8
+    hdr = int.from_bytes(image[:8], "little")
+    out = []
+    for f, t in enumerate(types):
+        if (hdr >> (8 + f)) & 1:
+            out.append(None)
+            continue
+        slot = image[nb + 8 * f:nb + 8 * f + 8]
+        kind = abi.KEY_FIELD_KINDS[t]
+        if kind == abi.KF_STRING:
+            w = int.from_bytes(slot, "little")
+            if w >> 63:  # inline: length in the high byte
+                ln = (w >> 56) & 0x7F
+                b = slot[:ln]
+            else:
+                o, ln = w >> 32, w & 0xFFFFFFFF
+                b = image[o:o + ln]
+            out.append(b.decode("utf-8") if t in ("VARCHAR", "CHAR", "STRING") else bytes(b))
+        elif t == "DOUBLE":
+            out.append(struct.unpack("<d", slot)[0])
+        elif t == "FLOAT":
+            out.append(struct.unpack("<f", slot[:4])[0])
+        elif t == "BOOLEAN":
+            out.append(slot[0] != 0)
+        else:
+            out.append(int.from_bytes(slot[:kind], "little", signed=True))
+    return tuple(out)

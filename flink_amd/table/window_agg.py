@@ -13,7 +13,7 @@ import numpy as np
 
 from .. import abi
 from ..runtime.handle import WindowAggHandle
-from .key_rows import KeyDictionary, KeyRowColumns
+from .key_rows import KeyRowColumns, decode_key_row
 from .slice_assigners import SliceAssigner
 
 GPU_AGGS = {"COUNT_STAR", "COUNT", "SUM", "MIN", "MAX", "AVG"}
@@ -60,7 +60,7 @@ class WindowAggOperator:
     def __init__(self, assigner, aggs, value_types, count_star_index=-1, key_type="BIGINT",
                  max_parallelism=128, parallelism=1, subtask_index=0, device=0,
                  state_capacity=1 << 20, max_batch_rows=1 << 22, output_capacity=1 << 22,
-                 nullable_cols=()):
+                 nullable_cols=(), key_row_max_bytes=0):
         """``assigner``: a SliceAssigner; a TIMESTAMP_LTZ window's assigner carries its shift time
         zone (``assigner.in_zone(zone)``, SliceAssigners.*(rowtimeIndex, shiftTimeZone, ...))."""
         zone = assigner.shift_zone
@@ -72,20 +72,21 @@ class WindowAggOperator:
             raise ValueError("Hopping window requires a COUNT(*) in the aggregate functions.")
         self.assigner = assigner
         self.aggs = list(aggs)
-        # key rows (VARCHAR / composite keys): dictionary ids as the state key, device-hashed rows
+        # key rows (VARCHAR / composite keys): the BinaryRowData images go to the device, which keys
+        # the state on their bytes and routes by their hashCode (FW_KEYHASH_KEYROW)
         self.key_types = list(key_type) if isinstance(key_type, (tuple, list)) else None
-        self.keys = KeyDictionary() if self.key_types else None
         self.cfg = abi.make_config(
             api=abi.API_SQL, window_kind=assigner.kind, size_ms=assigner.size,
             slide_ms=assigner.slide, offset_ms=assigner.offset,
             aggs=[(abi.AGG_NAMES[k], c, abi.TYPE_NAMES[t]) for k, c, t in aggs],
             count_star_index=count_star_index,
             value_col_types=[abi.TYPE_NAMES[t] for t in value_types],
-            key_hash=abi.KEYHASH_PRECOMPUTED if self.key_types else KEY_HASH[key_type],
+            key_hash=abi.KEYHASH_KEYROW if self.key_types else KEY_HASH[key_type],
             max_parallelism=max_parallelism,
             parallelism=parallelism, subtask_index=subtask_index, device=device,
             state_capacity=state_capacity, max_batch_rows=max_batch_rows,
-            output_capacity=output_capacity, nullable_cols=nullable_cols, shift_zone=zone)
+            output_capacity=output_capacity, nullable_cols=nullable_cols, shift_zone=zone,
+            key_row_max_bytes=key_row_max_bytes)
         self.handle = None
         self.current_watermark = -(1 << 63)
 
@@ -105,21 +106,18 @@ class WindowAggOperator:
     def process_batch(self, keys, rowtimes, values=(), key_hashes=None, nulls=None):
         """processElement for every row of a columnar batch (host arrays; ``nulls``: {column:
         per-row NULL flags} for NULL-able columns).  With key rows (``key_type`` a tuple of SQL
-        types) ``keys`` is a sequence of key tuples: their columns go to the device, which
-        computes BinaryRowData.hashCode (fw_key_row_hash) and routes by it."""
+        types) ``keys`` is a sequence of key tuples: the operator writes their BinaryRowData
+        images into the handle's pinned staging (fw_reserve, as the JNI shim copies each key row's
+        bytes) and the device interns them."""
         if self.key_types is None:
             self.handle.push_host(keys, rowtimes, values, key_hashes, nulls=nulls)
             return
-        import torch
-        dev = torch.device("cuda", self.cfg.device)
-        ids = self.keys.encode(keys)
-        kh = KeyRowColumns.from_rows(keys, self.key_types).to(dev).hash_device()
-        vals = [torch.from_numpy(np.ascontiguousarray(v).view(np.int64)).to(dev) for v in values]
-        nul = None if not nulls else {c: torch.from_numpy(np.ascontiguousarray(f).astype(np.uint8)).to(dev)
-                                      for c, f in nulls.items()}
-        self.handle.push_device(torch.from_numpy(ids).to(dev),
-                                torch.from_numpy(np.ascontiguousarray(rowtimes, dtype=np.int64)).to(dev),
-                                vals, kh, nulls=nul)
+        off, img = KeyRowColumns.from_rows(keys, self.key_types).images_host()
+        longest = int(np.diff(off).max()) if len(off) > 1 else 0
+        if longest > (self.cfg.key_row_max_bytes or 120):
+            raise ValueError(f"a key row of {longest} bytes exceeds key_row_max_bytes "
+                             f"({self.cfg.key_row_max_bytes or 120}); such keys stay on the reference operator")
+        self.handle.push_host_key_rows(off, img, rowtimes, values, nulls=nulls)
 
     def process_batch_device(self, keys, rowtimes, values=(), key_hashes=None, nulls=None):
         """processElement for a batch already resident in HBM (torch cuda tensors)."""
@@ -160,6 +158,6 @@ class WindowAggOperator:
                     vals.append(float(np.int64(res["values"][a][i]).view(np.float64)))
                 else:
                     vals.append(int(res["values"][a][i]))
-            key = self.keys.decode(res["key"][i]) if self.keys is not None else (int(res["key"][i]),)
+            key = decode_key_row(res["key_rows"][i], self.key_types) if self.key_types else (int(res["key"][i]),)
             rows.append((*key, *vals, int(res["window_start"][i]), int(res["window_end"][i])))
         return rows

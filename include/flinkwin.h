@@ -122,8 +122,14 @@ typedef enum {
     FW_KEYHASH_INT = 1,          /* DataStream Integer key: Integer.hashCode = v                */
     FW_KEYHASH_BINROW_BIGINT = 2,/* SQL key row (BIGINT): BinaryRowData.hashCode, 16-byte row  */
     FW_KEYHASH_BINROW_INT = 3,   /* SQL key row (INT):    BinaryRowData.hashCode, 16-byte row   */
-    FW_KEYHASH_PRECOMPUTED = 4   /* key column holds an opaque id; the Java hashCode of the real
+    FW_KEYHASH_PRECOMPUTED = 4,  /* key column holds an opaque id; the Java hashCode of the real
                                     key is passed in the key_hash column (VARCHAR, composite)   */
+    FW_KEYHASH_KEYROW = 5        /* v5, SQL: the key IS a key row (BinaryRowData image, any
+                                    VARCHAR / composite key).  Pushes carry the images
+                                    (fw_push_device_key_rows, or the key-row staging of
+                                    fw_reserve); the handle interns them in an HBM table keyed by
+                                    the image bytes (BinaryRowData.equals), routes by
+                                    BinaryRowData.hashCode, and returns each result's key row   */
 } fw_key_hash_kind;
 
 typedef struct {
@@ -174,7 +180,9 @@ typedef struct {
     int32_t tz_use_dst;          /* TimeZone.getTimeZone(shiftTimeZone).useDaylightTime()          */
     int32_t tz_n;                /* SQL TIMESTAMP_LTZ rowtime: entries of the shift time zone's
                                     offset table (TimeWindowUtil.getShiftTimeZone); 0 = UTC       */
-    int32_t reserved1;
+    int32_t key_row_max_bytes;   /* v5, FW_KEYHASH_KEYROW: largest key-row image (bytes, multiple
+                                    of 8, <= 4096; 0 = 120).  A longer key row is a device error
+                                    (the builder keeps such keys on the reference operator)       */
     const int64_t* tz_utc;       /* tz_n ascending UTC epoch ms, tz_utc[0] = INT64_MIN: offset
                                     tz_offset_ms[i] is in force from tz_utc[i] (ZoneRules
                                     .getOffset(Instant)); host memory, copied by fw_create        */
@@ -193,6 +201,13 @@ typedef struct {
     int32_t* key_hash;                 /* only for FW_KEYHASH_PRECOMPUTED              */
     int64_t* values[FW_MAX_COLS];      /* int64 or double bits, per value_col_types     */
     uint8_t* nulls[FW_MAX_COLS];       /* null flags of the nullable columns            */
+    /* v5, FW_KEYHASH_KEYROW (key unused): row i's key row image -- the bytes of its
+       BinaryRowData (the key projection's output, BinaryRowDataKeySelector.getKey) -- is
+       key_row_bytes[key_row_offsets[i] .. key_row_offsets[i + 1]); offsets 8-byte aligned,
+       key_row_offsets[0] = 0, at most key_row_bytes_cap bytes */
+    int64_t* key_row_offsets;          /* n + 1 entries                                 */
+    uint8_t* key_row_bytes;
+    int64_t key_row_bytes_cap;
 } fw_host_cols;
 
 /* Window results: SQL rows are key ++ aggs ++ (window_start, window_end); DataStream
@@ -209,6 +224,11 @@ typedef struct {
     uint32_t* null_mask;               /* bit a set => agg a is SQL NULL                */
     int64_t* first_ord;                /* v5, DataStream with ds_first_ordinals: arrival ordinal of
                                           the window's first element (value1), else NULL */
+    /* v5, FW_KEYHASH_KEYROW: row i's key row image is key_row_bytes[i * key_row_stride ..
+       + key_row_len[i]) (BinaryRowData.pointTo); key[] holds the handle's internal key ids */
+    int32_t* key_row_len;
+    uint8_t* key_row_bytes;
+    int64_t key_row_stride;
 } fw_result;
 
 typedef struct {
@@ -226,6 +246,9 @@ typedef struct {
     int64_t flush_launches;            /* fw_advance / flush launches that merged pending partials */
     int64_t partials_merged;           /* partial rows those flushes read                */
     int64_t state_entries_moved;       /* state entries loaded + written back by merge launches */
+    /* v5, FW_KEYHASH_KEYROW: key rows in the intern table (ids handed out and not collected) */
+    int64_t key_rows;
+    int64_t key_row_collections;       /* collections of unreferenced key rows so far    */
 } fw_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------- */
@@ -253,6 +276,13 @@ int fw_commit(fw_handle* h, int64_t n);
 int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t* d_ts,
                    const int32_t* d_key_hash, const void* const* d_values,
                    const uint8_t* const* d_nulls);
+
+/* FW_KEYHASH_KEYROW: device-resident key row images (Arrow layout: row i's BinaryRowData image is
+   d_key_row_bytes[d_key_row_offsets[i] .. d_key_row_offsets[i + 1]), offsets 8-byte aligned).  The
+   key's identity in the window state is the image bytes (BinaryRowData.equals); its hashCode
+   (MurmurHashUtils.hashBytesByWords, seed 42) routes it.  Otherwise as fw_push_device. */
+int fw_push_device_key_rows(fw_handle* h, int64_t n, const int64_t* d_key_row_offsets, const uint8_t* d_key_row_bytes,
+                            const int64_t* d_ts, const void* const* d_values, const uint8_t* const* d_nulls);
 
 /* The receive buffer of a padded all-to-all (the keyBy exchange without a host round trip for
    the row counts): n_segs segments of seg_len rows, one per sending subtask; segment s holds
@@ -388,6 +418,16 @@ typedef struct {
    in fields are device pointers; the key's identity in the window state (the int64 key column
    pushed alongside) is the caller's, e.g. a dictionary id. */
 int fw_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n, int32_t* d_hash, void* stream);
+/* BinaryRowWriter's image of each key row (what BinaryRowDataKeySelector.getKey holds), written at
+   d_offsets[i] of d_bytes (device pointers; d_offsets[i + 1] - d_offsets[i] must be the image
+   length, fw_host_key_row_image_lengths).  The input of fw_push_device_key_rows. */
+int fw_key_row_images(const fw_key_field* fields, int32_t n_fields, int64_t n, const int64_t* d_offsets,
+                      uint8_t* d_bytes, void* stream);
+/* host forms: image lengths (lens[i], bytes), images (host columns), and an image's hashCode */
+int fw_host_key_row_image_lengths(const fw_key_field* fields, int32_t n_fields, int64_t n, int64_t* lens);
+int fw_host_key_row_images(const fw_key_field* fields, int32_t n_fields, int64_t n, const int64_t* offsets,
+                           uint8_t* bytes);
+int32_t fw_host_key_row_image_hash(const uint8_t* image, int64_t len);
 
 /* ---- stand-alone device kernels (partitioner, tests) ---------------------------------- */
 /* d_kg[i] = key group, d_dest[i] = computeOperatorIndexForKeyGroup(maxP, p, kg). */
@@ -415,6 +455,15 @@ int fw_partition_packed(const int64_t* d_key, const int32_t* d_key_hash, const i
                         const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
                         int32_t max_parallelism, int32_t parallelism, int64_t seg_len, int64_t* d_out_rows,
                         int64_t* d_counts, void* d_workspace, int64_t workspace_bytes, void* stream);
+/* v5: fw_partition_packed whose rows past a destination's seg_len are not dropped: they go to
+   d_spill_rows (up to n rows of 2 + n_cols words), destination-major, each destination's in input
+   order -- destination d's max(0, d_counts[d] - seg_len) rows follow those of destinations < d.
+   The exchange sends them in an overflow round, so the segment size never has to bound a batch. */
+int fw_partition_packed_spill(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                              const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
+                              int32_t max_parallelism, int32_t parallelism, int64_t seg_len, int64_t* d_out_rows,
+                              int64_t* d_spill_rows, int64_t* d_counts, void* d_workspace, int64_t workspace_bytes,
+                              void* stream);
 
 /* Synthetic Nexmark-shaped generator: event i in [i0, i0+n). */
 typedef struct {

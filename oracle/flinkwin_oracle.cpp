@@ -121,7 +121,7 @@ int32_t binrow_hash_words(const int32_t* words, int nwords) {
 // :295-310 writeBytesToVarLenPart, :323-331 roundNumberOfBytesToNearestWord, :333-348
 // writeBytesToFixLenPart; setNullAt :59-62 writes the null bit and a 0 slot) on a
 // little-endian machine, then hashing the bytes as 4-byte ints (BinarySegmentUtils.hashByWords).
-int32_t key_row_hash_bytes(const fw_key_field* f, int nf, int64_t i) {
+std::vector<uint8_t> key_row_image(const fw_key_field* f, int nf, int64_t i) {
     const int null_bytes = ((nf + 63 + 8) / 64) * 8;  // calculateBitSetWidthInBytes (:71-73)
     std::vector<uint8_t> row((size_t)null_bytes + 8 * (size_t)nf, 0);
     auto put_long = [&](size_t at, uint64_t v) { for (int b = 0; b < 8; b++) row[at + b] = (uint8_t)(v >> (8 * b)); };
@@ -152,6 +152,11 @@ int32_t key_row_hash_bytes(const fw_key_field* f, int nf, int64_t i) {
             put_long(slot, ((uint64_t)cursor << 32) | (uint64_t)len);
         }
     }
+    return row;
+}
+// BinaryRowData.hashCode of the image (BinaryRowData.java:459 -> hashBytesByWords)
+int32_t key_row_hash_bytes(const fw_key_field* f, int nf, int64_t i) {
+    const std::vector<uint8_t> row = key_row_image(f, nf, i);
     std::vector<int32_t> words(row.size() / 4);
     memcpy(words.data(), row.data(), row.size());
     return binrow_hash_words(words.data(), (int)words.size());
@@ -997,6 +1002,12 @@ int32_t or_murmur_hash(int32_t code) { return murmur_hash(code); }
 int32_t or_java_key_hash(int32_t kind, int64_t key, int32_t pre) { return java_key_hash(kind, key, pre); }
 void or_key_row_hash(const fw_key_field* fields, int32_t n_fields, int64_t n, int32_t* out) {
     for (int64_t i = 0; i < n; i++) out[i] = key_row_hash_bytes(fields, n_fields, i);
+}
+// row i's BinaryRowWriter image; returns its length (bytes copied only if <= cap)
+int64_t or_key_row_image(const fw_key_field* fields, int32_t n_fields, int64_t i, uint8_t* out, int64_t cap) {
+    const std::vector<uint8_t> row = key_row_image(fields, n_fields, i);
+    if ((int64_t)row.size() <= cap) memcpy(out, row.data(), row.size());
+    return (int64_t)row.size();
 }
 int32_t or_key_group(int32_t kind, int64_t key, int32_t pre, int32_t max_p) {
     return key_group_for_hash(java_key_hash(kind, key, pre), max_p);

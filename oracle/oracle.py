@@ -56,6 +56,8 @@ def lib():
         L.or_java_key_hash.restype = i32
         L.or_java_key_hash.argtypes = [i32, i64, i32]
         L.or_key_row_hash.argtypes = [C.POINTER(abi.fw_key_field), i32, i64, vp]
+        L.or_key_row_image.restype = i64
+        L.or_key_row_image.argtypes = [C.POINTER(abi.fw_key_field), i32, i64, vp, i64]
         L.or_key_group.restype = i32
         L.or_key_group.argtypes = [i32, i64, i32, i32]
         L.or_operator_index.restype = i32
@@ -179,6 +181,16 @@ def key_row_hash(fields, n_fields, n):
     import numpy as np
     out = np.empty(n, dtype=np.int32)
     lib().or_key_row_hash(fields, n_fields, n, out.ctypes.data)
+    return out
+
+
+def key_row_images(fields, n_fields, n):
+    """Each key row's BinaryRowWriter image (bytes), the byte-image restatement behind key_row_hash."""
+    out = []
+    buf = C.create_string_buffer(1 << 16)
+    for i in range(n):
+        ln = lib().or_key_row_image(fields, n_fields, i, buf, len(buf))
+        out.append(buf.raw[:ln])
     return out
 
 

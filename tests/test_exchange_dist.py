@@ -63,16 +63,23 @@ def _worker(rank, port, n_batches, n, out_q):
         rows, received = [], 0
         for b in range(n_batches):
             k, t, v = _stream(rank, b, n)
+            my_wm = T0 + b * 3000 - 3000 + 500 * rank  # ranks propose different watermarks
+            wm = None
             if b % 3 == 0:
                 rk, rt, rv = ex.exchange(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)])
             elif b % 3 == 2:  # the bench's packed padded exchange: one buffer of (key, ts, value) rows
-                cap = n
-                packed, rc, w = ex.exchange_packed(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)], cap)
+                # segments of a quarter batch on odd steps: the overflow round carries the rest
+                cap = n // 4 if b % 2 else n
+                packed, rc, w, spill, wm = ex.exchange_packed(torch.from_numpy(k), torch.from_numpy(t),
+                                                              [torch.from_numpy(v)], cap, watermark=my_wm)
                 assert w == 3 and packed.numel() == WORLD * cap * w
                 seg = packed.view(WORLD, cap, w)
                 keep = torch.arange(cap)[None, :] < rc[:, None]
                 rk, rt, rv = seg[..., 0][keep], seg[..., 1][keep], [seg[..., 2][keep]]
-                ex.check_capacity()
+                assert (spill is not None) == bool(b % 2)
+                if spill is not None:
+                    sp = spill.view(-1, w)
+                    rk, rt, rv = torch.cat([rk, sp[:, 0]]), torch.cat([rt, sp[:, 1]]), [torch.cat([rv[0], sp[:, 2]])]
             else:  # the padded exchange: fixed segments + device-side counts, one all-to-all per column
                 cap = n  # a subtask never gets more than all of one sender's rows
                 pk, pt, pv, rc = ex.exchange_padded(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)], cap)
@@ -84,8 +91,9 @@ def _worker(rank, port, n_batches, n, out_q):
             kgs = {key_group(abi.KEYHASH_BINROW_BIGINT, int(x), 128) for x in np.unique(rk.numpy())}
             assert all(lo <= g <= hi for g in kgs), f"rank {rank}: foreign key group"
             op.process_batch(rk.numpy(), rt.numpy(), [rv[0].numpy()])
-            # ranks propose different watermarks; the valve takes the min
-            wm = ex.global_watermark(T0 + b * 3000 - 3000 + 500 * rank)
+            # the valve takes the min (agreed with the overflow decision in exchange_packed)
+            if wm is None:
+                wm = ex.global_watermark(my_wm)
             assert wm == T0 + b * 3000 - 3000
             op.process_watermark(wm)
             rows += _rows(op.results())

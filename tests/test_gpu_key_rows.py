@@ -1,10 +1,13 @@
-"""VARCHAR / composite keys on the device.  fw_key_row_hash computes
-BinaryRowData.hashCode (BinaryRowData.java:459 -> MurmurHashUtils.hashBytesByWords :70-170) of
-each key row from its columns (strings as offsets + bytes); the window operator routes by it
-(FW_KEYHASH_PRECOMPUTED) and keys its state by dictionary ids.  Checked on an MI355X against the
-oracle's byte-image restatement, the golden fixtures with their string keys, and a randomized
-stream at parallelism 2 (a wrong hash would route a row to a subtask that does not own its key
-group, which the device flags)."""
+"""VARCHAR / composite keys on the device, through the ABI only.
+fw_key_row_hash computes BinaryRowData.hashCode (BinaryRowData.java:459 -> MurmurHashUtils
+.hashBytesByWords :70-170) of each key row from its columns; fw_key_row_images writes the rows'
+BinaryRowData images; a FW_KEYHASH_KEYROW operator takes the images (pinned staging, as the JNI shim
+copies each key row) and interns them in an HBM table keyed by the bytes (BinaryRowDataKeySelector
+.getKey :54, RecordsWindowBuffer.addElement :81-104), routing by their hashCode.  Checked on an
+MI355X against the oracle: hashes and images, the golden fixtures with their string keys (with a
+snapshot/restore through the operator alone), a randomized stream at parallelism 2 (a wrong hash
+routes a row to a subtask that does not own its key group, which the device flags), a p -> p'
+key-group restore, and the collection of key rows no state holds any more."""
 import numpy as np
 import pytest
 
@@ -33,6 +36,19 @@ def test_device_key_row_hash_matches_host_and_oracle(types):
     got = cols.to(torch.device("cuda", 0)).hash_device().cpu().numpy()
     assert np.array_equal(got, want)
     assert np.array_equal(cols.hash_host(), want)
+
+
+@pytest.mark.parametrize("types", KEY_SHAPES, ids=["-".join(t) for t in KEY_SHAPES])
+def test_device_key_row_images_match_oracle(types):
+    import torch
+    from flink_amd.table.key_rows import KeyRowColumns
+    from oracle import oracle as O
+    rng = np.random.default_rng(200 + len(types))
+    rows = _rand_rows(rng, types, 2000)
+    cols = KeyRowColumns.from_rows(rows, types)
+    off, img = cols.to(torch.device("cuda", 0)).images_device()
+    off, img = off.cpu().numpy(), img.cpu().numpy()
+    assert [img[off[i]:off[i + 1]].tobytes() for i in range(len(rows))] == O.key_row_images(cols.fields(), len(types), len(rows))
 
 
 def test_device_key_row_hash_large_batch():
@@ -73,18 +89,18 @@ class VarcharKeyAdapter:
         self.op.process_batch([(self.names[int(x)],) for x in k], t, vals, nulls=nulls)
 
     def process_watermark(self, w):
+        from flink_amd.table.key_rows import decode_key_row
         res = self.op.process_watermark(w)
-        res["key"] = np.array([self.ids[self.op.keys.decode(x)[0]] for x in res["key"]], np.int64)
+        res["key"] = np.array([self.ids[decode_key_row(x, ("VARCHAR",))[0]] for x in res["key_rows"]], np.int64)
         return res
 
     def snapshot_restore(self):
+        # through the operator alone: the blob carries the key rows its state uses
         from flink_amd.table.window_agg import WindowAggOperator
         self.op.prepare_snapshot_pre_barrier()
         blob = self.op.snapshot_state()
-        keys = self.op.keys
         self.op.close()
         self.op = WindowAggOperator(**self.kw).open()
-        self.op.keys = keys  # the dictionary is host state restored with the operator
         self.op.initialize_state(blob)
 
     @property
@@ -106,7 +122,7 @@ def test_composite_key_rows_two_subtasks_vs_oracle():
     key-row hash assigns; each subtask's device-computed hash must agree (else the device flags
     a foreign key group) and the union of results equals one oracle operator."""
     from flink_amd import abi
-    from flink_amd.table.key_rows import KeyDictionary, KeyRowColumns
+    from flink_amd.table.key_rows import KeyRowColumns
     from flink_amd.table.slice_assigners import SliceAssigners
     from flink_amd.table.window_agg import WindowAggOperator
     from oracle import oracle as O
@@ -116,9 +132,9 @@ def test_composite_key_rows_two_subtasks_vs_oracle():
     aggs = [("COUNT_STAR", 0, "BIGINT"), ("SUM", 0, "BIGINT"), ("MAX", 0, "BIGINT")]
     kw = dict(assigner=SliceAssigners.hopping(0, 3000, 1000), aggs=aggs, value_types=["BIGINT"],
               count_star_index=0, key_type=types, parallelism=2, state_capacity=1 << 14,
-              max_batch_rows=1 << 14, output_capacity=1 << 16)
+              max_batch_rows=1 << 14, output_capacity=1 << 16, key_row_max_bytes=256)
     ops = [WindowAggOperator(subtask_index=i, **kw).open() for i in range(2)]
-    ids = KeyDictionary()
+    ids = _OracleKeys()
     ocfg = abi.make_config(api=abi.API_SQL, window_kind=abi.WIN_HOP, size_ms=3000, slide_ms=1000,
                            aggs=[(abi.AGG_NAMES[k], c, abi.TYPE_NAMES[t]) for k, c, t in aggs], count_star_index=0,
                            value_col_types=[abi.T_I64], key_hash=abi.KEYHASH_PRECOMPUTED)
@@ -143,11 +159,10 @@ def test_composite_key_rows_two_subtasks_vs_oracle():
             got = []
             for op in ops:
                 res = op.process_watermark(wm)
-                got += [op.keys.decode(k) + (int(ws), int(we)) + tuple(int(v[i]) for v in res["values"])
-                        for i, (k, ws, we) in enumerate(zip(res["key"], res["window_start"], res["window_end"]))]
+                got += op.output_rows(res)
             orc.process_watermark(wm)
             r = orc.results(clear=True)
-            want = [ids.decode(k) + (int(ws), int(we)) + tuple(int(v[i]) for v in r["values"])
+            want = [ids.decode(k) + tuple(int(v[i]) for v in r["values"]) + (int(ws), int(we))
                     for i, (k, ws, we) in enumerate(zip(r["key"], r["window_start"], r["window_end"]))]
             assert sorted(got, key=repr) == sorted(want, key=repr), f"batch {b}"
         assert all(op.handle.stats()["error_flags"] == 0 for op in ops)
@@ -155,3 +170,160 @@ def test_composite_key_rows_two_subtasks_vs_oracle():
         for op in ops:
             op.close()
         orc.close()
+
+
+class _OracleKeys:
+    """Test-side ids for the oracle, which keys on int64: one per distinct key row."""
+
+    def __init__(self):
+        self.ids, self.rows = {}, []
+
+    def encode(self, rows):
+        out = np.empty(len(rows), np.int64)
+        for i, r in enumerate(rows):
+            k = self.ids.get(r)
+            if k is None:
+                k = self.ids[r] = len(self.rows)
+                self.rows.append(r)
+            out[i] = k
+        return out
+
+    def decode(self, k):
+        return self.rows[int(k)]
+
+
+def _route(rows, types, p):
+    from flink_amd import abi
+    from flink_amd.table.key_rows import KeyRowColumns
+    from oracle import oracle as O
+    kc = KeyRowColumns.from_rows(rows, types)
+    h = O.key_row_hash(kc.fields(), len(types), len(rows))
+    return np.array([O.operator_index(128, p, O.key_group(abi.KEYHASH_PRECOMPUTED, 0, 128, pre=int(x))) for x in h])
+
+
+@pytest.mark.parametrize("p_from,p_to", [(2, 3), (3, 1)])
+def test_key_row_rescale_restore_by_key_group(p_from, p_to):
+    """(VARCHAR, BIGINT) keys, CUMULATE: checkpoint at parallelism p_from, restore the key groups
+    at p_to through the ABI (each blob carries its key rows; the restoring subtask interns them and
+    routes each by its hashCode), continue; the union of results equals one oracle restarted at the
+    same cut."""
+    from flink_amd import abi
+    from flink_amd.table.slice_assigners import SliceAssigners
+    from flink_amd.table.window_agg import WindowAggOperator
+    from oracle import oracle as O
+    rng = np.random.default_rng(7 + p_from)
+    types = ("VARCHAR", "BIGINT")
+    universe = _rand_rows(rng, types, 400, null_p=0.05)
+    aggs = [("COUNT_STAR", 0, "BIGINT"), ("SUM", 0, "BIGINT"), ("MIN", 0, "BIGINT")]
+    kw = dict(assigner=SliceAssigners.cumulative(0, 4000, 1000), aggs=aggs, value_types=["BIGINT"],
+              count_star_index=0, key_type=types, state_capacity=1 << 14, max_batch_rows=1 << 13,
+              output_capacity=1 << 16, key_row_max_bytes=256)
+    ocfg = abi.make_config(api=abi.API_SQL, window_kind=abi.WIN_CUMULATE, size_ms=4000, slide_ms=1000,
+                           aggs=[(abi.AGG_NAMES[k], c, abi.TYPE_NAMES[t]) for k, c, t in aggs], count_star_index=0,
+                           value_col_types=[abi.T_I64], key_hash=abi.KEYHASH_PRECOMPUTED)
+    orc = O.OracleOperator(ocfg)
+    ids = _OracleKeys()
+    ops = [WindowAggOperator(parallelism=p_from, subtask_index=i, **kw).open() for i in range(p_from)]
+    t0 = 1_600_000_000_000
+    try:
+        for b in range(16):
+            if b == 8:  # checkpoint, rescale, restore
+                blobs, wms = {}, []
+                for op in ops:
+                    op.prepare_snapshot_pre_barrier()
+                    bl, wm_ = op.handle.snapshot_key_groups()
+                    blobs.update(bl)
+                    wms.append(wm_)
+                    op.close()
+                ops = [WindowAggOperator(parallelism=p_to, subtask_index=i, **kw).open() for i in range(p_to)]
+                for op in ops:
+                    op.handle.restore_key_groups(blobs, wms)
+                orc.snapshot_restore()
+            p = len(ops)
+            rows = [universe[i] for i in rng.integers(0, len(universe), 1500)]
+            ts = t0 + b * 600 + rng.integers(-1200, 1200, len(rows))
+            val = rng.integers(-1000, 1000, len(rows)).astype(np.int64)
+            dest = _route(rows, types, p)
+            for d in range(p):
+                m = dest == d
+                if m.any():
+                    ops[d].process_batch([r for r, keep in zip(rows, m) if keep], ts[m], [val[m]])
+            orc.process_batch(ids.encode(rows), ts, [val])
+            wm = t0 + b * 600 - 1300
+            got = []
+            for op in ops:
+                got += op.output_rows(op.process_watermark(wm))
+            orc.process_watermark(wm)
+            r = orc.results(clear=True)
+            want = [ids.decode(k) + tuple(int(v[i]) for v in r["values"]) + (int(ws), int(we))
+                    for i, (k, ws, we) in enumerate(zip(r["key"], r["window_start"], r["window_end"]))]
+            assert sorted(got, key=repr) == sorted(want, key=repr), f"batch {b}"
+        assert all(op.handle.stats()["error_flags"] == 0 for op in ops)
+    finally:
+        for op in ops:
+            op.close()
+        orc.close()
+
+
+def test_key_rows_no_state_holds_are_collected():
+    """A stream whose keys change every few windows: the table keeps only the key rows some state
+    entry, pending partial or unread result holds -- collections run, the ids are reused, the
+    table never fills although 10x its capacity of distinct keys pass -- and the results stay
+    bit-exact against the oracle."""
+    from flink_amd import abi
+    from flink_amd.table.slice_assigners import SliceAssigners
+    from flink_amd.table.window_agg import WindowAggOperator
+    from oracle import oracle as O
+    rng = np.random.default_rng(3)
+    types = ("VARCHAR",)
+    aggs = [("COUNT_STAR", 0, "BIGINT"), ("MAX", 0, "BIGINT")]
+    op = WindowAggOperator(SliceAssigners.tumbling(0, 2000), aggs, ["BIGINT"], count_star_index=0, key_type=types,
+                           state_capacity=2048, max_batch_rows=512, output_capacity=1 << 14).open()
+    ocfg = abi.make_config(api=abi.API_SQL, window_kind=abi.WIN_TUMBLE, size_ms=2000,
+                           aggs=[(abi.AGG_NAMES[k], c, abi.TYPE_NAMES[t]) for k, c, t in aggs], count_star_index=0,
+                           value_col_types=[abi.T_I64], key_hash=abi.KEYHASH_PRECOMPUTED)
+    orc = O.OracleOperator(ocfg)
+    ids = _OracleKeys()
+    t0 = 1_600_000_000_000
+    distinct = 0
+    max_live = 0
+    try:
+        for b in range(120):
+            gen = b // 3  # a new key population every 3 watermarks
+            rows = [(f"k{gen}-{int(x)}",) for x in rng.integers(0, 700, 500)]
+            distinct += 0 if b % 3 else 700
+            ts = t0 + b * 1000 + rng.integers(0, 1000, len(rows))
+            val = rng.integers(0, 10**6, len(rows)).astype(np.int64)
+            op.process_batch(rows, ts, [val])
+            orc.process_batch(ids.encode(rows), ts, [val])
+            wm = t0 + b * 1000 + 999
+            got = op.output_rows(op.process_watermark(wm))
+            orc.process_watermark(wm)
+            r = orc.results(clear=True)
+            want = [ids.decode(k) + tuple(int(v[i]) for v in r["values"]) + (int(ws), int(we))
+                    for i, (k, ws, we) in enumerate(zip(r["key"], r["window_start"], r["window_end"]))]
+            assert sorted(got, key=repr) == sorted(want, key=repr), f"batch {b}"
+            st = op.handle.stats()
+            assert st["error_flags"] == 0, f"batch {b}: {st}"
+            max_live = max(max_live, st["key_rows"])
+        st = op.handle.stats()
+        assert st["key_row_collections"] > 0
+        assert distinct > 4 * (2048 + 8 * 512) and max_live <= 2048 + 8 * 512
+    finally:
+        op.close()
+        orc.close()
+
+
+def test_key_row_longer_than_the_limit_is_a_device_error():
+    from flink_amd._native import FlinkWinError
+    from flink_amd.table.slice_assigners import SliceAssigners
+    from flink_amd.table.window_agg import WindowAggOperator
+    op = WindowAggOperator(SliceAssigners.tumbling(0, 2000), [("COUNT_STAR", 0, "BIGINT")], ["BIGINT"],
+                           key_type=("VARCHAR",), state_capacity=1024, max_batch_rows=64, output_capacity=1024,
+                           key_row_max_bytes=32).open()
+    try:
+        with pytest.raises((FlinkWinError, ValueError)):
+            op.process_batch([("x" * 100,)], np.array([1_600_000_000_000]), [np.array([1])])
+            op.process_watermark(1_600_000_010_000)
+    finally:
+        op.close()

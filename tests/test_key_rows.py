@@ -12,7 +12,7 @@ import pytest
 
 from flink_amd import abi
 from flink_amd._native import lib
-from flink_amd.table.key_rows import KeyDictionary, KeyRowColumns
+from flink_amd.table.key_rows import KeyRowColumns, decode_key_row
 from oracle import oracle as O
 
 ALPHABET = "abcxyz0123é漢"
@@ -110,13 +110,43 @@ def test_invalid_key_field_descriptions_rejected():
     assert L.fw_host_key_row_hash(f, 1, 1, out.ctypes.data) == abi.FW_E_INVALID
 
 
-def test_key_dictionary_round_trip():
-    d = KeyDictionary()
-    rows = [("a", 1), ("b", 2), ("a", 1), (None, 3)]
-    ids = d.encode(rows)
-    assert ids.tolist() == [0, 1, 0, 2]
-    assert [d.decode(i) for i in ids] == rows
-    assert len(d) == 3
+@pytest.mark.parametrize("types", KEY_SHAPES, ids=["-".join(t) for t in KEY_SHAPES])
+def test_key_row_images_match_oracle_and_round_trip(types):
+    """The library's BinaryRowWriter images (fw_host_key_row_images, the code k_kr_images runs) are
+    byte-identical to the oracle's, hash (fw_host_key_row_image_hash, what k_kr_intern runs) like
+    the columnar hash, and decode back to the rows (BinaryRowData getters)."""
+    rng = np.random.default_rng(31 + len(types))
+    rows = _rand_rows(rng, types, 400)
+    cols = KeyRowColumns.from_rows(rows, types)
+    off, img = cols.images_host()
+    want = O.key_row_images(cols.fields(), len(types), len(rows))
+    got = [img[off[i]:off[i + 1]].tobytes() for i in range(len(rows))]
+    assert got == want
+    L = lib()
+    h = [L.fw_host_key_row_image_hash(np.frombuffer(g, np.uint64).ctypes.data, len(g)) for g in got]
+    assert h == cols.hash_host().tolist()
+    for r, g in zip(rows, got):
+        d = decode_key_row(g, types)
+        for t, x, y in zip(types, r, d):
+            if t == "FLOAT" and x is not None:
+                assert np.float32(x) == np.float32(y)
+            elif t == "BOOLEAN" and x is not None:
+                assert bool(x) == y
+            else:
+                assert x == y, (types, r, d)
+
+
+def test_key_row_identity_is_the_image_bytes():
+    """BinaryRowData.equals compares bytes: -0.0 and 0.0 are different DOUBLE keys, equal strings
+    are one key whatever Python object carried them, and NULL differs from the empty string."""
+    cols = KeyRowColumns.from_rows([(0.0,), (-0.0,), (0.0,)], ("DOUBLE",))
+    off, img = cols.images_host()
+    g = [img[off[i]:off[i + 1]].tobytes() for i in range(3)]
+    assert g[0] == g[2] and g[0] != g[1]
+    cols = KeyRowColumns.from_rows([("ab",), (b"ab",), (None,), ("",)], ("VARBINARY",))
+    off, img = cols.images_host()
+    g = [img[off[i]:off[i + 1]].tobytes() for i in range(4)]
+    assert g[0] == g[1] and g[2] != g[3]
 
 
 def test_host_partition_routes_precomputed_hash_like_oracle():

@@ -23,15 +23,33 @@ def test_library_loads_and_exports_header_symbols():
     assert L.fw_abi_version() == abi.FW_ABI_VERSION
 
 
-def test_config_struct_layout_matches_header():
+STRUCTS = ["fw_config", "fw_agg_desc", "fw_host_cols", "fw_result", "fw_stats", "fw_late_rows", "fw_ordinal_events",
+           "fw_kernel_times", "fw_key_field", "fw_gen_params"]
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Every ctypes mirror in flink_amd/abi.py has the size and field offsets the C compiler gives
+    include/flinkwin.h's struct (what a JNI / FFI binding must reproduce)."""
     import ctypes as C
-    # fw_config: 4 ints, 3 int64, 2 ints, 8 agg descs (16 B), int, 8 ints, nullable mask + phase,
-    # 4 ints + reserved, 3 int64; v4: lateness, side output / dst / tz_n / reserved, 2 pointers
-    assert C.sizeof(abi.fw_config) == 16 + 24 + 8 + 128 + 4 + 32 + 8 + 16 + 4 + 24 + 8 + 16 + 16
-    assert abi.fw_config.state_capacity.offset == 240
-    assert abi.fw_config.tz_utc.offset == 288
-    # fw_host_cols: key, ts, key_hash, 8 value and 8 null-flag pointers
-    assert C.sizeof(abi.fw_host_cols) == 8 * (3 + 2 * abi.FW_MAX_COLS)
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "flinkwin.h"', 'int main(void) {']
+    for st in STRUCTS:
+        lines.append(f'printf("{st} %zu\\n", sizeof({st}));')
+        for f, _ in getattr(abi, st)._fields_:
+            lines.append(f'printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(root, "include"), "-o", str(exe), str(src)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines())
+    for st in STRUCTS:
+        cls = getattr(abi, st)
+        assert int(got[st]) == C.sizeof(cls), st
+        for f, _ in cls._fields_:
+            assert int(got[f"{st}.{f}"]) == getattr(cls, f).offset, f"{st}.{f}"
 
 
 def test_window_start_matches_oracle():

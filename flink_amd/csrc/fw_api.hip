@@ -131,6 +131,7 @@ struct fw_handle {
     int nv = 0;
     int slot_col[MAX_KCOLS] = {};
     int nw_t = 1;  // template word count (layout stride)
+    int pwe = 4;   // words per state entry: key, slice (HOP block: block start), flags, accumulator words
     int n_out = 1; // result value columns (aggregates; LOCAL phase: accumulator fields)
     int64_t cap_rows = 0;     // rows per partial-buffer slot (= max rows per push piece)
     int64_t chunk_rows = 0;   // rows per ingest chunk (IG_BLOCK * ig_rpt(nw_t))
@@ -500,11 +501,24 @@ int validate_and_plan(fw_handle* h) {
     ks.kg_start = (c.subtask_index * c.max_parallelism + c.parallelism - 1) / c.parallelism;
     const int kg_end = ((c.subtask_index + 1) * c.max_parallelism - 1) / c.parallelism;
     ks.n_kg = kg_end - ks.kg_start + 1;
-    const int64_t cap_target = std::max<int64_t>(c.state_capacity, 1024);
+    // SQL HOP with few slices per window and plain accumulators keeps block state (k_merge_hopb):
+    // one entry per (key, HB_R consecutive slices) instead of one per (key, slice)
+    const char* hb_env = getenv("FW_HOPB");
+    w.hopb = c.api == FW_API_SQL && c.window_kind == FW_WIN_HOP && c.agg_phase != FW_PHASE_LOCAL && !wd.has_q &&
+             h->nw_t <= 2 && w.n_slices <= HB_R && !(hb_env && atoi(hb_env) == 0);
+    if (w.hopb) {
+        w.hb_span = HB_R * w.interval;
+        w.hb_span_div = make_udiv((uint64_t)w.hb_span);
+    }
+    h->pwe = 3 + (w.hopb ? HB_R * h->nw_t : h->nw_t);
+    // the hint counts (key, slice) entries; a key's live slices (a window plus the batch's newer
+    // ones) fit one or two blocks
+    const int64_t cap_target = std::max<int64_t>(
+        w.hopb ? c.state_capacity * 3 / (2 * (w.n_slices + 3)) : c.state_capacity, 1024);
     // aim for <= ~75% occupancy of the per-superbucket LDS entry table at the hinted capacity (the
     // index has 2E slots, so its load factor stays <= 38%); fewer, fuller superbuckets amortise the
     // merge kernel's per-workgroup costs (CFG5: 4096 -> 2048 superbuckets, merge -27%)
-    h->cap_e = mg_entries(h->nw_t, c.api == FW_API_DATASTREAM ? KIND_DSWIN : c.window_kind);
+    h->cap_e = mg_entries(h->nw_t, c.api == FW_API_DATASTREAM ? KIND_DSWIN : w.hopb ? KIND_HOPB : c.window_kind);
     const int64_t fill = h->cap_e * h->fill_pct / 100;
     int64_t per_kg = (cap_target + ks.n_kg - 1) / ks.n_kg;
     int64_t sbk = next_pow2((per_kg + fill - 1) / fill);
@@ -558,7 +572,7 @@ int allocate(fw_handle* h) {
     HIP_TRY(hipSetDevice(c.device));
     HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     int rc;
-    const int PW = 2 + h->nw_t, PWE = 3 + h->nw_t;
+    const int PW = 2 + h->nw_t, PWE = h->pwe;
     if ((rc = dalloc(&h->ctrl, 1))) return rc;
     if ((rc = dalloc(&h->parts, (size_t)FW_MAX_PENDING * h->cap_rows * PW))) return rc;
     if ((rc = dalloc(&h->cells, (size_t)FW_MAX_PENDING * h->ks.n_sb * h->cell_cols))) return rc;
@@ -853,6 +867,12 @@ int push_key_rows(fw_handle* h, int64_t n, const int64_t* d_off, const uint8_t* 
 // earliest watermark-visible time of an entry's timers, as a window end (is_fired(x, W) <=> due):
 // the maxTimestamp timer at its window end, a DataStream cleanup timer at cleanupTime + 1
 int64_t entry_timer_end(const fw_handle* h, int64_t slice, uint64_t flags) {
+    if (h->win.hopb) {  // block entry: no window of it is due before its oldest slice with data
+        const uint32_t mask = (uint32_t)flags >> 8;
+        for (int i = 0; i < HB_R; i++)
+            if ((mask >> i) & 1u) return wadd(slice, (int64_t)(i + 1) * h->win.interval);
+        return INT64_MAX;
+    }
     int64_t m = (flags & F_TIMER) ? slice : INT64_MAX;
     if (h->win.ds && (flags & F_CLEAN)) m = std::min(m, wadd(ds_cleanup_time(h->win, slice), 1));
     return m;
@@ -1112,7 +1132,7 @@ int fw_advance(fw_handle* h, int64_t watermark) {
     int rc = launch_merge(h, watermark, 0);
     if (rc) return rc;
     if (h->keyrow)  // key rows no state / partial / timer request / unread result holds any more
-        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->ks.n_sb, h->cap_e, 3 + h->nw_t,
+        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->ks.n_sb, h->cap_e, h->pwe,
                                   2 + h->nw_t, h->parts, h->cap_rows, h->treq, h->out_key, h->sb_out, h->slab_cap,
                                   h->stream));
     if (watermark > h->host_cur) h->host_cur = watermark;
@@ -1514,7 +1534,7 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     if (rc) return rc;
     Ctrl c;
     if ((rc = read_ctrl(h, &c))) return rc;
-    const int nsb = h->ks.n_sb, pwe = 3 + h->nw_t;
+    const int nsb = h->ks.n_sb, pwe = h->pwe;
     std::vector<int32_t> cnt(nsb);
     HIP_TRY(hipMemcpy(cnt.data(), h->state_count, sizeof(int32_t) * nsb, hipMemcpyDeviceToHost));
     int64_t total = 0;
@@ -1552,7 +1572,7 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     SnapHeader hd;
     if (size < (int64_t)sizeof hd) return fail(FW_E_INVALID, "snapshot truncated");
     memcpy(&hd, buf, sizeof hd);
-    const int nsb = h->ks.n_sb, pwe = 3 + h->nw_t;
+    const int nsb = h->ks.n_sb, pwe = h->pwe;
     if (hd.magic != SNAP_MAGIC || hd.n_sb != nsb || hd.pwe != pwe || hd.cap_e != h->cap_e ||
         hd.semantics != semantics_fingerprint(h))
         return fail(FW_E_INVALID, "snapshot layout does not match this operator configuration");
@@ -1643,7 +1663,7 @@ int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t ca
     if (rc) return rc;
     Ctrl c;
     if ((rc = read_ctrl(h, &c))) return rc;
-    const int L = ks.sb_per_kg_log2, nsub = 1 << L, pwe = 3 + h->nw_t;
+    const int L = ks.sb_per_kg_log2, nsub = 1 << L, pwe = h->pwe;
     std::vector<int32_t> cnt(nsub);
     HIP_TRY(hipMemcpy(cnt.data(), h->state_count + ((size_t)li << L), sizeof(int32_t) * nsub, hipMemcpyDeviceToHost));
     int64_t total = 0;
@@ -1677,7 +1697,7 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
     if (size < (int64_t)sizeof hd) return fail(FW_E_INVALID, "key-group snapshot truncated");
     memcpy(&hd, buf, sizeof hd);
     const KeySpace& ks = h->ks;
-    const int pwe = 3 + h->nw_t, L = ks.sb_per_kg_log2;
+    const int pwe = h->pwe, L = ks.sb_per_kg_log2;
     if (hd.magic != KG_MAGIC || hd.version != 3) return fail(FW_E_INVALID, "not a key-group snapshot");
     if (hd.pwe != pwe || hd.nw != h->wd.nw || hd.hash_kind != h->cfg.key_hash || hd.win_size != h->win.size ||
         hd.win_interval != h->win.interval || hd.semantics != semantics_fingerprint(h))

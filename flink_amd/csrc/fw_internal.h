@@ -47,6 +47,7 @@ constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a t
 // window kinds that keep several slices per key (HOP, CUMULATE, DataStream panes) keep 4096 entries
 // of capacity with a 2x index.
 constexpr int mg_entries(int nw, int kind) {
+    if (kind == 4) return nw <= 1 ? 1536 : 768;  // KIND_HOPB: HB_R slots of nw words per entry
     return nw <= 1 ? (kind == FW_WIN_TUMBLE ? 3072 : 4096) : nw <= 4 ? 2048 : 1024;
 }
 // LDS index slots of a table of E entries with NW accumulator words: a power of two, 4E when it
@@ -232,11 +233,16 @@ struct WinDesc {
     int64_t lateness;     // allowedLateness (cleanupTime = maxTimestamp + lateness, saturating)
     UDiv slide_div;
     int32_t n_win;
-    int32_t pad2;
+    // SQL HOP with block state (k_merge_hopb): one entry per (key, block of HB_R slices)
+    int32_t hopb;
+    int64_t hb_span;      // HB_R * interval
+    UDiv hb_span_div;
 };
 
 // merge/fire kernel variant of a handle: the SQL window kinds, or DataStream windows
 constexpr int KIND_DSWIN = 3;
+constexpr int KIND_HOPB = 4;  // SQL HOP, block state (fw_merge_hopb.h)
+constexpr int HB_R = 8;       // slices per HOP block entry
 
 // TimeWindowUtil.isWindowFired in the window's shift zone (UTC when tz.n == 0)
 FW_HD bool win_fired(const WinDesc& w, int64_t we, int64_t progress) {

@@ -1,0 +1,368 @@
+// fw_merge_hopb.h -- k_merge_hopb: the flush + fire kernel of SQL HOP windows with block state.
+//
+// The slice-per-entry state of k_merge_fire keeps one (key, slice) entry per live slice, and a HOP
+// fire follows the key's timer chain of windows, each probing the LDS index for its n slices
+// (SliceSharedSyncStateWindowAggProcessor.fireWindow :65-86 with merge :89-118 over
+// HoppingSlicesIterable).  Here one entry holds a BLOCK of HB_R consecutive slices of one key
+// (block start aligned to HB_R slice intervals from the window offset): (key, block start, data
+// mask, acc[HB_R][NWP]).  A partial folds into its slice's slot; a window is the register fold of
+// at most two neighbouring blocks, newest slice first (the reference's merge order); and the
+// timers become arithmetic: the reference fires exactly the non-empty windows whose end the
+// watermark passes (a flushed slice registers its own window end, and nextTriggerWindow chains on
+// while the window is not empty, HoppingSliceAssigner.nextTriggerWindow; a late record registers
+// the first unfired window holding it, AbstractSliceSyncStateWindowAggProcessor.processElement
+// :111-117), so an advance from W0 to W fires every window ending in (W0, W] that holds data --
+// each found by the block holding its end slice, or by the block before it when that block does
+// not exist.  clearWindow's expiry becomes: a slice is dropped once its last window has fired.
+//
+// Used for SQL HOP (ONE and GLOBAL phase) with n_slices <= HB_R, NWP <= 2 accumulator words and no
+// SQL MIN/MAX(DOUBLE) word groups; every other HOP configuration runs k_merge_fire.
+#pragma once
+#include "fw_merge_impl.h"
+
+namespace fw {
+
+constexpr uint32_t HB_MASK_SHIFT = 8;  // flag bits 8.. : slot i holds data
+
+// Finds (k, bs) or inserts it with an identity ring; *inserted tells the caller it was new.
+template <int NWP, int E, uint32_t OPS>
+__device__ int hb_find_or_insert(StateLds<HB_R * NWP, E>& S, int64_t k, int64_t bs, const WordDesc& wd) {
+    constexpr int NA = HB_R * NWP;
+    constexpr uint32_t MASK = StateLds<NA, E>::NI - 1;
+    uint32_t h = index_hash(k, bs) & MASK;
+    for (int probes = 0; probes < StateLds<NA, E>::NI;) {
+        const uint32_t st = __hip_atomic_load(&S.idx[h], __ATOMIC_RELAXED, LDS_SCOPE);
+        if (st == 1) continue;
+        if (st == 0) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     LDS_SCOPE)) {
+                const int e = atomicAdd(&S.n, 1);
+                if (e >= E) {
+                    S.overflow = 1;
+                    __hip_atomic_store(&S.idx[h], IDX_DEAD, __ATOMIC_RELAXED, LDS_SCOPE);
+                    return -1;
+                }
+                S.key[e] = k;
+                S.slice[e] = bs;
+                S.flag[e] = 0;
+#pragma unroll
+                for (int i = 0; i < NA; i++) {
+                    const int w = i % NWP;
+                    S.acc[i][e] = word_on<OPS>(wd, w) ? word_identity(word_op<OPS>(wd, w)) : 0;
+                }
+                compiler_fence();
+                __hip_atomic_store(&S.idx[h], 2u + (uint32_t)e, __ATOMIC_RELAXED, LDS_SCOPE);
+                return e;
+            }
+            continue;
+        }
+        const uint32_t e = st - 2;
+        if (e < (uint32_t)E && S.key[e] == k && S.slice[e] == bs) return (int)e;
+        h = (h + 1) & MASK;
+        probes++;
+    }
+    S.overflow = 1;
+    return -1;
+}
+
+// block start of a slice end and the slice's slot in it
+__device__ __forceinline__ int64_t hb_block_of(const WinDesc& w, int64_t se) {
+    return window_start(wsub(se, 1), w.offset, w.hb_span_div);
+}
+__device__ __forceinline__ int hb_slot_of(const WinDesc& w, int64_t se, int64_t bs) {
+    return (int)udiv((uint64_t)wsub(se, bs), w.slice_div) - 1;
+}
+
+// the fold of one slot into acc (merge in the reference's order: acc is the newer side)
+template <int NWP, int E, uint32_t OPS>
+__device__ __forceinline__ void hb_merge_slot(const MergeArgs& a, const StateLds<HB_R * NWP, E>& S, int e, int slot,
+                                              uint64_t* acc) {
+    uint64_t o[NWP];
+#pragma unroll
+    for (int w = 0; w < NWP; w++) o[w] = S.acc[slot * NWP + w][e];
+    merge_slice<NWP, false, OPS>(a.wd, a.ad, acc, o);
+}
+
+// Fires the windows entry e is responsible for: those ending in its block, and -- when the key has
+// no entry for the next block -- those ending in the next block that still hold slices of this one.
+// A window fires iff it ends in (W0, W] and holds data.  Returns the windows fired.
+template <int NWP, int E, uint32_t OPS>
+__device__ uint32_t hb_fire_entry(const MergeArgs& a, StateLds<HB_R * NWP, E>& S, int e, int64_t w_old, int sb,
+                                  int32_t* s_emit) {
+    const WinDesc& w = a.win;
+    const int n = w.n_slices;
+    const int64_t k = S.key[e], bs = S.slice[e];
+    const uint32_t mask = S.flag[e] >> HB_MASK_SHIFT;
+    if (!mask) return 0;
+    // candidate window ends: slot j's slice end, j in [0, HB_R + n - 1)
+    int prev = -2, next = -2;  // neighbouring blocks' entries, looked up on first need
+    uint32_t nf = 0;
+    for (int j = 0; j < HB_R + n - 1; j++) {
+        const int64_t we = wadd(bs, (int64_t)(j + 1) * w.interval);
+        if (!win_fired(w, we, a.wm) || win_fired(w, we, w_old)) continue;  // not due in this advance
+        // the window's slots: j, j-1, ..., j-n+1 (newest first); < 0: previous block, >= HB_R: next
+        const int lo = j - n + 1;
+        if (j >= HB_R) {  // the next block fires it if it exists
+            if (next == -2) next = find_entry(S, k, wadd(bs, w.hb_span));
+            if (next >= 0) continue;
+        }
+        // data in this block's part of the window?  (the next block's part is empty: no entry)
+        const int a0 = max(lo, 0), a1 = min(j, HB_R - 1);
+        uint32_t here = a1 >= a0 ? (mask >> a0) & ((2u << (a1 - a0)) - 1u) : 0u;
+        uint32_t before = 0;
+        if (lo < 0) {
+            if (prev == -2) prev = find_entry(S, k, wsub(bs, w.hb_span));
+            if (prev >= 0) {
+                const uint32_t pm = S.flag[prev] >> HB_MASK_SHIFT;
+                before = pm >> (HB_R + lo);  // slots HB_R+lo .. HB_R-1 of the previous block
+            }
+        }
+        if (!here && !before) continue;  // empty window: no output (its timer would fire silently)
+        uint64_t acc[NWP];
+        acc_identity<NWP, OPS>(a.wd, acc);
+        for (int t = min(j, HB_R - 1); t >= max(lo, 0); t--)
+            if ((mask >> t) & 1u) hb_merge_slot<NWP, E, OPS>(a, S, e, t, acc);
+        if (before)
+            for (int t = HB_R - 1; t >= HB_R + lo; t--)
+                if ((before >> (t - (HB_R + lo))) & 1u) hb_merge_slot<NWP, E, OPS>(a, S, prev, t, acc);
+        nf++;
+        if (a.ad.count_star_word < 0 || acc[a.ad.count_star_word] != 0) emit_row<NWP, false>(a, sb, s_emit, k, we, acc);
+    }
+    return nf;
+}
+
+template <int NWP, int E, uint32_t OPS>
+__global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
+    constexpr int NA = HB_R * NWP;  // ring words per entry
+    constexpr int PW = 2 + NWP;     // partial row words
+    constexpr int PWE = 3 + NA;     // state entry words
+    const int64_t CH = a.chunk_rows;
+    constexpr int GU = mg_rows_in_flight(NWP);
+    __shared__ StateLds<NA, E> S;
+    __shared__ int32_t s_work;
+    __shared__ int32_t s_nlive;
+    __shared__ int64_t s_newmin;
+    __shared__ uint32_t s_fired;
+    __shared__ int32_t s_emit;
+    __shared__ int32_t s_tk;
+
+    const int tid = threadIdx.x;
+    kt_start(a.kt);
+    Ctrl* c = a.ctrl;
+    const WinDesc& win = a.win;
+    const int64_t W = a.wm;
+    const int64_t cur = __hip_atomic_load(&c->cur, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t pend = __hip_atomic_load(&c->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t ntp = __hip_atomic_load(&c->ntp, __ATOMIC_RELAXED, DEV_SCOPE);
+    const int64_t minp = __hip_atomic_load(&c->min_pending, __ATOMIC_RELAXED, DEV_SCOPE);
+    const bool adv = !a.force_flush && W > cur;
+    const bool do_flush = pend > 0 && (a.force_flush || (adv && (W >= ntp && win_fired(win, minp, W))));
+    const bool do_fire = adv;
+    const int64_t w_old = cur;
+    const int64_t w_new = adv ? W : cur;  // the watermark after this launch (slice expiry)
+    // late-record timer requests (n_treq) need no work here: their windows fire by holding data
+
+    const bool xq = a.n_sb % 8 == 0 && gridDim.x % 8 == 0;
+    const int nq = xq ? a.n_sb / 8 : a.n_sb;
+    uint32_t* const wq = &a.tickets->work[xq ? blockIdx.x % 8 : 0][0];
+    const int qbase = xq ? (int)(blockIdx.x % 8) * nq : 0;
+    if (tid == 0) s_tk = (int32_t)__hip_atomic_fetch_add(wq, 1u, __ATOMIC_RELAXED, DEV_SCOPE);
+    if (!do_flush) {  // nothing to gather: work only where a window is due
+        bool due = false;
+        for (int i = tid; i < nq; i += MG_BLOCK) due |= do_fire && win_fired(win, a.sb_min_timer[qbase + i], W);
+        if (!__syncthreads_or(due)) {
+            if (a.reset_out)
+                for (int i = tid; i < nq; i += MG_BLOCK) a.sb_out[qbase + i] = 0;
+            s_tk = nq;
+        }
+    }
+    __syncthreads();
+    for (int tk = s_tk; tk < nq; tk = s_tk) {
+        const int sb = qbase + tk;
+        const int32_t n0 = a.state_count[sb];
+        __syncthreads();
+        if (tid == 0) {
+            s_tk = (int32_t)__hip_atomic_fetch_add(wq, 1u, __ATOMIC_RELAXED, DEV_SCOPE);
+            s_work = do_flush || (do_fire && win_fired(win, a.sb_min_timer[sb], W));
+            s_fired = 0;
+            s_emit = a.reset_out ? 0 : a.sb_out[sb];
+            if (!s_work && a.reset_out) a.sb_out[sb] = 0;
+        }
+        __syncthreads();
+        if (!s_work) continue;
+        auto cell_at = [&](int64_t pi, int f) -> uint32_t {
+            if (cell_chunk(f) >= a.slot_nch[pi]) return 0u;
+            const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
+            return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
+        };
+        const int lane = tid & 63, wv = tid >> 6;
+        auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
+        uint32_t v_first = 0;
+        if (do_flush && lane < gather_group((int)cell_pad(a.slot_nch[0])))
+            v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
+        // ---- load the superbucket's block entries into LDS
+        for (int i = tid; i < StateLds<NA, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
+        if (tid == 0) {
+            S.n = n0;
+            S.overflow = 0;
+        }
+        __syncthreads();
+        const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
+        for (int e = tid; e < n0; e += MG_BLOCK) {
+            uint64_t p[PWE];
+            load_words<PWE>(st + (size_t)e * PWE, p);
+            const int64_t k = (int64_t)p[0], bs = (int64_t)p[1];
+            S.key[e] = k;
+            S.slice[e] = bs;
+            S.flag[e] = (uint32_t)p[2];
+#pragma unroll
+            for (int i = 0; i < NA; i++) S.acc[i][e] = p[3 + i];
+            uint32_t h = index_hash(k, bs) & (StateLds<NA, E>::NI - 1);
+            for (;;) {
+                uint32_t expect = 0;
+                if (__hip_atomic_compare_exchange_strong(&S.idx[h], &expect, 2u + (uint32_t)e, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, LDS_SCOPE))
+                    break;
+                h = (h + 1) & (StateLds<NA, E>::NI - 1);
+            }
+        }
+        __syncthreads();
+        // ---- flush: every pending partial (key, sliceEnd, acc) folds into its block's slot
+        if (do_flush) {
+            for (int64_t pi = 0; pi < pend; pi++) {
+                const int ncell = (int)cell_pad(a.slot_nch[pi]);
+                const int G = gather_group(ncell);
+                const int ngroups = ncell / G;
+                const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
+                for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
+                    const int f = g * G + lane;
+                    const uint32_t v = lane >= G ? 0u : (pi == 0 && g == wv) ? v_first : cell_at(pi, f);
+                    const uint32_t cnt = v >> 16;
+                    uint32_t inc = cnt;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+                        if (lane >= d) inc += t;
+                    }
+                    const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+                    const uint32_t excl = inc - cnt;
+                    const uint32_t adj = (uint32_t)(cell_chunk(f) * CH + (v & 0xFFFFu)) - excl;
+                    for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
+                        uint64_t row[GU][PW];
+#pragma unroll
+                        for (int u = 0; u < GU; u++) {
+                            const uint32_t x = min(r0 + (uint32_t)(u * 64 + lane), tot - 1);
+                            int lo = 0;
+#pragma unroll
+                            for (int step = 32; step > 0; step >>= 1)
+                                if ((uint32_t)__shfl((int)excl, lo + step, 64) <= x) lo += step;
+                            const uint64_t* p = seg + (size_t)((uint32_t)__shfl((int)adj, lo, 64) + x) * PW;
+                            load_words<PW>(p, row[u]);
+                        }
+                        int ge[GU], slot[GU];
+                        {
+                            int64_t gk[GU], gb[GU];
+#pragma unroll
+                            for (int u = 0; u < GU; u++) {
+                                gk[u] = (int64_t)row[u][0];
+                                gb[u] = hb_block_of(win, (int64_t)row[u][1]);
+                                slot[u] = hb_slot_of(win, (int64_t)row[u][1], gb[u]);
+                                row[u][1] = (uint64_t)gb[u];
+                            }
+                            probe_batch<NA, E, GU>(S, gk, gb, ge);
+                        }
+                        static_for<GU>([&](auto UU) {
+                            constexpr int u = decltype(UU)::value;
+                            if (r0 + (uint32_t)(u * 64 + lane) >= tot) return;
+                            int e = ge[u];
+                            if (e < 0) e = hb_find_or_insert<NWP, E, OPS>(S, (int64_t)row[u][0], (int64_t)row[u][1], a.wd);
+                            if (e < 0) return;  // state overflow (flagged)
+                            const int sl = slot[u];
+#pragma unroll
+                            for (int w = 0; w < NWP; w++)
+                                if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[sl * NWP + w][e], row[u][2 + w]);
+                            atomicOr(&S.flag[e], F_ACC | (1u << (HB_MASK_SHIFT + sl)));
+                        });
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- fire: every due window that holds data, each by exactly one block entry
+        if (do_fire) {
+            const int n = min(S.n, E);
+            uint32_t nf = 0;
+            const int qlane = (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
+            for (int e = qlane; e < n; e += MG_BLOCK) nf += hb_fire_entry<NWP, E, OPS>(a, S, e, w_old, sb, &s_emit);
+            nf = wave_sum_u32(nf);
+            if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
+        }
+        // ---- write back: a slice is dropped once its last window has fired (clearWindow); an
+        // entry without live slices is dropped
+        if (tid == 0) {
+            s_nlive = 0;
+            s_newmin = INT64_MAX;
+        }
+        __syncthreads();
+        const int n = min(S.n, E);
+        uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
+        int64_t lnm = INT64_MAX;
+        // the first window end that is not fired at w_new (UTC: the slice grid point above w_new + 1)
+        const int64_t e_min = win.tz.n == 0 ? slice_end_of(win, wadd(w_new, 1)) : INT64_MIN;
+        for (int e = tid; e < n; e += MG_BLOCK) {
+            const int64_t bs = S.slice[e];
+            uint32_t mask = S.flag[e] >> HB_MASK_SHIFT;
+            uint64_t p[PWE];
+#pragma unroll
+            for (int i = 0; i < NA; i++) p[3 + i] = S.acc[i][e];
+            int64_t first = INT64_MAX;
+#pragma unroll
+            for (int i = 0; i < HB_R; i++) {
+                if (!((mask >> i) & 1u)) continue;
+                const int64_t se = wadd(bs, (int64_t)(i + 1) * win.interval);
+                if (win_fired(win, wadd(se, wsub(win.size, win.interval)), w_new)) {
+                    mask &= ~(1u << i);  // its last window fired: expired
+#pragma unroll
+                    for (int w = 0; w < NWP; w++)
+                        p[3 + i * NWP + w] = word_on<OPS>(a.wd, w) ? word_identity(word_op<OPS>(a.wd, w)) : 0;
+                } else if (first == INT64_MAX) {
+                    first = se;
+                }
+            }
+            if (!mask) continue;
+            const int pos = wave_claim(&s_nlive);
+            p[0] = (uint64_t)S.key[e];
+            p[1] = (uint64_t)bs;
+            p[2] = (uint64_t)(F_ACC | (mask << HB_MASK_SHIFT));
+            store_words<PWE>(so + (size_t)pos * PWE, p);
+            lnm = min(lnm, max(first, e_min));  // no window of this entry is due before it
+        }
+        lnm = wave_min_i64(lnm);
+        if ((tid & 63) == 0 && lnm != INT64_MAX) __hip_atomic_fetch_min(&s_newmin, lnm, __ATOMIC_RELAXED, LDS_SCOPE);
+        __syncthreads();
+        if (tid == 0) {
+            a.state_count[sb] = s_nlive;
+            a.sb_min_timer[sb] = s_newmin;
+            a.sb_out[sb] = min(s_emit, a.slab_cap);
+            if (s_fired) a.sb_fired[sb] += s_fired;
+            if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
+            __hip_atomic_fetch_add(&c->state_moved, (uint64_t)(n0 + s_nlive), __ATOMIC_RELAXED, DEV_SCOPE);
+        }
+        __syncthreads();
+    }
+    merge_ticket(a);
+}
+
+template <int NWP>
+static void merge_hopb_launch(const MergeArgs& a, hipStream_t s) {
+    constexpr int E = mg_entries(NWP, KIND_HOPB);
+    // COUNT(*) alone / COUNT(*) + SUM(BIGINT) with the word ops as constants; the rest at run time
+    constexpr uint32_t L = NWP == 1 ? ops_pack({W_SUM_I}) : ops_pack({W_SUM_I, W_SUM_I});
+    if (ops_layout(a.wd) == L)
+        hipLaunchKernelGGL((k_merge_hopb<NWP, E, L>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_merge_hopb<NWP, E, OPS_ANY>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+}
+
+}  // namespace fw

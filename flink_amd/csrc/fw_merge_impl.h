@@ -1152,8 +1152,20 @@ static bool merge_layout_launch(const MergeArgs& a, uint32_t lay, hipStream_t s)
     }
 }
 
+template <int NWP>
+static void merge_hopb_launch(const MergeArgs& a, hipStream_t s);  // fw_merge_hopb.h
+
 template <int NW>
 hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
+    if (a.win.hopb) {  // SQL HOP with block state
+        if constexpr (NW <= 2) {
+            if (a.cap_e != mg_entries(NW, KIND_HOPB)) return hipErrorInvalidValue;
+            merge_hopb_launch<NW>(a, s);
+            return hipGetLastError();
+        } else {
+            return hipErrorInvalidValue;
+        }
+    }
     if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
         if (a.wd.has_q) return hipErrorInvalidValue;
         constexpr int E = mg_entries(NW, KIND_DSWIN);

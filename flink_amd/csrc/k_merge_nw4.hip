@@ -1,5 +1,5 @@
 // k_merge_nw4.hip -- k_merge_fire instantiations for 4 accumulator word(s) per entry
-#include "fw_merge_impl.h"
+#include "fw_merge_hopb.h"
 
 namespace fw {
 template hipError_t merge_nw<4>(const MergeArgs& a, hipStream_t s);

@@ -50,12 +50,24 @@ WORKLOADS = {
                  window=("TUMBLE", 10_000, 0), aggs=[("SUM", 0, "DOUBLE"), ("AVG", 0, "DOUBLE")],
                  count_star=-1, keys=1_250_000, key_base=0, rate=1_000_000, value_kind=1, dist=0, w_in=24,
                  value_cols=["DOUBLE"], nw=2, state_per_key=2),
+    # CFG4's full key space on ONE GPU (10^7 keys, sharded over 8 GPUs in cfg4): the state
+    # outgrows the 8192 superbuckets the ingest histogram partitions into, so two merge passes share
+    # each ingest superbucket (KeySpace.pass_log2 = 1)
+    "cfg4_10m": dict(desc="TUMBLE(10 s) SUM(v), AVG(v) DOUBLE over 10^7 keys on one GPU",
+                     window=("TUMBLE", 10_000, 0), aggs=[("SUM", 0, "DOUBLE"), ("AVG", 0, "DOUBLE")],
+                     count_star=-1, keys=10_000_000, key_base=0, rate=1_000_000, value_kind=1, dist=0, w_in=24,
+                     keys_fixed=True, value_cols=["DOUBLE"], nw=2, state_per_key=2),
     "cfg5": dict(desc="CUMULATE(1 min step, 1 h) COUNT(*), SUM, MIN, MAX, Zipf(1.1) keys",
                  window=("CUMULATE", 3_600_000, 60_000),
                  aggs=[("COUNT_STAR", 0, "BIGINT"), ("SUM", 0, "BIGINT"), ("MIN", 0, "BIGINT"), ("MAX", 0, "BIGINT")],
                  count_star=0, keys=1_000_000, key_base=0, rate=27_778, value_kind=2, dist=1, w_in=24,
                  zipf_s=1.1, keys_fixed=True, value_cols=["BIGINT"], nw=4, state_per_key=3),
 }
+
+
+def chunk_rows(wl):
+    # rows per k_ingest chunk (fw_internal.h ig_block * ig_rpt): 4096 up to 4 accumulator words
+    return 4096 if wl["nw"] <= 4 else 2048
 
 
 def watermark(b, rate_per_gpu):
@@ -198,12 +210,14 @@ def main():
         if world == 1:
             handle.push_device(gk[b], gt[b], [gv[b]] if nv else [])
             return watermark(b, wl["rate"])
-        rows, rc, w, spill, wm = ex.exchange_packed(gk[b], gt[b], [gv[b]] if nv else [],
-                                                    watermark=watermark(b, wl["rate"]))
-        handle.push_device_packed_segments(rc, rows, w)
+        # the received segments' ingest is queued before the host waits for the partition's
+        # counts (overflow round + watermark valve), so the GPU stays busy through that host step
+        px = ex.exchange_packed_async(gk[b], gt[b], [gv[b]] if nv else [])
+        handle.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
+        spill, wm = px.finish(watermark=watermark(b, wl["rate"]))
         if spill is not None:
-            n_sp = spill.numel() // w
-            handle.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=dev), spill, w)
+            n_sp = spill.numel() // px.row_words
+            handle.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=dev), spill, px.row_words)
         return wm
 
     out_cap = 2 * keys_total // world + (1 << 20)
@@ -311,8 +325,8 @@ def main():
     merge_total = (sum(groups) * merged_share * w_partial + st["state_entries_moved"] * w_entry
                    + fired_total * w_out)
     merge_bytes = merge_total / max(mg_n, 1)
-    merge_read_total = (st["partials_merged"] * w_partial + st["state_entries_moved"] * w_entry
-                        + fired_total * w_out)
+    # partial bytes as written (compact chunks: (key, acc) or (key) rows + a rank byte, fw_internal.h PF_*)
+    merge_read_total = (st["partial_bytes_merged"] + st["state_entries_moved"] * w_entry + fired_total * w_out)
     avg_merge_s = mg_ms / max(mg_n, 1) / 1e3
     traffic = traffic_m = None
     tpath = args.traffic_json
@@ -326,38 +340,71 @@ def main():
             traffic = tj.get("k_ingest_hbm_bytes_per_launch")
             traffic_m = tj.get("k_merge_fire_hbm_bytes_per_launch")
 
-    # ---------------- end-to-end leg (N = 1): host-staged ingest + per-watermark D2H ----------
-    # What the JNI shim does: the host writes each batch into the operator's
-    # pinned staging columns (fw_reserve), fw_commit copies them over PCIe and ingests, and every
-    # watermark's results come back to host memory (fw_results copy_to_host).  Reported beside the
-    # device-resident `value`, never as it.
+    # ---------------- end-to-end leg (N = 1): host-staged, pipelined --------------------------
+    # What the JNI shim does, pipelined the way the handle allows: the host fills
+    # the operator's pinned staging columns (fw_reserve; 8 threads copying slices of the numpy
+    # batch, standing for the shim's record serialisation), fw_commit moves them over PCIe on the
+    # copy stream while the previous batch is still being ingested (double-buffered device staging),
+    # and each watermark's rows are collected into pinned host memory by fw_results_async and read
+    # one step later (fw_results_ready).  Reported beside the device-resident `value`, never as it.
     e2e = None
     if world == 1 and not args.no_e2e and args.e2e_steps > 0:
+        from concurrent.futures import ThreadPoolExecutor
         from flink_amd.runtime.handle import _np_view
-        hk = [gk[b].cpu().numpy() for b in range(args.e2e_steps)]
-        ht = [gt[b].cpu().numpy() for b in range(args.e2e_steps)]
-        hv = [gv[b].cpu().numpy() for b in range(args.e2e_steps)]
+        ns = args.e2e_steps
+        hk = [gk[b].cpu().numpy() for b in range(ns)]
+        ht = [gt[b].cpu().numpy() for b in range(ns)]
+        hv = [gv[b].cpu().numpy() for b in range(ns)]
         cfg_e = build_config(wl, 1, 0, keys_total, out_cap)
         he = WindowAggHandle(cfg_e)
+        pool = ThreadPoolExecutor(8)
+        parts = [(i * B // 8, (i + 1) * B // 8) for i in range(8)]
+
+        def fill(dst, src):  # ctypes.memmove releases the GIL: the slices copy in parallel
+            d = C.cast(dst, C.c_void_p).value
+            return [pool.submit(C.memmove, d + 8 * a, src.ctypes.data + 8 * a, 8 * (e - a)) for a, e in parts]
+
+        cols = abi.fw_host_cols()
+        _native.check(L.fw_reserve(he._h, 0, C.byref(cols)))  # allocates the staging (untimed)
+        _native.check(L.fw_commit(he._h, 0))
         rows_out = 0
+        t_reserve = t_fill = t_ready = 0.0
         te0 = time.perf_counter()
-        for b in range(args.e2e_steps):
+        for b in range(ns):
+            t1 = time.perf_counter()
             cols = abi.fw_host_cols()
-            _native.check(L.fw_reserve(he._h, B, C.byref(cols)))
-            _np_view(cols.key, B, np.int64)[:] = hk[b]
-            _np_view(cols.ts, B, np.int64)[:] = ht[b]
-            if nv:
-                _np_view(cols.values[0], B, np.int64)[:] = hv[b]
+            _native.check(L.fw_reserve(he._h, B, C.byref(cols)))  # waits for the H2D two commits back
+            t2 = time.perf_counter()
+            fs = fill(cols.key, hk[b]) + fill(cols.ts, ht[b]) + (fill(cols.values[0], hv[b]) if nv else [])
+            for f in fs:
+                f.result()
+            t3 = time.perf_counter()
             _native.check(L.fw_commit(he._h, B))
             he.advance(watermark(b, wl["rate"]))
-            rows_out += len(he.results(reset=True)["key"])
+            t4 = time.perf_counter()
+            if b:
+                rows_out += len(he.results_ready(copy=False)["key"])  # watermark b - 1's rows
+            t5 = time.perf_counter()
+            he.results_async()
+            t_reserve += t2 - t1
+            t_fill += t3 - t2
+            t_ready += t5 - t4
+        t6 = time.perf_counter()
+        rows_out += len(he.results_ready(copy=False)["key"])
         he.sync()
         te = time.perf_counter() - te0
+        t_ready += time.perf_counter() - t6
         he.close()
-        e2e = {"value": args.e2e_steps * B / te, "unit": "events/s", "steps": args.e2e_steps,
-               "ms_per_step": te / args.e2e_steps * 1e3, "result_rows": rows_out,
-               "path": "numpy batch -> pinned staging (fw_reserve) -> H2D + ingest (fw_commit) -> "
-                       "advance -> fw_results copy_to_host, one watermark per batch"}
+        pool.shutdown()
+        e2e = {"value": ns * B / te, "unit": "events/s", "steps": ns,
+               "ms_per_step": te / ns * 1e3, "result_rows": rows_out,
+               "host_ms_per_step": {"fill_pinned_8_threads": t_fill / ns * 1e3,
+                                    "reserve_wait_h2d": t_reserve / ns * 1e3,
+                                    "results_ready_wait": t_ready / ns * 1e3},
+               "fill_GBps": ns * B * wl["w_in"] / max(t_fill, 1e-9) / 1e9,
+               "path": "numpy batch -> pinned staging (fw_reserve, 8 fill threads) -> H2D on the copy stream, "
+                       "overlapping the previous batch's ingest (fw_commit) -> advance -> rows into pinned host "
+                       "memory (fw_results_async), read one watermark later (fw_results_ready)"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -399,6 +446,8 @@ def main():
                                            else "hipEvents around every launch of the timed region"),
                          "launches": red_n, "distinct_groups_per_launch": g_per_launch,
                          "partials_written_per_launch": st["partials_emitted"] / red_n,
+                         "partial_bytes_written_per_launch": st["partial_bytes_written"] / red_n,
+                         "compact_chunk_share": st["compact_chunks"] / max(1, red_n * -(-int(rows_per_launch) // chunk_rows(wl))),
                          "counter_rate_GBps": (traffic / avg_reduce_s / 1e9) if traffic else None,
                          "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None},
             "roofline_merge": {"bound": "hbm", "kernel": "fw::k_merge_fire (K4 flush into the HBM slice table + "
@@ -412,7 +461,7 @@ def main():
                                    "state_entries_moved_w_entry": st["state_entries_moved"] * w_entry / max(mg_n, 1),
                                    "F_w_out": fired_total * w_out / max(mg_n, 1)},
                                "flush_launches": st["flush_launches"], "live_state_entries_end": live,
-                               "partial_bytes_read_per_launch": st["partials_merged"] * w_partial / max(mg_n, 1),
+                               "partial_bytes_read_per_launch": st["partial_bytes_merged"] / max(mg_n, 1),
                                "design_bytes_per_launch": merge_read_total / max(mg_n, 1),
                                "avg_launch_us": avg_merge_s * 1e6, "launches": mg_n, "traffic": traffic_m,
                                "counter_rate_GBps": (traffic_m / avg_merge_s / 1e9) if traffic_m else None,

@@ -52,6 +52,8 @@ def lib():
         "fw_flush": (i32, [vp]),
         "fw_results": (i32, [vp, P(abi.fw_result), i32]),
         "fw_results_reset": (i32, [vp]),
+        "fw_results_async": (i32, [vp]),
+        "fw_results_ready": (i32, [vp, P(abi.fw_result)]),
         "fw_get_stats": (i32, [vp, P(abi.fw_stats)]),
         "fw_set_profiling": (i32, [vp, i32]),
         "fw_get_kernel_times": (i32, [vp, P(abi.fw_kernel_times)]),
@@ -91,7 +93,7 @@ def lib():
 # every symbol the public header declares (tests check they are exported)
 EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
             "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance",
-            "fw_flush", "fw_results", "fw_results_reset", "fw_get_stats", "fw_set_profiling",
+            "fw_flush", "fw_results", "fw_results_reset", "fw_results_async", "fw_results_ready", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_key_row_hash", "fw_host_key_row_hash",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_packed_spill", "fw_partition_workspace_bytes",

@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 5
+FW_ABI_VERSION = 6
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -143,7 +143,9 @@ class fw_stats(C.Structure):
                 ("num_superbuckets", C.c_int32),
                 ("flush_launches", C.c_int64), ("partials_merged", C.c_int64),
                 ("state_entries_moved", C.c_int64), ("key_rows", C.c_int64),
-                ("key_row_collections", C.c_int64)]
+                ("key_row_collections", C.c_int64),
+                ("partial_bytes_written", C.c_int64), ("partial_bytes_merged", C.c_int64),
+                ("compact_chunks", C.c_int64)]
 
 
 KT_PARTITION, KT_SCAN, KT_REDUCE, KT_MERGE, KT_OTHER = 0, 1, 2, 3, 4

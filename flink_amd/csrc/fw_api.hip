@@ -141,6 +141,9 @@ struct fw_handle {
 
     Ctrl* ctrl = nullptr;
     uint64_t* parts = nullptr;
+    int32_t narrow = 0;          // compact partial rows (IngestArgs::narrow)
+    int64_t* slot_base = nullptr;  // [FW_MAX_PENDING] rank base of each pending push
+    uint8_t* ranks = nullptr;      // [FW_MAX_PENDING][cap_rows] rank bytes of compact rows
     int64_t cell_cols = 0;       // cell_pad(max_nch): cells per superbucket per slot
     uint32_t* cells = nullptr;   // [FW_MAX_PENDING][cell_cols / 16][n_sb][16] (cell_index)
     int32_t* slot_nch = nullptr;  // [FW_MAX_PENDING]
@@ -186,13 +189,30 @@ struct fw_handle {
     int32_t* h_kh[2] = {};
     int64_t* h_val[2][FW_MAX_COLS] = {};
     uint8_t* h_nul[2][FW_MAX_COLS] = {};
-    hipEvent_t stage_ev[2] = {};
-    int64_t* d_key = nullptr;
-    int64_t* d_ts = nullptr;
-    int32_t* d_kh = nullptr;
-    int64_t* d_val[FW_MAX_COLS] = {};
-    uint8_t* d_nul[FW_MAX_COLS] = {};
+    hipEvent_t stage_ev[2] = {};   // H2D from host buffer b done (copy stream)
+    // device staging, double-buffered: batch b+1 crosses PCIe on the copy stream while batch b is
+    // ingested on the operator stream
+    hipStream_t cstream = nullptr;
+    hipEvent_t dstage_free[2] = {};  // the ingest that read device buffer b has run (operator stream)
+    int64_t* d_key[2] = {};
+    int64_t* d_ts[2] = {};
+    int32_t* d_kh[2] = {};
+    int64_t* d_val[2][FW_MAX_COLS] = {};
+    uint8_t* d_nul[2][FW_MAX_COLS] = {};
     int64_t reserved = -1;
+
+    // asynchronous result delivery (fw_results_async / fw_results_ready): rows compacted straight
+    // into one of two pinned, device-mapped host buffers
+    int64_t* ar_key[2] = {};
+    int64_t* ar_ws[2] = {};
+    int64_t* ar_we[2] = {};
+    uint64_t* ar_val[2][FW_MAX_AGGS] = {};
+    uint32_t* ar_null[2] = {};
+    int64_t* ar_n[2] = {};          // row count (written by the compaction kernel)
+    hipEvent_t ar_ev[2] = {};
+    int ar_cur = 0;                 // buffer of the next fw_results_async
+    int ar_last = -1;               // buffer of the last one (-1: none)
+    bool ar_empty[2] = {};          // that call had nothing to collect
 
     // FW_KEYHASH_KEYROW: the key-row intern table, per-push intern output, key-row staging
     bool keyrow = false;
@@ -203,8 +223,8 @@ struct fw_handle {
     int64_t* h_kro[2] = {};         // pinned staging: key row offsets / bytes (fw_reserve)
     uint8_t* h_krb[2] = {};
     int64_t krb_cap = 0;            // staging bytes per batch
-    int64_t* d_kro = nullptr;
-    uint8_t* d_krb = nullptr;
+    int64_t* d_kro[2] = {};
+    uint8_t* d_krb[2] = {};
     int32_t* res_kr_len = nullptr;  // result key rows (fw_results)
     uint64_t* res_kr_img = nullptr;
     std::vector<int32_t> r_kr_len;
@@ -522,12 +542,20 @@ int validate_and_plan(fw_handle* h) {
     const int64_t fill = h->cap_e * h->fill_pct / 100;
     int64_t per_kg = (cap_target + ks.n_kg - 1) / ks.n_kg;
     int64_t sbk = next_pow2((per_kg + fill - 1) / fill);
-    const int64_t max_sb = IG_MAX_SB;
+    // beyond IG_MAX_SB superbuckets the ingest partitions coarser than the state (KeySpace
+    // pass_log2): up to MAX_PASS_LOG2 merge passes share one ingest superbucket's partial rows.  A
+    // pass re-routes each row's key, so precomputed-hash keys (no hash in the partial rows) cap
+    // the state at IG_MAX_SB superbuckets
+    const int max_pl = ks.hash_kind == KH_PRE ? 0 : MAX_PASS_LOG2;
+    const int64_t max_sb = (int64_t)IG_MAX_SB << max_pl;
     while ((int64_t)ks.n_kg * sbk > max_sb && sbk > 1) sbk >>= 1;
     if ((int64_t)ks.n_kg * sbk > max_sb) return fail(FW_E_INVALID, "too many key groups per subtask for the ingest histogram");
     ks.sb_per_kg_log2 = 0;
     while ((1ll << ks.sb_per_kg_log2) < sbk) ks.sb_per_kg_log2++;
     ks.n_sb = ks.n_kg << ks.sb_per_kg_log2;
+    ks.pass_log2 = 0;
+    while ((ks.n_sb >> ks.pass_log2) > IG_MAX_SB) ks.pass_log2++;
+    if (ks.pass_log2 > ks.sb_per_kg_log2) return fail(FW_E_INVALID, "superbucket split finer than a key group's passes");
     if (c.max_batch_rows <= 0) return fail(FW_E_INVALID, "max_batch_rows must be > 0");
     if (c.output_capacity <= 0) return fail(FW_E_INVALID, "output_capacity must be > 0");
     h->chunk_rows = (int64_t)ig_block(h->nw_t, ig_nv(h->nv)) * ig_rpt(h->nw_t, ig_nv(h->nv));
@@ -536,6 +564,17 @@ int validate_and_plan(fw_handle* h) {
     if (wd.has_ord && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
         return fail(FW_E_INVALID, "max_batch_rows too large for MIN/MAX(DOUBLE) / first-element arrival ordinals");
     h->cell_cols = cell_pad(h->max_nch);
+    // compact partial rows: SQL rows on the UTC slice grid (the ingest kernel's common path; it falls
+    // back to PF_WIDE per chunk).  Key-row handles keep PF_WIDE: their collector reads the partial
+    // buffer's keys at a fixed stride.  FW_NARROW=0 switches them off (development).
+    {
+        const char* ne = getenv("FW_NARROW");
+        const bool count_only = wd.nw == 1 && wd.op[0] == W_CNT && wd.gate[0] < 0;
+        h->narrow = (c.api == FW_API_SQL && !h->keyrow && c.agg_phase != FW_PHASE_GLOBAL && h->tz_utc.empty() &&
+                     w.fast32 && !(ne && atoi(ne) == 0) && (h->chunk_rows & (h->chunk_rows - 1)) == 0)
+                        ? (count_only ? 2 : 1)
+                        : 0;
+    }
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     if (c.api == FW_API_DATASTREAM) {
         if (c.allowed_lateness_ms > 0 && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
@@ -575,8 +614,10 @@ int allocate(fw_handle* h) {
     const int PW = 2 + h->nw_t, PWE = h->pwe;
     if ((rc = dalloc(&h->ctrl, 1))) return rc;
     if ((rc = dalloc(&h->parts, (size_t)FW_MAX_PENDING * h->cap_rows * PW))) return rc;
-    if ((rc = dalloc(&h->cells, (size_t)FW_MAX_PENDING * h->ks.n_sb * h->cell_cols))) return rc;
+    if ((rc = dalloc(&h->cells, (size_t)FW_MAX_PENDING * (h->ks.n_sb >> h->ks.pass_log2) * h->cell_cols))) return rc;
     if ((rc = dalloc(&h->slot_nch, FW_MAX_PENDING))) return rc;
+    if ((rc = dalloc(&h->slot_base, FW_MAX_PENDING))) return rc;
+    if (h->narrow && (rc = dalloc(&h->ranks, (size_t)FW_MAX_PENDING * h->cap_rows))) return rc;
     if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
     if (h->lfire_cap && (rc = dalloc(&h->lfire, (size_t)h->lfire_cap * LFW))) return rc;
     if (h->side_cap && (rc = dalloc(&h->side, (size_t)h->side_cap * SOW))) return rc;
@@ -618,7 +659,7 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->sb_out, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->sb_fired, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->coff, h->ks.n_sb + 2))) return rc;
-    if ((rc = dalloc(&h->chunk_stats, 4 * h->max_nch + 4))) return rc;
+    if ((rc = dalloc(&h->chunk_stats, CS_WORDS * (h->max_nch + 1)))) return rc;
     if ((rc = dalloc(&h->stamps, N_STAMPS))) return rc;
     if ((rc = dalloc(&h->kt_dev, FW_KT_N * KT_WORDS))) return rc;
     if ((rc = dalloc(&h->tickets, 1))) return rc;
@@ -639,9 +680,11 @@ int allocate(fw_handle* h) {
 }
 
 int alloc_staging(fw_handle* h) {
-    if (h->d_key) return FW_OK;
+    if (h->d_ts[0]) return FW_OK;
     const fw_config& c = h->cfg;
     const size_t n = (size_t)h->stage_cap;
+    HIP_TRY(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
+    int rc;
     for (int b = 0; b < 2; b++) {
         HIP_TRY(hipHostMalloc((void**)&h->h_key[b], n * 8, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc((void**)&h->h_ts[b], n * 8, hipHostMallocDefault));
@@ -651,25 +694,48 @@ int alloc_staging(fw_handle* h) {
             if ((c.nullable_cols >> v) & 1u) HIP_TRY(hipHostMalloc((void**)&h->h_nul[b][v], n, hipHostMallocDefault));
         }
         HIP_TRY(hipEventCreateWithFlags(&h->stage_ev[b], hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(h->stage_ev[b], h->stream));
-    }
-    int rc;
-    if (h->keyrow) {
-        for (int b = 0; b < 2; b++) {
+        HIP_TRY(hipEventRecord(h->stage_ev[b], h->cstream));
+        HIP_TRY(hipEventCreateWithFlags(&h->dstage_free[b], hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(h->dstage_free[b], h->stream));
+        if (h->keyrow) {
             HIP_TRY(hipHostMalloc((void**)&h->h_kro[b], (n + 1) * 8, hipHostMallocDefault));
             HIP_TRY(hipHostMalloc((void**)&h->h_krb[b], (size_t)std::max<int64_t>(h->krb_cap, 8), hipHostMallocDefault));
+            if ((rc = dalloc(&h->d_kro[b], n + 1))) return rc;
+            if ((rc = dalloc(&h->d_krb[b], (size_t)std::max<int64_t>(h->krb_cap, 8)))) return rc;
+        } else {
+            if ((rc = dalloc(&h->d_key[b], n))) return rc;
         }
-        if ((rc = dalloc(&h->d_kro, n + 1))) return rc;
-        if ((rc = dalloc(&h->d_krb, (size_t)std::max<int64_t>(h->krb_cap, 8)))) return rc;
-    }
-    if ((rc = dalloc(&h->d_key, n))) return rc;
-    if ((rc = dalloc(&h->d_ts, n))) return rc;
-    if ((rc = dalloc(&h->d_kh, n))) return rc;
-    for (int v = 0; v < c.n_value_cols; v++) {
-        if ((rc = dalloc(&h->d_val[v], n))) return rc;
-        if (((c.nullable_cols >> v) & 1u) && (rc = dalloc(&h->d_nul[v], n))) return rc;
+        if ((rc = dalloc(&h->d_ts[b], n))) return rc;
+        if (c.key_hash == FW_KEYHASH_PRECOMPUTED && (rc = dalloc(&h->d_kh[b], n))) return rc;
+        for (int v = 0; v < c.n_value_cols; v++) {
+            if ((rc = dalloc(&h->d_val[b][v], n))) return rc;
+            if (((c.nullable_cols >> v) & 1u) && (rc = dalloc(&h->d_nul[b][v], n))) return rc;
+        }
     }
     return FW_OK;
+}
+
+// pinned, device-mapped result buffers of fw_results_async
+int alloc_async_results(fw_handle* h) {
+    if (h->ar_n[0]) return FW_OK;
+    const size_t n = (size_t)h->out_cap;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    for (int b = 0; b < 2; b++) {
+        HIP_TRY(hipHostMalloc((void**)&h->ar_key[b], n * 8, fl));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_ws[b], n * 8, fl));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_we[b], n * 8, fl));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_null[b], n * 4, fl));
+        for (int g = 0; g < h->n_out; g++) HIP_TRY(hipHostMalloc((void**)&h->ar_val[b][g], n * 8, fl));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_n[b], 8, fl));
+        HIP_TRY(hipEventCreateWithFlags(&h->ar_ev[b], hipEventDisableTiming));
+    }
+    return FW_OK;
+}
+
+template <typename T>
+T* mapped(T* host) {
+    void* d = nullptr;
+    return hipHostGetDevicePointer(&d, (void*)host, 0) == hipSuccess ? (T*)d : nullptr;
 }
 
 int read_ctrl(fw_handle* h, Ctrl* out) {
@@ -700,6 +766,7 @@ WinDesc device_win(const fw_handle* h) {
 
 MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     MergeArgs a{};
+    a.ks = h->ks;
     a.ctrl = h->ctrl;
     a.tickets = h->tickets;
     a.parts = h->parts;
@@ -740,6 +807,10 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.merge_seq = h->merge_seq;
     a.ordev = h->ordev;
     a.ordev_cap = h->ordev_cap;
+    a.slot_base = h->slot_base;
+    a.ranks = h->ranks;
+    a.ch_log2 = 0;
+    while ((1ll << a.ch_log2) < h->chunk_rows) a.ch_log2++;
     return a;
 }
 
@@ -832,6 +903,11 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.global = h->cfg.agg_phase == FW_PHASE_GLOBAL;
         a.ablate = h->ablate;
         a.kt = h->kt_device ? h->kt_dev + FW_KT_REDUCE * KT_WORDS : nullptr;
+        a.narrow = h->narrow;
+        a.rank_lim = std::min<int64_t>(PF_MAX_RANK + 1, ((1ll << 31) - 1) / std::max<int64_t>(h->win.interval, 1)) *
+                     h->win.interval;
+        a.slot_base = h->slot_base;
+        a.ranks = h->ranks;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
         h->pushes_total++;
@@ -915,6 +991,8 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->parts);
     hipFree(h->cells);
     hipFree(h->slot_nch);
+    hipFree(h->slot_base);
+    hipFree(h->ranks);
     hipFree(h->treq);
     if (h->mirror) hipHostFree((void*)h->mirror);
     hipFree(h->lfire);
@@ -926,8 +1004,6 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->kr.free_list);
     hipFree(h->d_kid);
     hipFree(h->d_khash);
-    hipFree(h->d_kro);
-    hipFree(h->d_krb);
     hipFree(h->res_kr_len);
     hipFree(h->res_kr_img);
     for (int b = 0; b < 2; b++) {
@@ -964,14 +1040,25 @@ int fw_destroy(fw_handle* h) {
             hipHostFree(h->h_nul[b][v]);
         }
         if (h->stage_ev[b]) hipEventDestroy(h->stage_ev[b]);
+        if (h->dstage_free[b]) hipEventDestroy(h->dstage_free[b]);
+        hipFree(h->d_kro[b]);
+        hipFree(h->d_krb[b]);
+        hipFree(h->d_key[b]);
+        hipFree(h->d_ts[b]);
+        hipFree(h->d_kh[b]);
+        for (int v = 0; v < FW_MAX_COLS; v++) {
+            hipFree(h->d_val[b][v]);
+            hipFree(h->d_nul[b][v]);
+        }
+        hipHostFree(h->ar_key[b]);
+        hipHostFree(h->ar_ws[b]);
+        hipHostFree(h->ar_we[b]);
+        hipHostFree(h->ar_null[b]);
+        for (int g = 0; g < FW_MAX_AGGS; g++) hipHostFree(h->ar_val[b][g]);
+        hipHostFree(h->ar_n[b]);
+        if (h->ar_ev[b]) hipEventDestroy(h->ar_ev[b]);
     }
-    hipFree(h->d_key);
-    hipFree(h->d_ts);
-    hipFree(h->d_kh);
-    for (int v = 0; v < FW_MAX_COLS; v++) {
-        hipFree(h->d_val[v]);
-        hipFree(h->d_nul[v]);
-    }
+    if (h->cstream) hipStreamDestroy(h->cstream);
     delete h->timer;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -1026,35 +1113,43 @@ int fw_commit(fw_handle* h, int64_t n) {
     const int b = h->stage_cur;
     h->stage_cur ^= 1;
     if (n == 0) return FW_OK;
-    // device staging is reused across commits; ingest of the previous commit is ordered before
-    // these copies on the same stream
     int64_t krb_n = 0;
     if (h->keyrow) {
         krb_n = h->h_kro[b][n];
         if (h->h_kro[b][0] != 0 || krb_n < 0 || krb_n > h->krb_cap)
             return fail(FW_E_INVALID, "key row offsets must start at 0 and end within key_row_bytes_cap");
-        HIP_TRY(hipMemcpyAsync(h->d_kro, h->h_kro[b], (n + 1) * 8, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(hipMemcpyAsync(h->d_krb, h->h_krb[b], (size_t)krb_n, hipMemcpyHostToDevice, h->stream));
-    } else {
-        HIP_TRY(hipMemcpyAsync(h->d_key, h->h_key[b], n * 8, hipMemcpyHostToDevice, h->stream));
     }
-    HIP_TRY(hipMemcpyAsync(h->d_ts, h->h_ts[b], n * 8, hipMemcpyHostToDevice, h->stream));
+    // H2D on the copy stream into device buffer b, once the ingest that last read it has run; the
+    // operator stream waits for the copies.  The previous batch's ingest and merge overlap them.
+    hipStream_t cs = h->cstream;
+    HIP_TRY(hipStreamWaitEvent(cs, h->dstage_free[b], 0));
+    if (h->keyrow) {
+        HIP_TRY(hipMemcpyAsync(h->d_kro[b], h->h_kro[b], (n + 1) * 8, hipMemcpyHostToDevice, cs));
+        HIP_TRY(hipMemcpyAsync(h->d_krb[b], h->h_krb[b], (size_t)krb_n, hipMemcpyHostToDevice, cs));
+    } else {
+        HIP_TRY(hipMemcpyAsync(h->d_key[b], h->h_key[b], n * 8, hipMemcpyHostToDevice, cs));
+    }
+    HIP_TRY(hipMemcpyAsync(h->d_ts[b], h->h_ts[b], n * 8, hipMemcpyHostToDevice, cs));
     if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED)
-        HIP_TRY(hipMemcpyAsync(h->d_kh, h->h_kh[b], n * 4, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->d_kh[b], h->h_kh[b], n * 4, hipMemcpyHostToDevice, cs));
     for (int s = 0; s < h->nv; s++) {
         const int v = h->slot_col[s];
-        HIP_TRY(hipMemcpyAsync(h->d_val[v], h->h_val[b][v], n * 8, hipMemcpyHostToDevice, h->stream));
-        if (h->d_nul[v]) HIP_TRY(hipMemcpyAsync(h->d_nul[v], h->h_nul[b][v], n, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->d_val[b][v], h->h_val[b][v], n * 8, hipMemcpyHostToDevice, cs));
+        if (h->d_nul[b][v]) HIP_TRY(hipMemcpyAsync(h->d_nul[b][v], h->h_nul[b][v], n, hipMemcpyHostToDevice, cs));
     }
-    HIP_TRY(hipEventRecord(h->stage_ev[b], h->stream));
+    HIP_TRY(hipEventRecord(h->stage_ev[b], cs));
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->stage_ev[b], 0));
     const void* vals[FW_MAX_COLS];
     const uint8_t* nuls[FW_MAX_COLS];
     for (int v = 0; v < FW_MAX_COLS; v++) {
-        vals[v] = h->d_val[v];
-        nuls[v] = h->d_nul[v];
+        vals[v] = h->d_val[b][v];
+        nuls[v] = h->d_nul[b][v];
     }
-    if (h->keyrow) return push_key_rows(h, n, h->d_kro, h->d_krb, h->d_ts, vals, nuls);
-    return push(h, n, h->d_key, h->d_ts, h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED ? h->d_kh : nullptr, vals, nuls);
+    const int rc = h->keyrow ? push_key_rows(h, n, h->d_kro[b], h->d_krb[b], h->d_ts[b], vals, nuls)
+                             : push(h, n, h->d_key[b], h->d_ts[b],
+                                    h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED ? h->d_kh[b] : nullptr, vals, nuls);
+    HIP_TRY(hipEventRecord(h->dstage_free[b], h->stream));
+    return rc;
 }
 
 int fw_push_device_key_rows(fw_handle* h, int64_t n, const int64_t* d_key_row_offsets, const uint8_t* d_key_row_bytes,
@@ -1242,6 +1337,68 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     return FW_OK;
 }
 
+int fw_results_async(fw_handle* h) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    if (h->keyrow) return fail(FW_E_INVALID, "key-row operators return their rows through fw_results");
+    int rc = alloc_async_results(h);
+    if (rc) return rc;
+    const int b = h->ar_cur;
+    h->ar_cur ^= 1;
+    h->ar_last = b;
+    h->ar_empty[b] = h->reset_pending;  // consumed and nothing emitted since
+    if (h->ar_empty[b]) return FW_OK;
+    CompactArgs ca{};
+    ca.ctrl = h->ctrl;
+    ca.sb_out = h->sb_out;
+    ca.off = h->coff;
+    ca.n_sb = h->ks.n_sb;
+    ca.n_aggs = h->n_out;
+    ca.slab_cap = h->slab_cap;
+    ca.out_key = h->out_key;
+    ca.out_ws = h->out_ws;
+    ca.out_we = h->out_we;
+    ca.out_null = h->out_null;
+    for (int g = 0; g < h->n_out; g++) {
+        ca.out_val[g] = h->out_val[g];
+        ca.res_val[g] = mapped(h->ar_val[b][g]);
+    }
+    ca.res_key = mapped(h->ar_key[b]);
+    ca.res_ws = mapped(h->ar_ws[b]);
+    ca.res_we = mapped(h->ar_we[b]);
+    ca.res_null = mapped(h->ar_null[b]);
+    ca.res_cap = h->out_cap;
+    ca.host_n = mapped(h->ar_n[b]);
+    if (!ca.res_key || !ca.res_ws || !ca.res_we || !ca.res_null || !ca.host_n)
+        return fail(FW_E_DEVICE, "mapped result buffers unavailable");
+    HIP_TRY(launch_compact(ca, h->stream, h->timer));
+    HIP_TRY(hipEventRecord(h->ar_ev[b], h->stream));
+    h->reset_pending = true;  // the rows are collected: the next merge launch starts the slabs afresh
+    return FW_OK;
+}
+
+int fw_results_ready(fw_handle* h, fw_result* out) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    memset(out, 0, sizeof *out);
+    const int b = h->ar_last;
+    if (b < 0) return fail(FW_E_STATE, "fw_results_ready without fw_results_async");
+    if (h->ar_empty[b]) return FW_OK;
+    HIP_TRY(hipEventSynchronize(h->ar_ev[b]));
+    const int64_t n = __atomic_load_n(h->ar_n[b], __ATOMIC_ACQUIRE);
+    if (n > h->out_cap)
+        return fail(FW_E_CAPACITY, "%lld result rows exceed output_capacity %lld (read results more often)",
+                    (long long)n, (long long)h->out_cap);
+    const int na = h->n_out;
+    const int nv = h->ad.first_word >= 0 ? na - 1 : na;
+    out->n = n;
+    out->key = h->ar_key[b];
+    out->window_start = h->ar_ws[b];
+    out->window_end = h->ar_we[b];
+    for (int g = 0; g < nv; g++) out->values[g] = (int64_t*)h->ar_val[b][g];
+    if (nv < na) out->first_ord = (int64_t*)h->ar_val[b][nv];
+    out->null_mask = h->ar_null[b];
+    return FW_OK;
+}
+
 int fw_first_element_events(fw_handle* h, fw_ordinal_events* out) {
     if (!h || !out) return fail(FW_E_INVALID, "null argument");
     memset(out, 0, sizeof *out);
@@ -1340,6 +1497,9 @@ int fw_get_stats(fw_handle* h, fw_stats* out) {
     out->flush_launches = (int64_t)c.flush_launches;
     out->partials_merged = (int64_t)c.parts_merged;
     out->state_entries_moved = (int64_t)c.state_moved;
+    out->partial_bytes_written = (int64_t)c.part_bytes;
+    out->partial_bytes_merged = (int64_t)c.part_bytes_merged;
+    out->compact_chunks = (int64_t)c.compact_chunks;
     out->key_rows = h->keyrow ? c.kr_next_id - std::max<int64_t>(0, c.kr_free_count - std::min(c.kr_free_cursor, c.kr_free_count)) : 0;
     out->key_row_collections = c.kr_collections;
     return FW_OK;

@@ -66,8 +66,11 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     int64_t* s_min = (int64_t*)&lds[0];
     unsigned long long* s_drop = (unsigned long long*)&lds[1];
     unsigned long long* s_rows = (unsigned long long*)&lds[2];
+    uint32_t* s_folded = (uint32_t*)&lds[3] + 1;  // a row of the chunk was folded into another
     uint32_t* wsum = (uint32_t*)&lds[4];  // IG_BLOCK / 64 words
-    const int n_sb = a.ks.n_sb;
+    const int PL = a.ks.pass_log2;
+    const int n_sb = a.ks.n_sb >> PL;  // ingest superbuckets: the histogram and the cells
+    const int n_units = a.ks.n_sb;     // state superbuckets (route_key's result)
     uint32_t* hist = (uint32_t*)(lds + IG_HDR_WORDS);  // partials per superbucket -> cell start
     uint64_t* area = lds + IG_HDR_WORDS + ig_hist_words(n_sb);
     const int area_words = (a.lds_bytes >> 3) - IG_HDR_WORDS - ig_hist_words(n_sb);
@@ -96,6 +99,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         *s_min = INT64_MAX;
         *s_drop = 0;
         *s_rows = 0;
+        *s_folded = 0;
     }
     for (int s = tid; s < n_sb; s += IG_BLOCK) hist[s] = 0;
 
@@ -183,6 +187,10 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     // per-row divergent branches of the general path cost as many scalar instructions as the
     // vector work itself.
     const bool simple = fast && !a.win.ds && !a.global && a.win.tz.n == 0;
+    // compact partial rows (PF_NARROW / PF_UNIT) count slices from the push's rank base: the first
+    // slice end that is not fired at the current watermark (every row that is not late ends at or
+    // after it); the merge kernel reads it from slot_base
+    const bool nar = a.narrow && simple && cur_wm != INT64_MIN;
     uint32_t slow = simple ? 0u : valid;
     // record words: the word op is uniform, so it is resolved once per launch into a mode and
     // the rows only select (no per-row switch over the op)
@@ -233,7 +241,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         const uint32_t r = d32 - udiv32(d32, a.win.slice_div32) * (uint32_t)a.win.interval;
         const int64_t se = rs[j] - (int64_t)r + a.win.interval;
         const bool live = (valid >> j) & 1u;
-        const bool ok = live && d < (1ull << 31) && (uint32_t)sb < (uint32_t)n_sb && (a.local || cur_wm < se - 1);
+        const bool ok = live && d < (1ull << 31) && (uint32_t)sb < (uint32_t)n_units && (a.local || cur_wm < se - 1);
         slow |= (uint32_t)(live && !ok) << j;
         rs[j] = ok ? se : rs[j];
         lmin = ok ? min(lmin, se) : lmin;
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     if (__ballot(slow != 0)) static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
         if (!((slow >> j) & 1u)) return;
-        if ((uint32_t)rsb[j] >= (uint32_t)n_sb) {  // key group not owned by this subtask
+        if ((uint32_t)rsb[j] >= (uint32_t)n_units) {  // key group not owned by this subtask
             __hip_atomic_fetch_or(&ctrl->error, ERR_KEYGROUP, __ATOMIC_RELAXED, DEV_SCOPE);
             valid &= ~(1u << j);
             return;
@@ -344,6 +352,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         lmin = min(lmin, target);
         lrows++;
     });
+    // a row left valid by the general path keeps its slice end in its partial row (PF_WIDE chunk)
+    const bool wide_row = (slow & valid) != 0;
+    __syncthreads();  // the header and histogram are initialised
     // ---- K3: fold equal (key, slice) rows, one 1024-row sub-tile at a time
     if (fold && !(FW_ABL(a) & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
         constexpr int s = decltype(S)::value;
@@ -378,6 +389,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                 for (int w = 0; w < NW; w++)
                     if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w * SL + h], racc[j][w]);
                 valid &= ~(1u << j);
+                *s_folded = 1u;
             }
         });
         __syncthreads();
@@ -394,9 +406,20 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     const bool sort = !(FW_ABL(a) & AB_NO_SORT);
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        rdst[j] = (sort && (valid & (1u << j))) ? atomicAdd(&hist[rsb[j]], 1u) : (uint32_t)(j * IG_BLOCK + tid);
+        rdst[j] = (sort && (valid & (1u << j))) ? atomicAdd(&hist[rsb[j] >> PL], 1u) : (uint32_t)(j * IG_BLOCK + tid);
     });
     __syncthreads();
+    // ---- the chunk's partial-row format (PF_*): compact unless a row kept its own slice end or
+    // the chunk's slice ends spread over more than rank_lim slices
+    bool wide = wide_row || !nar;
+    // (re-read here rather than kept live through the fold: the watermark does not change during a push)
+    const int64_t nbase = nar ? slice_end_of(a.win, wadd(__hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE), 1)) : 0;
+    if (!wide)
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if ((valid & (1u << j)) && (uint64_t)(rs[j] - nbase) >= (uint64_t)a.rank_lim) wide = true;
+        });
+    wide = __syncthreads_or(wide);
     uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch;
     const int per = (n_sb + IG_BLOCK - 1) / IG_BLOCK;
     const int sb0 = min(tid * per, n_sb), sb1 = min(sb0 + per, n_sb);
@@ -405,24 +428,39 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     uint32_t total;
     const uint32_t incl = block_incl_scan<IG_BLOCK>(seg, wsum, &total);
     uint32_t run = incl - seg;
+    // COUNT(*) alone and nothing folded in this chunk: every row counts 1
+    const uint32_t fmt = (wide || !sort) ? PF_WIDE
+                         : (!X && a.narrow == 2 && !*s_folded) ? PF_UNIT
+                                                                                        : PF_NARROW;
     if (sort)
         for (int i = sb0; i < sb1; i++) {
             const uint32_t v = hist[i];
             hist[i] = run;
-            cells[cell_index(c, n_sb, i)] = run | (v << 16);
+            cells[cell_index(c, n_sb, i)] = run | (v << 16) | (fmt << 30);
             run += v;
         }
+    if (fmt != PF_WIDE)  // compact rows keep their rank instead of their slice end
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            rs[j] = (int64_t)udiv32((uint32_t)(rs[j] - nbase), a.win.slice_div32);
+        });
     __syncthreads();
     if (sort)
         static_for<RPT>([&](auto J) {
             constexpr int j = decltype(J)::value;
-            if (valid & (1u << j)) rdst[j] += hist[rsb[j]];
+            if (valid & (1u << j)) rdst[j] += hist[rsb[j] >> PL];
         });
     else
         total = CH;
-    // ---- store the partials through an LDS stage so every global store is a full line
+    // ---- store the partials through an LDS stage so every global store is a full line.  The
+    // chunk's region keeps its PF_WIDE size; a compact format fills its front, and its rank bytes
+    // are staged behind the rows and stored to the side array.
+    const int PWX = pf_stride(fmt, NW);
+    const int aoff = fmt == PF_WIDE ? 2 : 1;  // first accumulator word of a row
     uint64_t* out = a.parts + ((size_t)slot * a.cap_rows + (size_t)base) * PW;
-    const uint32_t wrows = (uint32_t)(area_words / PW) & ~1u;
+    const uint32_t wrows = fmt == PF_WIDE ? (uint32_t)(area_words / PW) & ~15u
+                                          : (uint32_t)((int64_t)area_words * 8 / (8 * PWX + 1)) & ~15u;
+    uint8_t* rstage = (uint8_t*)(area + (size_t)wrows * PWX);
     if (!(FW_ABL(a) & AB_NO_STORE))
         for (uint32_t w0 = 0; w0 < total; w0 += wrows) {
             __syncthreads();  // fold table / previous window no longer read
@@ -430,20 +468,33 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                 constexpr int j = decltype(J)::value;
                 const uint32_t d = rdst[j] - w0;
                 if (!(valid & (1u << j)) || d >= wrows) return;
-                uint64_t* p = area + (size_t)d * PW;
+                uint64_t* p = area + (size_t)d * PWX;
                 p[0] = (uint64_t)rk[j];
-                p[1] = (uint64_t)rs[j];
+                if (fmt == PF_WIDE) p[1] = (uint64_t)rs[j];
+                else rstage[d] = (uint8_t)rs[j];  // the rank (set below the format decision)
+                if (fmt != PF_UNIT)
 #pragma unroll
-                for (int w = 0; w < NW; w++) p[2 + w] = racc[j][w];
+                    for (int w = 0; w < NW; w++) p[aoff + w] = racc[j][w];
             });
             __syncthreads();
-            const uint32_t nwords = min(wrows, total - w0) * PW;
-            uint64_t* dst = out + (size_t)w0 * PW;  // 16-B aligned: slot, chunk and window bases are even rows
+            const uint32_t nr = min(wrows, total - w0);
+            const uint32_t nwords = nr * PWX;
+            uint64_t* dst = out + (size_t)w0 * PWX;  // 16-B aligned: slot, chunk and window bases are 16-row multiples
             for (uint32_t q = 2 * tid; q < nwords; q += 2 * IG_BLOCK) {
                 if (q + 1 < nwords) {
                     *(ulonglong2*)(dst + q) = *(const ulonglong2*)(area + q);
                 } else {
                     dst[q] = area[q];
+                }
+            }
+            if (fmt != PF_WIDE) {
+                uint8_t* rd = a.ranks + (size_t)slot * a.cap_rows + (size_t)base + w0;  // 16-B aligned
+                for (uint32_t q = 16 * tid; q < nr; q += 16 * IG_BLOCK) {
+                    if (q + 16 <= nr) {
+                        *(uint4*)(rd + q) = *(const uint4*)(rstage + q);
+                    } else {
+                        for (uint32_t b = q; b < nr; b++) rd[b] = rstage[b];
+                    }
                 }
             }
         }
@@ -457,21 +508,26 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     __syncthreads();
     int32_t* s_last = (int32_t*)&lds[3];
     if (tid == 0) {
-        __hip_atomic_store(&a.chunk_stats[4 * c], *s_min, __ATOMIC_RELAXED, DEV_SCOPE);
-        __hip_atomic_store(&a.chunk_stats[4 * c + 1], (int64_t)*s_drop, __ATOMIC_RELAXED, DEV_SCOPE);
-        __hip_atomic_store(&a.chunk_stats[4 * c + 2], (int64_t)*s_rows, __ATOMIC_RELAXED, DEV_SCOPE);
-        __hip_atomic_store(&a.chunk_stats[4 * c + 3], (int64_t)total, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[CS_WORDS * c], *s_min, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[CS_WORDS * c + 1], (int64_t)*s_drop, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[CS_WORDS * c + 2], (int64_t)*s_rows, __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_store(&a.chunk_stats[CS_WORDS * c + 3], (int64_t)total, __ATOMIC_RELAXED, DEV_SCOPE);
+        // bytes of partial rows (+ rank bytes) this chunk wrote, and whether they are compact
+        __hip_atomic_store(&a.chunk_stats[CS_WORDS * c + 4],
+                           (int64_t)total * (8 * PWX + (fmt != PF_WIDE ? 1 : 0)) | ((int64_t)(fmt != PF_WIDE) << 40),
+                           __ATOMIC_RELAXED, DEV_SCOPE);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         *s_last = grid_last_wg(a.tickets->c[0]);
     }
     __syncthreads();
     if (!*s_last) return;
-    int64_t m = INT64_MAX, d = 0, r = 0, q = 0;
+    int64_t m = INT64_MAX, d = 0, r = 0, q = 0, y = 0;
     for (int64_t i = tid; i < (int64_t)gridDim.x; i += IG_BLOCK) {
-        m = min(m, __hip_atomic_load(&a.chunk_stats[4 * i], __ATOMIC_RELAXED, DEV_SCOPE));
-        d += __hip_atomic_load(&a.chunk_stats[4 * i + 1], __ATOMIC_RELAXED, DEV_SCOPE);
-        r += __hip_atomic_load(&a.chunk_stats[4 * i + 2], __ATOMIC_RELAXED, DEV_SCOPE);
-        q += __hip_atomic_load(&a.chunk_stats[4 * i + 3], __ATOMIC_RELAXED, DEV_SCOPE);
+        m = min(m, __hip_atomic_load(&a.chunk_stats[CS_WORDS * i], __ATOMIC_RELAXED, DEV_SCOPE));
+        d += __hip_atomic_load(&a.chunk_stats[CS_WORDS * i + 1], __ATOMIC_RELAXED, DEV_SCOPE);
+        r += __hip_atomic_load(&a.chunk_stats[CS_WORDS * i + 2], __ATOMIC_RELAXED, DEV_SCOPE);
+        q += __hip_atomic_load(&a.chunk_stats[CS_WORDS * i + 3], __ATOMIC_RELAXED, DEV_SCOPE);
+        y += __hip_atomic_load(&a.chunk_stats[CS_WORDS * i + 4], __ATOMIC_RELAXED, DEV_SCOPE);  // no carry: < 2^40 per chunk
     }
     m = wave_min_i64(m);
 #pragma unroll
@@ -479,14 +535,16 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         d += (int64_t)__shfl_xor((long long)d, k, 64);
         r += (int64_t)__shfl_xor((long long)r, k, 64);
         q += (int64_t)__shfl_xor((long long)q, k, 64);
+        y += (int64_t)__shfl_xor((long long)y, k, 64);
     }
-    int64_t* red = (int64_t*)area;  // [4][IG_BLOCK / 64]
+    int64_t* red = (int64_t*)area;  // [5][IG_BLOCK / 64]
     constexpr int NWV = IG_BLOCK / 64;
     if ((tid & 63) == 0) {
         red[tid >> 6] = m;
         red[NWV + (tid >> 6)] = d;
         red[2 * NWV + (tid >> 6)] = r;
         red[3 * NWV + (tid >> 6)] = q;
+        red[4 * NWV + (tid >> 6)] = y;
     }
     __syncthreads();
     if (tid == 0) {
@@ -495,12 +553,16 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             d += red[NWV + v];
             r += red[2 * NWV + v];
             q += red[3 * NWV + v];
+            y += red[4 * NWV + v];
         }
         a.slot_nch[slot] = (int32_t)gridDim.x;
+        a.slot_base[slot] = slice_end_of(a.win, wadd(cur_wm, 1));  // used by compact chunks only
         ctrl->pending_pushes = slot + 1;
         ctrl->min_pending = min(ctrl->min_pending, m);
         ctrl->pending_rows += (uint64_t)r;
         ctrl->partials += (uint64_t)q;
+        ctrl->part_bytes += (uint64_t)(y & ((1ll << 40) - 1));
+        ctrl->compact_chunks += (uint64_t)(y >> 40);
         if (fold) ctrl->fold_skip = q * 50 > r * 49;  // folded away fewer than 2 % of the rows
         ctrl->push_count += 1;
         ctrl->late_dropped += (uint64_t)d;
@@ -522,7 +584,8 @@ static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
         attr_set = true;
     }
     // the fold table and the histogram must fit the dynamic LDS
-    if ((int64_t)(IG_HDR_WORDS + ig_hist_words(a.ks.n_sb)) * 8 + ig_fold_bytes(NW) > a.lds_bytes) return hipErrorInvalidValue;
+    if ((int64_t)(IG_HDR_WORDS + ig_hist_words(a.ks.n_sb >> a.ks.pass_log2)) * 8 + ig_fold_bytes(NW) > a.lds_bytes)
+        return hipErrorInvalidValue;
     kt_mark(t, FW_KT_REDUCE, false, s);
     if (a.lds_bytes != ig_lds(BLK)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_ingest<NV, NW, RPT, X, BLK>), dim3((unsigned)nch), dim3(BLK), a.lds_bytes, s, a);

@@ -25,6 +25,7 @@ constexpr int IG_SRPT = 2;                      // rows per thread per fold sub-
 constexpr int IG_SUB = IG_BLOCK * IG_SRPT;      // rows per fold sub-tile (1024)
 constexpr int IG_LDS = 78 * 1024;               // dynamic LDS per workgroup: histogram + fold/stage area
 constexpr int IG_MAX_SB = 8192;                 // superbuckets the ingest histogram holds (32 KiB)
+constexpr int MAX_PASS_LOG2 = 3;                // state superbuckets per ingest superbucket, log2 (KeySpace)
 constexpr int IG_HDR_WORDS = 16;                // 8-B words of per-chunk counters at the LDS base
 constexpr int ig_hist_words(int n_sb) { return ((n_sb + 3) >> 2) << 1; }  // 16-B multiple
 // rows per thread by accumulator words and loaded value columns (template NV): the chunk's rows
@@ -78,6 +79,21 @@ __host__ __device__ inline int64_t cell_chunk(int64_t f) {
     const int64_t tile = f >> 4;
     return (tile >> 3) * 128 + (tile & 7) + 8 * (f & 15);
 }
+
+// Partial-row formats, one per (push slot, chunk); a cell word is start | count << 16 | format << 30
+// (chunks hold <= 4096 rows).  A chunk whose rows all took the ingest kernel's common path (UTC SQL
+// slice ends on the slice grid, within PF_MAX_RANK slices of the push's rank base) leaves the slice
+// end out of its rows: it is slot_base + rank * interval, with the rank byte in a side array.  A
+// COUNT(*)-only layout whose chunk folded nothing also leaves out the count (every row counts 1).
+constexpr uint32_t PF_WIDE = 0;    // (key, sliceEnd, acc[nw])
+constexpr uint32_t PF_NARROW = 1;  // (key, acc[nw]) + rank byte
+constexpr uint32_t PF_UNIT = 2;    // (key) + rank byte; acc = 1
+constexpr int64_t PF_MAX_RANK = 255;
+__host__ __device__ inline uint32_t cell_count(uint32_t v) { return (v >> 16) & 0x3FFFu; }
+__host__ __device__ inline uint32_t cell_start(uint32_t v) { return v & 0xFFFFu; }
+__host__ __device__ inline uint32_t cell_fmt(uint32_t v) { return v >> 30; }
+// words per row of a format
+__host__ __device__ inline int pf_stride(uint32_t fmt, int nw) { return fmt == PF_WIDE ? 2 + nw : fmt == PF_NARROW ? 1 + nw : 1; }
 
 // Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words, except SQL
 // MIN/MAX(DOUBLE), whose strict-comparison-in-arrival-order semantics need a small word group.
@@ -204,6 +220,9 @@ struct Ctrl {
     int64_t n_ordev;         // DataStream first-element retain / release events since the last read
     uint64_t flush_launches; // merge launches that flushed pending partials (cumulative)
     uint64_t parts_merged;   // partial rows those flushes read (cumulative)
+    uint64_t part_bytes;     // bytes of partial rows (and rank bytes) the ingest kernels wrote (cumulative)
+    uint64_t part_bytes_merged;  // of those, the bytes flushes read (cumulative)
+    uint64_t compact_chunks; // chunks written in a compact partial-row format (cumulative)
     uint64_t state_moved;    // state entries the merge launches loaded + wrote back (cumulative)
     // FW_KEYHASH_KEYROW: the key-row intern table's allocator (KeyRowTable)
     int64_t kr_next_id;      // ids handed out fresh so far (ids < kr_next_id exist)
@@ -286,6 +305,10 @@ FW_HD int64_t merge_target_of(const WinDesc& w, int64_t se) {
     return se;
 }
 
+// Superbuckets are the unit of state: each is one merge workgroup's LDS table.  The ingest kernel
+// partitions its partials by ingest superbucket = superbucket >> pass_log2 (its LDS histogram holds
+// IG_MAX_SB of them), so beyond IG_MAX_SB superbuckets the 2^pass_log2 superbuckets of one ingest
+// superbucket share its partial rows and each merge pass keeps the rows that route to its own.
 struct KeySpace {
     int32_t hash_kind;
     int32_t max_p;
@@ -294,6 +317,8 @@ struct KeySpace {
     int32_t sb_per_kg_log2;
     int32_t n_sb;          // superbuckets = n_kg << sb_per_kg_log2
     UDiv32 maxp_div;       // divisor max_p
+    int32_t pass_log2;     // superbuckets per ingest superbucket (log2); 0 unless n_sb > IG_MAX_SB
+    int32_t pad;
 };
 
 // Routing of one key: m = MathUtils.murmurHash(key.hashCode()) (>= 0), key group = m % maxP
@@ -377,6 +402,7 @@ struct AggDesc {
     int32_t first_word;       // DataStream: the W_FIRST word (-1: the first element is not tracked)
 };
 
+constexpr int CS_WORDS = 8;  // IngestArgs::chunk_stats words per chunk
 struct IngestArgs {
     const int64_t* key;
     const int64_t* ts;
@@ -396,7 +422,8 @@ struct IngestArgs {
                            // of each (superbucket, chunk) cell inside the chunk's region
     int32_t* slot_nch;     // [FW_MAX_PENDING] chunks of each pending push
     int64_t max_nch;       // cell_pad(chunks per slot): cells per superbucket per slot
-    int64_t* chunk_stats;  // [n_chunks][4]: min target slice, dropped rows, accepted rows, partials
+    int64_t* chunk_stats;  // [n_chunks][CS_WORDS]: min target slice, dropped rows, accepted rows, partials,
+                           // partial bytes | compact << 40
     Tickets* tickets;
     int64_t n_chunks;
     int64_t* treq;         // timer requests: (key, window, sb) triples
@@ -420,6 +447,11 @@ struct IngestArgs {
     unsigned long long* kt;  // launch timing (fw_set_profiling FW_PROF_DEVICE): KtSlot of this kernel class
     int64_t stride;        // words between consecutive rows of a key / ts / value column (1: plain
                            // columns; 2 + value columns: the packed rows of fw_push_device_packed_segments)
+    // compact partial rows (PF_*): 0 always PF_WIDE, 1 PF_NARROW allowed, 2 PF_UNIT too (COUNT(*) only)
+    int32_t narrow;
+    int64_t rank_lim;      // span of the ranks in ms: min(PF_MAX_RANK + 1, (2^31 - 1) / interval) * interval
+    int64_t* slot_base;    // [FW_MAX_PENDING]: rank base of each push (its last workgroup writes it)
+    uint8_t* ranks;        // [FW_MAX_PENDING][cap_rows]: rank byte of each narrow row
 };
 // Development ablations and phase stamps (FW_ABLATE) are compiled into the kernels only in a
 // diagnostic build (make DIAG=1): in the production build their checks fold away, so the hot loops
@@ -444,6 +476,7 @@ constexpr int AB_FSTAMPS = 8192;    // merge: per-lane cycles of fire_one's part
 constexpr int N_STAMPS = 16;
 
 struct MergeArgs {
+    KeySpace ks;             // routing of a partial row's key (ks.pass_log2 > 0: rows of other superbuckets are skipped)
     Ctrl* ctrl;
     Tickets* tickets;
     const uint64_t* parts;
@@ -489,6 +522,9 @@ struct MergeArgs {
     // window's first element), for the host shim that keeps those records (value1 of the reduce)
     int64_t* ordev;
     int64_t ordev_cap;
+    const int64_t* slot_base;   // compact partial rows (IngestArgs)
+    const uint8_t* ranks;
+    int32_t ch_log2;            // log2(chunk_rows)
 };
 constexpr int64_t ORDEV_RELEASE = (int64_t)1 << 62;
 constexpr int LFW = 3 + MAX_WORDS;  // words per late-fire row
@@ -512,6 +548,7 @@ struct CompactArgs {
     uint64_t* res_val[FW_MAX_AGGS];
     uint32_t* res_null;
     int64_t res_cap;
+    int64_t* host_n;         // fw_results_async: also store the row count here (mapped host memory)
 };
 
 // In-kernel launch timing (fw_set_profiling FW_PROF_DEVICE): per kernel class 4 words -- the

@@ -41,7 +41,7 @@ extern template hipError_t merge_nw<8>(const MergeArgs&, hipStream_t);
 
 // ---- result compaction: slabs (+ overflow) -> one contiguous result set ----------------------
 __global__ __launch_bounds__(BLOCK) void k_compact_scan(const int32_t* sb_out, int32_t n_sb, int64_t* off, Ctrl* ctrl,
-                                                        int64_t out_cap) {
+                                                        int64_t out_cap, int64_t* host_n) {
     __shared__ int64_t tmp[BLOCK];
     __shared__ int64_t carry;
     if (threadIdx.x == 0) carry = 0;
@@ -66,6 +66,8 @@ __global__ __launch_bounds__(BLOCK) void k_compact_scan(const int32_t* sb_out, i
         const int64_t ovf = (int64_t)min(ctrl->out_count[ctrl->ovf_sel & 1], (uint64_t)out_cap);
         off[n_sb] = carry;          // slab rows
         off[n_sb + 1] = carry + ovf;  // total rows
+        if (host_n)  // fw_results_async: the count, next to the rows in mapped host memory (vector store)
+            __hip_atomic_store(host_n, carry + ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -116,6 +118,9 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->n_ordev = 0;
         c->flush_launches = 0;
         c->parts_merged = 0;
+        c->part_bytes = 0;
+        c->part_bytes_merged = 0;
+        c->compact_chunks = 0;
         c->state_moved = 0;
         c->kr_next_id = 0;
         c->kr_free_count = 0;
@@ -128,7 +133,7 @@ __global__ void k_init_ctrl(Ctrl* c) {
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t) {
     kt_mark(t, FW_KT_OTHER, false, s);
-    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(BLOCK), 0, s, a.sb_out, a.n_sb, a.off, a.ctrl, a.res_cap);
+    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(BLOCK), 0, s, a.sb_out, a.n_sb, a.off, a.ctrl, a.res_cap, a.host_n);
     hipLaunchKernelGGL(k_compact_copy, dim3(a.n_sb + 1), dim3(BLOCK), 0, s, a);
     kt_mark(t, FW_KT_OTHER, true, s);
     return hipGetLastError();

@@ -132,7 +132,7 @@ __device__ uint32_t hb_fire_entry(const MergeArgs& a, StateLds<HB_R * NWP, E>& S
     return nf;
 }
 
-template <int NWP, int E, uint32_t OPS>
+template <int NWP, int E, uint32_t OPS, bool PS>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
     constexpr int NA = HB_R * NWP;  // ring words per entry
     constexpr int PW = 2 + NWP;     // partial row words
@@ -191,10 +191,12 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
         }
         __syncthreads();
         if (!s_work) continue;
-        auto cell_at = [&](int64_t pi, int f) -> uint32_t {
+        auto cell_at = [&](int64_t pi, int f) -> uint32_t {  // cells of this superbucket's ingest superbucket
             if (cell_chunk(f) >= a.slot_nch[pi]) return 0u;
-            const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
-            return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
+            const int pl = PS ? a.ks.pass_log2 : 0;
+            const int nis = a.n_sb >> pl;
+            const uint32_t* cl = a.cells + (size_t)pi * nis * a.max_nch;
+            return cl[((size_t)(f >> 4) * nis + (sb >> pl)) * CELL_LANES + (f & 15)];
         };
         const int lane = tid & 63, wv = tid >> 6;
         auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
@@ -234,32 +236,14 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
                 const int ncell = (int)cell_pad(a.slot_nch[pi]);
                 const int G = gather_group(ncell);
                 const int ngroups = ncell / G;
-                const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
                 for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                     const int f = g * G + lane;
                     const uint32_t v = lane >= G ? 0u : (pi == 0 && g == wv) ? v_first : cell_at(pi, f);
-                    const uint32_t cnt = v >> 16;
-                    uint32_t inc = cnt;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
-                        if (lane >= d) inc += t;
-                    }
-                    const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
-                    const uint32_t excl = inc - cnt;
-                    const uint32_t adj = (uint32_t)(cell_chunk(f) * CH + (v & 0xFFFFu)) - excl;
+                    const CellGroup cg = cell_group(v, f, CH);
+                    const uint32_t tot = cg.tot;
                     for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
                         uint64_t row[GU][PW];
-#pragma unroll
-                        for (int u = 0; u < GU; u++) {
-                            const uint32_t x = min(r0 + (uint32_t)(u * 64 + lane), tot - 1);
-                            int lo = 0;
-#pragma unroll
-                            for (int step = 32; step > 0; step >>= 1)
-                                if ((uint32_t)__shfl((int)excl, lo + step, 64) <= x) lo += step;
-                            const uint64_t* p = seg + (size_t)((uint32_t)__shfl((int)adj, lo, 64) + x) * PW;
-                            load_words<PW>(p, row[u]);
-                        }
+                        const uint32_t live = load_group_rows<NWP, GU, PS>(a, pi, cg, r0, sb, row);
                         int ge[GU], slot[GU];
                         {
                             int64_t gk[GU], gb[GU];
@@ -274,7 +258,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
                         }
                         static_for<GU>([&](auto UU) {
                             constexpr int u = decltype(UU)::value;
-                            if (r0 + (uint32_t)(u * 64 + lane) >= tot) return;
+                            if (!((live >> u) & 1u)) return;
                             int e = ge[u];
                             if (e < 0) e = hb_find_or_insert<NWP, E, OPS>(S, (int64_t)row[u][0], (int64_t)row[u][1], a.wd);
                             if (e < 0) return;  // state overflow (flagged)
@@ -354,15 +338,15 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
     merge_ticket(a);
 }
 
-template <int NWP>
+template <int NWP, bool PS>
 static void merge_hopb_launch(const MergeArgs& a, hipStream_t s) {
     constexpr int E = mg_entries(NWP, KIND_HOPB);
     // COUNT(*) alone / COUNT(*) + SUM(BIGINT) with the word ops as constants; the rest at run time
     constexpr uint32_t L = NWP == 1 ? ops_pack({W_SUM_I}) : ops_pack({W_SUM_I, W_SUM_I});
-    if (ops_layout(a.wd) == L)
-        hipLaunchKernelGGL((k_merge_hopb<NWP, E, L>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+    if (!PS && ops_layout(a.wd) == L)
+        hipLaunchKernelGGL((k_merge_hopb<NWP, E, L, false>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
     else
-        hipLaunchKernelGGL((k_merge_hopb<NWP, E, OPS_ANY>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_merge_hopb<NWP, E, OPS_ANY, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
 }
 
 }  // namespace fw

@@ -646,6 +646,7 @@ __device__ void merge_finalize(const MergeArgs& a) {
         c->n_lfire = 0;
         c->flush_launches += 1;
         c->parts_merged = c->partials;  // a flush reads every partial written so far
+        c->part_bytes_merged = c->part_bytes;
     }
     c->n_treq = 0;
     for (int q = 0; q < 8; q++) __hip_atomic_store(&a.tickets->work[q][0], 0u, __ATOMIC_RELAXED, DEV_SCOPE);
@@ -669,7 +670,88 @@ __device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
 // rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
 constexpr int mg_rows_in_flight(int nw) { return nw <= 1 ? 4 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1; }
 
-template <int NW, int E, bool Q, int KIND, uint32_t OPS>
+// ---- the gather's view of the pending partials.  A wave takes a group of up to 64 consecutive
+// cells of one push slot (lane l holds cell word v of flat cell position f), scans their row
+// counts and deals the group's rows over its lanes.
+struct CellGroup {
+    uint32_t tot;       // rows in the group
+    uint32_t excl;      // this lane's cell: rows of the group's cells before it
+    uint32_t adj;       // this lane's cell: slot row index of its first row, less excl (mod 2^32)
+    uint32_t fmt;       // this lane's cell: its chunk's partial-row format (PF_*)
+};
+__device__ __forceinline__ CellGroup cell_group(uint32_t v, int f, int64_t CH) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t cnt = cell_count(v);
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= d) inc += t;
+    }
+    CellGroup g;
+    g.tot = (uint32_t)__shfl((int)inc, 63, 64);
+    g.excl = inc - cnt;
+    g.adj = (uint32_t)(cell_chunk(f) * CH + cell_start(v)) - g.excl;
+    g.fmt = cell_fmt(v);
+    return g;
+}
+// Row r0 + u * 64 + lane of the group (clamped to the last row), in the PF_WIDE layout (key,
+// sliceEnd, acc[NW]) whatever its chunk's format: the compact formats' slice end is the push's rank
+// base + rank * interval, PF_UNIT's count is 1.  Returns the rows to fold (bit u): those inside the
+// group and -- when several superbuckets share the ingest superbucket (ks.pass_log2 > 0) -- routed
+// to superbucket `sb`.
+template <int NW, int GU, bool PS>
+__device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t pi, const CellGroup& g, uint32_t r0,
+                                                    int sb, uint64_t (&row)[GU][2 + NW]) {
+    constexpr int PW = 2 + NW;
+    const int lane = threadIdx.x & 63;
+    const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
+#pragma unroll
+    for (int u = 0; u < GU; u++) {
+        // the group's row x lives in the last cell whose first row is <= x
+        const uint32_t x = min(r0 + (uint32_t)(u * 64 + lane), g.tot - 1);
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+            if ((uint32_t)__shfl((int)g.excl, lo + step, 64) <= x) lo += step;
+        const uint32_t rg = (uint32_t)__shfl((int)g.adj, lo, 64) + x;  // row index in the slot
+        const uint32_t fmt = (uint32_t)__shfl((int)g.fmt, lo, 64);
+        if (fmt == PF_WIDE) {
+            load_words<PW>(seg + (size_t)rg * PW, row[u]);
+        } else {
+            // a compact chunk fills the front of its PF_WIDE-sized region
+            const uint32_t within = rg & ((1u << a.ch_log2) - 1u);
+            const uint64_t* p = seg + (size_t)(rg - within) * PW;
+            const uint32_t rank = a.ranks[(size_t)pi * a.cap_rows + rg];
+            // slot_base + rank * interval: 32-bit product (rank * interval < 2^31, IngestArgs::rank_lim)
+            row[u][1] = (uint64_t)(a.slot_base[pi] + (int64_t)(rank * (uint32_t)a.win.interval));
+            if (fmt == PF_NARROW) {
+                uint64_t t[1 + NW];
+                load_words<1 + NW>(p + (size_t)within * (1 + NW), t);
+                row[u][0] = t[0];
+#pragma unroll
+                for (int w = 0; w < NW; w++) row[u][2 + w] = t[1 + w];
+            } else {  // PF_UNIT: COUNT(*) alone, nothing folded
+                row[u][0] = p[within];
+#pragma unroll
+                for (int w = 0; w < NW; w++) row[u][2 + w] = w == 0 ? 1ull : 0ull;
+            }
+        }
+    }
+    uint32_t live = 0;
+#pragma unroll
+    for (int u = 0; u < GU; u++) live |= (uint32_t)(r0 + (uint32_t)(u * 64 + lane) < g.tot) << u;
+    if constexpr (PS)
+#pragma unroll
+        for (int u = 0; u < GU; u++) {
+            uint32_t m;
+            if ((live >> u) & 1u) live &= ~((uint32_t)(route_key(a.ks, (int64_t)row[u][0], 0, &m) != sb) << u);
+        }
+    return live;
+}
+
+// PS: the superbuckets outnumber the ingest superbuckets (KeySpace.pass_log2 > 0), rows are routed again
+template <int NW, int E, bool Q, int KIND, uint32_t OPS, bool PS>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
@@ -743,10 +825,12 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // this thread's first cell word, loaded while the state loads (the gather below walks the
     // cells of every pending push, one cell per thread per pass, in flat tile order f:
     // cell_chunk(f) is the chunk, positions past the push's last chunk are padding)
-    auto cell_at = [&](int64_t pi, int f) -> uint32_t {
+    auto cell_at = [&](int64_t pi, int f) -> uint32_t {  // cells of this superbucket's ingest superbucket
         if (cell_chunk(f) >= a.slot_nch[pi]) return 0u;
-        const uint32_t* cl = a.cells + (size_t)pi * a.n_sb * a.max_nch;
-        return cl[((size_t)(f >> 4) * a.n_sb + sb) * CELL_LANES + (f & 15)];
+        const int pl = PS ? a.ks.pass_log2 : 0;
+        const int nis = a.n_sb >> pl;
+        const uint32_t* cl = a.cells + (size_t)pi * nis * a.max_nch;
+        return cl[((size_t)(f >> 4) * nis + (sb >> pl)) * CELL_LANES + (f & 15)];
     };
     // the gather splits a push's cells into groups of gather_group(ncell) <= 64 consecutive
     // cells, one group per wave per pass (16 groups when a push has <= 1024 cells)
@@ -803,7 +887,6 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             const int ncell = (int)cell_pad(a.slot_nch[pi]);
             const int G = gather_group(ncell);
             const int ngroups = ncell / G;
-            const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
             for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                 const int f = g * G + lane;
                 uint64_t gc0 = gst ? __builtin_amdgcn_s_memtime() : 0;
@@ -814,32 +897,13 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     stm.acc[13] += g1 - gc0;
                     gc0 = g1;
                 }
-                const uint32_t cnt = v >> 16;
-                uint32_t inc = cnt;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
-                    if (lane >= d) inc += t;
-                }
-                const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
-                const uint32_t excl = inc - cnt;
-                // segment row of this cell's first row, less the rows of the group before it
-                const uint32_t adj = (uint32_t)(cell_chunk(f) * CH + (v & 0xFFFFu)) - excl;
+                const CellGroup cg = cell_group(v, f, CH);
+                const uint32_t tot = cg.tot;
                 if (gst) stm.acc[14] += __builtin_amdgcn_s_memtime() - gc0;  // diagnostic: scan
                 for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
                     uint64_t row[GU][PW];
                     uint64_t g0 = gst ? __builtin_amdgcn_s_memtime() : 0;
-#pragma unroll
-                    for (int u = 0; u < GU; u++) {
-                        // the group's row x lives in the last cell whose first row is <= x
-                        const uint32_t x = min(r0 + (uint32_t)(u * 64 + lane), tot - 1);
-                        int lo = 0;
-#pragma unroll
-                        for (int step = 32; step > 0; step >>= 1)
-                            if ((uint32_t)__shfl((int)excl, lo + step, 64) <= x) lo += step;
-                        const uint64_t* p = seg + (size_t)((uint32_t)__shfl((int)adj, lo, 64) + x) * PW;
-                        load_words<PW>(p, row[u]);
-                    }
+                    const uint32_t live = load_group_rows<NW, GU, PS>(a, pi, cg, r0, sb, row);
                     if (gst) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         const uint64_t g1 = __builtin_amdgcn_s_memtime();
@@ -856,7 +920,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     if constexpr (KIND == KIND_DSWIN) {
                         static_for<GU>([&](auto UU) {
                             constexpr int u = decltype(UU)::value;
-                            if (r0 + (uint32_t)(u * 64 + lane) < tot)
+                            if ((live >> u) & 1u)
                                 ds_add_to_windows<NW, E>(a, S, (int64_t)row[u][0], (int64_t)row[u][1], &row[u][2], w_old, false);
                         });
                         continue;
@@ -885,7 +949,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                     uint32_t miss = 0;
                     static_for<GU>([&](auto UU) {
                         constexpr int u = decltype(UU)::value;
-                        if (r0 + (uint32_t)(u * 64 + lane) >= tot) return;
+                        if (!((live >> u) & 1u)) return;
                         const int e = ge[u];  // -1 / -2: not found by the batched first probe
                         if (e < 0) {
                             miss |= 1u << u;
@@ -1127,13 +1191,13 @@ template <> struct MergeLayouts<8> {
     static constexpr uint32_t L[] = {OPS_ANY};
 };
 
-template <int NW, bool Q, uint32_t OPS>
+template <int NW, bool Q, uint32_t OPS, bool PS = false>
 static void merge_launch(const MergeArgs& a, hipStream_t s) {
     constexpr int ET = mg_entries(NW, FW_WIN_TUMBLE), EH = mg_entries(NW, FW_WIN_HOP), EC = mg_entries(NW, FW_WIN_CUMULATE);
     switch (a.win.kind) {
-        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE, OPS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
-        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP, OPS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE, OPS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE, OPS, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP, OPS, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE, OPS, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
     }
 }
 
@@ -1152,15 +1216,19 @@ static bool merge_layout_launch(const MergeArgs& a, uint32_t lay, hipStream_t s)
     }
 }
 
-template <int NWP>
+template <int NWP, bool PS>
 static void merge_hopb_launch(const MergeArgs& a, hipStream_t s);  // fw_merge_hopb.h
 
 template <int NW>
 hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
+    // more superbuckets than the ingest partitions into (KeySpace.pass_log2): the run-time layout
+    // variants, which route every partial row again (PS)
+    const bool ps = a.ks.pass_log2 > 0;
     if (a.win.hopb) {  // SQL HOP with block state
         if constexpr (NW <= 2) {
             if (a.cap_e != mg_entries(NW, KIND_HOPB)) return hipErrorInvalidValue;
-            merge_hopb_launch<NW>(a, s);
+            if (ps) merge_hopb_launch<NW, true>(a, s);
+            else merge_hopb_launch<NW, false>(a, s);
             return hipGetLastError();
         } else {
             return hipErrorInvalidValue;
@@ -1169,13 +1237,20 @@ hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
     if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
         if (a.wd.has_q) return hipErrorInvalidValue;
         constexpr int E = mg_entries(NW, KIND_DSWIN);
-        hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+        if (ps) hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY, true>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+        else hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY, false>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
         return hipGetLastError();
     }
     // the planner sized the superbuckets for mg_entries(nw, kind) entries (fw_api.hip)
     if (a.cap_e != mg_entries(NW, a.win.kind)) return hipErrorInvalidValue;
-    if (a.wd.has_q) merge_launch<NW, true, OPS_ANY>(a, s);
-    else if (!merge_layout_launch<NW, 0>(a, ops_layout(a.wd), s)) merge_launch<NW, false, OPS_ANY>(a, s);
+    if (ps) {
+        if (a.wd.has_q) merge_launch<NW, true, OPS_ANY, true>(a, s);
+        else merge_launch<NW, false, OPS_ANY, true>(a, s);
+    } else if (a.wd.has_q) {
+        merge_launch<NW, true, OPS_ANY>(a, s);
+    } else if (!merge_layout_launch<NW, 0>(a, ops_layout(a.wd), s)) {
+        merge_launch<NW, false, OPS_ANY>(a, s);
+    }
     return hipGetLastError();
 }
 

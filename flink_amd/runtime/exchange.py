@@ -172,11 +172,20 @@ class KeyByExchange:
         rows, one for the counts.  Rows past a destination's segment come in ``spill`` (packed
         rows, None when no subtask overflowed).  ``watermark``: this subtask's input watermark;
         the returned one is the valve's minimum over all subtasks (StatusWatermarkValve)."""
+        px = self.exchange_packed_async(key, ts, values, capacity)
+        spill, wm = px.finish(watermark)
+        return px.rows, px.recv_counts, px.row_words, spill, wm
+
+    def exchange_packed_async(self, key, ts, values, capacity=None):
+        """The packed exchange in two halves, so the caller can queue the ingest of the received
+        segments before the host waits: this call enqueues the partition and both all-to-alls and
+        returns a PackedExchange (rows, recv_counts, row_words); its finish(watermark) waits for
+        this subtask's partition kernel only, agrees on the overflow round and the watermark with
+        the other subtasks (one host all-reduce) and returns (spill, watermark)."""
         p, n, dev = self.world, key.numel(), key.device
         w = 2 + len(values)
         cap = int(capacity) if capacity is not None else self.segment_capacity(n, p)
         vals64 = [v.view(torch.int64) if v.dtype == torch.float64 else v for v in values]
-        spill = None
         if key.is_cuda:
             L = lib()
             ws = L.fw_partition_workspace_bytes(n, p)
@@ -220,28 +229,7 @@ class KeyByExchange:
             recv, rc = back(recv), back(rc)
         else:
             recv, rc = send, counts
-        # the overflow round: wait for this subtask's partition only (the all-to-all stays in flight)
-        if part_done is not None:
-            part_done.synchronize()
-        over = [max(0, c - cap) for c in counts_h.tolist()]
-        any_over, wm = self._agree(sum(over) > 0, watermark)
-        out_spill = None
-        if any_over:
-            self.spill_rounds += 1
-            if p == 1:
-                out_spill = spill[:over[0] * w] if over[0] else None
-            else:
-                g = self._cpu_group if self._cpu_group is not None else self.group
-                sc = torch.tensor(over, dtype=torch.int64)
-                rsc = torch.empty_like(sc)
-                dist.all_to_all_single(rsc, sc, group=g)
-                rin = rsc.tolist()
-                total = sum(over)
-                src = mv(spill[:total * w] if total else spill[:0])
-                dst = torch.empty(sum(rin) * w, dtype=torch.int64, device=src.device)
-                dist.all_to_all_single(dst, src, [r * w for r in rin], [o * w for o in over], group=self.group)
-                out_spill = back(dst) if sum(rin) else None
-        return recv, rc, w, out_spill, wm
+        return PackedExchange(self, recv, rc, w, cap, spill, counts_h, part_done, mv, back)
 
     def _agree(self, overflow, watermark):
         """One host all-reduce for the overflow decision and the watermark valve's minimum."""
@@ -286,3 +274,38 @@ class KeyByExchange:
         t = torch.tensor([int(w)], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=g)
         return int(t.item())
+
+
+class PackedExchange:
+    """One step's packed keyBy exchange in flight (KeyByExchange.exchange_packed_async)."""
+
+    def __init__(self, ex, rows, recv_counts, row_words, cap, spill, counts_h, part_done, mv, back):
+        self.ex, self.rows, self.recv_counts, self.row_words = ex, rows, recv_counts, row_words
+        self._cap, self._spill, self._counts_h, self._part_done = cap, spill, counts_h, part_done
+        self._mv, self._back = mv, back
+
+    def finish(self, watermark=None):
+        """The overflow round and the watermark valve: waits for this subtask's partition kernel
+        only (the all-to-all and whatever the caller queued after it stay in flight)."""
+        ex, w, cap = self.ex, self.row_words, self._cap
+        if self._part_done is not None:
+            self._part_done.synchronize()
+        over = [max(0, c - cap) for c in self._counts_h.tolist()]
+        any_over, wm = ex._agree(sum(over) > 0, watermark)
+        out_spill = None
+        if any_over:
+            ex.spill_rounds += 1
+            if ex.world == 1:
+                out_spill = self._spill[:over[0] * w] if over[0] else None
+            else:
+                g = ex._cpu_group if ex._cpu_group is not None else ex.group
+                sc = torch.tensor(over, dtype=torch.int64)
+                rsc = torch.empty_like(sc)
+                dist.all_to_all_single(rsc, sc, group=g)
+                rin = rsc.tolist()
+                total = sum(over)
+                src = self._mv(self._spill[:total * w] if total else self._spill[:0])
+                dst = torch.empty(sum(rin) * w, dtype=torch.int64, device=src.device)
+                dist.all_to_all_single(dst, src, [r * w for r in rin], [o * w for o in over], group=ex.group)
+                out_spill = self._back(dst) if sum(rin) else None
+        return out_spill, wm

@@ -227,6 +227,28 @@ class WindowAggHandle:
             self.reset_results()
         return out
 
+    def results_async(self):
+        """Queue the collection of the rows emitted since the last collection into pinned host
+        memory (fw_results_async); they count as consumed.  results_ready() returns them."""
+        check(lib().fw_results_async(self._h))
+
+    def results_ready(self, copy=True):
+        """The rows of the last results_async() (waits for them): the dict results() returns.  With
+        copy=False the arrays are views of the handle's pinned buffers, valid until the second
+        results_async() after that one."""
+        r = abi.fw_result()
+        check(lib().fw_results_ready(self._h, C.byref(r)))
+        n = r.n
+        cp = (lambda a: a.copy()) if copy else (lambda a: a)
+        v = lambda p, t: cp(_np_view(p, n, t)) if n else np.zeros(0, dtype=t)
+        out = {"key": v(r.key, np.int64), "window_start": v(r.window_start, np.int64),
+               "window_end": v(r.window_end, np.int64),
+               "values": [v(r.values[a], np.int64) for a in range(self.n_aggs)],
+               "null_mask": v(r.null_mask, np.uint32)}
+        if self.cfg.ds_first_ordinals:
+            out["first_ord"] = v(r.first_ord, np.int64)
+        return out
+
     def device_results(self):
         """(n, fw_result with device pointers) -- for device-side sinks."""
         r = abi.fw_result()

@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 5
+#define FW_ABI_VERSION 6
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -249,6 +249,10 @@ typedef struct {
     /* v5, FW_KEYHASH_KEYROW: key rows in the intern table (ids handed out and not collected) */
     int64_t key_rows;
     int64_t key_row_collections;       /* collections of unreferenced key rows so far    */
+    /* v6: partial-row traffic (cumulative, device-side) */
+    int64_t partial_bytes_written;     /* bytes of partial rows (+ rank bytes) the ingest wrote */
+    int64_t partial_bytes_merged;      /* of those, the bytes flushes have read          */
+    int64_t compact_chunks;            /* ingest chunks written in a compact row format  */
 } fw_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------- */
@@ -343,6 +347,16 @@ int fw_flush(fw_handle* h);
    otherwise device pointers. */
 int fw_results(fw_handle* h, fw_result* out, int copy_to_host);
 int fw_results_reset(fw_handle* h);
+/* v6, pipelined emission (the shim's collector side of WindowAggOperator.onTimer ->
+   output.collect, WindowAggOperator.java:227-238, and WindowOperator.emitWindowContents :568-575):
+   fw_results_async queues the collection of every result row emitted since the last collection
+   straight into one of two pinned host buffers of the handle and returns at once (the rows count as
+   consumed, as after fw_results_reset); fw_results_ready waits for the LAST fw_results_async's rows
+   and returns them as host arrays, valid until the second fw_results_async after it.  So a caller
+   emits watermark b's rows while batch b + 1 is ingested.  Not for FW_KEYHASH_KEYROW operators
+   (fw_results returns their key rows). */
+int fw_results_async(fw_handle* h);
+int fw_results_ready(fw_handle* h, fw_result* out);
 int fw_get_stats(fw_handle* h, fw_stats* out);
 
 /* ---- per-kernel device timing (in-kernel clock stamps, or hipEvents around each launch) --- */

@@ -82,8 +82,8 @@ def _stream(seed, n, n_keys, ooo, step_ms, n_wm, dup_wm=False):
     return batches
 
 
-def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None):
-    """nulls: per batch {column: flags} (or None)."""
+def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None, stats=None):
+    """nulls: per batch {column: flags} (or None); stats: a dict that receives the handle's final fw_stats."""
     from flink_amd.runtime.handle import WindowAggHandle
     from oracle.oracle import OracleOperator
     o = OracleOperator(cfg)
@@ -116,6 +116,8 @@ def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None):
                 sorted(zip(so["push_seq"].tolist(), so["row"].tolist())) or split > 1
     assert g.stats()["num_late_records_dropped"] == o.late_dropped
     assert g.stats()["error_flags"] == 0
+    if stats is not None:
+        stats.update(g.stats())
     return o.late_dropped
 
 
@@ -514,7 +516,7 @@ def test_key_group_restore_rejects_foreign_and_mismatched_blobs():
 # checked on a key subset against the oracle (window results of a key depend only on that
 # key's records, so the oracle replays only the subset) plus size-independent properties
 # ------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("wl_name", ["cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("wl_name", ["cfg2", "cfg3", "cfg4", "cfg5", "cfg4_10m"])
 def test_bench_workload_full_size_key_subset(wl_name):
     torch = _torch_cuda()
     import ctypes as C
@@ -533,8 +535,10 @@ def test_bench_workload_full_size_key_subset(wl_name):
         cdf = np.cumsum(w)
         zipf_t = torch.tensor(cdf / cdf[-1], device="cuda")
     gp, keys_total = bench.gen_params(wl, 1, zipf_t.data_ptr() if zipf_t is not None else None)
-    cfg = bench.build_config(wl, 1, 0, keys_total, 8 * keys_total + (1 << 20))
+    cfg = bench.build_config(wl, 1, 0, keys_total, (8 if keys_total <= 2_000_000 else 2) * keys_total + (1 << 20))
     g, o = WindowAggHandle(cfg), OracleOperator(cfg)
+    if wl_name == "cfg4_10m":  # the state outgrows the ingest histogram's 8192 superbuckets
+        assert g.stats()["num_superbuckets"] > 8192
     k = torch.empty(B, dtype=torch.int64, device="cuda")
     t, v = torch.empty_like(k), torch.empty_like(k)
     s = torch.cuda.current_stream().cuda_stream
@@ -868,3 +872,47 @@ def test_partition_packed_equals_partition_by_dest():
         assert (seg[d, :m] == ref[o:o + m]).all(), d
         assert (seg[d, m:] == -7).all(), d  # padding untouched
         o += int(cnt[d])
+
+
+@pytest.mark.parametrize("name", ["sql_tumble_int_aggs", "sql_hop", "sql_tumble_double", "ds_sliding_max"])
+def test_async_results_pipeline_matches_oracle(name):
+    """fw_results_async / fw_results_ready: watermark b's rows are collected into pinned host memory
+    while batch b + 1 is pushed (three pushes per watermark through the double-buffered staging)
+    and read one step later -- the same rows as the oracle's, watermark by watermark."""
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = CASES[name]
+    cfg = _cfg(kw)
+    dc = _double_cols(kw)
+    o, g = OracleOperator(cfg), WindowAggHandle(cfg)
+    pending = None
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(zlib.crc32(name.encode()) % 997, 30000, 500, ooo=2 * kw["size_ms"],
+                                                    step_ms=1500, n_wm=16)):
+        vals = [iv, dv.view(np.int64)]
+        o.process_batch(k, t, vals)
+        for part in np.array_split(np.arange(len(k)), 3):
+            g.push_host(k[part], t[part], [v[part] for v in vals])
+        o.process_watermark(wm)
+        g.advance(wm)
+        want = _rows(o.results(clear=True), cfg, dc)
+        if pending is not None:
+            _compare(_rows(g.results_ready(), cfg, dc), pending, dc, f"watermark before batch {bi}")
+        g.results_async()
+        pending = want
+    _compare(_rows(g.results_ready(), cfg, dc), pending, dc, "last watermark")
+    assert g.stats()["error_flags"] == 0 and g.stats()["num_late_records_dropped"] == o.late_dropped
+    g.close()
+
+
+@pytest.mark.parametrize("name", ["sql_tumble_int_aggs", "sql_hop", "sql_cumulate_countstar", "ds_sliding_max",
+                                  "sql_tumble_double"])
+def test_state_beyond_ingest_superbuckets_matches_oracle(name):
+    """A state hint past 8192 LDS-sized superbuckets: the ingest partitions into 8192 and several
+    merge passes share each ingest superbucket's partial rows, each keeping the keys that route to
+    its own superbucket (KeySpace.pass_log2) -- the same results as the oracle, snapshot included."""
+    kw = CASES[name]
+    st = {}
+    cfg = _cfg(kw, state_capacity=40_000_000, output_capacity=1 << 20)
+    _run_both(cfg, _stream(zlib.crc32(name.encode()) % 991, 40000, 3000, ooo=2 * kw["size_ms"] + 1500,
+                           step_ms=1500, n_wm=16), _double_cols(kw), split=2, snapshot_at=9, stats=st)
+    assert st["num_superbuckets"] > 8192, st["num_superbuckets"]

@@ -141,6 +141,9 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=6)
     ap.add_argument("--kernel-timing", default="device", choices=["device", "events"],
                     help="per-launch kernel timing: in-kernel device-clock stamps (default) or hipEvents")
+    ap.add_argument("--plan", default="auto", choices=["auto", "one", "two"],
+                    help="one- or two-phase window aggregation; auto: two-phase for cfg4/cfg5 at N>1 (partials on "
+                         "the wire), one-phase otherwise")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
                          "one-GPU box: ranks share the GPUs round robin and the exchange is staged "
@@ -225,8 +228,57 @@ def main():
         # every step of every active key's window fires; a 2^22 batch spans ~151 s = up to 3 steps
         out_cap = 4 * keys_total + (1 << 20)
 
+    two_phase = args.plan == "two" or (args.plan == "auto" and world > 1 and args.workload in ("cfg4", "cfg5"))
+
+    class TwoPhaseOp:
+        """The two-phase plan (TwoStageOptimizedWindowAggregateRule.java:80-109, Flink's default for these
+        mergeable aggregates) on this rank: a LOCAL operator over the rank's own batch, its partial rows
+        exchanged on the device (TwoPhaseWindowAgg.step_device), the GLOBAL operator of this subtask."""
+
+        def __init__(self, cfg):
+            from flink_amd.table.two_phase import TwoPhaseWindowAgg
+            # the LOCAL operator sees every key group: its flush table is sized for all keys
+            self.tp = TwoPhaseWindowAgg(cfg, exchange=ex, device=dev,
+                                        local_state_capacity=int(keys_total * wl["state_per_key"]))
+
+        def step(self, b):
+            self.tp.local.push_device(gk[b], gt[b], [gv[b]] if nv else [])
+            self.tp.glob.reset_results()  # blackhole sink
+            self.tp.step_device(watermark(b, wl["rate"]))
+
+        def set_profiling(self, *a, **k):
+            self.tp.local.set_profiling(*a, **k)
+            self.tp.glob.set_profiling(*a, **k)
+
+        def sync(self):
+            self.tp.local.sync()
+            self.tp.glob.sync()
+
+        def stats(self):  # the GLOBAL operator's state and merges, the LOCAL operator's ingest
+            st, sl = self.tp.glob.stats(), self.tp.local.stats()
+            for f in ("partials_emitted", "partial_bytes_written", "compact_chunks"):
+                st[f] = sl[f]
+            st["error_flags"] |= sl["error_flags"]
+            return st
+
+        def kernel_times(self):
+            kl, kg = self.tp.local.kernel_times(), self.tp.glob.kernel_times()
+            out = {"reduce": kl["reduce"], "merge": kg["merge"]}
+            out.update({"local_" + k: v for k, v in kl.items() if k not in ("reduce", "merge_phase_cycles")})
+            out.update({"global_" + k: v for k, v in kg.items() if k not in ("merge", "merge_phase_cycles")})
+            return out
+
+        def close(self):
+            self.tp.close()
+
+    def make_op(cfg):
+        return TwoPhaseOp(cfg) if two_phase else WindowAggHandle(cfg)
+
     def run(first, nsteps, handle):
         for b in range(first, first + nsteps):
+            if two_phase:
+                handle.step(b)
+                continue
             wm = push_step(b, handle)
             handle.reset_results()       # blackhole sink: results of the previous watermark consumed
             handle.advance(wm)
@@ -250,7 +302,9 @@ def main():
         interval = math.gcd(wl["window"][1], wl["window"][2])
     groups = []
     for b in range(args.warmup, total_steps):
-        k, t, _ = exchange(b)
+        # one-phase: the batch this subtask ingests after the exchange; two-phase: the LOCAL
+        # operator's own batch (its k_ingest is the segmented reduce measured below)
+        k, t = (gk[b], gt[b]) if two_phase else exchange(b)[:2]
         sl = torch.div(t, interval, rounding_mode="floor")
         sl = sl - sl.min()
         groups.append(int(torch.unique(k * (int(sl.max()) + 1) + sl).numel()))
@@ -260,11 +314,11 @@ def main():
     cfg = build_config(wl, world, rank, keys_total, out_cap)
     # warmup on its own operator instance (first batches of the same stream)
     if args.warmup:
-        hw = WindowAggHandle(cfg)
+        hw = make_op(cfg)
         run(0, args.warmup, hw)
         hw.sync()
         hw.close()
-    h = WindowAggHandle(cfg)
+    h = make_op(cfg)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -427,6 +481,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64" if wl["value_kind"] != 1 else "f64",
             "data": "synthetic (SplitMix64 Nexmark-shaped generator, seed 42, device-resident)",
             "config": {"workload": f"{args.workload}: {wl['desc']}", "events_per_gpu_per_step": B,
+                       "plan": "two-phase (LOCAL -> partials on the device exchange -> GLOBAL)" if two_phase else "one-phase",
                        "keys_total": keys_total, "rate_per_gpu_ev_s": wl["rate"],
                        "parallelism": f"key-group sharded x{world}" + (
                            "" if world == 1 else " + RCCL all-to-all" if args.dist_backend == "nccl"

@@ -10,6 +10,8 @@ from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libflinkwin.so")
+if os.environ.get("FW_LIB_VARIANT"):  # development A/B builds (make OUT=../libflinkwin_<v>.so); never set by default
+    LIB_PATH = os.path.join(_HERE, f"libflinkwin_{os.environ['FW_LIB_VARIANT']}.so")
 
 
 class FlinkWinError(RuntimeError):
@@ -48,12 +50,14 @@ def lib():
         "fw_push_device_packed_segments": (i32, [vp, i32, i64, vp, vp, i32]),
         "fw_partition_packed": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, i64, vp]),
         "fw_partition_packed_spill": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, vp, i64, vp]),
+        "fw_partition_packed_spill_dn": (i32, [vp, vp, vp, vp, i32, i64, vp, i32, i32, i32, i64, vp, vp, vp, vp, i64, vp]),
         "fw_advance": (i32, [vp, i64]),
         "fw_flush": (i32, [vp]),
         "fw_results": (i32, [vp, P(abi.fw_result), i32]),
         "fw_results_reset": (i32, [vp]),
         "fw_results_async": (i32, [vp]),
         "fw_results_ready": (i32, [vp, P(abi.fw_result)]),
+        "fw_results_device": (i32, [vp, P(abi.fw_result), P(vp)]),
         "fw_get_stats": (i32, [vp, P(abi.fw_stats)]),
         "fw_set_profiling": (i32, [vp, i32]),
         "fw_get_kernel_times": (i32, [vp, P(abi.fw_kernel_times)]),
@@ -93,10 +97,10 @@ def lib():
 # every symbol the public header declares (tests check they are exported)
 EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
             "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance",
-            "fw_flush", "fw_results", "fw_results_reset", "fw_results_async", "fw_results_ready", "fw_get_stats", "fw_set_profiling",
+            "fw_flush", "fw_results", "fw_results_reset", "fw_results_async", "fw_results_ready", "fw_results_device", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_key_row_hash", "fw_host_key_row_hash",
-            "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_packed_spill", "fw_partition_workspace_bytes",
+            "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_packed_spill", "fw_partition_packed_spill_dn", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
             "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records", "fw_first_element_events",
             "fw_push_device_key_rows", "fw_key_row_images", "fw_host_key_row_image_lengths", "fw_host_key_row_images",

@@ -242,7 +242,9 @@ def global_config(cfg, **overrides):
     """The GLOBAL-phase operator of a two-phase plan (TwoStageOptimizedWindowAggregateRule): same
     window, key and aggregates, fed with the LOCAL phase's accumulator rows -- value column j is
     accumulator field j (see result_columns), SUM / MIN / MAX fields NULL-able; the ts column
-    carries the slice end."""
+    carries the slice end.  With NOT NULL inputs (cfg.nullable_cols == 0) no field is NULL-able:
+    the LOCAL phase emits a (key, slice) partial only for a slice that received a record, so its
+    SUM / MIN / MAX are never NULL."""
     aggs, types, nullable, j = [], [], [], 0
     for i in range(cfg.n_aggs):
         kind, typ = cfg.aggs[i].kind, cfg.aggs[i].type
@@ -253,7 +255,8 @@ def global_config(cfg, **overrides):
             types += [T_F64 if typ == T_F64 else T_I64, T_I64]
         else:
             types.append(typ)
-            nullable.append(j)
+            if cfg.nullable_cols:
+                nullable.append(j)
         j += 2 if kind == AGG_AVG else 1
     kw = dict(api=cfg.api, window_kind=cfg.window_kind, size_ms=cfg.size_ms, slide_ms=cfg.slide_ms,
               offset_ms=cfg.offset_ms, aggs=aggs, count_star_index=cfg.count_star_index, value_col_types=types,

@@ -565,14 +565,17 @@ int validate_and_plan(fw_handle* h) {
         return fail(FW_E_INVALID, "max_batch_rows too large for MIN/MAX(DOUBLE) / first-element arrival ordinals");
     h->cell_cols = cell_pad(h->max_nch);
     // compact partial rows: SQL rows on the UTC slice grid (the ingest kernel's common path; it falls
-    // back to PF_WIDE per chunk).  Key-row handles keep PF_WIDE: their collector reads the partial
-    // buffer's keys at a fixed stride.  FW_NARROW=0 switches them off (development).
+    // back to PF_WIDE per chunk), planned for COUNT(*)-only layouts, whose compact row is the key alone:
+    // for the others the merge gather's cost of reading two formats outweighed the bytes saved
+    // (DESIGN.md 5).  Key-row handles keep PF_WIDE: their collector reads the partial buffer's keys at
+    // a fixed stride; split superbuckets (pass_log2) too.  FW_NARROW=0 switches them off (development).
     {
         const char* ne = getenv("FW_NARROW");
         const bool count_only = wd.nw == 1 && wd.op[0] == W_CNT && wd.gate[0] < 0;
         h->narrow = (c.api == FW_API_SQL && !h->keyrow && c.agg_phase != FW_PHASE_GLOBAL && h->tz_utc.empty() &&
-                     w.fast32 && !(ne && atoi(ne) == 0) && (h->chunk_rows & (h->chunk_rows - 1)) == 0)
-                        ? (count_only ? 2 : 1)
+                     w.fast32 && count_only && ks.pass_log2 == 0 && !(ne && atoi(ne) == 0) &&
+                     (h->chunk_rows & (h->chunk_rows - 1)) == 0)
+                        ? 2
                         : 0;
     }
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
@@ -809,6 +812,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.ordev_cap = h->ordev_cap;
     a.slot_base = h->slot_base;
     a.ranks = h->ranks;
+    a.compact = h->narrow != 0;
     a.ch_log2 = 0;
     while ((1ll << a.ch_log2) < h->chunk_rows) a.ch_log2++;
     return a;
@@ -1373,6 +1377,49 @@ int fw_results_async(fw_handle* h) {
     HIP_TRY(launch_compact(ca, h->stream, h->timer));
     HIP_TRY(hipEventRecord(h->ar_ev[b], h->stream));
     h->reset_pending = true;  // the rows are collected: the next merge launch starts the slabs afresh
+    return FW_OK;
+}
+
+int fw_results_device(fw_handle* h, fw_result* out, int64_t** d_n) {
+    if (!h || !out || !d_n) return fail(FW_E_INVALID, "null argument");
+    if (h->keyrow) return fail(FW_E_INVALID, "key-row operators return their rows through fw_results");
+    memset(out, 0, sizeof *out);
+    *d_n = h->coff + h->ks.n_sb + 1;
+    if (h->reset_pending) {  // consumed and nothing emitted since: zero rows
+        HIP_TRY(hipMemsetAsync(*d_n, 0, sizeof(int64_t), h->stream));
+    } else {
+        CompactArgs ca{};
+        ca.ctrl = h->ctrl;
+        ca.sb_out = h->sb_out;
+        ca.off = h->coff;
+        ca.n_sb = h->ks.n_sb;
+        ca.n_aggs = h->n_out;
+        ca.slab_cap = h->slab_cap;
+        ca.out_key = h->out_key;
+        ca.out_ws = h->out_ws;
+        ca.out_we = h->out_we;
+        ca.out_null = h->out_null;
+        for (int g = 0; g < h->n_out; g++) {
+            ca.out_val[g] = h->out_val[g];
+            ca.res_val[g] = h->res_val[g];
+        }
+        ca.res_key = h->res_key;
+        ca.res_ws = h->res_ws;
+        ca.res_we = h->res_we;
+        ca.res_null = h->res_null;
+        ca.res_cap = h->out_cap;
+        HIP_TRY(launch_compact(ca, h->stream, h->timer));
+        h->reset_pending = true;
+    }
+    const int na = h->n_out;
+    const int nv = h->ad.first_word >= 0 ? na - 1 : na;
+    out->n = h->out_cap;
+    out->key = h->res_key;
+    out->window_start = h->res_ws;
+    out->window_end = h->res_we;
+    for (int g = 0; g < nv; g++) out->values[g] = (int64_t*)h->res_val[g];
+    if (nv < na) out->first_ord = (int64_t*)h->res_val[nv];
+    out->null_mask = h->res_null;
     return FW_OK;
 }
 

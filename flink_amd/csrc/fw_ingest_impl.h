@@ -59,6 +59,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int NVR = NV > 0 ? NV : 1;
     constexpr int PW = 2 + NW;
     constexpr int SL = ig_slots(NW);
+    constexpr bool CAN_COMPACT = NW == 1;  // compact partial rows (PF_NARROW / PF_UNIT)
     static_assert(RPT % IG_SRPT == 0, "fold sub-tiles must tile the chunk");
     // dynamic LDS only (16-B aligned base, G17): [header 16 words][hist: n_sb u32, padded to
     // 16 B][area: fold table, later the store stage]
@@ -190,7 +191,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     // compact partial rows (PF_NARROW / PF_UNIT) count slices from the push's rank base: the first
     // slice end that is not fired at the current watermark (every row that is not late ends at or
     // after it); the merge kernel reads it from slot_base
-    const bool nar = a.narrow && simple && cur_wm != INT64_MIN;
+    // (planned for COUNT(*)-only layouts, fw_api.hip: the variants with wider accumulators carry
+    // none of this code, which would cost them registers)
+    const bool nar = CAN_COMPACT && a.narrow && simple && cur_wm != INT64_MIN;
     uint32_t slow = simple ? 0u : valid;
     // record words: the word op is uniform, so it is resolved once per launch into a mode and
     // the rows only select (no per-row switch over the op)
@@ -354,9 +357,11 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     });
     // a row left valid by the general path keeps its slice end in its partial row (PF_WIDE chunk)
     const bool wide_row = (slow & valid) != 0;
-    __syncthreads();  // the header and histogram are initialised
+    const uint32_t valid_unfolded = valid;
+    const bool do_fold = fold && !(FW_ABL(a) & AB_NO_FOLD);
+    if (!do_fold) __syncthreads();  // the header and histogram are initialised (the fold's first barrier does it)
     // ---- K3: fold equal (key, slice) rows, one 1024-row sub-tile at a time
-    if (fold && !(FW_ABL(a) & AB_NO_FOLD)) static_for<NSUB>([&](auto S) {
+    if (do_fold) static_for<NSUB>([&](auto S) {
         constexpr int s = decltype(S)::value;
         uint32_t rh[IG_SRPT];
         __syncthreads();  // previous sub-tile's owners are done with claim/cacc
@@ -389,7 +394,6 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                 for (int w = 0; w < NW; w++)
                     if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w * SL + h], racc[j][w]);
                 valid &= ~(1u << j);
-                *s_folded = 1u;
             }
         });
         __syncthreads();
@@ -401,6 +405,8 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             for (int w = 0; w < NW; w++) racc[j][w] = cacc[w * SL + rh[q]];
         });
     });
+    // PF_UNIT needs a chunk in which no row folded into another: one LDS flag store per wave that folded
+    if (a.narrow == 2 && do_fold && __ballot(valid != valid_unfolded) && (tid & 63) == 0) *s_folded = 1u;
     // ---- rank the partials per superbucket, scan, publish the cells
     uint32_t rdst[RPT];
     const bool sort = !(FW_ABL(a) & AB_NO_SORT);
@@ -414,12 +420,14 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     bool wide = wide_row || !nar;
     // (re-read here rather than kept live through the fold: the watermark does not change during a push)
     const int64_t nbase = nar ? slice_end_of(a.win, wadd(__hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE), 1)) : 0;
-    if (!wide)
-        static_for<RPT>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            if ((valid & (1u << j)) && (uint64_t)(rs[j] - nbase) >= (uint64_t)a.rank_lim) wide = true;
-        });
-    wide = __syncthreads_or(wide);
+    if (nar) {  // uniform: the block-wide vote only when compact rows are possible
+        if (!wide)
+            static_for<RPT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                if ((valid & (1u << j)) && (uint64_t)(rs[j] - nbase) >= (uint64_t)a.rank_lim) wide = true;
+            });
+        wide = __syncthreads_or(wide);
+    }
     uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch;
     const int per = (n_sb + IG_BLOCK - 1) / IG_BLOCK;
     const int sb0 = min(tid * per, n_sb), sb1 = min(sb0 + per, n_sb);
@@ -429,7 +437,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     const uint32_t incl = block_incl_scan<IG_BLOCK>(seg, wsum, &total);
     uint32_t run = incl - seg;
     // COUNT(*) alone and nothing folded in this chunk: every row counts 1
-    const uint32_t fmt = (wide || !sort) ? PF_WIDE
+    const uint32_t fmt = (!CAN_COMPACT || wide || !sort) ? PF_WIDE
                          : (!X && a.narrow == 2 && !*s_folded) ? PF_UNIT
                                                                                         : PF_NARROW;
     if (sort)
@@ -548,6 +556,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     }
     __syncthreads();
     if (tid == 0) {
+#pragma unroll 1
         for (int v = 1; v < NWV; v++) {
             m = min(m, red[v]);
             d += red[NWV + v];

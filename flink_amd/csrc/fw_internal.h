@@ -40,7 +40,10 @@ constexpr int ig_slots(int nw) { return nw <= 2 ? 1024 : nw <= 4 ? 512 : 256; }
 constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw); }
 
 // ---- merge/fire (K4+K5): one 1024-thread workgroup per superbucket
-constexpr int MG_BLOCK = 1024;
+#ifndef FW_MG_BLOCK
+#define FW_MG_BLOCK 1024
+#endif
+constexpr int MG_BLOCK = FW_MG_BLOCK;
 constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a time per pending push (one per thread)
 // LDS slice-state capacity (entries) per superbucket by accumulator words
 // (kind: FW_WIN_* of a SQL operator, KIND_DSWIN (3) for DataStream windows).  One accumulator word
@@ -525,6 +528,7 @@ struct MergeArgs {
     const int64_t* slot_base;   // compact partial rows (IngestArgs)
     const uint8_t* ranks;
     int32_t ch_log2;            // log2(chunk_rows)
+    int32_t compact;            // chunks may hold compact rows (IngestArgs::narrow != 0)
 };
 constexpr int64_t ORDEV_RELEASE = (int64_t)1 << 62;
 constexpr int LFW = 3 + MAX_WORDS;  // words per late-fire row

@@ -188,9 +188,11 @@ constexpr int PART_TILE = 4096;
 constexpr int PART_MAXP = 64;
 
 __global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, const int32_t* kh, int64_t n, int32_t kind,
-                                                     int32_t max_p, int32_t p, uint32_t* counts) {
+                                                     int32_t max_p, int32_t p, uint32_t* counts,
+                                                     const int64_t* n_dev = nullptr) {
     __shared__ uint32_t h[PART_MAXP];
     const int tid = threadIdx.x;
+    if (n_dev) n = min(n, *n_dev);  // a row count known only on the device (<= the launch's n)
     if (tid < PART_MAXP) h[tid] = 0;
     __syncthreads();
     const int64_t b = (int64_t)blockIdx.x * PART_TILE;
@@ -233,7 +235,8 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
                                                         int32_t p, const uint32_t* offsets, int64_t* okey, int64_t* ots,
                                                         uint64_t* const* ovals, int64_t* orows = nullptr,
                                                         int64_t seg_len = 0, const int64_t* totals = nullptr,
-                                                        int64_t* spill = nullptr) {
+                                                        int64_t* spill = nullptr, const int64_t* n_dev = nullptr) {
+    if (n_dev) n = min(n, *n_dev);
     // Stable: rows keep their input order within a destination (the order a Netty channel
     // delivers them in, ChannelSelectorRecordWriter.emit :54), so a DOUBLE SUM downstream adds in
     // the same order on every run.  Each wave ranks its 64 rows per destination with ballots;
@@ -444,11 +447,37 @@ extern "C" int fw_partition_packed(const int64_t* d_key, const int32_t* d_key_ha
                                      stream);
 }
 
+static int partition_packed(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                            const void* const* d_values, int32_t n_cols, int64_t n, const int64_t* d_n,
+                            int32_t key_hash_kind, int32_t max_parallelism, int32_t parallelism, int64_t seg_len,
+                            int64_t* d_out_rows, int64_t* d_spill_rows, int64_t* d_counts, void* d_workspace,
+                            int64_t workspace_bytes, void* stream);
+
 extern "C" int fw_partition_packed_spill(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
                                          const void* const* d_values, int32_t n_cols, int64_t n, int32_t key_hash_kind,
                                          int32_t max_parallelism, int32_t parallelism, int64_t seg_len,
                                          int64_t* d_out_rows, int64_t* d_spill_rows, int64_t* d_counts,
                                          void* d_workspace, int64_t workspace_bytes, void* stream) {
+    return partition_packed(d_key, d_key_hash, d_ts, d_values, n_cols, n, nullptr, key_hash_kind, max_parallelism,
+                            parallelism, seg_len, d_out_rows, d_spill_rows, d_counts, d_workspace, workspace_bytes, stream);
+}
+
+extern "C" int fw_partition_packed_spill_dn(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                                            const void* const* d_values, int32_t n_cols, int64_t n_max,
+                                            const int64_t* d_n, int32_t key_hash_kind, int32_t max_parallelism,
+                                            int32_t parallelism, int64_t seg_len, int64_t* d_out_rows,
+                                            int64_t* d_spill_rows, int64_t* d_counts, void* d_workspace,
+                                            int64_t workspace_bytes, void* stream) {
+    if (!d_n) return FW_E_INVALID;
+    return partition_packed(d_key, d_key_hash, d_ts, d_values, n_cols, n_max, d_n, key_hash_kind, max_parallelism,
+                            parallelism, seg_len, d_out_rows, d_spill_rows, d_counts, d_workspace, workspace_bytes, stream);
+}
+
+static int partition_packed(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                            const void* const* d_values, int32_t n_cols, int64_t n, const int64_t* d_n,
+                            int32_t key_hash_kind, int32_t max_parallelism, int32_t parallelism, int64_t seg_len,
+                            int64_t* d_out_rows, int64_t* d_spill_rows, int64_t* d_counts, void* d_workspace,
+                            int64_t workspace_bytes, void* stream) {
     if (parallelism <= 0 || parallelism > PART_MAXP || n_cols < 0 || n_cols > FW_MAX_COLS || seg_len < 1) return FW_E_INVALID;
     if (key_hash_kind == FW_KEYHASH_PRECOMPUTED && n > 0 && !d_key_hash) return FW_E_INVALID;
     if (key_hash_kind != FW_KEYHASH_PRECOMPUTED) d_key_hash = nullptr;
@@ -465,12 +494,12 @@ extern "C" int fw_partition_packed_spill(const int64_t* d_key, const int32_t* d_
     for (int c = 0; c < n_cols; c++) hv[c] = d_values[c];
     if (hipMemcpyAsync(dv, hv, sizeof(hv), hipMemcpyHostToDevice, s) != hipSuccess) return FW_E_DEVICE;
     hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, n, key_hash_kind,
-                       max_parallelism, parallelism, counts);
+                       max_parallelism, parallelism, counts, d_n);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(BLOCK), 0, s, counts, nblk, parallelism, d_counts);
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, d_ts,
                        (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
                        (int64_t*)nullptr, (int64_t*)nullptr, (uint64_t* const*)nullptr, d_out_rows, seg_len,
-                       (const int64_t*)d_counts, d_spill_rows);
+                       (const int64_t*)d_counts, d_spill_rows, d_n);
     return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
 }
 

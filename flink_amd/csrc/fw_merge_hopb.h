@@ -132,8 +132,9 @@ __device__ uint32_t hb_fire_entry(const MergeArgs& a, StateLds<HB_R * NWP, E>& S
     return nf;
 }
 
-template <int NWP, int E, uint32_t OPS, bool PS>
+template <int NWP, int E, uint32_t OPS, int GF>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
+    constexpr bool PS = (GF & GF_PASS) != 0;
     constexpr int NA = HB_R * NWP;  // ring words per entry
     constexpr int PW = 2 + NWP;     // partial row words
     constexpr int PWE = 3 + NA;     // state entry words
@@ -200,9 +201,16 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
         };
         const int lane = tid & 63, wv = tid >> 6;
         auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
-        uint32_t v_first = 0;
-        if (do_flush && lane < gather_group((int)cell_pad(a.slot_nch[0])))
-            v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
+        // this lane's cell word of its wave's first group in every pending push, loaded beside the state
+        uint32_t v_first[MG_PREFETCH];
+#pragma unroll
+        for (int q = 0; q < MG_PREFETCH; q++) {
+            v_first[q] = 0;
+            if (do_flush && q < pend) {
+                const int G0 = gather_group((int)cell_pad(a.slot_nch[q]));
+                if (lane < G0) v_first[q] = cell_at(q, wv * G0 + lane);
+            }
+        }
         // ---- load the superbucket's block entries into LDS
         for (int i = tid; i < StateLds<NA, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
         if (tid == 0) {
@@ -238,12 +246,12 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
                 const int ngroups = ncell / G;
                 for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                     const int f = g * G + lane;
-                    const uint32_t v = lane >= G ? 0u : (pi == 0 && g == wv) ? v_first : cell_at(pi, f);
+                    const uint32_t v = lane >= G ? 0u : (g == wv && pi < MG_PREFETCH) ? pick_pending(v_first, pi) : cell_at(pi, f);
                     const CellGroup cg = cell_group(v, f, CH);
                     const uint32_t tot = cg.tot;
                     for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
                         uint64_t row[GU][PW];
-                        const uint32_t live = load_group_rows<NWP, GU, PS>(a, pi, cg, r0, sb, row);
+                        const uint32_t live = load_group_rows<NWP, GU, GF>(a, pi, cg, r0, sb, row);
                         int ge[GU], slot[GU];
                         {
                             int64_t gk[GU], gb[GU];
@@ -338,15 +346,19 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
     merge_ticket(a);
 }
 
-template <int NWP, bool PS>
+template <int NWP, int GF>
 static void merge_hopb_launch(const MergeArgs& a, hipStream_t s) {
     constexpr int E = mg_entries(NWP, KIND_HOPB);
     // COUNT(*) alone / COUNT(*) + SUM(BIGINT) with the word ops as constants; the rest at run time
     constexpr uint32_t L = NWP == 1 ? ops_pack({W_SUM_I}) : ops_pack({W_SUM_I, W_SUM_I});
-    if (!PS && ops_layout(a.wd) == L)
-        hipLaunchKernelGGL((k_merge_hopb<NWP, E, L, false>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
-    else
-        hipLaunchKernelGGL((k_merge_hopb<NWP, E, OPS_ANY, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+    if constexpr (GF == GF_COMPACT) {  // COUNT(*) alone with compact rows (the planner's only narrow layout)
+        hipLaunchKernelGGL((k_merge_hopb<NWP, E, L, GF_COMPACT>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+    } else {
+        if (GF == 0 && ops_layout(a.wd) == L)
+            hipLaunchKernelGGL((k_merge_hopb<NWP, E, L, 0>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_merge_hopb<NWP, E, OPS_ANY, GF>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+    }
 }
 
 }  // namespace fw

@@ -668,7 +668,25 @@ __device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
 }
 
 // rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
-constexpr int mg_rows_in_flight(int nw) { return nw <= 1 ? 4 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1; }
+#ifndef FW_GU1
+#define FW_GU1 4
+#endif
+constexpr int mg_rows_in_flight(int nw) {
+    return MG_BLOCK <= 512 ? (nw <= 1 ? 2 * FW_GU1 : nw <= 2 ? 6 : nw <= 4 ? 4 : 2) : (nw <= 1 ? FW_GU1 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1);
+}
+
+// element i of the per-push cell-word prefetch (no dynamic register indexing)
+#ifndef FW_MG_PREFETCH
+#define FW_MG_PREFETCH 1
+#endif
+constexpr int MG_PREFETCH = FW_MG_PREFETCH;  // pending pushes whose first cell words a merge wave loads up front
+__device__ __forceinline__ uint32_t pick_pending(const uint32_t (&v)[MG_PREFETCH], int64_t i) {
+    uint32_t r = v[0];
+#pragma unroll
+    for (int q = 1; q < MG_PREFETCH; q++)
+        if (i == q) r = v[q];
+    return r;
+}
 
 // ---- the gather's view of the pending partials.  A wave takes a group of up to 64 consecutive
 // cells of one push slot (lane l holds cell word v of flat cell position f), scans their row
@@ -700,10 +718,18 @@ __device__ __forceinline__ CellGroup cell_group(uint32_t v, int f, int64_t CH) {
 // base + rank * interval, PF_UNIT's count is 1.  Returns the rows to fold (bit u): those inside the
 // group and -- when several superbuckets share the ingest superbucket (ks.pass_log2 > 0) -- routed
 // to superbucket `sb`.
-template <int NW, int GU, bool PS>
+// gather variants of the merge kernels (template GF): the superbuckets outnumber the ingest
+// superbuckets (rows are routed again), and / or the chunks may hold compact rows.  Reading compact
+// rows costs the wide-row gather of the other layouts ~10 % even when no chunk is compact, so only
+// the COUNT(*)-only layouts, whose compact rows are the key alone, are built with it.
+constexpr int GF_PASS = 1;
+constexpr int GF_COMPACT = 2;
+
+template <int NW, int GU, int GF>
 __device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t pi, const CellGroup& g, uint32_t r0,
                                                     int sb, uint64_t (&row)[GU][2 + NW]) {
     constexpr int PW = 2 + NW;
+    constexpr bool PS = (GF & GF_PASS) != 0, CR = (GF & GF_COMPACT) != 0;
     const int lane = threadIdx.x & 63;
     const uint64_t* seg = a.parts + (size_t)pi * a.cap_rows * PW;
 #pragma unroll
@@ -716,7 +742,7 @@ __device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t 
             if ((uint32_t)__shfl((int)g.excl, lo + step, 64) <= x) lo += step;
         const uint32_t rg = (uint32_t)__shfl((int)g.adj, lo, 64) + x;  // row index in the slot
         const uint32_t fmt = (uint32_t)__shfl((int)g.fmt, lo, 64);
-        if (fmt == PF_WIDE) {
+        if (!CR || fmt == PF_WIDE) {
             load_words<PW>(seg + (size_t)rg * PW, row[u]);
         } else {
             // a compact chunk fills the front of its PF_WIDE-sized region
@@ -750,9 +776,10 @@ __device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t 
     return live;
 }
 
-// PS: the superbuckets outnumber the ingest superbuckets (KeySpace.pass_log2 > 0), rows are routed again
-template <int NW, int E, bool Q, int KIND, uint32_t OPS, bool PS>
+// GF: gather variant (GF_PASS: KeySpace.pass_log2 > 0, GF_COMPACT: compact partial rows)
+template <int NW, int E, bool Q, int KIND, uint32_t OPS, int GF>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
+    constexpr bool PS = (GF & GF_PASS) != 0;
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
     const int64_t CH = a.chunk_rows;  // chunk rows of the ingest kernel that wrote the cells
@@ -836,9 +863,17 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // cells, one group per wave per pass (16 groups when a push has <= 1024 cells)
     const int lane = tid & 63, wv = tid >> 6;
     auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
-    uint32_t v_first = 0;
-    if (gather && lane < gather_group((int)cell_pad(a.slot_nch[0])))
-        v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
+    // this lane's cell word of its wave's first group in EVERY pending push, loaded beside the state
+    // (a wave usually has one group per push: its cell round trip leaves the gather loop)
+    uint32_t v_first[MG_PREFETCH];
+#pragma unroll
+    for (int q = 0; q < MG_PREFETCH; q++) {
+        v_first[q] = 0;
+        if (gather && q < pend) {
+            const int G0 = gather_group((int)cell_pad(a.slot_nch[q]));
+            if (lane < G0) v_first[q] = cell_at(q, wv * G0 + lane);
+        }
+    }
     // ---- load this superbucket's entries into LDS
     for (int i = tid; i < StateLds<NW, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
     if (tid == 0) {
@@ -890,7 +925,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                 const int f = g * G + lane;
                 uint64_t gc0 = gst ? __builtin_amdgcn_s_memtime() : 0;
-                const uint32_t v = lane >= G ? 0u : (pi == 0 && g == wv) ? v_first : cell_at(pi, f);
+                const uint32_t v = lane >= G ? 0u : (g == wv && pi < MG_PREFETCH) ? pick_pending(v_first, pi) : cell_at(pi, f);
                 if (gst) {  // diagnostic: cell word wait
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     const uint64_t g1 = __builtin_amdgcn_s_memtime();
@@ -903,7 +938,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                 for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {
                     uint64_t row[GU][PW];
                     uint64_t g0 = gst ? __builtin_amdgcn_s_memtime() : 0;
-                    const uint32_t live = load_group_rows<NW, GU, PS>(a, pi, cg, r0, sb, row);
+                    const uint32_t live = load_group_rows<NW, GU, GF>(a, pi, cg, r0, sb, row);
                     if (gst) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         const uint64_t g1 = __builtin_amdgcn_s_memtime();
@@ -1191,13 +1226,13 @@ template <> struct MergeLayouts<8> {
     static constexpr uint32_t L[] = {OPS_ANY};
 };
 
-template <int NW, bool Q, uint32_t OPS, bool PS = false>
+template <int NW, bool Q, uint32_t OPS, int GF = 0>
 static void merge_launch(const MergeArgs& a, hipStream_t s) {
     constexpr int ET = mg_entries(NW, FW_WIN_TUMBLE), EH = mg_entries(NW, FW_WIN_HOP), EC = mg_entries(NW, FW_WIN_CUMULATE);
     switch (a.win.kind) {
-        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE, OPS, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
-        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP, OPS, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
-        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE, OPS, PS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_TUMBLE: hipLaunchKernelGGL((k_merge_fire<NW, ET, Q, FW_WIN_TUMBLE, OPS, GF>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        case FW_WIN_HOP: hipLaunchKernelGGL((k_merge_fire<NW, EH, Q, FW_WIN_HOP, OPS, GF>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
+        default: hipLaunchKernelGGL((k_merge_fire<NW, EC, Q, FW_WIN_CUMULATE, OPS, GF>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a); break;
     }
 }
 
@@ -1209,6 +1244,13 @@ static bool merge_layout_launch(const MergeArgs& a, uint32_t lay, hipStream_t s)
     } else {
         constexpr uint32_t L = MergeLayouts<NW>::L[I];
         if (L != OPS_ANY && lay == L) {
+            // compact rows come only with the COUNT(*)-only layout (fw_api.hip plans narrow for it alone)
+            if constexpr (NW == 1 && L == ops_pack({W_SUM_I})) {
+                if (a.compact) {
+                    merge_launch<NW, false, L, GF_COMPACT>(a, s);
+                    return true;
+                }
+            }
             merge_launch<NW, false, L>(a, s);
             return true;
         }
@@ -1216,7 +1258,7 @@ static bool merge_layout_launch(const MergeArgs& a, uint32_t lay, hipStream_t s)
     }
 }
 
-template <int NWP, bool PS>
+template <int NWP, int GF>
 static void merge_hopb_launch(const MergeArgs& a, hipStream_t s);  // fw_merge_hopb.h
 
 template <int NW>
@@ -1227,8 +1269,9 @@ hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
     if (a.win.hopb) {  // SQL HOP with block state
         if constexpr (NW <= 2) {
             if (a.cap_e != mg_entries(NW, KIND_HOPB)) return hipErrorInvalidValue;
-            if (ps) merge_hopb_launch<NW, true>(a, s);
-            else merge_hopb_launch<NW, false>(a, s);
+            if (ps) merge_hopb_launch<NW, GF_PASS>(a, s);
+            else if (NW == 1 && a.compact) merge_hopb_launch<NW, GF_COMPACT>(a, s);
+            else merge_hopb_launch<NW, 0>(a, s);
             return hipGetLastError();
         } else {
             return hipErrorInvalidValue;
@@ -1237,15 +1280,15 @@ hipError_t merge_nw(const MergeArgs& a, hipStream_t s) {
     if (a.win.ds) {  // DataStream: per-window state, no SQL MIN/MAX(DOUBLE) word groups
         if (a.wd.has_q) return hipErrorInvalidValue;
         constexpr int E = mg_entries(NW, KIND_DSWIN);
-        if (ps) hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY, true>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
-        else hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY, false>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+        if (ps) hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY, GF_PASS>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
+        else hipLaunchKernelGGL((k_merge_fire<NW, E, false, KIND_DSWIN, OPS_ANY, 0>), dim3(merge_grid(a.n_sb)), dim3(MG_BLOCK), 0, s, a);
         return hipGetLastError();
     }
     // the planner sized the superbuckets for mg_entries(nw, kind) entries (fw_api.hip)
     if (a.cap_e != mg_entries(NW, a.win.kind)) return hipErrorInvalidValue;
     if (ps) {
-        if (a.wd.has_q) merge_launch<NW, true, OPS_ANY, true>(a, s);
-        else merge_launch<NW, false, OPS_ANY, true>(a, s);
+        if (a.wd.has_q) merge_launch<NW, true, OPS_ANY, GF_PASS>(a, s);
+        else merge_launch<NW, false, OPS_ANY, GF_PASS>(a, s);
     } else if (a.wd.has_q) {
         merge_launch<NW, true, OPS_ANY>(a, s);
     } else if (!merge_layout_launch<NW, 0>(a, ops_layout(a.wd), s)) {

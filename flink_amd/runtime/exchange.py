@@ -53,6 +53,7 @@ class KeyByExchange:
             self._cpu_group = dist.new_group(ranks=ranks, backend="gloo")
         self._max_count = None  # running max of rows per destination (padded exchanges), on the device
         self.spill_rounds = 0
+        self._dn_share = 1 << 16  # largest per-destination share of the last device-counted exchange
 
     # ---- routing ------------------------------------------------------------------------
     def partition(self, key, ts, values, key_hash=None):
@@ -176,15 +177,24 @@ class KeyByExchange:
         spill, wm = px.finish(watermark)
         return px.rows, px.recv_counts, px.row_words, spill, wm
 
-    def exchange_packed_async(self, key, ts, values, capacity=None):
+    def exchange_packed_async(self, key, ts, values, capacity=None, n_dev=None):
         """The packed exchange in two halves, so the caller can queue the ingest of the received
         segments before the host waits: this call enqueues the partition and both all-to-alls and
         returns a PackedExchange (rows, recv_counts, row_words); its finish(watermark) waits for
         this subtask's partition kernel only, agrees on the overflow round and the watermark with
-        the other subtasks (one host all-reduce) and returns (spill, watermark)."""
+        the other subtasks (one host all-reduce) and returns (spill, watermark).  ``n_dev``: a
+        one-element device int64 tensor holding the row count (the columns are only its bound, e.g.
+        fw_results_device's): the rows are partitioned without a host round trip, and the segment
+        size comes from the largest share the previous such exchange saw (rows past it take the
+        overflow round)."""
         p, n, dev = self.world, key.numel(), key.device
         w = 2 + len(values)
-        cap = int(capacity) if capacity is not None else self.segment_capacity(n, p)
+        if capacity is not None:
+            cap = int(capacity)
+        elif n_dev is not None:
+            cap = int(self._dn_share * 1.25) + 1024
+        else:
+            cap = self.segment_capacity(n, p)
         vals64 = [v.view(torch.int64) if v.dtype == torch.float64 else v for v in values]
         if key.is_cuda:
             L = lib()
@@ -195,10 +205,16 @@ class KeyByExchange:
             spill = torch.empty(max(n, 1) * w, dtype=torch.int64, device=dev)
             counts = torch.empty(p, dtype=torch.int64, device=dev)
             vin = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in vals64])
-            check(L.fw_partition_packed_spill(key.data_ptr(), None, ts.data_ptr(), vin, len(values), n, self.kind,
-                                              self.max_p, p, cap, send.data_ptr(), spill.data_ptr(), counts.data_ptr(),
-                                              self._ws.data_ptr(), self._ws.numel(),
-                                              torch.cuda.current_stream(dev).cuda_stream))
+            if n_dev is None:
+                check(L.fw_partition_packed_spill(key.data_ptr(), None, ts.data_ptr(), vin, len(values), n, self.kind,
+                                                  self.max_p, p, cap, send.data_ptr(), spill.data_ptr(),
+                                                  counts.data_ptr(), self._ws.data_ptr(), self._ws.numel(),
+                                                  torch.cuda.current_stream(dev).cuda_stream))
+            else:
+                check(L.fw_partition_packed_spill_dn(key.data_ptr(), None, ts.data_ptr(), vin, len(values), n,
+                                                     n_dev.data_ptr(), self.kind, self.max_p, p, cap, send.data_ptr(),
+                                                     spill.data_ptr(), counts.data_ptr(), self._ws.data_ptr(),
+                                                     self._ws.numel(), torch.cuda.current_stream(dev).cuda_stream))
             counts_h = torch.empty(p, dtype=torch.int64, pin_memory=True)
             counts_h.copy_(counts, non_blocking=True)
             part_done = torch.cuda.Event()
@@ -231,15 +247,16 @@ class KeyByExchange:
             recv, rc = send, counts
         return PackedExchange(self, recv, rc, w, cap, spill, counts_h, part_done, mv, back)
 
-    def _agree(self, overflow, watermark):
-        """One host all-reduce for the overflow decision and the watermark valve's minimum."""
+    def _agree(self, overflow, watermark, share=0):
+        """One host all-reduce for the overflow decision, the watermark valve's minimum and the
+        largest per-destination share."""
         wm = None if watermark is None else int(watermark)
         if self.world == 1:
-            return overflow, wm
+            return overflow, wm, int(share)
         g = self.group if self._cpu_group is None else self._cpu_group
-        t = torch.tensor([1 if overflow else 0, -wm if wm is not None else 0], dtype=torch.int64)
+        t = torch.tensor([1 if overflow else 0, -wm if wm is not None else 0, int(share)], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
-        return bool(t[0].item()), (None if wm is None else -int(t[1].item()))
+        return bool(t[0].item()), (None if wm is None else -int(t[1].item())), int(t[2].item())
 
     def _note_counts(self, counts, cap):
         """Keep the running max of rows per destination on the device (check_capacity)."""
@@ -290,8 +307,13 @@ class PackedExchange:
         ex, w, cap = self.ex, self.row_words, self._cap
         if self._part_done is not None:
             self._part_done.synchronize()
-        over = [max(0, c - cap) for c in self._counts_h.tolist()]
-        any_over, wm = ex._agree(sum(over) > 0, watermark)
+        cnt = self._counts_h.tolist()
+        over = [max(0, c - cap) for c in cnt]
+        # the next device-counted exchange sizes its segments from the largest share any subtask
+        # sent this time: every subtask must pick the same segment size, so it rides in the same
+        # all-reduce as the overflow decision and the watermark
+        any_over, wm, share = ex._agree(sum(over) > 0, watermark, max(cnt) if cnt else 0)
+        ex._dn_share = share
         out_spill = None
         if any_over:
             ex.spill_rounds += 1

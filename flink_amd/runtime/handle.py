@@ -249,6 +249,30 @@ class WindowAggHandle:
             out["first_ord"] = v(r.first_ord, np.int64)
         return out
 
+    def device_results_async(self, device):
+        """The rows emitted since the last collection as device tensors, WITHOUT a host round trip
+        (fw_results_device): returns (n, key, window_start, window_end, [values], null_mask) where n is
+        a one-element device int64 tensor and the columns are views of output_capacity rows (only the
+        first n are rows).  The rows count as consumed; the caller's current stream is ordered after
+        the collection, and the views stay valid until the handle collects results again."""
+        import torch
+        r = abi.fw_result()
+        dn = C.c_void_p()
+        check(lib().fw_results_device(self._h, C.byref(r), C.byref(dn)))
+        cap = int(r.n)
+        cur = self._begin_read(device)  # (the handle stream also waits for the caller's earlier work)
+        self._end_read(cur)             # the caller's stream waits for the collection
+
+        class _View:
+            def __init__(self, ptr, n, typestr):
+                self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
+                                                 "version": 3, "strides": None}
+
+        def t(ptr, n=cap, typestr="<i8"):
+            return torch.as_tensor(_View(C.cast(ptr, C.c_void_p).value, n, typestr), device=device)
+        return (t(dn.value, 1), t(r.key), t(r.window_start), t(r.window_end),
+                [t(r.values[a]) for a in range(self.n_aggs)], t(r.null_mask, typestr="<i4"))
+
     def device_results(self):
         """(n, fw_result with device pointers) -- for device-side sinks."""
         r = abi.fw_result()

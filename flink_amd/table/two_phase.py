@@ -20,9 +20,11 @@ from ..runtime.handle import WindowAggHandle
 
 
 class TwoPhaseWindowAgg:
-    def __init__(self, cfg, exchange=None, device=None):
+    def __init__(self, cfg, exchange=None, device=None, local_state_capacity=None):
         """cfg: the one-phase SQL operator configuration of this subtask (its parallelism and
-        subtask_index are the GLOBAL operator's).  exchange: a KeyByExchange for parallelism > 1."""
+        subtask_index are the GLOBAL operator's).  exchange: a KeyByExchange for parallelism > 1.
+        local_state_capacity: the LOCAL operator's sizing hint (it sees every key group; default the
+        GLOBAL operator's)."""
         if cfg.api != abi.API_SQL:
             raise ValueError("two-phase window aggregation is a SQL plan")
         if cfg.key_hash == abi.KEYHASH_PRECOMPUTED:
@@ -37,12 +39,13 @@ class TwoPhaseWindowAgg:
             count_star_index=cfg.count_star_index,
             value_col_types=[cfg.value_col_types[c] for c in range(cfg.n_value_cols)],
             key_hash=cfg.key_hash, max_parallelism=cfg.max_parallelism, parallelism=1, subtask_index=0,
-            device=cfg.device, state_capacity=cfg.state_capacity, max_batch_rows=cfg.max_batch_rows,
+            device=cfg.device, state_capacity=local_state_capacity or cfg.state_capacity, max_batch_rows=cfg.max_batch_rows,
             output_capacity=cfg.output_capacity,
             nullable_cols=[c for c in range(cfg.n_value_cols) if cfg.nullable_cols >> c & 1],
             agg_phase=abi.PHASE_LOCAL)
         self.local_cfg = local
         self.global_cfg = abi.global_config(local, parallelism=cfg.parallelism, subtask_index=cfg.subtask_index,
+                                            state_capacity=cfg.state_capacity,
                                             max_batch_rows=max(cfg.max_batch_rows, cfg.output_capacity))
         self.local = WindowAggHandle(local)
         self.glob = WindowAggHandle(self.global_cfg)
@@ -85,6 +88,30 @@ class TwoPhaseWindowAgg:
         self.global_ingest(key, se, fields, nm)
         self.glob.advance(watermark if global_watermark is None else global_watermark)
         return self.glob.results(reset=True)
+
+    def step_device(self, watermark):
+        """One watermark interval of the plan with the partials kept on the device and no host round
+        trip before the exchange: the LOCAL advance, its partial rows collected on the device
+        (fw_results_device: the count stays a device value), the packed partition by that count and
+        the all-to-all (KeyByExchange.exchange_packed_async, n_dev), the GLOBAL ingest of the received
+        segments queued, then the overflow round and the watermark valve in one host all-reduce, and
+        the GLOBAL advance.  Returns the valve's watermark; the GLOBAL rows stay in its handle."""
+        from ..runtime.exchange import KeyByExchange
+        if self.global_cfg.nullable_cols:
+            raise ValueError("step_device moves packed rows, which carry no NULL flags: NOT NULL inputs only")
+        if self.exchange is None:
+            self.exchange = KeyByExchange(self.global_cfg.key_hash, self.global_cfg.max_parallelism)
+        self.local.advance(watermark)
+        n, key, _, se, fields, _ = self.local.device_results_async(self.device)
+        px = self.exchange.exchange_packed_async(key, se, fields, n_dev=n)
+        self.glob.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
+        spill, wm = px.finish(watermark)
+        if spill is not None:
+            n_sp = spill.numel() // px.row_words
+            self.glob.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=self.device), spill,
+                                                  px.row_words)
+        self.glob.advance(wm)
+        return wm
 
     def flush(self):
         """prepareSnapshotPreBarrier of both operators: the local buffer is emitted downstream

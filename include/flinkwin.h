@@ -357,6 +357,12 @@ int fw_results_reset(fw_handle* h);
    (fw_results returns their key rows). */
 int fw_results_async(fw_handle* h);
 int fw_results_ready(fw_handle* h, fw_result* out);
+/* v6, device-side consumers (the two-phase plan's LOCAL -> GLOBAL exchange): queues the collection
+   of the rows emitted since the last collection into the handle's device result columns and
+   returns their device pointers without waiting; the row count is the device int64 at *d_n and
+   out->n is only its bound (output_capacity).  The rows count as consumed; read them on the
+   handle's stream (fw_get_stream) or after it, before the next call that collects results. */
+int fw_results_device(fw_handle* h, fw_result* out, int64_t** d_n);
 int fw_get_stats(fw_handle* h, fw_stats* out);
 
 /* ---- per-kernel device timing (in-kernel clock stamps, or hipEvents around each launch) --- */
@@ -478,6 +484,14 @@ int fw_partition_packed_spill(const int64_t* d_key, const int32_t* d_key_hash, c
                               int32_t max_parallelism, int32_t parallelism, int64_t seg_len, int64_t* d_out_rows,
                               int64_t* d_spill_rows, int64_t* d_counts, void* d_workspace, int64_t workspace_bytes,
                               void* stream);
+/* v6: fw_partition_packed_spill of the first *d_n (a device int64, <= n_max) rows: the batch's size
+   is known only on the device, e.g. the LOCAL phase's partial rows of fw_results_device, so the
+   two-phase exchange (TwoStageOptimizedWindowAggregateRule.java:80-109) needs no host round trip. */
+int fw_partition_packed_spill_dn(const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                                 const void* const* d_values, int32_t n_cols, int64_t n_max, const int64_t* d_n,
+                                 int32_t key_hash_kind, int32_t max_parallelism, int32_t parallelism, int64_t seg_len,
+                                 int64_t* d_out_rows, int64_t* d_spill_rows, int64_t* d_counts, void* d_workspace,
+                                 int64_t workspace_bytes, void* stream);
 
 /* Synthetic Nexmark-shaped generator: event i in [i0, i0+n). */
 typedef struct {

@@ -1,18 +1,19 @@
 """GPU parity of the compact partial-row formats (fw_internal.h PF_NARROW / PF_UNIT).
 
-An ingest chunk whose rows all take the common SQL path stores (key, acc) or, for COUNT(*) alone
-with nothing folded, only the key, and the slice end as a rank byte against the push's rank base;
-any other chunk of the same push stores full (key, sliceEnd, acc) rows.  These streams mix both in
-every push (late rows and far-future rows force single chunks wide), run several pushes per
-watermark, and compare every watermark's results with the oracle; the device counters must show
-that compact chunks were written."""
+For COUNT(*)-only layouts an ingest chunk whose rows all take the common SQL path stores only the
+key (PF_UNIT; (key, count) when rows folded: PF_NARROW) and the slice end as a rank byte against the
+push's rank base; any other chunk of the same push stores full (key, sliceEnd, acc) rows.  These
+streams mix both in every push (late rows and far-future rows force single chunks wide), run several
+pushes per watermark, and compare every watermark's results with the oracle; the device counters
+must show that compact chunks were written -- and none for the other layouts, which keep full rows
+(DESIGN.md 3)."""
 import zlib
 
 import numpy as np
 import pytest
 
 from flink_amd import abi
-from test_gpu_parity import F64, I64, _cfg, _double_cols, _run_both
+from parity_common import F64, I64, _cfg, _double_cols, _run_both
 
 pytestmark = pytest.mark.gpu
 
@@ -64,6 +65,10 @@ CASES = {
     "cumulate_4aggs": dict(window_kind=abi.WIN_CUMULATE, size_ms=12000, slide_ms=2000, count_star_index=0,
                            aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MIN, 0, I64),
                                  (abi.AGG_MAX, 0, I64)]),
+    "cumulate_count_star": dict(window_kind=abi.WIN_CUMULATE, size_ms=12000, slide_ms=3000, count_star_index=0,
+                                aggs=[(abi.AGG_COUNT_STAR, 0, I64)]),
+    "tumble_offset_count_star": dict(window_kind=abi.WIN_TUMBLE, size_ms=7000, offset_ms=-2500, count_star_index=0,
+                                     aggs=[(abi.AGG_COUNT_STAR, 0, I64)]),
     "tumble_offset_min": dict(window_kind=abi.WIN_TUMBLE, size_ms=7000, offset_ms=-2500,
                               aggs=[(abi.AGG_MIN, 0, I64), (abi.AGG_COUNT_STAR, 0, I64)]),
 }
@@ -83,8 +88,11 @@ def test_compact_partial_rows_match_oracle(name, hot):
     st = {}
     _run_both(_cfg(kw, state_capacity=1 << 18, max_batch_rows=1 << 15), batches, _double_cols(kw), split=2, stats=st)
     chunks = 14 * 2 * 4  # 14 watermarks x 2 pushes x 4 chunks (per = 6 chunks + 333 rows, split in two)
-    assert st["compact_chunks"] > chunks // 2, st   # the common path writes compact rows ...
-    assert st["compact_chunks"] < chunks, st        # ... and the late / far rows force some chunks wide
+    if kw["aggs"] == [(abi.AGG_COUNT_STAR, 0, I64)]:
+        assert st["compact_chunks"] > chunks // 2, st   # the common path writes compact rows ...
+        assert st["compact_chunks"] < chunks, st        # ... and the late / far rows force some chunks wide
+    else:
+        assert st["compact_chunks"] == 0, st
     assert st["partial_bytes_written"] > 0 and st["partial_bytes_merged"] <= st["partial_bytes_written"]
 
 
@@ -92,7 +100,7 @@ def test_compact_rows_local_phase_matches_oracle():
     """The LOCAL phase (two-phase, LocalSlicingWindowAggOperator) keeps no late handling: compact
     chunks there, and every flushed (key, slice) partial is emitted."""
     kw = dict(window_kind=abi.WIN_HOP, size_ms=8000, slide_ms=2000, count_star_index=0, agg_phase=abi.PHASE_LOCAL,
-              aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64)])
+              aggs=[(abi.AGG_COUNT_STAR, 0, I64)])
     batches = _stream(7, n_wm=10, per=5 * CH, n_keys=20000, step_ms=3000, ooo=4000, slice_ms=2000)
     st = {}
     _run_both(_cfg(kw, max_batch_rows=1 << 15), batches, set(), split=1, stats=st)
@@ -102,7 +110,8 @@ def test_compact_rows_local_phase_matches_oracle():
 def test_compact_rows_off_matches_compact_rows_on(monkeypatch):
     """FW_NARROW=0 (every chunk PF_WIDE) and the default give the same results and late counts."""
     from flink_amd.runtime.handle import WindowAggHandle
-    kw = CASES["cumulate_4aggs"]
+    kw = dict(window_kind=abi.WIN_CUMULATE, size_ms=12000, slide_ms=2000, count_star_index=0,
+              aggs=[(abi.AGG_COUNT_STAR, 0, I64)])
     batches = _stream(11, n_wm=8, per=5 * CH, n_keys=5000, step_ms=3000, ooo=4000, slice_ms=2000)
     outs = []
     for env in ("0", "1"):

@@ -37,8 +37,9 @@ def per_kernel(d, counter):
             if row.get("Counter_Name") != counter:
                 continue
             name = row["Kernel_Name"]
+            # the flush + fire kernel: k_merge_fire, or k_merge_hopb for SQL HOP with block state
             key = "k_ingest" if "k_ingest" in name else "k_key_groups" if "k_key_groups" in name else \
-                  "k_merge_fire" if "k_merge_fire" in name else None
+                  "k_merge_fire" if ("k_merge_fire" in name or "k_merge_hopb" in name) else None
             if key:
                 vals.setdefault(key, []).append(float(row["Counter_Value"]))
     return vals

@@ -105,6 +105,12 @@ class fw_key_field(C.Structure):
                 ("offsets", C.c_void_p), ("bytes", C.c_void_p), ("nulls", C.c_void_p)]
 
 
+class fw_heap_state_ids(C.Structure):
+    """state ids of the heap backend's key-group data (HeapSnapshotStrategy.java:171)"""
+    _fields_ = [("window_state", C.c_int16), ("event_timers", C.c_int16),
+                ("processing_timers", C.c_int16), ("reserved", C.c_int16)]
+
+
 class fw_host_cols(C.Structure):
     _fields_ = [("key", C.POINTER(C.c_int64)), ("ts", C.POINTER(C.c_int64)),
                 ("key_hash", C.POINTER(C.c_int32)),

@@ -14,8 +14,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "fw_internal.h"
@@ -244,6 +246,13 @@ struct fw_handle {
     uint64_t pushes_at_merge[64] = {};  // pushes_total when merge launch (seq % 64) was issued
     bool reset_pending = false;  // fw_results_reset called: the next merge launch empties the results
     int64_t host_cur = INT64_MIN;
+    // the device's currentProgress / nextTriggerProgress as the launched merges leave them (mirrored
+    // on the host from the watermarks it launched; merge_finalize applies the same rule), so fw_advance
+    // can tell a watermark that crosses no slice end -- the merge launch would change nothing -- and
+    // skip it (FW_SKIP_IDLE=0: launch every advance)
+    int64_t dev_cur = INT64_MIN;
+    int64_t dev_ntp = INT64_MIN;
+    bool skip_idle = true;
     KTimer* timer = nullptr;  // non-null while fw_set_profiling is on
     int ablate = 0;           // FW_ABLATE (development timing builds only; results are wrong)
     int fold_always = 0;      // FW_FOLD=1 (development A/B): no adaptive fold skip
@@ -823,6 +832,10 @@ int launch_merge(fw_handle* h, int64_t wm, int force) {
     h->pushes_at_merge[h->merge_seq % 64] = h->pushes_total;
     h->merge_seq++;
     h->reset_pending = false;  // the launch started every output slab (and the overflow) afresh
+    if (!force && wm > h->dev_cur) {  // merge_finalize's advanceProgress bookkeeping, mirrored
+        h->dev_cur = wm;
+        if (wm >= h->dev_ntp) h->dev_ntp = tz_next_trigger_watermark(h->win.tz, wm, h->win.slice_div);
+    }
     return FW_OK;
 }
 
@@ -974,6 +987,7 @@ int fw_create(const fw_config* cfg, fw_handle** out) {
     if (const char* ab = getenv("FW_ABLATE")) h->ablate = atoi(ab);
     if (const char* fo = getenv("FW_FOLD")) h->fold_always = atoi(fo);
     if (const char* fp = getenv("FW_FILL_PCT")) h->fill_pct = std::min(95, std::max(10, atoi(fp)));
+    if (const char* si = getenv("FW_SKIP_IDLE")) h->skip_idle = atoi(si) != 0;
     int rc = validate_and_plan(h);
     h->cfg.tz_utc = nullptr;  // the shift-zone table was copied (h->tz_*); never read the caller's
     h->cfg.tz_offset_ms = nullptr;
@@ -1082,6 +1096,7 @@ int fw_initialize_watermark(fw_handle* h, int64_t watermark) {
     HIP_TRY(hipMemcpyAsync(&h->ctrl->cur, &watermark, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->host_cur = watermark;
+    h->dev_cur = watermark;
     return FW_OK;
 }
 
@@ -1228,6 +1243,22 @@ int fw_push_device_packed_segments(fw_handle* h, int32_t n_segs, int64_t seg_len
 
 int fw_advance(fw_handle* h, int64_t watermark) {
     if (!h) return fail(FW_E_INVALID, "null handle");
+    // A SQL watermark below the next trigger watermark crosses no slice end: no window fires, no
+    // buffer flush is due (AbstractSliceSyncStateWindowAggProcessor.advanceProgress :139-153 only
+    // flushes at a trigger) and lateness is unchanged (no window end lies between the old and the
+    // new watermark), so the merge launch would only move currentProgress.  It is skipped; the next
+    // launch moves currentProgress past it and registers any pending late-record timers before it
+    // fires.  DataStream cleanup timers are off the slice grid (cleanupTime), so DataStream and
+    // key-row operators (whose collector runs with the merge) always launch.
+    // The trigger grid is the slice-end grid only in UTC with an offset on the grid: otherwise a
+    // timer or a lateness bound can lie between two trigger watermarks, and only a repeated
+    // watermark is skipped.
+    const bool on_grid = h->win.tz.n == 0 && h->win.offset % h->win.interval == 0;
+    if (h->skip_idle && !h->always_flush && !h->keyrow &&
+        (watermark <= h->dev_cur || (on_grid && watermark < h->dev_ntp))) {
+        if (watermark > h->host_cur) h->host_cur = watermark;
+        return FW_OK;
+    }
     int rc = launch_merge(h, watermark, 0);
     if (rc) return rc;
     if (h->keyrow)  // key rows no state / partial / timer request / unread result holds any more
@@ -1531,7 +1562,7 @@ int fw_get_stats(fw_handle* h, fw_stats* out) {
     }
     if (h->reset_pending) avail = 0;
     memset(out, 0, sizeof *out);
-    out->current_watermark = c.cur;
+    out->current_watermark = std::max<int64_t>(c.cur, h->host_cur);  // skipped idle advances included
     out->next_trigger_progress = c.ntp;
     out->num_late_records_dropped = (int64_t)c.late_dropped;
     out->live_state_entries = live;
@@ -1840,6 +1871,8 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
     h->pushes_ub = 0;
     h->host_cur = c.cur;
+    h->dev_cur = c.cur;
+    h->dev_ntp = INT64_MIN;
     h->push_seq = std::max<int64_t>(h->push_seq, hd.push_seq);
     return FW_OK;
 }
@@ -1983,9 +2016,459 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
     if (rc) return rc;
     c.live_entries += added;
     c.ntp = INT64_MIN;  // next trigger recomputed at the next advance
+    h->dev_ntp = INT64_MIN;
     HIP_TRY(hipMemcpy(h->ctrl, &c, sizeof c, hipMemcpyHostToDevice));
     h->push_seq = std::max<int64_t>(h->push_seq, hd.push_seq);
     return FW_OK;
+}
+
+// ---- heap keyed-state backend key-group format ------------------------------------------
+// The bytes the heap backend writes for one key group of a window-aggregate operator
+// (HeapSnapshotStrategy.java:161-172): writeInt(keyGroup), then per registered state
+// writeShort(stateId) and that state's key-group writer --
+//   window-aggs ValueState (CopyOnWriteStateMapSnapshot.writeState :127-149):
+//       writeInt(n), then per entry namespace (LongSerializer: 8 B big-endian sliceEnd),
+//       key (BinaryRowData: writeInt(len) + bytes), accumulator (RowDataSerializer -> BinaryRowData)
+//   event / processing window-timers queues (KeyGroupPartitioner.java:241-254 with
+//       TimerSerializer.serialize :147-152): writeInt(n), then per timer
+//       writeLong(flipSignBit(ts)), key, namespace
+// The accumulator row holds every aggregate's buffer fields in order (COUNT(*) / COUNT: count
+// BIGINT; SUM / MIN / MAX: value of the aggregate's type, NULL-able; AVG: sum BIGINT|DOUBLE, count
+// BIGINT), the LOCAL phase's output fields.  A timer's timestamp is
+// toEpochMillsForTimer(window - 1) (SlicingWindowTimerServiceImpl.java:43-46).
+namespace {
+
+constexpr int HEAP_MAX_FIELDS = 2 * FW_MAX_AGGS;
+
+struct HeapWriter {
+    std::vector<uint8_t> b;
+    void u8(uint8_t v) { b.push_back(v); }
+    void be32(uint32_t v) { for (int i = 3; i >= 0; i--) b.push_back((uint8_t)(v >> (8 * i))); }
+    void be16(uint16_t v) { b.push_back((uint8_t)(v >> 8)); b.push_back((uint8_t)v); }
+    void be64(uint64_t v) { for (int i = 7; i >= 0; i--) b.push_back((uint8_t)(v >> (8 * i))); }
+    void bytes(const uint8_t* p, size_t n) { b.insert(b.end(), p, p + n); }
+};
+
+struct HeapReader {
+    const uint8_t* p;
+    size_t n, at = 0;
+    bool bad = false;
+    bool need(size_t k) { if (at + k > n) bad = true; return !bad; }
+    uint32_t be32() { if (!need(4)) return 0; uint32_t v = 0; for (int i = 0; i < 4; i++) v = v << 8 | p[at++]; return v; }
+    uint16_t be16() { if (!need(2)) return 0; uint16_t v = (uint16_t)(p[at] << 8 | p[at + 1]); at += 2; return v; }
+    uint64_t be64() { if (!need(8)) return 0; uint64_t v = 0; for (int i = 0; i < 8; i++) v = v << 8 | p[at++]; return v; }
+    const uint8_t* take(size_t k) { if (!need(k)) return nullptr; const uint8_t* q = p + at; at += k; return q; }
+};
+
+// the accumulator row's field types (FW_T_*), in order
+int heap_fields(const fw_handle* h, int32_t* type) {
+    int j = 0;
+    for (int g = 0; g < h->ad.n; g++) {
+        const int k = h->ad.kind[g], t = h->ad.type[g];
+        if (k == FW_AGG_COUNT_STAR || k == FW_AGG_COUNT) type[j++] = FW_T_I64;
+        else if (k == FW_AGG_AVG) { type[j++] = t == FW_T_F64 ? FW_T_F64 : FW_T_I64; type[j++] = FW_T_I64; }
+        else type[j++] = t;
+    }
+    return j;
+}
+
+int heap_bitset_bytes(int arity) { return ((arity + 63 + 8) / 64) * 8; }  // BinaryRowData.calculateBitSetWidthInBytes
+
+// accumulator words -> buffer field values + NULL mask (emit_partial, restated on the host)
+void heap_words_to_fields(const fw_handle* h, const uint64_t* acc, uint64_t* v, uint32_t* nm) {
+    const AggDesc& ad = h->ad;
+    *nm = 0;
+    int j = 0;
+    for (int g = 0; g < ad.n; g++) {
+        const int kind = ad.kind[g], type = ad.type[g];
+        const uint64_t w0 = acc[ad.w0[g]];
+        const bool no_rows = ad.nn[g] >= 0 && acc[ad.nn[g]] == 0;
+        uint64_t x = w0;
+        bool isnull = false;
+        if (kind == FW_AGG_SUM) {
+            x = type == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)w0 : w0;
+            isnull = no_rows;
+        } else if (kind == FW_AGG_MIN || kind == FW_AGG_MAX) {
+            if (ad.qf[g] >= 0) {  // q_result (fw_kernel_common.h)
+                const uint64_t f = acc[ad.qf[g]];
+                isnull = f == Q_EMPTY;
+                if (isnull) x = 0;
+                else if ((uint32_t)f) x = (f << 32) | (acc[ad.qn[g]] & 0xFFFFFFFFull);
+                else if ((int64_t)w0 != 0) x = dkey_inv((int64_t)w0);
+                else x = acc[ad.qz[g]] != Q_EMPTY ? ((acc[ad.qz[g]] & 1ull) << 63) : 0ull;
+            } else {
+                x = type == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
+                isnull = no_rows;
+            }
+        } else if (kind == FW_AGG_AVG) {
+            v[j++] = w0;
+            x = acc[ad.w1[g]];
+        }
+        if (isnull) *nm |= 1u << j;
+        v[j++] = isnull ? 0ull : x;
+    }
+}
+
+// buffer field values -> accumulator words (the inverse; a hidden non-NULL count word becomes 1,
+// its only observable property being != 0, and a MIN/MAX(DOUBLE) group is one element of ordinal 0)
+void heap_fields_to_words(const fw_handle* h, const uint64_t* v, uint32_t nm, uint64_t* acc) {
+    const AggDesc& ad = h->ad;
+    const WordDesc& wd = h->wd;
+    for (int w = 0; w < h->nw_t; w++) acc[w] = w < wd.nw ? word_identity(wd.op[w]) : 0;
+    bool set[MAX_WORDS] = {};
+    int j = 0;
+    for (int g = 0; g < ad.n; g++) {
+        const int kind = ad.kind[g], type = ad.type[g];
+        const int w0 = ad.w0[g];
+        if (kind == FW_AGG_COUNT_STAR || kind == FW_AGG_COUNT) {
+            acc[w0] = v[j++];
+            set[w0] = true;
+            continue;
+        }
+        if (kind == FW_AGG_AVG) {
+            acc[w0] = v[j++];
+            acc[ad.w1[g]] = v[j++];
+            set[w0] = set[ad.w1[g]] = true;
+            continue;
+        }
+        const bool isnull = (nm >> j) & 1u;
+        const uint64_t x = v[j++];
+        if (isnull) continue;  // identity words
+        if (ad.qf[g] >= 0) {  // merge_q_groups' re-encoding
+            const bool nan = f64_isnan(x);
+            acc[ad.qf[g]] = nan ? (x >> 32) : 0ull;
+            if (nan) acc[ad.qn[g]] = x & 0xFFFFFFFFull;
+            if (f64_iszero(x)) acc[ad.qz[g]] = x >> 63;
+            if (!nan) acc[w0] = f64_iszero(x) ? 0ull : (uint64_t)dkey(x);
+            continue;
+        }
+        if ((kind == FW_AGG_MIN || kind == FW_AGG_MAX) && type == FW_T_F64) acc[w0] = (uint64_t)dkey(x);
+        else if (type == FW_T_I32) acc[w0] = (uint64_t)(int64_t)(int32_t)(uint32_t)x;
+        else acc[w0] = x;
+        set[w0] = true;
+    }
+    for (int g = 0; g < ad.n; g++) {  // hidden non-NULL counts of SUM / MIN / MAX
+        const int nn = ad.nn[g];
+        if (nn < 0 || set[nn]) continue;
+        int jj = 0;  // field index of aggregate g
+        for (int q = 0; q < g; q++) jj += ad.kind[q] == FW_AGG_AVG ? 2 : 1;
+        if (!((nm >> jj) & 1u)) acc[nn] = 1;
+    }
+}
+
+void heap_write_row(HeapWriter& w, const fw_handle* h, const uint64_t* v, uint32_t nm) {
+    int32_t type[HEAP_MAX_FIELDS];
+    const int n = heap_fields(h, type);
+    const int bs = heap_bitset_bytes(n);
+    w.be32((uint32_t)(bs + 8 * n));
+    std::vector<uint8_t> row((size_t)(bs + 8 * n), 0);  // header byte 0 = RowKind.INSERT
+    for (int j = 0; j < n; j++) {
+        if ((nm >> j) & 1u) {
+            row[(size_t)(j + 8) / 8] |= (uint8_t)(1u << ((j + 8) % 8));
+            continue;
+        }
+        const uint64_t x = type[j] == FW_T_I32 ? (uint32_t)v[j] : v[j];
+        memcpy(row.data() + bs + 8 * j, &x, 8);  // little-endian slot; an INT in its low 4 bytes
+    }
+    w.bytes(row.data(), row.size());
+}
+
+bool heap_read_row(HeapReader& r, const fw_handle* h, uint64_t* v, uint32_t* nm) {
+    int32_t type[HEAP_MAX_FIELDS];
+    const int n = heap_fields(h, type);
+    const int bs = heap_bitset_bytes(n);
+    const uint32_t len = r.be32();
+    if (r.bad || len != (uint32_t)(bs + 8 * n)) return false;
+    const uint8_t* p = r.take(len);
+    if (!p) return false;
+    *nm = 0;
+    for (int j = 0; j < n; j++) {
+        if ((p[(j + 8) / 8] >> ((j + 8) % 8)) & 1u) { *nm |= 1u << j; v[j] = 0; continue; }
+        uint64_t x;
+        memcpy(&x, p + bs + 8 * j, 8);
+        v[j] = type[j] == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)x : x;
+    }
+    return true;
+}
+
+// the key's BinaryRowData image: BINROW_BIGINT / BINROW_INT keys are the one-field row the key
+// projection writes (8 B header, the value slot); key rows carry their interned image
+int heap_key_kind(const fw_handle* h) {
+    if (h->keyrow) return FW_KEYHASH_KEYROW;
+    const int k = h->cfg.key_hash;
+    return k == FW_KEYHASH_BINROW_BIGINT || k == FW_KEYHASH_BINROW_INT ? k : -1;
+}
+
+int heap_check(const fw_handle* h, const fw_heap_state_ids* ids) {
+    if (!ids) return fail(FW_E_INVALID, "null state ids");
+    if (h->cfg.api != FW_API_SQL || h->cfg.agg_phase == FW_PHASE_LOCAL)
+        return fail(FW_E_INVALID, "the heap key-group format is the SQL window-aggregate operator's keyed state");
+    if (heap_key_kind(h) < 0)
+        return fail(FW_E_INVALID, "the heap key-group format needs SQL key rows (BINROW_BIGINT, BINROW_INT or KEYROW keys)");
+    if (ids->window_state == ids->event_timers || ids->window_state == ids->processing_timers ||
+        ids->event_timers == ids->processing_timers)
+        return fail(FW_E_INVALID, "state ids must differ");
+    return FW_OK;
+}
+
+}  // namespace
+
+int fw_snapshot_key_group_heap(fw_handle* h, int32_t key_group, const fw_heap_state_ids* ids, void* buf,
+                               int64_t capacity, int64_t* size) {
+    if (!h || !size) return fail(FW_E_INVALID, "null argument");
+    int rc = heap_check(h, ids);
+    if (rc) return rc;
+    // the device state of the key group, in this library's own key-group format
+    int64_t n_int = 0;
+    if ((rc = fw_snapshot_key_group(h, key_group, nullptr, 0, &n_int))) return rc;
+    std::vector<uint64_t> blob((size_t)(n_int + 7) / 8);
+    if ((rc = fw_snapshot_key_group(h, key_group, blob.data(), (int64_t)blob.size() * 8, &n_int))) return rc;
+    KgHeader hd;
+    memcpy(&hd, blob.data(), sizeof hd);
+    const int pwe = h->pwe, nw = h->nw_t;
+    const uint64_t* ent = blob.data() + sizeof hd / 8;
+    // key images
+    std::unordered_map<int64_t, std::pair<const uint8_t*, uint32_t>> img;
+    if (h->keyrow) {
+        const uint64_t* sec = ent + (size_t)hd.n * pwe;
+        const int64_t nk = (int64_t)sec[0];
+        size_t p = 1;
+        for (int64_t k = 0; k < nk; k++) {
+            const uint32_t len = (uint32_t)sec[p + 1];
+            img[(int64_t)sec[p]] = {(const uint8_t*)(sec + p + 2), len};
+            p += 2 + len / 8;
+        }
+    }
+    const int kk = heap_key_kind(h);
+    auto write_key = [&](HeapWriter& w, int64_t key) {
+        if (kk == FW_KEYHASH_KEYROW) {
+            const auto& im = img.at(key);
+            w.be32(im.second);
+            w.bytes(im.first, im.second);
+            return;
+        }
+        uint8_t row[16] = {};
+        const uint64_t x = kk == FW_KEYHASH_BINROW_INT ? (uint32_t)key : (uint64_t)key;
+        memcpy(row + 8, &x, 8);
+        w.be32(16);
+        w.bytes(row, 16);
+    };
+    struct St { int64_t key, ns; const uint64_t* acc; };
+    std::vector<St> states;
+    std::vector<std::pair<int64_t, int64_t>> timers;  // (key, window)
+    std::vector<uint64_t> slot_acc;
+    const WinDesc& win = h->win;
+    if (win.hopb) {
+        // block entries -> one (key, sliceEnd) state per slot with data.  Timers: the reference holds
+        // one per unfired slice end with data (AggCombiner.combine step 5) and one at the first
+        // unfired window end whose window holds data (the nextTriggerWindow chain, or a late
+        // record's registration).  A chain timer at an EMPTY window (its predecessor's only data
+        // was in the slice that window expired) is not derivable from the expired state; it fires
+        // without output, and is the one timer the export leaves out.
+        std::unordered_map<int64_t, std::vector<int64_t>> ends;  // key -> slice ends with data
+        for (int64_t i = 0; i < hd.n; i++) {
+            const uint64_t* e = ent + (size_t)i * pwe;
+            const uint32_t mask = (uint32_t)e[2] >> HB_MASK_SHIFT;
+            for (int s = 0; s < HB_R; s++)
+                if ((mask >> s) & 1u) {
+                    const int64_t se = wadd((int64_t)e[1], (int64_t)(s + 1) * win.interval);
+                    states.push_back({(int64_t)e[0], se, e + 3 + s * nw});
+                    ends[(int64_t)e[0]].push_back(se);
+                }
+        }
+        for (auto& kv : ends) {
+            auto& v = kv.second;
+            std::sort(v.begin(), v.end());
+            for (int64_t se : v)
+                if (!win_fired(win, se, hd.cur)) timers.push_back({kv.first, se});
+            if (win_fired(win, v.front(), hd.cur)) {  // some data slice fired: the chain's next window
+                int64_t e1 = v.front();
+                while (win_fired(win, e1, hd.cur)) e1 = wadd(e1, win.interval);
+                const int64_t lo = wsub(e1, win.size);  // window (e1 - size, e1] holds data?
+                const bool data = std::any_of(v.begin(), v.end(), [&](int64_t se) { return se > lo && se <= e1; });
+                if (data && !std::binary_search(v.begin(), v.end(), e1)) timers.push_back({kv.first, e1});
+            }
+        }
+    } else {
+        for (int64_t i = 0; i < hd.n; i++) {
+            const uint64_t* e = ent + (size_t)i * pwe;
+            if (e[2] & F_ACC) states.push_back({(int64_t)e[0], (int64_t)e[1], e + 3});
+            if (e[2] & F_TIMER) timers.push_back({(int64_t)e[0], (int64_t)e[1]});
+        }
+    }
+    std::sort(timers.begin(), timers.end(), [&](const std::pair<int64_t, int64_t>& a, const std::pair<int64_t, int64_t>& b) {
+        return a.second != b.second ? a.second < b.second : a.first < b.first;
+    });
+    HeapWriter w;
+    w.be32((uint32_t)key_group);
+    const int16_t order[3] = {ids->window_state, ids->event_timers, ids->processing_timers};
+    int16_t sorted[3] = {order[0], order[1], order[2]};
+    std::sort(sorted, sorted + 3);
+    for (int16_t sid : sorted) {
+        w.be16((uint16_t)sid);
+        if (sid == ids->window_state) {
+            w.be32((uint32_t)states.size());
+            uint64_t v[HEAP_MAX_FIELDS];
+            uint32_t nm;
+            for (const St& s : states) {
+                w.be64((uint64_t)s.ns);
+                write_key(w, s.key);
+                heap_words_to_fields(h, s.acc, v, &nm);
+                heap_write_row(w, h, v, nm);
+            }
+        } else if (sid == ids->event_timers) {
+            w.be32((uint32_t)timers.size());
+            for (const auto& t : timers) {
+                const int64_t ts = tz_epoch_for_timer(win.tz, wsub(t.second, 1));
+                w.be64((uint64_t)ts ^ (1ull << 63));  // MathUtils.flipSignBit
+                write_key(w, t.first);
+                w.be64((uint64_t)t.second);
+            }
+        } else {
+            w.be32(0);  // event-time operator: no processing-time timers
+        }
+    }
+    *size = (int64_t)w.b.size();
+    if (!buf) return FW_OK;
+    if (capacity < *size) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)*size);
+    memcpy(buf, w.b.data(), w.b.size());
+    return FW_OK;
+}
+
+int fw_restore_key_group_heap(fw_handle* h, const void* buf, int64_t size, const fw_heap_state_ids* ids) {
+    if (!h || !buf || size < 0) return fail(FW_E_INVALID, "null argument");
+    int rc = heap_check(h, ids);
+    if (rc) return rc;
+    HeapReader r{(const uint8_t*)buf, (size_t)size};
+    const int32_t kg = (int32_t)r.be32();
+    const int kk = heap_key_kind(h);
+    // keys: BIGINT / INT values, or key-row images numbered in order of appearance
+    std::vector<std::vector<uint8_t>> images;
+    std::map<std::vector<uint8_t>, int64_t> image_id;
+    auto read_key = [&](int64_t* key) -> bool {
+        const uint32_t len = r.be32();
+        if (r.bad || len > (1u << 24)) return false;
+        const uint8_t* p = r.take(len);
+        if (!p) return false;
+        if (kk == FW_KEYHASH_KEYROW) {
+            if (len % 8) return false;
+            std::vector<uint8_t> im(p, p + len);
+            auto it = image_id.find(im);
+            if (it == image_id.end()) {
+                it = image_id.emplace(im, (int64_t)images.size()).first;
+                images.push_back(im);
+            }
+            *key = it->second;
+            return true;
+        }
+        if (len != 16) return false;
+        for (int i = 0; i < 8; i++)
+            if (p[i]) return false;  // RowKind INSERT, key field not NULL
+        uint64_t x;
+        memcpy(&x, p + 8, 8);
+        *key = kk == FW_KEYHASH_BINROW_INT ? (int64_t)(int32_t)(uint32_t)x : (int64_t)x;
+        return kk == FW_KEYHASH_BINROW_BIGINT || (x >> 32) == 0;
+    };
+    struct Acc { uint64_t v[HEAP_MAX_FIELDS]; uint32_t nm; };
+    std::map<std::pair<int64_t, int64_t>, std::pair<int, int>> ent;  // (key, ns) -> (state index or -1, timer)
+    std::vector<Acc> accs;
+    bool seen[3] = {};
+    while (!r.bad && r.at < r.n) {
+        const int16_t sid = (int16_t)r.be16();
+        const uint32_t n = r.be32();
+        if (r.bad) break;
+        if (sid == ids->window_state && !seen[0]) {
+            seen[0] = true;
+            for (uint32_t i = 0; i < n && !r.bad; i++) {
+                const int64_t ns = (int64_t)r.be64();
+                int64_t key;
+                Acc a;
+                if (!read_key(&key) || !heap_read_row(r, h, a.v, &a.nm)) { r.bad = true; break; }
+                auto& slot = ent.emplace(std::make_pair(key, ns), std::make_pair(-1, 0)).first->second;
+                if (slot.first >= 0) return fail(FW_E_INVALID, "duplicate window state (key, namespace) in key group %d", kg);
+                slot.first = (int)accs.size();
+                accs.push_back(a);
+            }
+        } else if (sid == ids->event_timers && !seen[1]) {
+            seen[1] = true;
+            for (uint32_t i = 0; i < n && !r.bad; i++) {
+                const int64_t ts = (int64_t)(r.be64() ^ (1ull << 63));
+                int64_t key;
+                if (!read_key(&key)) { r.bad = true; break; }
+                const int64_t ns = (int64_t)r.be64();
+                if (ts != tz_epoch_for_timer(h->win.tz, wsub(ns, 1)))
+                    return fail(FW_E_INVALID, "timer %lld of window %lld is not the window's end timer", (long long)ts, (long long)ns);
+                ent.emplace(std::make_pair(key, ns), std::make_pair(-1, 0)).first->second.second = 1;
+            }
+        } else if (sid == ids->processing_timers && !seen[2]) {
+            seen[2] = true;
+            if (n != 0) return fail(FW_E_INVALID, "processing-time timers in an event-time window operator");
+        } else {
+            return fail(FW_E_INVALID, "unexpected state id %d in key group %d", (int)sid, kg);
+        }
+    }
+    if (r.bad) return fail(FW_E_INVALID, "heap key-group data truncated or malformed");
+    // -> this library's key-group blob, restored by fw_restore_key_group
+    const int pwe = h->pwe, nw = h->nw_t;
+    const WinDesc& win = h->win;
+    std::vector<uint64_t> out;
+    int64_t n_out = 0;
+    if (win.hopb) {  // (key, sliceEnd) states -> blocks; timers are arithmetic there
+        std::map<std::pair<int64_t, int64_t>, size_t> blk;  // (key, block start) -> word offset
+        for (const auto& kv : ent) {
+            if (kv.second.first < 0) continue;  // a timer without state fires without output
+            const int64_t key = kv.first.first, se = kv.first.second;
+            const int64_t bs = window_start(wsub(se, 1), win.offset, win.hb_span_div);
+            const int slot = (int)((se - bs) / win.interval) - 1;
+            if (slot < 0 || slot >= HB_R || wadd(bs, (int64_t)(slot + 1) * win.interval) != se)
+                return fail(FW_E_INVALID, "namespace %lld is not a slice end of this window", (long long)se);
+            auto it = blk.find({key, bs});
+            if (it == blk.end()) {
+                it = blk.emplace(std::make_pair(key, bs), out.size()).first;
+                out.resize(out.size() + pwe, 0);
+                uint64_t* e = out.data() + it->second;
+                e[0] = (uint64_t)key;
+                e[1] = (uint64_t)bs;
+                for (int s = 0; s < HB_R; s++)
+                    for (int x = 0; x < nw; x++) e[3 + s * nw + x] = x < h->wd.nw ? word_identity(h->wd.op[x]) : 0;
+                n_out++;
+            }
+            uint64_t* e = out.data() + it->second;
+            e[2] |= (uint64_t)(1u << slot) << HB_MASK_SHIFT;
+            const Acc& a = accs[(size_t)kv.second.first];
+            heap_fields_to_words(h, a.v, a.nm, e + 3 + slot * nw);
+        }
+    } else {
+        for (const auto& kv : ent) {
+            out.resize(out.size() + pwe, 0);
+            uint64_t* e = out.data() + (size_t)n_out * pwe;
+            e[0] = (uint64_t)kv.first.first;
+            e[1] = (uint64_t)kv.first.second;
+            e[2] = (kv.second.first >= 0 ? F_ACC : 0u) | (kv.second.second ? F_TIMER : 0u);
+            if (kv.second.first >= 0) heap_fields_to_words(h, accs[(size_t)kv.second.first].v, accs[(size_t)kv.second.first].nm, e + 3);
+            else
+                for (int x = 0; x < nw; x++) e[3 + x] = x < h->wd.nw ? word_identity(h->wd.op[x]) : 0;
+            n_out++;
+        }
+    }
+    Ctrl c;
+    if ((rc = read_ctrl(h, &c))) return rc;
+    KgHeader hd{KG_MAGIC, 3, kg, pwe, h->wd.nw, h->ks.sb_per_kg_log2, h->cfg.key_hash, h->win.size, h->win.interval,
+                c.cur, n_out, semantics_fingerprint(h), (int64_t)h->push_seq};
+    std::vector<uint64_t> blob(sizeof hd / 8);
+    memcpy(blob.data(), &hd, sizeof hd);
+    blob.insert(blob.end(), out.begin(), out.end());
+    if (h->keyrow) {  // key-row section: [n][id, length, image words]
+        blob.push_back((uint64_t)images.size());
+        for (size_t k = 0; k < images.size(); k++) {
+            blob.push_back((uint64_t)k);
+            blob.push_back((uint64_t)images[k].size());
+            const size_t at = blob.size();
+            blob.resize(at + images[k].size() / 8);
+            memcpy(blob.data() + at, images[k].data(), images[k].size());
+        }
+    }
+    return fw_restore_key_group(h, blob.data(), (int64_t)blob.size() * 8);
 }
 
 // ---- host-side restatements (the exact code the kernels run), for host partitioners/tests

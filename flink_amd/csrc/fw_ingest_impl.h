@@ -84,12 +84,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     Ctrl* ctrl = a.ctrl;
     const int64_t c = blockIdx.x;
     kt_start(a.kt);
-    // the push's slot in the partial buffer; k_push_stats (next launch) advances pending_pushes
+    // the push's slot in the partial buffer (the last workgroup of the launch advances
+    // pending_pushes); checked after the column loads are issued, so they need not wait for it
     const int64_t slot = __hip_atomic_load(&ctrl->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
-    if (slot >= FW_MAX_PENDING) {
-        if (tid == 0) __hip_atomic_fetch_or(&ctrl->error, ERR_CHUNKS, __ATOMIC_RELAXED, DEV_SCOPE);
-        return;
-    }
     const int64_t cur_wm = __hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE);
     // adaptive fold: when the LDS fold of the previous push merged < 2 % of its rows (uniform keys
     // spread over many more groups than a chunk holds), skip it -- the merge kernel folds those
@@ -157,6 +154,10 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             const int64_t cnt = a.seg_counts[sg];
             valid &= ~((uint32_t)((int64_t)(g - sg * a.seg_div.d) >= cnt) << j);
         });
+    if (slot >= FW_MAX_PENDING) {  // (uniform) the partial buffer is full: the host sizes pushes so it never is
+        if (tid == 0) __hip_atomic_fetch_or(&ctrl->error, ERR_CHUNKS, __ATOMIC_RELAXED, DEV_SCOPE);
+        return;
+    }
     // arrival ordinal base of this chunk within the flush (W_Q* words; >= 1, see record_word)
     const uint32_t ord0 = (uint32_t)(slot * a.cap_rows + base) + 1u;
     // TIMESTAMP_LTZ: slices live on the shift zone's wall clock (AbstractSliceAssigner

@@ -151,6 +151,8 @@ FW_HD uint64_t word_identity(int32_t op) {
 FW_HD bool is_qword(int32_t op) { return op >= W_QMIN && op <= W_QZERO; }
 FW_HD bool is_dnword(int32_t op) { return op == W_DNHI || op == W_DNLO; }
 constexpr uint64_t Q_EMPTY = ~0ull;
+FW_HD bool f64_isnan(uint64_t b) { return (b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull; }
+FW_HD bool f64_iszero(uint64_t b) { return (b & 0x7FFFFFFFFFFFFFFFull) == 0; }
 
 // Entry flags of the HBM slice-state table.
 constexpr uint32_t F_ACC = 1u;    // windowState(key, slice) != null
@@ -265,6 +267,7 @@ struct WinDesc {
 constexpr int KIND_DSWIN = 3;
 constexpr int KIND_HOPB = 4;  // SQL HOP, block state (fw_merge_hopb.h)
 constexpr int HB_R = 8;       // slices per HOP block entry
+constexpr uint32_t HB_MASK_SHIFT = 8;  // block entry flag bits 8.. : slot i holds data
 
 // TimeWindowUtil.isWindowFired in the window's shift zone (UTC when tz.n == 0)
 FW_HD bool win_fired(const WinDesc& w, int64_t we, int64_t progress) {

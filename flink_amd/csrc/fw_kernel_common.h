@@ -42,8 +42,6 @@ __device__ __forceinline__ uint64_t pick_col(const uint64_t (&v)[N], int32_t col
     return r;
 }
 
-__device__ __forceinline__ bool f64_isnan(uint64_t b) { return (b & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull; }
-__device__ __forceinline__ bool f64_iszero(uint64_t b) { return (b & 0x7FFFFFFFFFFFFFFFull) == 0; }
 
 // value of one accumulator word for a single non-NULL record (accumulate on the identity);
 // `ord` >= 1 is the record's arrival ordinal within the flush (W_Q*, W_DN* words), `gord` its

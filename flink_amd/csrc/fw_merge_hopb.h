@@ -22,7 +22,6 @@
 
 namespace fw {
 
-constexpr uint32_t HB_MASK_SHIFT = 8;  // flag bits 8.. : slot i holds data
 
 // Finds (k, bs) or inserts it with an identity ring; *inserted tells the caller it was new.
 template <int NWP, int E, uint32_t OPS>
@@ -201,16 +200,11 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
         };
         const int lane = tid & 63, wv = tid >> 6;
         auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
-        // this lane's cell word of its wave's first group in every pending push, loaded beside the state
-        uint32_t v_first[MG_PREFETCH];
-#pragma unroll
-        for (int q = 0; q < MG_PREFETCH; q++) {
-            v_first[q] = 0;
-            if (do_flush && q < pend) {
-                const int G0 = gather_group((int)cell_pad(a.slot_nch[q]));
-                if (lane < G0) v_first[q] = cell_at(q, wv * G0 + lane);
-            }
-        }
+        // this lane's cell word of its wave's first group in push 0 (the next push's is loaded at the top
+        // of each push's loop, FW_MG_ROLL)
+        uint32_t v_first = 0;
+        if (do_flush && lane < gather_group((int)cell_pad(a.slot_nch[0])))
+            v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
         // ---- load the superbucket's block entries into LDS
         for (int i = tid; i < StateLds<NA, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
         if (tid == 0) {
@@ -246,7 +240,14 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
                 const int ngroups = ncell / G;
                 for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                     const int f = g * G + lane;
-                    const uint32_t v = lane >= G ? 0u : (g == wv && pi < MG_PREFETCH) ? pick_pending(v_first, pi) : cell_at(pi, f);
+                    const uint32_t v = lane >= G ? 0u : (g == wv && (FW_MG_ROLL || pi == 0)) ? v_first : cell_at(pi, f);
+                    if (FW_MG_ROLL && g == wv) {  // the next push's first cell word, in flight during this push
+                        v_first = 0;
+                        if (pi + 1 < pend) {
+                            const int G1 = gather_group((int)cell_pad(a.slot_nch[pi + 1]));
+                            if (lane < G1) v_first = cell_at(pi + 1, wv * G1 + lane);
+                        }
+                    }
                     const CellGroup cg = cell_group(v, f, CH);
                     const uint32_t tot = cg.tot;
                     for (uint32_t r0 = 0; r0 < tot; r0 += 64 * GU) {

@@ -675,18 +675,9 @@ constexpr int mg_rows_in_flight(int nw) {
     return MG_BLOCK <= 512 ? (nw <= 1 ? 2 * FW_GU1 : nw <= 2 ? 6 : nw <= 4 ? 4 : 2) : (nw <= 1 ? FW_GU1 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1);
 }
 
-// element i of the per-push cell-word prefetch (no dynamic register indexing)
-#ifndef FW_MG_PREFETCH
-#define FW_MG_PREFETCH 1
+#ifndef FW_MG_ROLL
+#define FW_MG_ROLL 1
 #endif
-constexpr int MG_PREFETCH = FW_MG_PREFETCH;  // pending pushes whose first cell words a merge wave loads up front
-__device__ __forceinline__ uint32_t pick_pending(const uint32_t (&v)[MG_PREFETCH], int64_t i) {
-    uint32_t r = v[0];
-#pragma unroll
-    for (int q = 1; q < MG_PREFETCH; q++)
-        if (i == q) r = v[q];
-    return r;
-}
 
 // ---- the gather's view of the pending partials.  A wave takes a group of up to 64 consecutive
 // cells of one push slot (lane l holds cell word v of flat cell position f), scans their row
@@ -863,17 +854,12 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // cells, one group per wave per pass (16 groups when a push has <= 1024 cells)
     const int lane = tid & 63, wv = tid >> 6;
     auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
-    // this lane's cell word of its wave's first group in EVERY pending push, loaded beside the state
-    // (a wave usually has one group per push: its cell round trip leaves the gather loop)
-    uint32_t v_first[MG_PREFETCH];
-#pragma unroll
-    for (int q = 0; q < MG_PREFETCH; q++) {
-        v_first[q] = 0;
-        if (gather && q < pend) {
-            const int G0 = gather_group((int)cell_pad(a.slot_nch[q]));
-            if (lane < G0) v_first[q] = cell_at(q, wv * G0 + lane);
-        }
-    }
+    // this lane's cell word of its wave's first group in push 0, loaded beside the state; each
+    // push's loop then loads the next push's first cell word before it gathers (FW_MG_ROLL), so that
+    // round trip overlaps the current push's rows
+    uint32_t v_first = 0;
+    if (gather && lane < gather_group((int)cell_pad(a.slot_nch[0])))
+        v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
     // ---- load this superbucket's entries into LDS
     for (int i = tid; i < StateLds<NW, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
     if (tid == 0) {
@@ -925,7 +911,14 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                 const int f = g * G + lane;
                 uint64_t gc0 = gst ? __builtin_amdgcn_s_memtime() : 0;
-                const uint32_t v = lane >= G ? 0u : (g == wv && pi < MG_PREFETCH) ? pick_pending(v_first, pi) : cell_at(pi, f);
+                const uint32_t v = lane >= G ? 0u : (g == wv && (FW_MG_ROLL || pi == 0)) ? v_first : cell_at(pi, f);
+                    if (FW_MG_ROLL && g == wv) {  // the next push's first cell word, in flight during this push
+                        v_first = 0;
+                        if (pi + 1 < pend) {
+                            const int G1 = gather_group((int)cell_pad(a.slot_nch[pi + 1]));
+                            if (lane < G1) v_first = cell_at(pi + 1, wv * G1 + lane);
+                        }
+                    }
                 if (gst) {  // diagnostic: cell word wait
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     const uint64_t g1 = __builtin_amdgcn_s_memtime();
@@ -1035,11 +1028,27 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // WindowOperator.java:418-426).  Every such element emits the window's contents as of its own
     // arrival: the state before this flush plus the late elements of the same (key, window) up to
     // it (arrival ordinals).  Pass 1 emits from the unchanged state, pass 2 adds the elements to
-    // all their live windows.  Quadratic in the late rows of a superbucket (bounded by lfire_cap).
+    // all their live windows.  The superbucket's rows are listed in LDS first (one scan of the
+    // launch's rows), so both passes cost O(rows of this superbucket^2 x windows per row); beyond
+    // LF_LDS rows the passes scan the launch's rows instead.
     if (KIND == KIND_DSWIN && gather && nlf > 0) {
+        constexpr int LF_LDS = 1024;
+        __shared__ int32_t s_lf[LF_LDS];
+        __shared__ int s_nlf;
+        if (tid == 0) s_nlf = 0;
+        __syncthreads();
+        for (int64_t r = tid; r < nlf; r += MG_BLOCK)
+            if ((uint32_t)a.lfire[(size_t)r * LFW + 2] == (uint32_t)sb) {
+                const int q = atomicAdd(&s_nlf, 1);
+                if (q < LF_LDS) s_lf[q] = (int32_t)r;
+            }
+        __syncthreads();
+        const bool listed = s_nlf <= LF_LDS;
+        const int64_t nscan = listed ? (int64_t)s_nlf : nlf;
+        auto lf_row = [&](int64_t i) { return a.lfire + (size_t)(listed ? (int64_t)s_lf[i] : i) * LFW; };
         const WinDesc& w = a.win;
-        for (int64_t r = tid; r < nlf; r += MG_BLOCK) {
-            const uint64_t* p = a.lfire + (size_t)r * LFW;
+        for (int64_t r = tid; r < nscan; r += MG_BLOCK) {
+            const uint64_t* p = lf_row(r);
             if ((uint32_t)p[2] != (uint32_t)sb) continue;
             const int64_t k = (int64_t)p[0], pe = (int64_t)p[1];
             const uint32_t ord = (uint32_t)(p[2] >> 32);
@@ -1055,8 +1064,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                 } else {
                     acc_identity<NW>(a.wd, acc);
                 }
-                for (int64_t q2 = 0; q2 < nlf; q2++) {
-                    const uint64_t* o = a.lfire + (size_t)q2 * LFW;
+                for (int64_t q2 = 0; q2 < nscan; q2++) {
+                    const uint64_t* o = lf_row(q2);
                     if ((uint32_t)o[2] != (uint32_t)sb || (int64_t)o[0] != k || (uint32_t)(o[2] >> 32) > ord) continue;
                     if (!ds_pane_in_window(w, (int64_t)o[1], e)) continue;
 #pragma unroll
@@ -1067,8 +1076,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             }
         }
         __syncthreads();
-        for (int64_t r = tid; r < nlf; r += MG_BLOCK) {
-            const uint64_t* p = a.lfire + (size_t)r * LFW;
+        for (int64_t r = tid; r < nscan; r += MG_BLOCK) {
+            const uint64_t* p = lf_row(r);
             if ((uint32_t)p[2] != (uint32_t)sb) continue;
             uint64_t v[NW];
 #pragma unroll

@@ -387,6 +387,23 @@ class WindowAggHandle:
         check(lib().fw_restore_key_group(self._h, buf, len(blob)))
         self.push_seq = max(self.push_seq, _snapshot_push_seq(blob))
 
+    def snapshot_key_group_heap(self, kg: int, ids=(0, 1, 2)) -> bytes:
+        """Key group `kg` in the heap keyed-state backend's byte format (flinkwin.h
+        fw_snapshot_key_group_heap); ids = (window-aggs, event timers, processing timers) state ids."""
+        sid = abi.fw_heap_state_ids(*ids, 0)
+        size = C.c_int64()
+        check(lib().fw_snapshot_key_group_heap(self._h, kg, C.byref(sid), None, 0, C.byref(size)))
+        buf = C.create_string_buffer(max(size.value, 1))
+        check(lib().fw_snapshot_key_group_heap(self._h, kg, C.byref(sid), buf, size.value, C.byref(size)))
+        return buf.raw[:size.value]
+
+    def restore_key_group_heap(self, blob: bytes, ids=(0, 1, 2)):
+        """Adds one key group written in the heap backend's format (by this library or by a heap
+        backend) to this handle."""
+        sid = abi.fw_heap_state_ids(*ids, 0)
+        buf = C.create_string_buffer(blob, max(len(blob), 1))
+        check(lib().fw_restore_key_group_heap(self._h, buf, len(blob), C.byref(sid)))
+
     def restore(self, blob: bytes):
         buf = C.create_string_buffer(blob, len(blob))
         check(lib().fw_restore(self._h, buf, len(blob)))

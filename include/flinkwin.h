@@ -412,6 +412,34 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size);
 int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t capacity, int64_t* size);
 int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size);
 
+/* v6: one key group in the HEAP keyed-state backend's own byte format, so a savepoint writer /
+   reader on the Java side can move window state between this library and a heap-backend
+   WindowAggOperator.  Layout (HeapSnapshotStrategy.java:161-172): writeInt(keyGroup), then per
+   state in ascending id order writeShort(id) and
+     window_state  ("window-aggs" ValueState, CopyOnWriteStateMapSnapshot.writeState :127-149):
+                   writeInt(n), n x [namespace: 8 B big-endian slice end][key: writeInt(len) +
+                   BinaryRowData bytes][accumulator: writeInt(len) + BinaryRowData bytes]
+     event_timers  ("_timer_state/event_window-timers", KeyGroupPartitioner.java:241-254 +
+                   TimerSerializer.serialize :147-152): writeInt(n), n x [writeLong(flipSignBit(
+                   toEpochMillsForTimer(window - 1)))][key][namespace]
+     processing_timers: writeInt(0).
+   The accumulator row holds the aggregates' buffer fields in order (COUNT(*)/COUNT: BIGINT count;
+   SUM/MIN/MAX: the aggregate's type, NULL-able; AVG: sum BIGINT|DOUBLE, count BIGINT) -- the
+   LOCAL phase's output columns.  SQL ONE / GLOBAL phase with BINROW_BIGINT, BINROW_INT or KEYROW
+   keys only.  HOP operators with block state export every slice with data and the
+   timers the reference holds, except a chain timer at an EMPTY window (it fires without output);
+   on restore they derive their timers from the data.  The restore side accepts the states in any
+   order; restoring twice into one key group, or a key of another group, is an error. */
+typedef struct {
+    int16_t window_state;
+    int16_t event_timers;
+    int16_t processing_timers;
+    int16_t reserved;
+} fw_heap_state_ids;
+int fw_snapshot_key_group_heap(fw_handle* h, int32_t key_group, const fw_heap_state_ids* ids, void* buf,
+                               int64_t capacity, int64_t* size);
+int fw_restore_key_group_heap(fw_handle* h, const void* buf, int64_t size, const fw_heap_state_ids* ids);
+
 /* ---- key rows: VARCHAR / composite keys ------------------------------------------------ */
 /* A key row field, as the key projection writes it into a BinaryRowData (BinaryRowWriter,
    TR/data/writer/BinaryRowWriter.java:39-122 + AbstractBinaryWriter.java:83-106,242-345).

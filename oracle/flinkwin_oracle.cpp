@@ -940,6 +940,37 @@ int64_t or_state_size(void* h) { return (int64_t)((Oracle*)h)->state.size(); }
 int64_t or_timer_count(void* h) { return (int64_t)((Oracle*)h)->timers.size(); }
 int64_t or_current_watermark(void* h) { return ((Oracle*)h)->current_watermark; }
 
+// Keyed state and timers as the heap backend holds them: (key, namespace, accumulator fields) per
+// window state entry and (timestamp, key, namespace) per event-time timer, for checking
+// fw_snapshot_key_group_heap.  Return the entry counts (rows beyond cap are not written);
+// fields[i * FW_MAX_AGGS * 2 + j].
+int64_t or_state_dump(void* h, int64_t* key, int64_t* ns, uint64_t* fields, uint32_t* nm, int64_t cap) {
+    Oracle* o = (Oracle*)h;
+    int64_t i = 0;
+    for (const auto& kv : o->state) {
+        if (i < cap) {
+            key[i] = kv.first.first;
+            ns[i] = kv.first.second;
+            o->acc_fields(kv.second, fields + i * FW_MAX_AGGS * 2, nm + i);
+        }
+        i++;
+    }
+    return i;
+}
+int64_t or_timer_dump(void* h, int64_t* ts, int64_t* key, int64_t* ns, int64_t cap) {
+    Oracle* o = (Oracle*)h;
+    int64_t i = 0;
+    for (const auto& t : o->timers) {
+        if (i < cap) {
+            ts[i] = std::get<0>(t);
+            key[i] = std::get<1>(t);
+            ns[i] = std::get<2>(t);
+        }
+        i++;
+    }
+    return i;
+}
+
 int64_t or_num_results(void* h) { return (int64_t)((Oracle*)h)->out.size(); }
 // result value columns: the aggregates, or the LOCAL phase's accumulator fields
 int32_t or_num_value_columns(void* h) {

@@ -44,6 +44,10 @@ def lib():
             getattr(L, f).restype = i64
             getattr(L, f).argtypes = [vp]
         L.or_get_results.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.or_state_dump.restype = i64
+        L.or_state_dump.argtypes = [vp, vp, vp, vp, vp, i64]
+        L.or_timer_dump.restype = i64
+        L.or_timer_dump.argtypes = [vp, vp, vp, vp, i64]
         L.or_clear_results.argtypes = [vp]
         L.or_get_first.argtypes = [vp, vp]
         L.or_num_side_rows.restype = i64
@@ -130,6 +134,24 @@ class OracleOperator:
     @property
     def state_size(self):
         return lib().or_state_size(self.h)
+
+    def keyed_state(self):
+        """(key, namespace, fields[nf], null_mask) of every window state entry, and (timestamp, key,
+        namespace) of every event-time timer -- the contents a heap backend would snapshot."""
+        L = lib()
+        n = L.or_state_dump(self.h, None, None, None, None, 0)
+        key, ns = np.zeros(n, np.int64), np.zeros(n, np.int64)
+        fields = np.zeros((n, 2 * abi.FW_MAX_AGGS), np.uint64)
+        nm = np.zeros(n, np.uint32)
+        L.or_state_dump(self.h, _ptr(key), _ptr(ns), _ptr(fields), _ptr(nm), n)
+        m = L.or_timer_dump(self.h, None, None, None, 0)
+        ts, tk, tn = np.zeros(m, np.int64), np.zeros(m, np.int64), np.zeros(m, np.int64)
+        L.or_timer_dump(self.h, _ptr(ts), _ptr(tk), _ptr(tn), m)
+        nf = L.or_num_value_columns(self.h) if self.cfg.agg_phase == abi.PHASE_LOCAL else sum(
+            2 if self.cfg.aggs[g].kind == abi.AGG_AVG else 1 for g in range(self.cfg.n_aggs))
+        states = [(int(key[i]), int(ns[i]), [int(x) for x in fields[i, :nf]], int(nm[i])) for i in range(n)]
+        timers = [(int(ts[i]), int(tk[i]), int(tn[i])) for i in range(m)]
+        return states, timers
 
     def results(self, clear=True):
         L = lib()

@@ -802,3 +802,44 @@ def test_two_phase_device_step_matches_one_phase(name):
                  f"{name} batch {bi}")
     assert tp.glob.stats()["error_flags"] == 0 and tp.local.stats()["error_flags"] == 0
     tp.close()
+
+
+@pytest.mark.parametrize("n_keys", [3, 5000])
+def test_ds_many_late_fire_rows_match_oracle(n_keys):
+    """A burst of late elements within allowedLateness: each fires its window at once with the
+    element added (EventTimeTrigger.onElement -> FIRE).  3 keys put ~2000 late rows into one
+    superbucket (beyond the merge kernel's LDS list of 1024: the scan path), 5000 keys spread them
+    (the LDS list path); every late row emits one window row, bit-exact with the oracle."""
+    _torch_cuda()
+    import time
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = CASES["ds_tumble_lateness"]  # 4 s windows, 3 s lateness
+    cfg = _cfg(kw)
+    o, g = OracleOperator(cfg), WindowAggHandle(cfg)
+    rng = np.random.default_rng(n_keys)
+    t0 = 1_600_000_000_000
+    n = 6000
+    k = rng.integers(0, n_keys, n).astype(np.int64)
+    t = (t0 + rng.integers(0, 8000, n)).astype(np.int64)
+    iv = rng.integers(-1000, 1000, n).astype(np.int64)
+    batches = [(k, t, iv, t0 + 8000)]
+    # late elements into the fired windows [t0, t0+4000) and [t0+4000, t0+8000): cleanup at +3 s
+    k2 = rng.integers(0, n_keys, n).astype(np.int64)
+    t2 = (t0 + 4000 + rng.integers(0, 4000, n)).astype(np.int64)
+    batches.append((k2, t2, rng.integers(-1000, 1000, n).astype(np.int64), t0 + 9000))
+    batches.append((k2[:100], t2[:100] + 4000, iv[:100], t0 + 20000))
+    dt = 0.0
+    for bi, (kk, tt, vv, wm) in enumerate(batches):
+        vals = [vv, np.zeros(len(kk), np.int64)]
+        o.process_batch(kk, tt, vals)
+        g.push_host(kk, tt, vals)
+        o.process_watermark(wm)
+        t_start = time.perf_counter()
+        g.advance(wm)
+        res = g.results(reset=True)
+        dt = max(dt, time.perf_counter() - t_start)
+        _compare(_rows(res, cfg, set()), _rows(o.results(clear=True), cfg, set()), set(), f"batch {bi}")
+    assert g.stats()["error_flags"] == 0
+    print(f"n_keys={n_keys}: slowest advance {dt * 1e3:.1f} ms")
+    g.close()

@@ -138,7 +138,7 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged end-to-end leg (N=1 only)")
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: time the steps without the per-launch hipEvents (no roofline)")
-    ap.add_argument("--e2e-steps", type=int, default=6)
+    ap.add_argument("--e2e-steps", type=int, default=8)
     ap.add_argument("--kernel-timing", default="device", choices=["device", "events"],
                     help="per-launch kernel timing: in-kernel device-clock stamps (default) or hipEvents")
     ap.add_argument("--plan", default="auto", choices=["auto", "one", "two"],
@@ -405,7 +405,7 @@ def main():
     if world == 1 and not args.no_e2e and args.e2e_steps > 0:
         from concurrent.futures import ThreadPoolExecutor
         from flink_amd.runtime.handle import _np_view
-        ns = args.e2e_steps
+        ns = min(args.e2e_steps, gk.shape[0])
         hk = [gk[b].cpu().numpy() for b in range(ns)]
         ht = [gt[b].cpu().numpy() for b in range(ns)]
         hv = [gv[b].cpu().numpy() for b in range(ns)]
@@ -421,8 +421,10 @@ def main():
         cols = abi.fw_host_cols()
         _native.check(L.fw_reserve(he._h, 0, C.byref(cols)))  # allocates the staging (untimed)
         _native.check(L.fw_commit(he._h, 0))
+        he.results_async()  # allocates the pinned result buffers (untimed); nothing to collect yet
+        he.results_ready(copy=False)
         rows_out = 0
-        t_reserve = t_fill = t_ready = 0.0
+        t_reserve = t_fill = t_ready = t_commit = t_adv = t_async = 0.0
         te0 = time.perf_counter()
         for b in range(ns):
             t1 = time.perf_counter()
@@ -434,6 +436,7 @@ def main():
                 f.result()
             t3 = time.perf_counter()
             _native.check(L.fw_commit(he._h, B))
+            t3c = time.perf_counter()
             he.advance(watermark(b, wl["rate"]))
             t4 = time.perf_counter()
             if b:
@@ -442,7 +445,10 @@ def main():
             he.results_async()
             t_reserve += t2 - t1
             t_fill += t3 - t2
+            t_commit += t3c - t3
+            t_adv += t4 - t3c
             t_ready += t5 - t4
+            t_async += time.perf_counter() - t5
         t6 = time.perf_counter()
         rows_out += len(he.results_ready(copy=False)["key"])
         he.sync()
@@ -454,7 +460,10 @@ def main():
                "ms_per_step": te / ns * 1e3, "result_rows": rows_out,
                "host_ms_per_step": {"fill_pinned_8_threads": t_fill / ns * 1e3,
                                     "reserve_wait_h2d": t_reserve / ns * 1e3,
-                                    "results_ready_wait": t_ready / ns * 1e3},
+                                    "commit_enqueue_h2d_ingest": t_commit / ns * 1e3,
+                                    "advance_enqueue": t_adv / ns * 1e3,
+                                    "results_ready_wait": t_ready / ns * 1e3,
+                                    "results_async_enqueue": t_async / ns * 1e3},
                "fill_GBps": ns * B * wl["w_in"] / max(t_fill, 1e-9) / 1e9,
                "path": "numpy batch -> pinned staging (fw_reserve, 8 fill threads) -> H2D on the copy stream, "
                        "overlapping the previous batch's ingest (fw_commit) -> advance -> rows into pinned host "

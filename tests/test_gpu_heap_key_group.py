@@ -23,7 +23,7 @@ HEAP_CASES = {
                                   aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MIN, 1, F64),
                                         (abi.AGG_COUNT, 0, I64)]),
     "tumble_avg_nullable": dict(window_kind=abi.WIN_TUMBLE, size_ms=5000, nullable_cols=[0, 1],
-                                aggs=[(abi.AGG_AVG, 1, F64), (abi.AGG_MAX, 0, I64), (abi.AGG_COUNT, 1, I64),
+                                aggs=[(abi.AGG_AVG, 1, F64), (abi.AGG_MAX, 0, I64), (abi.AGG_COUNT, 1, F64),
                                       (abi.AGG_SUM, 1, F64)]),
     "tumble_int_offset": dict(window_kind=abi.WIN_TUMBLE, size_ms=7000, offset_ms=-2500, value_col_types=[I32, F64],
                               aggs=[(abi.AGG_SUM, 0, I32), (abi.AGG_MAX, 0, I32), (abi.AGG_AVG, 0, I32)]),

@@ -211,7 +211,12 @@ def main():
     def push_step(b, handle):
         """Ingest step b; returns the watermark to advance to (the valve's minimum over subtasks)."""
         if world == 1:
-            handle.push_device(gk[b], gt[b], [gv[b]] if nv else [])
+            if isinstance(handle, WindowAggHandle):
+                # the batches were generated and synchronised before the timed region: the C-ABI
+                # push as a JNI shim makes it, without torch stream events
+                handle.push_device(gk[b], gt[b], [gv[b]] if nv else [], producer_synced=True)
+            else:
+                handle.push_device(gk[b], gt[b], [gv[b]] if nv else [])
             return watermark(b, wl["rate"])
         # the received segments' ingest is queued before the host waits for the partition's
         # counts (overflow round + watermark valve), so the GPU stays busy through that host step

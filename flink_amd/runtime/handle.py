@@ -146,12 +146,23 @@ class WindowAggHandle:
         self.push_seq += 1
         self._end_read(cur)
 
-    def push_device(self, keys, ts, values=(), key_hashes=None, nulls=None):
+    def push_device(self, keys, ts, values=(), key_hashes=None, nulls=None, producer_synced=False):
         """Device-resident columns (torch cuda tensors, int64 / float64; ``nulls``: {column:
         uint8 tensor}).  The handle's stream waits for the producer's current stream before
-        reading them."""
+        reading them -- unless ``producer_synced``: the caller guarantees the columns are complete
+        (synchronised) and stay unmodified until the handle has read them (the C-ABI contract of
+        fw_push_device, as a JNI shim calls it), and no stream events are recorded."""
         n = keys.numel()
         if n == 0:
+            return
+        if producer_synced:
+            arr = (C.c_void_p * abi.FW_MAX_COLS)(*[v.data_ptr() for v in values])
+            nul = (C.c_void_p * abi.FW_MAX_COLS)()
+            for c, v in (nulls or {}).items():
+                nul[c] = v.data_ptr()
+            check(lib().fw_push_device(self._h, n, keys.data_ptr(), ts.data_ptr(),
+                                       key_hashes.data_ptr() if key_hashes is not None else None, arr, nul))
+            self.push_seq += 1
             return
         cur = self._begin_read(keys.device)
         arr = (C.c_void_p * abi.FW_MAX_COLS)()

@@ -511,9 +511,22 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     // the XCD's L2, so any XCD reads them), then takes a ticket; the last workgroup of the launch
     // reduces every chunk's stats into the control block and commits the push's slot
     // (RecordsWindowBuffer's minSliceEnd and the late-drop counter).  No extra launch.
-    if (lmin != INT64_MAX) __hip_atomic_fetch_min(s_min, lmin, __ATOMIC_RELAXED, LDS_SCOPE);
-    if (ldrop) atomicAdd(s_drop, (unsigned long long)ldrop);
-    if (lrows) atomicAdd(s_rows, (unsigned long long)lrows);
+    // wave reductions first: one LDS atomic per wave, not 3 x 512 on the same three words (they
+    // serialise: ~10 us of a CFG2 launch)
+    {
+        const int64_t wm = wave_min_i64(lmin);
+        uint32_t wd = ldrop, wr = lrows;
+#pragma unroll
+        for (int k = 32; k > 0; k >>= 1) {
+            wd += __shfl_xor(wd, k, 64);
+            wr += __shfl_xor(wr, k, 64);
+        }
+        if ((tid & 63) == 0) {
+            if (wm != INT64_MAX) __hip_atomic_fetch_min(s_min, wm, __ATOMIC_RELAXED, LDS_SCOPE);
+            if (wd) atomicAdd(s_drop, (unsigned long long)wd);
+            if (wr) atomicAdd(s_rows, (unsigned long long)wr);
+        }
+    }
     __syncthreads();
     int32_t* s_last = (int32_t*)&lds[3];
     if (tid == 0) {

@@ -50,10 +50,10 @@ def main():
             for b in range(nb):
                 h.push_device(gk[b], gt[b], [gv[b]] if wl["value_cols"] else [])
             ms, n = h.kernel_times()["reduce"]
-            if rep:
+            if rep and n:
                 times.append(ms / n * 1e3)
             h.close()
-        out[ab] = sum(times) / len(times)
+        out[ab] = sum(times) / len(times) if times else float("nan")  # early-exit ablations: time with rocprofv3
         print(json.dumps({"workload": wl_name, "ablate": ab, "k_ingest_us": round(out[ab], 2)}), flush=True)
     os.environ.pop("FW_ABLATE", None)
 

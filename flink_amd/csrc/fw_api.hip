@@ -1792,7 +1792,7 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    SnapHeader hd{SNAP_MAGIC, 3, nsb, h->cap_e, pwe, c.cur, (int64_t)c.late_dropped, 0, total, semantics_fingerprint(h),
+    SnapHeader hd{SNAP_MAGIC, 3, nsb, h->cap_e, pwe, std::max(c.cur, h->host_cur), (int64_t)c.late_dropped, 0, total, semantics_fingerprint(h),
                   (int64_t)h->push_seq};
     char* p = (char*)buf;
     memcpy(p, &hd, sizeof hd);
@@ -1923,7 +1923,8 @@ int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t ca
     *size = need;
     if (!buf) return FW_OK;
     if (capacity < need) return fail(FW_E_INVALID, "snapshot buffer too small (%lld < %lld)", (long long)capacity, (long long)need);
-    KgHeader hd{KG_MAGIC, 3, key_group, pwe, h->wd.nw, L, h->cfg.key_hash, h->win.size, h->win.interval, c.cur, total,
+    KgHeader hd{KG_MAGIC, 3, key_group, pwe, h->wd.nw, L, h->cfg.key_hash, h->win.size, h->win.interval,
+                std::max(c.cur, h->host_cur), total,
                 semantics_fingerprint(h), (int64_t)h->push_seq};
     memcpy(buf, &hd, sizeof hd);
     memcpy((char*)buf + sizeof hd, ent.data(), ent.size() * 8);

@@ -32,6 +32,9 @@ HEAP_CASES = {
     "hop_slices": CASES["sql_hop"],
     "cumulate": CASES["sql_cumulate_countstar"],
     "cumulate_nocount": CASES["sql_cumulate_nocount"],
+    # GLOBAL phase: the value columns are LOCAL accumulator fields (count, DOUBLE max), rows at slice ends
+    "global_tumble": dict(window_kind=abi.WIN_TUMBLE, size_ms=4000, agg_phase=abi.PHASE_GLOBAL, nullable_cols=[1],
+                          aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_MAX, 1, F64)]),
     "tumble_shift_zone": dict(window_kind=abi.WIN_TUMBLE, size_ms=3600000, shift_zone="America/Los_Angeles",
                               aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_MIN, 0, I64)]),
 }
@@ -76,6 +79,9 @@ def _heap_stream(kw, seed):
     nulls = None
     if kw.get("nullable_cols"):
         nulls = [{c: (rng.random(len(b[0])) < 0.2).astype(np.uint8) for c in kw["nullable_cols"]} for b in batches]
+    if kw.get("agg_phase") == abi.PHASE_GLOBAL:  # local rows: slice-end timestamps, counts >= 1
+        size = kw["size_ms"]
+        batches = [(k, (t // size + 1) * size, np.abs(iv) + 1, dv, wm) for k, t, iv, dv, wm in batches]
     if kw.get("value_col_types", [I64])[0] == I32:
         batches = [(k, t, (iv * 2_000_003) % (1 << 31) - (1 << 30), dv, wm) for k, t, iv, dv, wm in batches]
     return batches, nulls

@@ -201,12 +201,13 @@ def _route(rows, types, p):
     return np.array([O.operator_index(128, p, O.key_group(abi.KEYHASH_PRECOMPUTED, 0, 128, pre=int(x))) for x in h])
 
 
-@pytest.mark.parametrize("p_from,p_to", [(2, 3), (3, 1)])
-def test_key_row_rescale_restore_by_key_group(p_from, p_to):
+@pytest.mark.parametrize("p_from,p_to,fmt", [(2, 3, "own"), (3, 1, "own"), (2, 3, "heap")])
+def test_key_row_rescale_restore_by_key_group(p_from, p_to, fmt):
     """(VARCHAR, BIGINT) keys, CUMULATE: checkpoint at parallelism p_from, restore the key groups
     at p_to through the ABI (each blob carries its key rows; the restoring subtask interns them and
     routes each by its hashCode), continue; the union of results equals one oracle restarted at the
-    same cut."""
+    same cut.  fmt "heap": the key groups travel in the heap backend's bytes
+    (fw_snapshot_key_group_heap: key = the key row's BinaryRowData image)."""
     from flink_amd import abi
     from flink_amd.table.slice_assigners import SliceAssigners
     from flink_amd.table.window_agg import WindowAggOperator
@@ -232,12 +233,20 @@ def test_key_row_rescale_restore_by_key_group(p_from, p_to):
                 for op in ops:
                     op.prepare_snapshot_pre_barrier()
                     bl, wm_ = op.handle.snapshot_key_groups()
+                    if fmt == "heap":
+                        bl = {kg: op.handle.snapshot_key_group_heap(kg) for kg in bl}
                     blobs.update(bl)
                     wms.append(wm_)
                     op.close()
                 ops = [WindowAggOperator(parallelism=p_to, subtask_index=i, **kw).open() for i in range(p_to)]
                 for op in ops:
-                    op.handle.restore_key_groups(blobs, wms)
+                    if fmt == "heap":
+                        lo, hi = op.handle.key_group_range()
+                        for kg in range(lo, hi + 1):
+                            op.handle.restore_key_group_heap(blobs[kg])
+                        op.handle.initialize_watermark(min(wms))
+                    else:
+                        op.handle.restore_key_groups(blobs, wms)
                 orc.snapshot_restore()
             p = len(ops)
             rows = [universe[i] for i in rng.integers(0, len(universe), 1500)]

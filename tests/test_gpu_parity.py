@@ -843,3 +843,27 @@ def test_ds_many_late_fire_rows_match_oracle(n_keys):
     assert g.stats()["error_flags"] == 0
     print(f"n_keys={n_keys}: slowest advance {dt * 1e3:.1f} ms")
     g.close()
+
+
+def test_skipped_advance_keeps_watermark_through_snapshot():
+    """An advance that crosses no slice end launches nothing (fw_advance's idle skip), yet the
+    operator's currentWatermark is the new one: in stats, in a full snapshot and in a key-group
+    blob (the union-list watermark state each subtask contributes)."""
+    _torch_cuda()
+    from flink_amd.runtime.handle import WindowAggHandle
+    cfg = _cfg(CASES["sql_tumble_int_aggs"], key_hash=abi.KEYHASH_BINROW_BIGINT)
+    g = WindowAggHandle(cfg)
+    t0 = 1_600_000_000_000  # a multiple of the 10 s window
+    k = np.arange(1000, dtype=np.int64)
+    g.push_host(k, t0 + k, [k, k])
+    g.advance(t0 + 10_000)      # fires [t0, t0 + 10 s)
+    g.advance(t0 + 12_345)      # crosses no slice end: skipped
+    assert g.stats()["current_watermark"] == t0 + 12_345
+    blob = g.snapshot()
+    h = WindowAggHandle(cfg)
+    h.restore(blob)
+    assert h.stats()["current_watermark"] == t0 + 12_345
+    _, wm = g.snapshot_key_groups()
+    assert wm == t0 + 12_345
+    for x in (g, h):
+        x.close()

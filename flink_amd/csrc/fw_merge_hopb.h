@@ -232,8 +232,90 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
             }
         }
         __syncthreads();
-        // ---- flush: every pending partial (key, sliceEnd, acc) folds into its block's slot
-        if (do_flush) {
+        // ---- flush: every pending partial (key, sliceEnd, acc) folds into its block's slot.  One
+        // accumulator word (COUNT(*)): software-pipelined over the wave's blocks of rows, as in
+        // k_merge_fire (the next block's rows in flight while the current one folds)
+        constexpr bool PIPE = FW_MG_PIPE && FW_MG_PIPE1 && NWP == 1;
+        if (PIPE && do_flush) {
+            constexpr int GP = GU;  // two full blocks fit beside the block-state code
+            auto ngroups_of = [&](int64_t p) {
+                const int nc = (int)cell_pad(a.slot_nch[p]);
+                return nc / gather_group(nc);
+            };
+            auto norm = [&](int64_t& p, int& q) {
+                while (p < pend && q >= ngroups_of(p)) {
+                    p++;
+                    q = wv;
+                }
+            };
+            auto fpos = [&](int64_t p, int q) { return q * gather_group((int)cell_pad(a.slot_nch[p])) + lane; };
+            auto cword = [&](int64_t p, int q) -> uint32_t {
+                return lane < gather_group((int)cell_pad(a.slot_nch[p])) ? cell_at(p, fpos(p, q)) : 0u;
+            };
+            CellGroup cg;
+            cg.tot = cg.excl = cg.adj = cg.fmt = 0;
+            int64_t cp = 0;
+            uint32_t r0 = 0;
+            int64_t np = 0;
+            int nq = wv;
+            norm(np, nq);
+            uint32_t vn = np < pend ? ((np == 0 && nq == wv) ? v_first : cword(np, nq)) : 0u;
+            auto next_block = [&]() -> bool {
+                r0 += 64 * GP;
+                while (r0 >= cg.tot) {
+                    if (np >= pend) return false;
+                    const uint32_t vc = vn;
+                    const int f = fpos(np, nq);
+                    cp = np;
+                    nq += MG_BLOCK / 64;
+                    norm(np, nq);
+                    vn = np < pend ? cword(np, nq) : 0u;
+                    cg = cell_group(vc, f, CH);
+                    r0 = 0;
+                }
+                return true;
+            };
+            auto process = [&](auto& row, uint32_t live) {
+                constexpr int GX = std::extent<std::remove_reference_t<decltype(row)>>::value;
+                int ge[GX], slot[GX];
+                {
+                    int64_t gk[GX], gb[GX];
+#pragma unroll
+                    for (int u = 0; u < GX; u++) {
+                        gk[u] = (int64_t)row[u][0];
+                        gb[u] = hb_block_of(win, (int64_t)row[u][1]);
+                        slot[u] = hb_slot_of(win, (int64_t)row[u][1], gb[u]);
+                        row[u][1] = (uint64_t)gb[u];
+                    }
+                    probe_batch<NA, E, GX>(S, gk, gb, ge);
+                }
+                static_for<GX>([&](auto UU) {
+                    constexpr int u = decltype(UU)::value;
+                    if (!((live >> u) & 1u)) return;
+                    int e = ge[u];
+                    if (e < 0) e = hb_find_or_insert<NWP, E, OPS>(S, (int64_t)row[u][0], (int64_t)row[u][1], a.wd);
+                    if (e < 0) return;  // state overflow (flagged)
+                    const int sl = slot[u];
+#pragma unroll
+                    for (int w = 0; w < NWP; w++)
+                        if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[sl * NWP + w][e], row[u][2 + w]);
+                    atomicOr(&S.flag[e], F_ACC | (1u << (HB_MASK_SHIFT + sl)));
+                });
+            };
+            uint64_t ra[GP][PW], rb[GP][PW];
+            uint32_t la = 0, lb = 0;
+            bool ha = next_block();
+            if (ha) la = load_group_rows<NWP, GP, GF>(a, cp, cg, r0, sb, ra);
+            while (ha) {  // unrolled by two: the buffers alternate without copies
+                const bool hb = next_block();
+                if (hb) lb = load_group_rows<NWP, GP, GF>(a, cp, cg, r0, sb, rb);
+                process(ra, la);
+                if (!hb) break;
+                ha = next_block();
+                if (ha) la = load_group_rows<NWP, GP, GF>(a, cp, cg, r0, sb, ra);
+                process(rb, lb);
+            }
+        } else if (do_flush) {
             for (int64_t pi = 0; pi < pend; pi++) {
                 const int ncell = (int)cell_pad(a.slot_nch[pi]);
                 const int G = gather_group(ncell);

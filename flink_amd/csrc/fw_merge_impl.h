@@ -1,6 +1,8 @@
 // fw_merge_impl.h -- k_merge_fire (K4+K5) and its launchers, instantiated per accumulator word
 // count in k_merge_nw*.hip.
 #pragma once
+#include <type_traits>
+
 #include "fw_kernel_common.h"
 
 namespace fw {
@@ -668,6 +670,12 @@ __device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
 }
 
 // rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
+#ifndef FW_MG_PIPE
+#define FW_MG_PIPE 1  // software-pipelined gather for one-word layouts (0: the plain loop, A/B)
+#endif
+#ifndef FW_MG_PIPE1
+#define FW_MG_PIPE1 0  // ... also for one-word layouts and HOP block state (A/B: CFG2 slower with half blocks)
+#endif
 #ifndef FW_GU1
 #define FW_GU1 4
 #endif
@@ -903,7 +911,125 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // folded; the misses of a lane are then inserted one at a time.
     // diagnostic (AB_GSTAMPS): thread 0's cycles in row loads / first probes / fold + insert
     const bool gst = (FW_ABL(a) & AB_GSTAMPS) && stm.on && tid == 0;
-    if (gather) {
+    // TUMBLE and CUMULATE with up to 4 accumulator words (HOP runs k_merge_hopb or, with wider or
+    // SQL-double layouts, the plain loop: its chain code leaves no registers): the gather is
+    // software-pipelined over the wave's blocks of rows -- the next block's rows (and the next
+    // group's cell word) are in flight while the current block is probed and folded.  Two blocks of
+    // GU / 2 rows per lane take the registers of one block of GU rows.
+    constexpr bool PIPE = FW_MG_PIPE && (NW >= 2 || FW_MG_PIPE1) && NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
+    if (PIPE && gather) {
+        constexpr int GP = NW == 1 ? GU : GU / 2 > 0 ? GU / 2 : 1;  // one word: two full blocks fit
+        auto flags_of = [&](int64_t sl) -> uint32_t {
+            return (a.local || win_fired(a.win, sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
+        };
+        auto ngroups_of = [&](int64_t p) {
+            const int nc = (int)cell_pad(a.slot_nch[p]);
+            return nc / gather_group(nc);
+        };
+        auto norm = [&](int64_t& p, int& q) {  // the first group (p, q) of this wave that exists
+            while (p < pend && q >= ngroups_of(p)) {
+                p++;
+                q = wv;
+            }
+        };
+        auto fpos = [&](int64_t p, int q) { return q * gather_group((int)cell_pad(a.slot_nch[p])) + lane; };
+        auto cword = [&](int64_t p, int q) -> uint32_t {
+            return lane < gather_group((int)cell_pad(a.slot_nch[p])) ? cell_at(p, fpos(p, q)) : 0u;
+        };
+        // current block: group (cp) with scan cg, rows r0 + [0, 64 * GP); next group (np, nq) with
+        // its cell word vn loaded one group ahead
+        CellGroup cg;
+        cg.tot = cg.excl = cg.adj = cg.fmt = 0;
+        int64_t cp = 0;
+        uint32_t r0 = 0;
+        int64_t np = 0;
+        int nq = wv;
+        norm(np, nq);
+        uint32_t vn = np < pend ? ((np == 0 && nq == wv) ? v_first : cword(np, nq)) : 0u;
+        auto next_block = [&]() -> bool {
+            r0 += 64 * GP;
+            while (r0 >= cg.tot) {
+                if (np >= pend) return false;
+                const uint32_t vc = vn;
+                const int f = fpos(np, nq);
+                cp = np;
+                nq += MG_BLOCK / 64;
+                norm(np, nq);
+                vn = np < pend ? cword(np, nq) : 0u;
+                cg = cell_group(vc, f, CH);
+                r0 = 0;
+            }
+            return true;
+        };
+        auto process = [&](auto& row, uint32_t live) {
+            constexpr int GX = std::extent<std::remove_reference_t<decltype(row)>>::value;
+            if (FW_ABL(a) & AB_M_NO_HASH) {  // diagnostic: loads only
+                uint64_t x = 0;
+#pragma unroll
+                for (int u = 0; u < GX; u++) x ^= row[u][0] ^ row[u][1] ^ row[u][PW - 1];
+                asm volatile("" ::"v"(x));
+                return;
+            }
+            int ge[GX];
+            {
+                int64_t gk[GX], gs[GX];
+#pragma unroll
+                for (int u = 0; u < GX; u++) {
+                    gk[u] = (int64_t)row[u][0];
+                    gs[u] = (int64_t)row[u][1];
+                }
+                probe_batch<NW, E, GX>(S, gk, gs, ge);
+            }
+            uint32_t miss = 0;
+            static_for<GX>([&](auto UU) {
+                constexpr int u = decltype(UU)::value;
+                if (!((live >> u) & 1u)) return;
+                const int e = ge[u];
+                if (e < 0) {
+                    miss |= 1u << u;
+                    return;
+                }
+                if (FW_ABL(a) & AB_M_NO_FOLDOP) return;
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
+                atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
+            });
+            while (miss) {
+                const int um = __ffs(miss) - 1;
+                miss &= miss - 1;
+                uint64_t r[PW];
+                static_for<GX>([&](auto UU) {
+                    constexpr int u = decltype(UU)::value;
+                    if (u == um) {
+#pragma unroll
+                        for (int w = 0; w < PW; w++) r[w] = row[u][w];
+                    }
+                });
+                const uint32_t fl = flags_of((int64_t)r[1]);
+                bool ins = false;
+                const int e = find_or_insert<NW, E, OPS>(S, (int64_t)r[0], (int64_t)r[1], a.wd, &r[2], fl, &ins);
+                if (e < 0 || ins || (FW_ABL(a) & AB_M_NO_FOLDOP)) continue;
+#pragma unroll
+                for (int w = 0; w < NW; w++)
+                    if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], r[2 + w]);
+                atomicOr(&S.flag[e], fl);
+            }
+        };
+        uint64_t ra[GP][PW], rb[GP][PW];
+        uint32_t la = 0, lb = 0;
+        bool ha = next_block();
+        if (ha) la = load_group_rows<NW, GP, GF>(a, cp, cg, r0, sb, ra);
+        while (ha) {  // unrolled by two: the buffers alternate, no copies (a copy would wait for the loads)
+            const bool hb = next_block();
+            if (hb) lb = load_group_rows<NW, GP, GF>(a, cp, cg, r0, sb, rb);
+            process(ra, la);
+            if (!hb) break;
+            ha = next_block();
+            if (ha) la = load_group_rows<NW, GP, GF>(a, cp, cg, r0, sb, ra);
+            process(rb, lb);
+        }
+    } else if (gather) {
         for (int64_t pi = 0; pi < pend; pi++) {
             const int ncell = (int)cell_pad(a.slot_nch[pi]);
             const int G = gather_group(ncell);

@@ -289,11 +289,9 @@ def test_rescale_restore_by_key_group(p_from, p_to, case):
     and the run continues.  The union of all window results equals one unsharded oracle that
     checkpoints and restarts at the same cut.
 
-    Known DataStream sliding-window deviation: a record that arrives after a restore
-    but before the first watermark, into a sliding window that fired before the checkpoint, finds
-    a fresh window state in the reference but the window's still-live shared slices here.  The
-    sliding case therefore feeds no such record at the cut; the tumbling case (no shared slices)
-    does, and is exact."""
+    DataStream state is per window (KIND_DSWIN), so records that arrive between the
+    restore and the first watermark into windows that fired before the checkpoint are exact for
+    the sliding case too (round 1's shared-slice restore deviation is gone)."""
     torch = _torch_cuda()
     from flink_amd.runtime.exchange import KeyByExchange
     from flink_amd.runtime.handle import WindowAggHandle

@@ -98,27 +98,55 @@ def gen_params(wl, world, zipf_ptr):
                              value_kind=wl["value_kind"], zipf_cdf=zipf_ptr), keys_total
 
 
-def cpu_baseline(wl, sample_events):
-    """Oracle (CPU restatement, single thread) on the first `sample_events` events of the same
-    stream with the same watermarks; returns events/s of the record + watermark processing."""
+def cpu_baseline(wl, sample_events, threads=1):
+    """Oracle (CPU restatement) on the first `sample_events` events of the same stream with the
+    same watermarks; returns events/s of the record + watermark processing.  threads > 1 runs the
+    sample as a keyBy at parallelism `threads` does: every thread is one subtask (its own oracle
+    operator) fed the rows of its key-group range (KeyGroupRangeAssignment), pre-partitioned
+    before the timed region; the oracle's C calls release the GIL, so the subtasks run in
+    parallel and the rate is the sample over the slowest subtask's wall clock."""
+    import threading
     from flink_amd import abi
     from oracle import oracle as O
     zcdf = O.zipf_cdf(wl["keys"], wl["zipf_s"]) if wl["dist"] == 1 else None
     gp = abi.fw_gen_params(seed=42, t0_ms=T0, rate_per_s=wl["rate"], ooo_ms=J, key_base=wl["key_base"],
                            key_count=wl["keys"], key_dist=wl["dist"], value_kind=wl["value_kind"], zipf_cdf=None)
-    cfg = build_config(wl, 1, 0, wl["keys"], 1 << 22)
-    op = O.OracleOperator(cfg)
+    p = max(1, int(threads))
     steps = max(1, sample_events // B)
-    batches = [O.generate(gp, b * B, B, zcdf) for b in range(steps)]
+    ops = [O.OracleOperator(build_config(wl, p, i, wl["keys"], 1 << 22)) for i in range(p)]
+    nvc = ops[0].cfg.n_value_cols
+    shards = [[] for _ in range(p)]
+    for b in range(steps):
+        k, t, v = O.generate(gp, b * B, B, zcdf)
+        dest = O.operator_indices(abi.KEYHASH_BINROW_BIGINT, k, 128, p) if p > 1 else np.zeros(len(k), np.int32)
+        for i in range(p):
+            m = dest == i
+            shards[i].append((k[m], t[m], v[m]))
+    n_out = [0] * p
+    err = []
+
+    def run(i):
+        try:
+            op = ops[i]
+            for b, (k, t, v) in enumerate(shards[i]):
+                op.process_batch(k, t, [v] if nvc else [])
+                op.process_watermark(watermark(b, wl["rate"]))
+                n_out[i] += len(op.results(clear=True)["key"])
+        except Exception as e:  # surfaced below
+            err.append(e)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(p)]
     t0 = time.perf_counter()
-    n_out = 0
-    for b, (k, t, v) in enumerate(batches):
-        op.process_batch(k, t, [v] if cfg.n_value_cols else [])
-        op.process_watermark(watermark(b, wl["rate"]))
-        n_out += len(op.results(clear=True)["key"])
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
     dt = time.perf_counter() - t0
-    op.close()
-    return steps * B / dt, steps * B, dt, n_out
+    for op in ops:
+        op.close()
+    if err:
+        raise err[0]
+    return steps * B / dt, steps * B, dt, sum(n_out)
 
 
 def main():
@@ -127,7 +155,10 @@ def main():
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-sample", type=int, default=B, help="events for the CPU baseline leg")
+    ap.add_argument("--cpu-sample", type=int, default=4 * B, help="events for the CPU baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="CPU baseline subtasks (threads), capped at the usable CPUs; 16 = the GPU box's "
+                         "CPU share per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/traffic.py); default: newest profiles/r*/traffic_<workload>.json")
@@ -476,16 +507,18 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        v, n, dt, _ = cpu_baseline(wl, args.cpu_sample)
         try:
             host_cpus = len(os.sched_getaffinity(0))
         except AttributeError:
             host_cpus = os.cpu_count()
-        cpu = {"value": v, "unit": "events/s", "cores": 1, "kind": "port",
+        thr = max(1, min(args.cpu_threads, host_cpus))
+        v, n, dt, _ = cpu_baseline(wl, args.cpu_sample, thr)
+        cpu = {"value": v, "unit": "events/s", "cores": thr, "kind": "port",
                "host_nproc": host_cpus,
                "sample": f"first {n} events of the same {args.workload} stream through the C++ oracle "
-                         f"(oracle/flinkwin_oracle.cpp, single thread on a host with {host_cpus} usable "
-                         f"CPUs), {dt:.1f} s; the reference Flink operator needs a JDK, absent here"}
+                         f"(oracle/flinkwin_oracle.cpp) as a keyBy at parallelism {thr}: one thread and one "
+                         f"operator per subtask over its key-group range (rows pre-partitioned, untimed), on a "
+                         f"host with {host_cpus} usable CPUs, {dt:.1f} s wall; the reference Flink operator needs a JDK, absent here"}
 
     if rank == 0:
         line = {

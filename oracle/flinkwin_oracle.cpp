@@ -1044,6 +1044,13 @@ int32_t or_key_group(int32_t kind, int64_t key, int32_t pre, int32_t max_p) {
     return key_group_for_hash(java_key_hash(kind, key, pre), max_p);
 }
 int32_t or_operator_index(int32_t max_p, int32_t p, int32_t kg) { return operator_index_for_kg(max_p, p, kg); }
+// the subtask of each key (assignKeyToParallelOperator, KeyGroupRangeAssignment.java:49-73): the
+// bench's multi-threaded CPU baseline partitions its sample like a keyBy at parallelism p
+void or_operator_indices(int32_t kind, const int64_t* keys, int64_t n, int32_t pre, int32_t max_p, int32_t p,
+                         int32_t* out) {
+    for (int64_t i = 0; i < n; i++)
+        out[i] = operator_index_for_kg(max_p, p, key_group_for_hash(java_key_hash(kind, keys[i], pre), max_p));
+}
 void or_key_group_range(int32_t max_p, int32_t p, int32_t idx, int32_t* start, int32_t* end) {
     // computeKeyGroupRangeForOperatorIndex (:93-106)
     *start = (idx * max_p + p - 1) / p;

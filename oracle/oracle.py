@@ -67,6 +67,7 @@ def lib():
         L.or_operator_index.restype = i32
         L.or_operator_index.argtypes = [i32, i32, i32]
         L.or_key_group_range.argtypes = [i32, i32, i32, C.POINTER(i32), C.POINTER(i32)]
+        L.or_operator_indices.argtypes = [i32, vp, i64, i32, i32, i32, vp]
         L.or_window_start_with_offset.restype = i64
         L.or_window_start_with_offset.argtypes = [i64, i64, i64]
         L.or_next_trigger_watermark.restype = i64
@@ -222,6 +223,14 @@ def key_group(kind, key, max_p, pre=0):
 
 def operator_index(max_p, p, kg):
     return lib().or_operator_index(max_p, p, kg)
+
+
+def operator_indices(kind, keys, max_p, p, pre=0):
+    """Subtask of every key at parallelism p (a keyBy's channel selection, vectorised)."""
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    out = np.empty(len(keys), dtype=np.int32)
+    lib().or_operator_indices(kind, _ptr(keys), len(keys), int(pre), max_p, p, _ptr(out))
+    return out
 
 
 def key_group_range(max_p, p, idx):

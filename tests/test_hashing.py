@@ -91,3 +91,13 @@ def test_key_group_ranges_partition_all_groups():
 def test_self_computed_key_groups():
     # values recorded in SURVEY.md 8c from a scratch restatement (self-computed, not reference)
     assert [O.key_group(abi.KEYHASH_INT, h, 128) for h in (0, 1, 42, -1)] == [94, 86, 29, 80]
+
+
+def test_batched_operator_indices_match_scalar():
+    """or_operator_indices (the bench's CPU-baseline keyBy) = key_group + operator_index per key."""
+    keys = np.random.default_rng(5).integers(-2**63, 2**63 - 1, 2000, dtype=np.int64)
+    for kind in (abi.KEYHASH_BINROW_BIGINT, abi.KEYHASH_LONG):
+        for p in (1, 3, 16):
+            got = O.operator_indices(kind, keys, 128, p)
+            want = [O.operator_index(128, p, O.key_group(kind, int(k), 128)) for k in keys]
+            assert got.tolist() == want

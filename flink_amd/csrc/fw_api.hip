@@ -149,6 +149,14 @@ struct fw_handle {
     int64_t cell_cols = 0;       // cell_pad(max_nch): cells per superbucket per slot
     uint32_t* cells = nullptr;   // [FW_MAX_PENDING][cell_cols / 16][n_sb][16] (cell_index)
     int32_t* slot_nch = nullptr;  // [FW_MAX_PENDING]
+    // runs (IngestArgs::runs): superbucket-contiguous partial rows; run_rows == 0: off
+    int64_t run_rows = 0;
+    int32_t sub_cap = 0;
+    uint64_t* runs = nullptr;
+    uint8_t* run_ranks = nullptr;
+    uint32_t* run_fill = nullptr;
+    uint32_t* run_ovf = nullptr;
+    int32_t* slot_fmt = nullptr;
     int64_t* treq = nullptr;
     int64_t treq_cap = 0;
     uint64_t* lfire = nullptr;   // DataStream late-fire rows
@@ -298,8 +306,15 @@ int validate_and_plan(fw_handle* h) {
             break;
         case FW_WIN_HOP:
             if (c.slide_ms <= 0) return fail(FW_E_INVALID, "Hopping Window must satisfy slide > 0 and size > 0");
-            if (c.size_ms % c.slide_ms != 0)
+            // SQL slices need slide | size (SliceAssigners.HoppingSliceAssigner); DataStream sliding
+            // windows do not (SlidingEventTimeWindows.java:77-90): panes of gcd(size, slide) ms, each in
+            // floor or ceil(size / slide) windows
+            if (c.api != FW_API_DATASTREAM && c.size_ms % c.slide_ms != 0)
                 return fail(FW_E_INVALID, "Slicing Hopping Window requires size must be an integral multiple of slide");
+            if (c.api == FW_API_DATASTREAM && c.size_ms < c.slide_ms)  // gaps: panes in no window (not eligible)
+                return fail(FW_E_INVALID, "sliding windows with size < slide run on the reference operator");
+            if (c.api == FW_API_DATASTREAM && !(c.offset_ms > -c.slide_ms && c.offset_ms < c.slide_ms))
+                return fail(FW_E_INVALID, "SlidingEventTimeWindows parameters must satisfy abs(offset) < slide and size > 0");
             w.interval = gcd64(c.size_ms, c.slide_ms);
             w.n_slices = (int32_t)(c.size_ms / w.interval);
             break;
@@ -314,7 +329,7 @@ int validate_and_plan(fw_handle* h) {
     }
     w.ds = c.api == FW_API_DATASTREAM;
     w.slide = c.window_kind == FW_WIN_HOP ? c.slide_ms : c.size_ms;
-    w.n_win = (w.ds && c.window_kind == FW_WIN_HOP) ? (int32_t)(c.size_ms / c.slide_ms) : 1;
+    w.n_win = (w.ds && c.window_kind == FW_WIN_HOP) ? (int32_t)((c.size_ms + c.slide_ms - 1) / c.slide_ms) : 1;
     w.slide_div = make_udiv((uint64_t)w.slide);
     // ---- lateness (DataStream) and shift time zone (SQL TIMESTAMP_LTZ)
     if (c.allowed_lateness_ms < 0) return fail(FW_E_INVALID, "The allowed lateness cannot be negative.");
@@ -587,6 +602,25 @@ int validate_and_plan(fw_handle* h) {
                         ? 2
                         : 0;
     }
+    // runs: every chunk claims its stretch of each superbucket's sub-runs, so the merge streams a
+    // superbucket's rows (fw_internal.h RUN_X).  Sub-runs hold 5/4 of a uniform share of a full push
+    // (+16 rows); skew beyond that stays in the chunks' regions (overflow flags).  Off for key-row
+    // handles (their collector reads the chunk regions), split superbuckets (pass_log2: several
+    // readers per ingest superbucket) and superbucket counts the ingest LDS cannot book-keep;
+    // FW_RUNS=0 switches them off (development A/B).
+    {
+        const char* re = getenv("FW_RUNS");
+        const int n_isb = ks.n_sb >> ks.pass_log2;
+        const int blk = ig_block(h->nw_t, ig_nv(h->nv)), rpt = ig_rpt(h->nw_t, ig_nv(h->nv));
+        if (!h->keyrow && ks.pass_log2 == 0 && ig_runs_fit(n_isb, blk, rpt, h->nw_t) && !(re && atoi(re) == 0)) {
+            const int64_t subs = (int64_t)n_isb * RUN_X;
+            const int64_t sc = ((h->cap_rows * 5 / 4 + subs - 1) / subs + 16 + 15) / 16 * 16;
+            if (sc * subs < (1ll << 31)) {
+                h->sub_cap = (int32_t)sc;
+                h->run_rows = sc * subs;
+            }
+        }
+    }
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     if (c.api == FW_API_DATASTREAM) {
         if (c.allowed_lateness_ms > 0 && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
@@ -630,6 +664,17 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->slot_nch, FW_MAX_PENDING))) return rc;
     if ((rc = dalloc(&h->slot_base, FW_MAX_PENDING))) return rc;
     if (h->narrow && (rc = dalloc(&h->ranks, (size_t)FW_MAX_PENDING * h->cap_rows))) return rc;
+    if (h->run_rows) {
+        const size_t n_isb = (size_t)(h->ks.n_sb >> h->ks.pass_log2);
+        if ((rc = dalloc(&h->runs, (size_t)FW_MAX_PENDING * h->run_rows * PW))) return rc;
+        if (h->narrow && (rc = dalloc(&h->run_ranks, (size_t)FW_MAX_PENDING * h->run_rows))) return rc;
+        if ((rc = dalloc(&h->run_fill, (size_t)FW_MAX_PENDING * RUN_X * n_isb))) return rc;
+        if ((rc = dalloc(&h->run_ovf, (size_t)FW_MAX_PENDING * n_isb))) return rc;
+        if ((rc = dalloc(&h->slot_fmt, FW_MAX_PENDING))) return rc;
+        HIP_TRY(hipMemsetAsync(h->run_fill, 0, sizeof(uint32_t) * FW_MAX_PENDING * RUN_X * n_isb, h->stream));
+        HIP_TRY(hipMemsetAsync(h->run_ovf, 0, sizeof(uint32_t) * FW_MAX_PENDING * n_isb, h->stream));
+        HIP_TRY(hipMemsetAsync(h->slot_fmt, 0, sizeof(int32_t) * FW_MAX_PENDING, h->stream));
+    }
     if ((rc = dalloc(&h->treq, (size_t)h->treq_cap * 3))) return rc;
     if (h->lfire_cap && (rc = dalloc(&h->lfire, (size_t)h->lfire_cap * LFW))) return rc;
     if (h->side_cap && (rc = dalloc(&h->side, (size_t)h->side_cap * SOW))) return rc;
@@ -822,6 +867,13 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.slot_base = h->slot_base;
     a.ranks = h->ranks;
     a.compact = h->narrow != 0;
+    a.runs = h->runs;
+    a.run_ranks = h->run_ranks;
+    a.run_fill = h->run_fill;
+    a.run_ovf = h->run_ovf;
+    a.slot_fmt = h->slot_fmt;
+    a.run_rows = h->run_rows;
+    a.sub_cap = h->sub_cap;
     a.ch_log2 = 0;
     while ((1ll << a.ch_log2) < h->chunk_rows) a.ch_log2++;
     return a;
@@ -925,6 +977,13 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
                      h->win.interval;
         a.slot_base = h->slot_base;
         a.ranks = h->ranks;
+        a.runs = h->runs;
+        a.run_ranks = h->run_ranks;
+        a.run_fill = h->run_fill;
+        a.run_ovf = h->run_ovf;
+        a.slot_fmt = h->slot_fmt;
+        a.run_rows = h->run_rows;
+        a.sub_cap = h->sub_cap;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
         h->pushes_total++;
@@ -1007,6 +1066,11 @@ int fw_destroy(fw_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     hipFree(h->ctrl);
     hipFree(h->parts);
+    hipFree(h->runs);
+    hipFree(h->run_ranks);
+    hipFree(h->run_fill);
+    hipFree(h->run_ovf);
+    hipFree(h->slot_fmt);
     hipFree(h->cells);
     hipFree(h->slot_nch);
     hipFree(h->slot_base);

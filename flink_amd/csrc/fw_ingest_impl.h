@@ -309,7 +309,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                 const uint64_t d = (uint64_t)wsub(wsub(e0, 1), cur_wm);
                 uint64_t kf = udiv(d, a.win.slide_div);
                 kf += (kf * (uint64_t)a.win.slide != d);
-                if (kf < (uint64_t)a.win.n_win)
+                if (kf < (uint64_t)a.win.n_win && ds_window_holds_pane(a.win, wsub(e0, (int64_t)kf * a.win.slide), se))
                     late_fire = ds_cleanup_time(a.win, wsub(e0, (int64_t)kf * a.win.slide)) > cur_wm;
             }
             if (late_fire) {
@@ -437,17 +437,59 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     uint32_t total;
     const uint32_t incl = block_incl_scan<IG_BLOCK>(seg, wsum, &total);
     uint32_t run = incl - seg;
+    // runs (IngestArgs::runs): a push's run rows share one format -- compact when the push is (COUNT(*)
+    // alone: PF_UNIT when no chunk folds, else PF_NARROW); a chunk that must write PF_WIDE rows in a
+    // compact push keeps them all in its own region
+    const bool runs = a.runs != nullptr && sort;
+    const uint32_t push_fmt = (runs && CAN_COMPACT && nar) ? ((!X && a.narrow == 2 && !do_fold) ? PF_UNIT : PF_NARROW) : PF_WIDE;
     // COUNT(*) alone and nothing folded in this chunk: every row counts 1
-    const uint32_t fmt = (!CAN_COMPACT || wide || !sort) ? PF_WIDE
+    const uint32_t fmt = runs ? (wide ? PF_WIDE : push_fmt)
+                         : (!CAN_COMPACT || wide || !sort) ? PF_WIDE
                          : (!X && a.narrow == 2 && !*s_folded) ? PF_UNIT
-                                                                                        : PF_NARROW;
+                                                                 : PF_NARROW;
+    const bool to_runs = runs && fmt == push_fmt;
     if (sort)
         for (int i = sb0; i < sb1; i++) {
             const uint32_t v = hist[i];
             hist[i] = run;
-            cells[cell_index(c, n_sb, i)] = run | (v << 16) | (fmt << 30);
+            if (!runs) cells[cell_index(c, n_sb, i)] = run | (v << 16) | (fmt << 30);
             run += v;
         }
+    // (runs) per superbucket: chunk positions below rbound go to the run at position + roff; then
+    // every row's destination, RUN_LOCAL | position for the rows that stay in the chunk's region.
+    // They live where the fold table was; the store stage follows them.
+    const int n_sb_pad = (n_sb + 3) & ~3;
+    uint32_t* rbound = (uint32_t*)area;
+    uint32_t* roff = rbound + n_sb_pad;
+    uint32_t* sdst = roff + n_sb_pad;
+    if (runs) {
+        __syncthreads();  // hist holds every superbucket's chunk position
+        // superbuckets strided over the threads (the host enables runs for n_sb <= RUN_KMAX *
+        // IG_BLOCK): a wave's claims hit 64 neighbouring counters, all in flight before the first use
+        const uint32_t xr = (uint32_t)c & (RUN_X - 1);
+        const uint32_t scap = (uint32_t)a.sub_cap;
+        uint32_t pos[RUN_KMAX];
+#pragma unroll
+        for (int k = 0; k < RUN_KMAX; k++) {
+            const int i = tid + k * IG_BLOCK;
+            pos[k] = 0;
+            if (i < n_sb && to_runs) {
+                const uint32_t v = (i + 1 < n_sb ? hist[i + 1] : total) - hist[i];
+                if (v) pos[k] = atomicAdd(a.run_fill + ((size_t)slot * RUN_X + xr) * n_sb + i, v);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < RUN_KMAX; k++) {
+            const int i = tid + k * IG_BLOCK;
+            if (i >= n_sb) break;
+            const uint32_t st0 = hist[i], v = (i + 1 < n_sb ? hist[i + 1] : total) - st0;
+            const uint32_t n_in = to_runs ? (pos[k] >= scap ? 0u : min(v, scap - pos[k])) : 0u;
+            rbound[i] = st0 + n_in;
+            roff[i] = (uint32_t)(((size_t)i * RUN_X + xr) * scap + pos[k]) - st0;
+            cells[cell_index(c, n_sb, i)] = (st0 + n_in) | ((v - n_in) << 16) | (fmt << 30);
+            if (n_in < v) a.run_ovf[(size_t)slot * n_sb + i] = 1u;
+        }
+    }
     if (fmt != PF_WIDE)  // compact rows keep their rank instead of their slice end
         static_for<RPT>([&](auto J) {
             constexpr int j = decltype(J)::value;
@@ -461,15 +503,27 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         });
     else
         total = CH;
-    // ---- store the partials through an LDS stage so every global store is a full line.  The
-    // chunk's region keeps its PF_WIDE size; a compact format fills its front, and its rank bytes
-    // are staged behind the rows and stored to the side array.
+    if (runs)
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if (!(valid & (1u << j))) return;
+            const uint32_t d = rdst[j];
+            const int i = rsb[j] >> PL;
+            sdst[d] = d < rbound[i] ? d + roff[i] : (RUN_LOCAL | d);
+        });
+    // ---- store the partials through an LDS stage so every global store is a full line (runs:
+    // word by word to each row's destination, neighbouring lanes on neighbouring words of a
+    // superbucket's stretch).  The chunk's region keeps its PF_WIDE size; a compact format fills its
+    // front, and its rank bytes are staged behind the rows and stored to the side array.
     const int PWX = pf_stride(fmt, NW);
     const int aoff = fmt == PF_WIDE ? 2 : 1;  // first accumulator word of a row
     uint64_t* out = a.parts + ((size_t)slot * a.cap_rows + (size_t)base) * PW;
-    const uint32_t wrows = fmt == PF_WIDE ? (uint32_t)(area_words / PW) & ~15u
-                                          : (uint32_t)((int64_t)area_words * 8 / (8 * PWX + 1)) & ~15u;
-    uint8_t* rstage = (uint8_t*)(area + (size_t)wrows * PWX);
+    uint64_t* stage = runs ? area + (((size_t)2 * n_sb_pad + CH + 3) / 4) * 2 : area;  // 16-B aligned
+    const int64_t stage_words = area_words - (int64_t)(stage - area);
+    const uint32_t wrows = fmt == PF_WIDE ? (uint32_t)(stage_words / PW) & ~15u
+                                          : (uint32_t)(stage_words * 8 / (8 * PWX + 1)) & ~15u;
+    uint8_t* rstage = (uint8_t*)(stage + (size_t)wrows * PWX);
+    uint64_t* rslot = runs ? a.runs + (size_t)slot * a.run_rows * PW : nullptr;
     if (!(FW_ABL(a) & AB_NO_STORE))
         for (uint32_t w0 = 0; w0 < total; w0 += wrows) {
             __syncthreads();  // fold table / previous window no longer read
@@ -477,7 +531,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                 constexpr int j = decltype(J)::value;
                 const uint32_t d = rdst[j] - w0;
                 if (!(valid & (1u << j)) || d >= wrows) return;
-                uint64_t* p = area + (size_t)d * PWX;
+                uint64_t* p = stage + (size_t)d * PWX;
                 p[0] = (uint64_t)rk[j];
                 if (fmt == PF_WIDE) p[1] = (uint64_t)rs[j];
                 else rstage[d] = (uint8_t)rs[j];  // the rank (set below the format decision)
@@ -488,12 +542,35 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             __syncthreads();
             const uint32_t nr = min(wrows, total - w0);
             const uint32_t nwords = nr * PWX;
+            if (runs) {
+                // word q of the window: row q / P, word q % P of it (the stride as a constant)
+                auto copy_out = [&](auto PC) {
+                    constexpr uint32_t P = decltype(PC)::value;
+                    for (uint32_t q = tid; q < nwords; q += IG_BLOCK) {
+                        const uint32_t d = q / P, w = q - d * P;
+                        const uint32_t dd = sdst[w0 + d];
+                        uint64_t* dst = (dd & RUN_LOCAL) ? out + (size_t)(dd & ~RUN_LOCAL) * P + w : rslot + (size_t)dd * P + w;
+                        *dst = stage[q];
+                    }
+                };
+                if (fmt == PF_WIDE) copy_out(std::integral_constant<uint32_t, (uint32_t)PW>{});
+                else if (fmt == PF_NARROW) copy_out(std::integral_constant<uint32_t, (uint32_t)(1 + NW)>{});
+                else copy_out(std::integral_constant<uint32_t, 1u>{});
+                if (fmt != PF_WIDE)
+                    for (uint32_t r = tid; r < nr; r += IG_BLOCK) {
+                        const uint32_t dd = sdst[w0 + r];
+                        uint8_t* rd = (dd & RUN_LOCAL) ? a.ranks + (size_t)slot * a.cap_rows + (size_t)base + (dd & ~RUN_LOCAL)
+                                                       : a.run_ranks + (size_t)slot * a.run_rows + dd;
+                        *rd = rstage[r];
+                    }
+                continue;
+            }
             uint64_t* dst = out + (size_t)w0 * PWX;  // 16-B aligned: slot, chunk and window bases are 16-row multiples
             for (uint32_t q = 2 * tid; q < nwords; q += 2 * IG_BLOCK) {
                 if (q + 1 < nwords) {
-                    *(ulonglong2*)(dst + q) = *(const ulonglong2*)(area + q);
+                    *(ulonglong2*)(dst + q) = *(const ulonglong2*)(stage + q);
                 } else {
-                    dst[q] = area[q];
+                    dst[q] = stage[q];
                 }
             }
             if (fmt != PF_WIDE) {
@@ -580,6 +657,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         }
         a.slot_nch[slot] = (int32_t)gridDim.x;
         a.slot_base[slot] = slice_end_of(a.win, wadd(cur_wm, 1));  // used by compact chunks only
+        if (a.runs) a.slot_fmt[slot] = (int32_t)push_fmt;
         ctrl->pending_pushes = slot + 1;
         ctrl->min_pending = min(ctrl->min_pending, m);
         ctrl->pending_rows += (uint64_t)r;
@@ -609,8 +687,9 @@ static hipError_t ingest_x(const IngestArgs& a, hipStream_t s, KTimer* t) {
     // the fold table and the histogram must fit the dynamic LDS
     if ((int64_t)(IG_HDR_WORDS + ig_hist_words(a.ks.n_sb >> a.ks.pass_log2)) * 8 + ig_fold_bytes(NW) > a.lds_bytes)
         return hipErrorInvalidValue;
-    kt_mark(t, FW_KT_REDUCE, false, s);
     if (a.lds_bytes != ig_lds(BLK)) return hipErrorInvalidValue;
+    if (a.runs && !ig_runs_fit(a.ks.n_sb >> a.ks.pass_log2, BLK, RPT, NW)) return hipErrorInvalidValue;
+    kt_mark(t, FW_KT_REDUCE, false, s);
     hipLaunchKernelGGL((k_ingest<NV, NW, RPT, X, BLK>), dim3((unsigned)nch), dim3(BLK), a.lds_bytes, s, a);
     kt_mark(t, FW_KT_REDUCE, true, s);
     return hipGetLastError();

@@ -83,6 +83,27 @@ __host__ __device__ inline int64_t cell_chunk(int64_t f) {
     return (tile >> 3) * 128 + (tile & 7) + 8 * (f & 15);
 }
 
+// ---- runs: the partial rows of one push, superbucket-contiguous.  Each ingest chunk claims, per
+// ingest superbucket, a stretch of that superbucket's sub-run with one agent-scope atomic add on the
+// sub-run's fill counter, and stores its rows there; there are RUN_X sub-runs per (push, superbucket),
+// one per XCD (chunk c -> c % RUN_X, the dispatcher's XCD), so the pieces that share a line come from
+// one L2.  The merge kernel then reads each superbucket's rows as RUN_X contiguous stretches per push
+// (no per-chunk cell words, no dependent cell -> row round trip).  A sub-run holds sub_cap rows;
+// rows past it, and every row of a chunk whose format differs from its push's, stay in the chunk's
+// own region of the partial buffer with their cell word (count > 0), and the (push, superbucket)
+// overflow flag sends the merge there too.
+constexpr int RUN_X = 8;
+constexpr int RUN_KMAX = 4;             // ingest superbuckets per ingest thread for the run claims
+constexpr uint32_t RUN_LOCAL = 1u << 31;  // k_ingest staging: the row stays in the chunk's region
+
+// the ingest kernel's LDS holds the run bookkeeping of n_isb superbuckets and chunks of block * rpt
+// rows beside a store stage of at least 256 rows, and its threads claim every superbucket's stretch
+constexpr bool ig_runs_fit(int n_isb, int block, int rpt, int nw) {
+    const int64_t lds = block == 1024 ? 156 * 1024 : 78 * 1024;
+    const int64_t fixed = 8 * (16 + ((n_isb + 3) >> 2) * 2) + 4 * (2 * (int64_t)((n_isb + 3) & ~3) + block * rpt) + 16;
+    return n_isb <= RUN_KMAX * block && lds - fixed >= 256 * 8 * (2 + nw);
+}
+
 // Partial-row formats, one per (push slot, chunk); a cell word is start | count << 16 | format << 30
 // (chunks hold <= 4096 rows).  A chunk whose rows all took the ingest kernel's common path (UTC SQL
 // slice ends on the slice grid, within PF_MAX_RANK slices of the push's rank base) leaves the slice
@@ -283,6 +304,13 @@ FW_HD int64_t ds_first_window_end(const WinDesc& w, int64_t pe) {
     const int64_t ts0 = wsub(pe, w.interval);  // the pane's first millisecond
     return wadd(window_start(ts0, w.offset, w.slide_div), w.size);
 }
+// does the window ending at e hold pane pe?  SlidingEventTimeWindows.assignWindows' loop condition
+// start > timestamp - size for the pane's last millisecond (the windows of a pane are e0, e0 - slide,
+// ...: n_win = ceil(size / slide) candidates, the last one outside the pane when slide does not
+// divide size)
+FW_HD bool ds_window_holds_pane(const WinDesc& w, int64_t e, int64_t pe) {
+    return wsub(e, w.size) > wsub(wsub(pe, 1), w.size);
+}
 // WindowOperator.cleanupTime (:670-677) of the window ending at we: maxTimestamp + lateness,
 // Long.MAX_VALUE on overflow (then no cleanup timer is registered, registerCleanupTimer :616-628)
 FW_HD int64_t ds_cleanup_time(const WinDesc& w, int64_t we) {
@@ -458,6 +486,14 @@ struct IngestArgs {
     int64_t rank_lim;      // span of the ranks in ms: min(PF_MAX_RANK + 1, (2^31 - 1) / interval) * interval
     int64_t* slot_base;    // [FW_MAX_PENDING]: rank base of each push (its last workgroup writes it)
     uint8_t* ranks;        // [FW_MAX_PENDING][cap_rows]: rank byte of each narrow row
+    // runs (nullptr: every chunk keeps its rows in its own region, the cells tell where)
+    uint64_t* runs;        // [FW_MAX_PENDING][run_rows] rows, at the push format's stride
+    uint8_t* run_ranks;    // [FW_MAX_PENDING][run_rows]: rank bytes of compact run rows
+    uint32_t* run_fill;    // [FW_MAX_PENDING][RUN_X][n_isb]: rows claimed in each sub-run (may exceed sub_cap)
+    uint32_t* run_ovf;     // [FW_MAX_PENDING][n_isb]: a chunk left rows of this superbucket in its region
+    int32_t* slot_fmt;     // [FW_MAX_PENDING]: the run rows' format (PF_*) of each push
+    int64_t run_rows;      // rows per slot: n_isb * RUN_X * sub_cap
+    int32_t sub_cap;       // rows per sub-run
 };
 // Development ablations and phase stamps (FW_ABLATE) are compiled into the kernels only in a
 // diagnostic build (make DIAG=1): in the production build their checks fold away, so the hot loops
@@ -532,6 +568,14 @@ struct MergeArgs {
     const uint8_t* ranks;
     int32_t ch_log2;            // log2(chunk_rows)
     int32_t compact;            // chunks may hold compact rows (IngestArgs::narrow != 0)
+    // runs (IngestArgs); the merge zeroes a flushed push's fill counters and overflow flags
+    const uint64_t* runs;
+    const uint8_t* run_ranks;
+    uint32_t* run_fill;
+    uint32_t* run_ovf;
+    const int32_t* slot_fmt;
+    int64_t run_rows;
+    int32_t sub_cap;
 };
 constexpr int64_t ORDEV_RELEASE = (int64_t)1 << 62;
 constexpr int LFW = 3 + MAX_WORDS;  // words per late-fire row

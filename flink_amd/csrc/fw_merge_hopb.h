@@ -87,7 +87,7 @@ __device__ __forceinline__ void hb_merge_slot(const MergeArgs& a, const StateLds
 // no entry for the next block -- those ending in the next block that still hold slices of this one.
 // A window fires iff it ends in (W0, W] and holds data.  Returns the windows fired.
 template <int NWP, int E, uint32_t OPS>
-__device__ uint32_t hb_fire_entry(const MergeArgs& a, StateLds<HB_R * NWP, E>& S, int e, int64_t w_old, int sb,
+__device__ __forceinline__ uint32_t hb_fire_entry(const MergeArgs& a, StateLds<HB_R * NWP, E>& S, int e, int64_t w_old, int sb,
                                   int32_t* s_emit) {
     const WinDesc& w = a.win;
     const int n = w.n_slices;
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
         // this lane's cell word of its wave's first group in push 0 (the next push's is loaded at the top
         // of each push's loop, FW_MG_ROLL)
         uint32_t v_first = 0;
-        if (do_flush && lane < gather_group((int)cell_pad(a.slot_nch[0])))
+        if (do_flush && !a.runs && lane < gather_group((int)cell_pad(a.slot_nch[0])))
             v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
         // ---- load the superbucket's block entries into LDS
         for (int i = tid; i < StateLds<NA, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
@@ -236,7 +236,42 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
         // accumulator word (COUNT(*)): software-pipelined over the wave's blocks of rows, as in
         // k_merge_fire (the next block's rows in flight while the current one folds)
         constexpr bool PIPE = FW_MG_PIPE && FW_MG_PIPE1 && NWP == 1;
-        if (PIPE && do_flush) {
+        if (do_flush && a.runs) {  // runs (IngestArgs::runs), then the rows chunks kept in their regions
+            auto fold_rows = [&](auto& row, uint32_t live) __attribute__((always_inline)) {
+                constexpr int GX = std::extent<std::remove_reference_t<decltype(row)>>::value;
+                int ge[GX], slot[GX];
+                {
+                    int64_t gk[GX], gb[GX];
+#pragma unroll
+                    for (int u = 0; u < GX; u++) {
+                        gk[u] = (int64_t)row[u][0];
+                        gb[u] = hb_block_of(win, (int64_t)row[u][1]);
+                        slot[u] = hb_slot_of(win, (int64_t)row[u][1], gb[u]);
+                        row[u][1] = (uint64_t)gb[u];
+                    }
+                    probe_batch<NA, E, GX>(S, gk, gb, ge);
+                }
+                static_for<GX>([&](auto UU) {
+                    constexpr int u = decltype(UU)::value;
+                    if (!((live >> u) & 1u)) return;
+                    int e = ge[u];
+                    if (e < 0) e = hb_find_or_insert<NWP, E, OPS>(S, (int64_t)row[u][0], (int64_t)row[u][1], a.wd);
+                    if (e < 0) return;  // state overflow (flagged)
+                    const int sl = slot[u];
+#pragma unroll
+                    for (int w = 0; w < NWP; w++)
+                        if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[sl * NWP + w][e], row[u][2 + w]);
+                    atomicOr(&S.flag[e], F_ACC | (1u << (HB_MASK_SHIFT + sl)));
+                });
+            };
+            gather_runs<NWP, GU, GF, FW_MG_PIPE1 != 0>(a, sb, pend, fold_rows);
+            uint32_t ovf = run_overflow(a, sb, pend);
+            while (ovf) {
+                const int pi = __ffs(ovf) - 1;
+                ovf &= ovf - 1;
+                gather_cells_push<NWP, GU, GF>(a, sb, pi, fold_rows);
+            }
+        } else if (PIPE && do_flush) {
             constexpr int GP = GU;  // two full blocks fit beside the block-state code
             auto ngroups_of = [&](int64_t p) {
                 const int nc = (int)cell_pad(a.slot_nch[p]);
@@ -364,6 +399,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
             }
         }
         __syncthreads();
+        if (do_flush && a.runs) run_release(a, sb, pend);
         // ---- fire: every due window that holds data, each by exactly one block entry
         if (do_fire) {
             const int n = min(S.n, E);

@@ -101,7 +101,7 @@ __device__ int find_entry(StateLds<NW, E>& S, int64_t k, int64_t s) {
 // Finds (k, s) or inserts it.  A new entry starts from `v` folded into the identity (or the
 // identity when v is null) with flags `flag0`; *inserted tells the caller it must not fold v again.
 template <int NW, int E, uint32_t OPS = OPS_ANY>
-__device__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd,
+__device__ __forceinline__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int64_t s, const WordDesc& wd,
                               const uint64_t* v = nullptr, uint32_t flag0 = 0, bool* inserted = nullptr) {
     constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
     uint32_t h = index_hash(k, s) & MASK;
@@ -202,7 +202,7 @@ __device__ __forceinline__ int64_t claim_out_row(const MergeArgs& a, int sb, int
 }
 
 template <int NW, bool Q>
-__device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
+__device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t we, const uint64_t* acc) {
     if (FW_ABL(a) & AB_M_NO_EMIT) return;
     const int64_t i = claim_out_row(a, sb, s_emit);
     if (i < 0) return;
@@ -260,7 +260,7 @@ __device__ void emit_row(const MergeArgs& a, int sb, int32_t* s_emit, int64_t ke
 // (COUNT(*) / COUNT: count; SUM, MIN, MAX: value, NULL-able; AVG: sum, count), window_end =
 // window_start = sliceEnd.  The GLOBAL phase ingests exactly these columns.
 template <int NW, bool Q>
-__device__ void emit_partial(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t se, const uint64_t* acc) {
+__device__ __forceinline__ void emit_partial(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t se, const uint64_t* acc) {
     const int64_t i = claim_out_row(a, sb, s_emit);
     if (i < 0) return;
     a.out_key[i] = key;
@@ -363,7 +363,7 @@ __device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW,
 // (An entry absent when cached may since have been inserted by another chain of the key, but only
 // empty -- without F_ACC -- which merges like an absent one.)
 template <int NW, int E, bool Q, uint32_t OPS>
-__device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit,
+__device__ __forceinline__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit,
                                    uint64_t* fst = nullptr) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
@@ -455,7 +455,7 @@ __device__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e
 // clearWindow expires we (and the first slice at the last step).  The merged accumulator stays in
 // registers across the chain and is written back to the first slice once.
 template <int NW, int E, bool Q, uint32_t OPS>
-__device__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+__device__ __forceinline__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
     const int64_t k = S.key[e];
@@ -544,12 +544,13 @@ __device__ __forceinline__ void mark_hop_successor(const MergeArgs& a, StateLds<
 // (registerCleanupTimer).  Windows the watermark already fired are not reached here: their rows
 // took the late-fire path.
 template <int NW, int E>
-__device__ void ds_add_to_windows(const MergeArgs& a, StateLds<NW, E>& S, int64_t k, int64_t pe, const uint64_t* v,
+__device__ __forceinline__ void ds_add_to_windows(const MergeArgs& a, StateLds<NW, E>& S, int64_t k, int64_t pe, const uint64_t* v,
                                   int64_t w_old, bool late_rows) {
     const WinDesc& w = a.win;
     const int64_t e0 = ds_first_window_end(w, pe);
     for (int i = 0; i < w.n_win; i++) {
         const int64_t e = wsub(e0, (int64_t)i * w.slide);
+        if (!ds_window_holds_pane(w, e, pe)) break;
         const int64_t ct = ds_cleanup_time(w, e);
         if (ct <= w_old) continue;  // isWindowLate
         const bool fired_already = is_fired(e, w_old);
@@ -571,7 +572,7 @@ __device__ __forceinline__ bool ds_pane_in_window(const WinDesc& w, int64_t pe, 
     const uint64_t d = (uint64_t)wsub(e0, e);
     if ((int64_t)d < 0) return false;
     const uint64_t q = udiv(d, w.slide_div);
-    return q * (uint64_t)w.slide == d && q < (uint64_t)w.n_win;
+    return q * (uint64_t)w.slide == d && q < (uint64_t)w.n_win && ds_window_holds_pane(w, e, pe);
 }
 
 // DataStream timers of one entry at watermark W (WindowOperator.onEventTime :450-494): the
@@ -606,7 +607,7 @@ struct Stamps {
         for (int i = 0; i < N_STAMPS; i++) acc[i] = 0;
         if (on) t = __builtin_amdgcn_s_memtime();
     }
-    __device__ void mark(int phase) {  // call right after a __syncthreads()
+    __device__ __forceinline__ void mark(int phase) {  // call right after a __syncthreads()
         if (!on) return;
         const uint64_t n = __builtin_amdgcn_s_memtime();
         acc[phase] += n - t;
@@ -775,6 +776,182 @@ __device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t 
     return live;
 }
 
+// ---- the gather over runs (IngestArgs::runs).  The pending pushes' rows of one ingest superbucket
+// lie in RUN_X contiguous sub-runs per push; lane l of every wave holds segment l = (push l / RUN_X,
+// sub-run l % RUN_X), so the 64 lanes cover FW_MAX_PENDING pushes.  A wave deals a block of 64 * G
+// consecutive rows of the concatenated segments over its lanes: neighbouring lanes load neighbouring
+// rows, and no load depends on another (no cell words).
+static_assert(FW_MAX_PENDING * RUN_X <= 64, "one lane per (push, sub-run)");
+struct RunSegs {
+    uint32_t tot;   // rows in all segments
+    uint32_t excl;  // this lane's segment: rows of the segments before it
+    uint32_t adj;   // this lane's segment: run row index of its first row, less excl (mod 2^32)
+    uint32_t pf;    // this lane's segment: push | run format << 4
+};
+__device__ __forceinline__ RunSegs run_segs(const MergeArgs& a, int isb, int64_t pend) {
+    const int lane = threadIdx.x & 63;
+    const int p = lane / RUN_X, x = lane % RUN_X;
+    uint32_t n = 0, fm = 0;
+    if (p < pend) {
+        n = min(a.run_fill[((size_t)p * RUN_X + x) * a.n_sb + isb], (uint32_t)a.sub_cap);
+        fm = (uint32_t)a.slot_fmt[p];
+    }
+    uint32_t inc = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= d) inc += t;
+    }
+    RunSegs g;
+    g.tot = (uint32_t)__shfl((int)inc, 63, 64);
+    g.excl = inc - n;
+    g.adj = (uint32_t)(((size_t)isb * RUN_X + x) * (size_t)a.sub_cap) - g.excl;
+    g.pf = (uint32_t)p | (fm << 4);
+    return g;
+}
+// rows r0 + u * 64 + lane of the segments (clamped to the last), in the PF_WIDE layout whatever their
+// push's format (as load_group_rows); returns the rows inside the segments (bit u).  r0 is
+// wave-uniform, so the segments a block touches are found with scalar reads of the lanes' segment
+// words (v_readlane): the block's first row by a scalar binary search, then the (few) segment
+// boundaries inside the block -- no per-row cross-lane shuffles.
+template <int NW, int GU, int GF>
+__device__ __forceinline__ uint32_t load_run_rows(const MergeArgs& a, const RunSegs& g, uint32_t r0_,
+                                                  uint64_t (&row)[GU][2 + NW]) {
+    constexpr int PW = 2 + NW;
+    constexpr bool CR = (GF & GF_COMPACT) != 0;
+    const int lane = threadIdx.x & 63;
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0_);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)g.tot);
+    const uint32_t last = min(r0 + (uint32_t)(64 * GU), tot) - 1u;  // the block's last row (tot > 0)
+    const uint32_t first = min(r0, tot - 1u);  // a block past the end re-reads the last row
+    int cur = 0;
+#pragma unroll
+    for (int step = 32; step > 0; step >>= 1)
+        if ((uint32_t)__builtin_amdgcn_readlane((int)g.excl, cur + step) <= first) cur += step;
+    uint32_t x[GU], adj[GU], pf[GU];
+    {
+        const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)g.adj, cur);
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane((int)g.pf, cur);
+#pragma unroll
+        for (int u = 0; u < GU; u++) {
+            x[u] = min(r0 + (uint32_t)(u * 64 + lane), tot - 1u);
+            adj[u] = a0;
+            pf[u] = p0;
+        }
+    }
+    while (cur < 63) {  // (uniform) the boundaries inside the block, empty segments included
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)g.excl, cur + 1);
+        if (b > last) break;
+        cur++;
+        const uint32_t an = (uint32_t)__builtin_amdgcn_readlane((int)g.adj, cur);
+        const uint32_t pn = (uint32_t)__builtin_amdgcn_readlane((int)g.pf, cur);
+#pragma unroll
+        for (int u = 0; u < GU; u++) {
+            adj[u] = x[u] >= b ? an : adj[u];
+            pf[u] = x[u] >= b ? pn : pf[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < GU; u++) {
+        const uint32_t ri = adj[u] + x[u];  // row index in its push's run region
+        const uint32_t p = pf[u] & 15u, fmt = pf[u] >> 4;
+        const uint64_t* base = a.runs + (size_t)p * a.run_rows * PW;
+        if (!CR || fmt == PF_WIDE) {
+            load_words<PW>(base + (size_t)ri * PW, row[u]);
+        } else {
+            const uint32_t rank = a.run_ranks[(size_t)p * a.run_rows + ri];
+            row[u][1] = (uint64_t)(a.slot_base[p] + (int64_t)(rank * (uint32_t)a.win.interval));
+            if (fmt == PF_NARROW) {
+                uint64_t t[1 + NW];
+                load_words<1 + NW>(base + (size_t)ri * (1 + NW), t);
+                row[u][0] = t[0];
+#pragma unroll
+                for (int w = 0; w < NW; w++) row[u][2 + w] = t[1 + w];
+            } else {  // PF_UNIT: COUNT(*) alone, nothing folded
+                row[u][0] = base[ri];
+#pragma unroll
+                for (int w = 0; w < NW; w++) row[u][2 + w] = w == 0 ? 1ull : 0ull;
+            }
+        }
+    }
+    uint32_t live = 0;
+#pragma unroll
+    for (int u = 0; u < GU; u++) live |= (uint32_t)(r0 + (uint32_t)(u * 64 + lane) < tot) << u;
+    return live;
+}
+// every run row of superbucket sb's pending pushes through process(rows, live): waves take blocks of
+// 64 * G rows in turn; PIPE: the next block's rows are in flight while the current one is processed
+template <int NW, int G, int GF, bool PIPE, typename F>
+__device__ __forceinline__ void gather_runs(const MergeArgs& a, int sb, int64_t pend, F&& process) {
+    constexpr int PW = 2 + NW;
+    constexpr uint32_t STEP = (uint32_t)MG_BLOCK * G;  // (MG_BLOCK / 64) waves x 64 lanes x G rows
+    const RunSegs g = run_segs(a, sb, pend);
+    uint32_t r0 = (uint32_t)(threadIdx.x >> 6) * 64u * G;
+    if (r0 >= g.tot) return;  // (wave-uniform)
+    if constexpr (PIPE) {
+        // unrolled by two: the buffers alternate without copies.  The next block's loads are issued
+        // unconditionally (past the end they re-read the last row, live bits 0), so the wait for the
+        // current block's rows is a counted s_waitcnt that leaves the next block's loads in flight
+        uint64_t ra[G][PW], rb[G][PW];
+        uint32_t la = load_run_rows<NW, G, GF>(a, g, r0, ra);
+        for (;;) {
+            const uint32_t r1 = r0 + STEP;
+            const uint32_t lb = load_run_rows<NW, G, GF>(a, g, r1, rb);
+            process(ra, la);
+            if (r1 >= g.tot) break;
+            r0 = r1 + STEP;
+            la = load_run_rows<NW, G, GF>(a, g, r0, ra);
+            process(rb, lb);
+            if (r0 >= g.tot) break;
+        }
+    } else {
+        for (; r0 < g.tot; r0 += STEP) {
+            uint64_t row[G][PW];
+            const uint32_t live = load_run_rows<NW, G, GF>(a, g, r0, row);
+            process(row, live);
+        }
+    }
+}
+// the pushes (bit p) in which some chunk left rows of superbucket sb in its own region (wave-uniform)
+__device__ __forceinline__ uint32_t run_overflow(const MergeArgs& a, int sb, int64_t pend) {
+    const int lane = threadIdx.x & 63;
+    const bool o = lane < pend && a.run_ovf[(size_t)lane * a.n_sb + sb] != 0;
+    return (uint32_t)__ballot(o);
+}
+// after the flush has read them: superbucket sb's fill counters and overflow flags start the next
+// pushes at 0 (one reader per superbucket: runs are planned without pass_log2)
+__device__ __forceinline__ void run_release(const MergeArgs& a, int sb, int64_t pend) {
+    const int t = threadIdx.x;
+    if (t >= 64) return;
+    const int p = t / RUN_X, x = t % RUN_X;
+    if (p >= pend) return;
+    a.run_fill[((size_t)p * RUN_X + x) * a.n_sb + sb] = 0u;
+    if (x == 0) a.run_ovf[(size_t)p * a.n_sb + sb] = 0u;
+}
+// the rows push pi's chunks kept in their own regions (their cell words) through process(rows, live)
+template <int NW, int GU, int GF, typename F>
+__device__ __forceinline__ void gather_cells_push(const MergeArgs& a, int sb, int64_t pi, F&& process) {
+    constexpr int PW = 2 + NW;
+    constexpr bool PS = (GF & GF_PASS) != 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ncell = (int)cell_pad(a.slot_nch[pi]);
+    const int G = min(64, ncell / (MG_BLOCK / 64));
+    const int ngroups = ncell / G;
+    const int pl = PS ? a.ks.pass_log2 : 0;
+    const int nis = a.n_sb >> pl;
+    const uint32_t* cl = a.cells + (size_t)pi * nis * a.max_nch;
+    for (int gi = wv; gi < ngroups; gi += MG_BLOCK / 64) {
+        const int f = gi * G + lane;
+        const uint32_t v = (lane >= G || cell_chunk(f) >= a.slot_nch[pi]) ? 0u : cl[((size_t)(f >> 4) * nis + (sb >> pl)) * CELL_LANES + (f & 15)];
+        const CellGroup cg = cell_group(v, f, a.chunk_rows);
+        for (uint32_t r0 = 0; r0 < cg.tot; r0 += 64 * GU) {
+            uint64_t row[GU][PW];
+            const uint32_t live = load_group_rows<NW, GU, GF>(a, pi, cg, r0, sb, row);
+            process(row, live);
+        }
+    }
+}
+
 // GF: gather variant (GF_PASS: KeySpace.pass_log2 > 0, GF_COMPACT: compact partial rows)
 template <int NW, int E, bool Q, int KIND, uint32_t OPS, int GF>
 __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
@@ -866,7 +1043,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // push's loop then loads the next push's first cell word before it gathers (FW_MG_ROLL), so that
     // round trip overlaps the current push's rows
     uint32_t v_first = 0;
-    if (gather && lane < gather_group((int)cell_pad(a.slot_nch[0])))
+    if (gather && !a.runs && lane < gather_group((int)cell_pad(a.slot_nch[0])))
         v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
     // ---- load this superbucket's entries into LDS
     for (int i = tid; i < StateLds<NW, E>::NI; i += MG_BLOCK) S.idx[i] = 0;
@@ -917,7 +1094,92 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     // group's cell word) are in flight while the current block is probed and folded.  Two blocks of
     // GU / 2 rows per lane take the registers of one block of GU rows.
     constexpr bool PIPE = FW_MG_PIPE && (NW >= 2 || FW_MG_PIPE1) && NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
-    if (PIPE && gather) {
+    if (gather && a.runs) {
+        // runs (IngestArgs::runs): the superbucket's rows of every pending push as RUN_X contiguous
+        // stretches per push, then the rows chunks kept in their own regions (overflow)
+        auto flags_of = [&](int64_t sl) -> uint32_t {
+            // register the window timer unless already fired (AggCombiner.java:103-110); the LOCAL
+            // phase keeps no timers (LocalAggCombiner.java:69-97)
+            return (a.local || win_fired(a.win, sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
+        };
+        auto fold_rows = [&](auto& row, uint32_t live) __attribute__((always_inline)) {
+            constexpr int GX = std::extent<std::remove_reference_t<decltype(row)>>::value;
+            if (FW_ABL(a) & AB_M_NO_HASH) {  // diagnostic: loads only
+                uint64_t x = 0;
+#pragma unroll
+                for (int u = 0; u < GX; u++) x ^= row[u][0] ^ row[u][1] ^ row[u][PW - 1];
+                asm volatile("" ::"v"(x));
+                return;
+            }
+            if constexpr (KIND == KIND_DSWIN) {
+                static_for<GX>([&](auto UU) {
+                    constexpr int u = decltype(UU)::value;
+                    if ((live >> u) & 1u)
+                        ds_add_to_windows<NW, E>(a, S, (int64_t)row[u][0], (int64_t)row[u][1], &row[u][2], w_old, false);
+                });
+            } else {
+                int ge[GX];
+                {
+                    int64_t gk[GX], gs[GX];
+#pragma unroll
+                    for (int u = 0; u < GX; u++) {
+                        gk[u] = (int64_t)row[u][0];
+                        gs[u] = (int64_t)row[u][1];
+                    }
+                    probe_batch<NW, E, GX>(S, gk, gs, ge);
+                }
+                uint32_t miss = 0;
+                static_for<GX>([&](auto UU) {
+                    constexpr int u = decltype(UU)::value;
+                    if (!((live >> u) & 1u)) return;
+                    const int e = ge[u];  // -1 / -2: not decided by the batched first probe
+                    if (e < 0) {
+                        miss |= 1u << u;
+                        return;
+                    }
+                    if (FW_ABL(a) & AB_M_NO_FOLDOP) return;
+#pragma unroll
+                    for (int w = 0; w < NW; w++)
+                        if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
+                    atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
+                });
+                while (miss) {  // the wave loops max(popcount) times, not GX times
+                    const int um = __ffs(miss) - 1;
+                    miss &= miss - 1;
+                    uint64_t r[PW];
+                    static_for<GX>([&](auto UU) {
+                        constexpr int u = decltype(UU)::value;
+                        if (u == um) {
+#pragma unroll
+                            for (int w = 0; w < PW; w++) r[w] = row[u][w];
+                        }
+                    });
+                    const uint32_t fl = flags_of((int64_t)r[1]);
+                    bool ins = false;
+                    const int e = find_or_insert<NW, E, OPS>(S, (int64_t)r[0], (int64_t)r[1], a.wd, &r[2], fl, &ins);
+                    if (e < 0 || ins || (FW_ABL(a) & AB_M_NO_FOLDOP)) continue;
+#pragma unroll
+                    for (int w = 0; w < NW; w++)
+                        if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], r[2 + w]);
+                    atomicOr(&S.flag[e], fl);
+                }
+            }
+        };
+        // TUMBLE / CUMULATE up to 4 words: software-pipelined (two blocks in flight); the others
+        // (HOP chains, DataStream windows) leave no registers for a second block
+        constexpr bool RP = FW_MG_PIPE && NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
+#ifndef FW_GR
+#define FW_GR 0  // rows per lane per pipelined block (0: half of mg_rows_in_flight)
+#endif
+        constexpr int GR = RP ? (FW_GR > 0 ? FW_GR : GU / 2 > 0 ? GU / 2 : 1) : GU;
+        gather_runs<NW, GR, GF, RP>(a, sb, pend, fold_rows);
+        uint32_t ovf = run_overflow(a, sb, pend);
+        while (ovf) {
+            const int pi = __ffs(ovf) - 1;
+            ovf &= ovf - 1;
+            gather_cells_push<NW, GU, GF>(a, sb, pi, fold_rows);
+        }
+    } else if (PIPE && gather) {
         constexpr int GP = NW == 1 ? GU : GU / 2 > 0 ? GU / 2 : 1;  // one word: two full blocks fit
         auto flags_of = [&](int64_t sl) -> uint32_t {
             return (a.local || win_fired(a.win, sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
@@ -1149,6 +1411,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     }
     __syncthreads();
     stm.mark(1);
+    if (gather && a.runs) run_release(a, sb, pend);
     // ---- DataStream late-fire rows: an element for a fired window that is not cleaned yet fires
     // that window at once with the element added (EventTimeTrigger.onElement -> FIRE,
     // WindowOperator.java:418-426).  Every such element emits the window's contents as of its own
@@ -1181,6 +1444,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
             const int64_t e0 = ds_first_window_end(w, pe);
             for (int i = 0; i < w.n_win; i++) {
                 const int64_t e = wsub(e0, (int64_t)i * w.slide);
+                if (!ds_window_holds_pane(w, e, pe)) break;
                 if (ds_cleanup_time(w, e) <= w_old || !is_fired(e, w_old)) continue;
                 uint64_t acc[NW];
                 const int es = find_entry(S, k, e);

@@ -2,7 +2,7 @@
 
 WindowOperatorBuilder.buildWindowOperator (flink-runtime/.../windowing/WindowOperatorBuilder.java:432-446)
 would return this operator iff: the assigner is TumblingEventTimeWindows or
-SlidingEventTimeWindows (size % slide == 0), the trigger is EventTimeTrigger, there is no
+SlidingEventTimeWindows (any size and slide), the trigger is EventTimeTrigger, there is no
 evictor, and the function is a built-in field aggregation (SumAggregator / ComparableAggregator
 for min/max, WindowedStream.java:660-880) on a numeric field.  Any allowedLateness and a
 late-data side output (sideOutputLateData) are supported.  Anything else stays on the reference
@@ -42,8 +42,8 @@ def is_gpu_eligible(assigner, trigger, aggregation, *, evictor=None, allowed_lat
                     late_data_output_tag=None):
     if not isinstance(assigner, (TumblingEventTimeWindows, SlidingEventTimeWindows)):
         return False, "assigner is not Tumbling/SlidingEventTimeWindows"
-    if isinstance(assigner, SlidingEventTimeWindows) and assigner.size % assigner.slide != 0:
-        return False, "sliding windows need size % slide == 0 to share slices"
+    if isinstance(assigner, SlidingEventTimeWindows) and assigner.size < assigner.slide:
+        return False, "sliding windows with gaps (size < slide)"
     if not isinstance(trigger, EventTimeTrigger):
         return False, "custom trigger"
     if evictor is not None:

@@ -134,6 +134,12 @@ CASES = {
                                             allowed_lateness_ms=2500, late_side_output=True, aggs=[(abi.AGG_MAX, 0, I64)]),
     "ds_sliding_side_output": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=4000, slide_ms=1000,
                                    late_side_output=True, aggs=[(abi.AGG_MIN, 1, F64)]),
+    # slide not dividing size (SlidingEventTimeWindows.java:77-90): 1 s panes, each in 2 or 3 windows
+    "ds_sliding_nondiv_sum": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=5000, slide_ms=2000,
+                                  aggs=[(abi.AGG_SUM, 0, I64)]),
+    "ds_sliding_nondiv_lateness_side_output": dict(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=7000,
+                                                   slide_ms=3000, offset_ms=1000, allowed_lateness_ms=2500,
+                                                   late_side_output=True, aggs=[(abi.AGG_MAX, 1, F64)]),
 }
 
 

@@ -117,6 +117,8 @@ def test_datastream_eligible():
     # allowedLateness and sideOutputLateData (WindowOperator.java:609-682, :440-446)
     assert dso.is_gpu_eligible(**dict(DS_OK, allowed_lateness=1000, late_data_output_tag="late")) == (True, "")
     assert dso.is_gpu_eligible(SlidingEventTimeWindows.of(6000, 2000), EventTimeTrigger(), ("max", "DOUBLE"))[0]
+    # slide need not divide size (SlidingEventTimeWindows.java:77-90): panes of gcd(size, slide)
+    assert dso.is_gpu_eligible(SlidingEventTimeWindows.of(5000, 2000), EventTimeTrigger(), ("sum", "LONG"))[0]
 
 
 class _CountTrigger:  # a custom trigger (CountTrigger, ContinuousEventTimeTrigger, ...)
@@ -132,7 +134,7 @@ class _Sessions:  # a merging assigner (EventTimeSessionWindows)
     (dict(evictor=object()), "evictor"),
     (dict(trigger=_CountTrigger()), "custom trigger"),
     (dict(assigner=_Sessions()), "assigner"),
-    (dict(assigner=SlidingEventTimeWindows.of(5000, 2000)), "size % slide"),
+    (dict(assigner=SlidingEventTimeWindows.of(2000, 5000)), "size < slide"),
     (dict(aggregation=("reduce", "LONG")), "built-in field aggregation"),
     (dict(aggregation=("sum", "FLOAT")), "built-in field aggregation"),
 ])

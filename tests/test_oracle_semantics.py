@@ -141,3 +141,33 @@ def test_datastream_first_element_ordinal():
     got = dict(zip(r["window_end"].tolist(), r["first_ord"].tolist()))
     assert got == {T0 + 1000: 1, T0 + 2000: 0, T0 + 3000: 0, T0 + 4000: (1 << 32) | 0}
     o.close()
+
+
+def test_datastream_sliding_windows_slide_not_dividing_size():
+    """SlidingEventTimeWindows with slide not dividing size (5 s / 2 s, offset 1 s): every element
+    belongs to the windows SlidingEventTimeWindows.assignWindows (:77-90) lists for it -- 2 or 3 of
+    them here -- and each fired window holds the sum of exactly those elements.  The expected rows
+    come from the assigner's own loop (windowing.py mirrors it), not from the oracle."""
+    from flink_amd.datastream.windowing import SlidingEventTimeWindows
+    size, slide, off = 5000, 2000, 1000
+    asg = SlidingEventTimeWindows.of(size, slide, off)
+    cfg = abi.make_config(api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP, size_ms=size, slide_ms=slide, offset_ms=off,
+                          aggs=[(abi.AGG_SUM, 0, abi.T_I64)], value_col_types=[abi.T_I64], key_hash=abi.KEYHASH_LONG)
+    rng = np.random.default_rng(7)
+    n = 4000
+    keys = rng.integers(0, 17, n).astype(np.int64)
+    ts = (T0 + rng.integers(0, 40_000, n)).astype(np.int64)
+    vals = rng.integers(-1000, 1000, n).astype(np.int64)
+    want = {}
+    for k, t, v in zip(keys.tolist(), ts.tolist(), vals.tolist()):
+        wins = asg.assign_windows(t)
+        assert len(wins) in (2, 3)
+        for s, e in wins:
+            want[(k, e)] = want.get((k, e), 0) + v
+    o = OracleOperator(cfg)
+    o.process_batch(keys, ts, [vals])
+    o.process_watermark(T0 + 60_000)
+    r = o.results()
+    got = {(int(k), int(e)): int(v) for k, e, v in zip(r["key"], r["window_end"], r["values"][0])}
+    o.close()
+    assert got == want

@@ -175,6 +175,10 @@ def main():
     ap.add_argument("--plan", default="auto", choices=["auto", "one", "two"],
                     help="one- or two-phase window aggregation; auto: two-phase for cfg4/cfg5 at N>1 (partials on "
                          "the wire), one-phase otherwise")
+    ap.add_argument("--valve", default="device", choices=["device", "host"],
+                    help="N>1: the watermark valve / overflow agreement as one device all-reduce read by "
+                         "fw_advance_device (no host wait per step), or on the host (gloo all-reduce after "
+                         "waiting for the partition kernel)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
                          "one-GPU box: ranks share the GPUs round robin and the exchange is staged "
@@ -249,6 +253,22 @@ def main():
             else:
                 handle.push_device(gk[b], gt[b], [gv[b]] if nv else [])
             return watermark(b, wl["rate"])
+        if args.valve == "device":
+            # the device-side valve: the previous step's overflow round (settled one step late: its
+            # all-reduce is long done), then partition + all-to-all + ingest + ONE device all-reduce of
+            # (overflow, watermark, share) + fw_advance_device -- no host wait on this step's GPU work
+            vs = handle.__dict__.setdefault("_valve", {"px": None, "wm": None})
+            if vs["px"] is not None:
+                spill = vs["px"].settle()
+                if spill is not None:
+                    n_sp = spill.numel() // vs["px"].row_words
+                    handle.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=dev), spill,
+                                                       vs["px"].row_words)
+            px = ex.exchange_packed_async(gk[b], gt[b], [gv[b]] if nv else [])
+            handle.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
+            wm = px.finish_device(watermark(b, wl["rate"]), vs["wm"])
+            vs.update(px=px, wm=wm)
+            return wm
         # the received segments' ingest is queued before the host waits for the partition's
         # counts (overflow round + watermark valve), so the GPU stays busy through that host step
         px = ex.exchange_packed_async(gk[b], gt[b], [gv[b]] if nv else [])
@@ -280,7 +300,13 @@ def main():
         def step(self, b):
             self.tp.local.push_device(gk[b], gt[b], [gv[b]] if nv else [])
             self.tp.glob.reset_results()  # blackhole sink
-            self.tp.step_device(watermark(b, wl["rate"]))
+            if args.valve == "device":
+                self.tp.step_device_valve(watermark(b, wl["rate"]))
+            else:
+                self.tp.step_device(watermark(b, wl["rate"]))
+
+        def settle(self):
+            self.tp.settle()
 
         def set_profiling(self, *a, **k):
             self.tp.local.set_profiling(*a, **k)
@@ -317,7 +343,20 @@ def main():
                 continue
             wm = push_step(b, handle)
             handle.reset_results()       # blackhole sink: results of the previous watermark consumed
-            handle.advance(wm)
+            if torch.is_tensor(wm):
+                handle.advance_device(wm)
+            else:
+                handle.advance(wm)
+        # the device valve's last overflow round (settled one step late)
+        if two_phase:
+            handle.settle()
+        elif getattr(handle, "_valve", None) and handle._valve["px"] is not None:
+            spill = handle._valve["px"].settle()
+            if spill is not None:
+                n_sp = spill.numel() // handle._valve["px"].row_words
+                handle.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=dev), spill,
+                                                   handle._valve["px"].row_words)
+            handle._valve["px"] = None
 
     if args.calibrate_traffic:
         # same access width as k_ingest's column loads (global_load_dwordx2 per lane), sized far
@@ -536,6 +575,8 @@ def main():
                        "max_parallelism": 128, "superbuckets": st["num_superbuckets"],
                        "exchange": None if world == 1 else {
                            "kind": "packed padded all-to-all, segments of the batch's even share + 25 %",
+                           "watermark_valve": ("device all-reduce (overflow, watermark, share) -> fw_advance_device"
+                                               if args.valve == "device" else "host gloo all-reduce"),
                            "segment_rows": ex.segment_capacity(B, world),
                            "overflow_rounds": ex.spill_rounds}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -52,6 +52,7 @@ def lib():
         "fw_partition_packed_spill": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, vp, i64, vp]),
         "fw_partition_packed_spill_dn": (i32, [vp, vp, vp, vp, i32, i64, vp, i32, i32, i32, i64, vp, vp, vp, vp, i64, vp]),
         "fw_advance": (i32, [vp, i64]),
+        "fw_advance_device": (i32, [vp, vp]),
         "fw_flush": (i32, [vp]),
         "fw_results": (i32, [vp, P(abi.fw_result), i32]),
         "fw_results_reset": (i32, [vp]),
@@ -98,7 +99,7 @@ def lib():
 
 # every symbol the public header declares (tests check they are exported)
 EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
-            "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance",
+            "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance", "fw_advance_device",
             "fw_flush", "fw_results", "fw_results_reset", "fw_results_async", "fw_results_ready", "fw_results_device", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_snapshot_key_group_heap", "fw_restore_key_group_heap", "fw_key_row_hash", "fw_host_key_row_hash",

@@ -1333,6 +1333,23 @@ int fw_advance(fw_handle* h, int64_t watermark) {
     return FW_OK;
 }
 
+int fw_advance_device(fw_handle* h, const int64_t* d_watermark) {
+    if (!h || !d_watermark) return fail(FW_E_INVALID, "null argument");
+    MergeArgs a = merge_args(h, INT64_MIN, 0);
+    a.wm_dev = d_watermark;
+    HIP_TRY(launch_merge_fire(a, h->stream, h->timer));
+    // launch_merge's bookkeeping; the host mirrors of currentProgress stay behind the device (they
+    // only ever skip launches, so a stale, lower value skips fewer)
+    h->pushes_at_merge[h->merge_seq % 64] = h->pushes_total;
+    h->merge_seq++;
+    h->reset_pending = false;
+    if (h->keyrow)
+        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->ks.n_sb, h->cap_e, h->pwe,
+                                  2 + h->nw_t, h->parts, h->cap_rows, h->treq, h->out_key, h->sb_out, h->slab_cap,
+                                  h->stream));
+    return FW_OK;
+}
+
 int fw_flush(fw_handle* h) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     return force_flush(h);

@@ -548,6 +548,7 @@ struct MergeArgs {
     int64_t slab_cap;
     int64_t out_cap;         // overflow rows
     int64_t wm;              // watermark of this advance
+    const int64_t* wm_dev;   // (fw_advance_device) the watermark in device memory instead of wm
     int32_t force_flush;     // prepareCheckpoint: flush, no timers
     int32_t reset_out;       // the results were consumed (fw_results_reset): emit from slab row 0
     int32_t ablate;          // development only (FW_ABLATE)

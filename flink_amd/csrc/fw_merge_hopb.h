@@ -87,7 +87,7 @@ __device__ __forceinline__ void hb_merge_slot(const MergeArgs& a, const StateLds
 // no entry for the next block -- those ending in the next block that still hold slices of this one.
 // A window fires iff it ends in (W0, W] and holds data.  Returns the windows fired.
 template <int NWP, int E, uint32_t OPS>
-__device__ __forceinline__ uint32_t hb_fire_entry(const MergeArgs& a, StateLds<HB_R * NWP, E>& S, int e, int64_t w_old, int sb,
+__device__ __forceinline__ uint32_t hb_fire_entry(const MergeArgs& a, int64_t W, StateLds<HB_R * NWP, E>& S, int e, int64_t w_old, int sb,
                                   int32_t* s_emit) {
     const WinDesc& w = a.win;
     const int n = w.n_slices;
@@ -99,7 +99,7 @@ __device__ __forceinline__ uint32_t hb_fire_entry(const MergeArgs& a, StateLds<H
     uint32_t nf = 0;
     for (int j = 0; j < HB_R + n - 1; j++) {
         const int64_t we = wadd(bs, (int64_t)(j + 1) * w.interval);
-        if (!win_fired(w, we, a.wm) || win_fired(w, we, w_old)) continue;  // not due in this advance
+        if (!win_fired(w, we, W) || win_fired(w, we, w_old)) continue;  // not due in this advance
         // the window's slots: j, j-1, ..., j-n+1 (newest first); < 0: previous block, >= HB_R: next
         const int lo = j - n + 1;
         if (j >= HB_R) {  // the next block fires it if it exists
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
     kt_start(a.kt);
     Ctrl* c = a.ctrl;
     const WinDesc& win = a.win;
-    const int64_t W = a.wm;
+    const int64_t W = merge_watermark(a);
     const int64_t cur = __hip_atomic_load(&c->cur, __ATOMIC_RELAXED, DEV_SCOPE);
     const int64_t pend = __hip_atomic_load(&c->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
     const int64_t ntp = __hip_atomic_load(&c->ntp, __ATOMIC_RELAXED, DEV_SCOPE);
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
             const int n = min(S.n, E);
             uint32_t nf = 0;
             const int qlane = (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
-            for (int e = qlane; e < n; e += MG_BLOCK) nf += hb_fire_entry<NWP, E, OPS>(a, S, e, w_old, sb, &s_emit);
+            for (int e = qlane; e < n; e += MG_BLOCK) nf += hb_fire_entry<NWP, E, OPS>(a, W, S, e, w_old, sb, &s_emit);
             nf = wave_sum_u32(nf);
             if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
         }
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
         }
         __syncthreads();
     }
-    merge_ticket(a);
+    merge_ticket(a, W);
 }
 
 template <int NWP, int GF>

@@ -363,7 +363,7 @@ __device__ __forceinline__ uint32_t fire_tumble(const MergeArgs& a, StateLds<NW,
 // (An entry absent when cached may since have been inserted by another chain of the key, but only
 // empty -- without F_ACC -- which merges like an absent one.)
 template <int NW, int E, bool Q, uint32_t OPS>
-__device__ __forceinline__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit,
+__device__ __forceinline__ uint32_t fire_hop_chain(const MergeArgs& a, int64_t W, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit,
                                    uint64_t* fst = nullptr) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
@@ -432,7 +432,7 @@ __device__ __forceinline__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<
         const int en = find_or_insert<NW, E, OPS>(S, k, nx, wd);
         lap(2);
         if (en < 0) break;  // state overflow (flagged)
-        if (!win_fired(w, nx, a.wm)) {
+        if (!win_fired(w, nx, W)) {
             atomicOr(&S.flag[en], F_TIMER);
             break;
         }
@@ -455,7 +455,7 @@ __device__ __forceinline__ uint32_t fire_hop_chain(const MergeArgs& a, StateLds<
 // clearWindow expires we (and the first slice at the last step).  The merged accumulator stays in
 // registers across the chain and is written back to the first slice once.
 template <int NW, int E, bool Q, uint32_t OPS>
-__device__ __forceinline__ uint32_t fire_cumulate_chain(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+__device__ __forceinline__ uint32_t fire_cumulate_chain(const MergeArgs& a, int64_t W, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
     const WinDesc& w = a.win;
     const WordDesc& wd = a.wd;
     const int64_t k = S.key[e];
@@ -486,7 +486,7 @@ __device__ __forceinline__ uint32_t fire_cumulate_chain(const MergeArgs& a, Stat
             break;
         }
         const int64_t nx = wadd(we, w.interval);
-        if (!win_fired(w, nx, a.wm)) {
+        if (!win_fired(w, nx, W)) {
             const int en = find_or_insert<NW, E, OPS>(S, k, nx, wd);
             if (en >= 0) atomicOr(&S.flag[en], F_TIMER);
             break;
@@ -506,14 +506,14 @@ __device__ __forceinline__ uint32_t fire_cumulate_chain(const MergeArgs& a, Stat
 // chain (CUMULATE chains never stop before the window's last step), so it starts no chain of its
 // own.  Each due step marks the next due step of its window.
 template <int NW, int E>
-__device__ __forceinline__ void mark_cumulate_successor(const MergeArgs& a, StateLds<NW, E>& S, int e) {
+__device__ __forceinline__ void mark_cumulate_successor(const MergeArgs& a, int64_t W, StateLds<NW, E>& S, int e) {
     const WinDesc& w = a.win;
     const int64_t k = S.key[e];
     const int64_t we = S.slice[e];
     const int64_t last = wadd(window_start_of(w, we), w.size);
     for (int64_t s = we; s != last;) {
         s = wadd(s, w.interval);
-        if (!win_fired(w, s, a.wm)) break;
+        if (!win_fired(w, s, W)) break;
         const int e2 = find_entry(S, k, s);
         if (e2 >= 0 && (S.flag[e2] & F_TIMER)) {
             atomicOr(&S.flag[e2], F_NOTHEAD);
@@ -528,11 +528,11 @@ __device__ __forceinline__ void mark_cumulate_successor(const MergeArgs& a, Stat
 // an accumulator (with its COUNT(*) > 0) proves the predecessor window non-empty; a window whose
 // predecessor cannot be proven so starts a chain, and the F_FIRED claim settles any overlap.
 template <int NW, int E>
-__device__ __forceinline__ void mark_hop_successor(const MergeArgs& a, StateLds<NW, E>& S, int e) {
+__device__ __forceinline__ void mark_hop_successor(const MergeArgs& a, int64_t W, StateLds<NW, E>& S, int e) {
     const int64_t k = S.key[e];
     const int64_t pe = wsub(S.slice[e], a.win.interval);
     const int p = find_entry(S, k, pe);
-    if (p >= 0 && (S.flag[p] & (F_TIMER | F_ACC)) == (F_TIMER | F_ACC) && win_fired(a.win, pe, a.wm) &&
+    if (p >= 0 && (S.flag[p] & (F_TIMER | F_ACC)) == (F_TIMER | F_ACC) && win_fired(a.win, pe, W) &&
         (a.ad.count_star_word < 0 || S.acc[a.ad.count_star_word][p] != 0))
         atomicOr(&S.flag[e], F_NOTHEAD);
 }
@@ -579,11 +579,11 @@ __device__ __forceinline__ bool ds_pane_in_window(const WinDesc& w, int64_t pe, 
 // maxTimestamp timer FIREs (emitWindowContents), the cleanup timer clears the window state; with
 // allowedLateness 0 they are the same timer (fire, then clear)
 template <int NW, int E>
-__device__ __forceinline__ uint32_t fire_ds(const MergeArgs& a, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
+__device__ __forceinline__ uint32_t fire_ds(const MergeArgs& a, int64_t W, StateLds<NW, E>& S, int e, int sb, int32_t* s_emit) {
     const int64_t we = S.slice[e];
     const uint32_t f = S.flag[e];
-    const bool fire = (f & F_TIMER) && is_fired(we, a.wm);
-    const bool clean = (f & F_CLEAN) && ds_cleanup_time(a.win, we) <= a.wm;
+    const bool fire = (f & F_TIMER) && is_fired(we, W);
+    const bool clean = (f & F_CLEAN) && ds_cleanup_time(a.win, we) <= W;
     if (fire && (f & F_ACC)) {
         uint64_t acc[NW];
 #pragma unroll
@@ -628,13 +628,19 @@ __device__ __forceinline__ int sb_of_block(int b, int n_sb) {
     return (b % 8) * (n_sb / 8) + b / 8;
 }
 
+// the watermark of this advance: the launch argument, or (fw_advance_device) the value a device-side
+// watermark valve left in device memory (StatusWatermarkValve min over input channels, computed on the
+// device without a host round trip)
+__device__ __forceinline__ int64_t merge_watermark(const MergeArgs& a) {
+    return a.wm_dev ? __hip_atomic_load(a.wm_dev, __ATOMIC_RELAXED, DEV_SCOPE) : a.wm;
+}
+
 // the last workgroup of a k_merge_fire launch applies the launch's control decisions (every
 // workgroup read the old values at its start): advanceProgress bookkeeping of the processor
 // (AbstractSliceSyncStateWindowAggProcessor.java:139-153), the buffer reset after a flush, the
 // consumed timer requests, and the overflow-counter switch of a result reset.
-__device__ void merge_finalize(const MergeArgs& a) {
+__device__ void merge_finalize(const MergeArgs& a, int64_t W) {
     Ctrl* c = a.ctrl;
-    const int64_t W = a.wm;
     const int64_t cur = c->cur, pend = c->pending_pushes, ntp = c->ntp;
     const bool adv = !a.force_flush && W > cur;
     const bool do_flush = pend > 0 && (a.force_flush || (adv && (a.always_flush || (W >= ntp && win_fired(a.win, c->min_pending, W)))));
@@ -661,11 +667,11 @@ __device__ void merge_finalize(const MergeArgs& a) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ void merge_ticket(const MergeArgs& a) {
+__device__ __forceinline__ void merge_ticket(const MergeArgs& a, int64_t W) {
     if (threadIdx.x != 0) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (grid_last_wg(a.tickets->c[1])) {
-        merge_finalize(a);
+        merge_finalize(a, W);
         kt_end(a.kt);
     }
 }
@@ -970,7 +976,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     const int tid = threadIdx.x;
     kt_start(a.kt);
     Ctrl* c = a.ctrl;
-    const int64_t W = a.wm;
+    const int64_t W = merge_watermark(a);
     // control decisions; the launch's last workgroup applies them to the control block (merge_finalize)
     const int64_t cur = __hip_atomic_load(&c->cur, __ATOMIC_RELAXED, DEV_SCOPE);
     const int64_t pend = __hip_atomic_load(&c->pending_pushes, __ATOMIC_RELAXED, DEV_SCOPE);
@@ -1496,8 +1502,8 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         const int qlane = (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
         if (KIND == FW_WIN_CUMULATE || KIND == FW_WIN_HOP) {
             for (int q = qlane; q < nd; q += MG_BLOCK) {
-                if (KIND == FW_WIN_CUMULATE) mark_cumulate_successor<NW, E>(a, S, S.due[q]);
-                else mark_hop_successor<NW, E>(a, S, S.due[q]);
+                if (KIND == FW_WIN_CUMULATE) mark_cumulate_successor<NW, E>(a, W, S, S.due[q]);
+                else mark_hop_successor<NW, E>(a, W, S, S.due[q]);
             }
             __syncthreads();
         }
@@ -1508,13 +1514,13 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
         for (int q = qlane; q < nd; q += MG_BLOCK) {
             const int e = S.due[q];
             if (KIND == KIND_DSWIN) {
-                nf += fire_ds<NW, E>(a, S, e, sb, &s_emit);
+                nf += fire_ds<NW, E>(a, W, S, e, sb, &s_emit);
             } else if (KIND == FW_WIN_TUMBLE) {
                 nf += fire_tumble<NW, E, Q, OPS>(a, S, e, sb, &s_emit);
             } else if (KIND == FW_WIN_HOP) {
-                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_hop_chain<NW, E, Q, OPS>(a, S, e, sb, &s_emit, fs ? fst : nullptr);
+                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_hop_chain<NW, E, Q, OPS>(a, W, S, e, sb, &s_emit, fs ? fst : nullptr);
             } else {
-                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_cumulate_chain<NW, E, Q, OPS>(a, S, e, sb, &s_emit);
+                if (!(S.flag[e] & F_NOTHEAD)) nf += fire_cumulate_chain<NW, E, Q, OPS>(a, W, S, e, sb, &s_emit);
             }
         }
         if (fs && a.stamps) {
@@ -1593,7 +1599,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     stm.mark(3);
     }  // superbuckets of this workgroup (s_tk was published before the last barrier)
     stm.flush(a.stamps);
-    merge_ticket(a);
+    merge_ticket(a, W);
 }
 
 // persistent grid of the merge kernel: one workgroup per CU, at most one per superbucket

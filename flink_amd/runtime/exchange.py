@@ -219,6 +219,7 @@ class KeyByExchange:
             counts_h.copy_(counts, non_blocking=True)
             part_done = torch.cuda.Event()
             part_done.record(torch.cuda.current_stream(dev))
+            counts_d = counts
         else:  # host batch: the host partition, then the same padded layout
             pk, pt, pv, counts = self.partition(key, ts, vals64)
             send = torch.zeros(p * cap * w, dtype=torch.int64)
@@ -232,7 +233,7 @@ class KeyByExchange:
                 sp.append(rows[o + m:o + c])
                 o += c
             spill = torch.cat(sp).reshape(-1) if sp else torch.zeros(0, dtype=torch.int64)
-            counts_h, part_done = counts, None
+            counts_h, part_done, counts_d = counts, None, counts
         stage = key.is_cuda and p > 1 and dist.get_backend(self.group) != "nccl"
         mv = (lambda x: x.cpu()) if stage else (lambda x: x)
         back = (lambda x: x.to(dev)) if stage else (lambda x: x)
@@ -245,7 +246,7 @@ class KeyByExchange:
             recv, rc = back(recv), back(rc)
         else:
             recv, rc = send, counts
-        return PackedExchange(self, recv, rc, w, cap, spill, counts_h, part_done, mv, back)
+        return PackedExchange(self, recv, rc, w, cap, spill, counts_h, part_done, mv, back, counts_d)
 
     def _agree(self, overflow, watermark, share=0):
         """One host all-reduce for the overflow decision, the watermark valve's minimum and the
@@ -294,26 +295,82 @@ class KeyByExchange:
 
 
 class PackedExchange:
-    """One step's packed keyBy exchange in flight (KeyByExchange.exchange_packed_async)."""
+    """One step's packed keyBy exchange in flight (KeyByExchange.exchange_packed_async).
 
-    def __init__(self, ex, rows, recv_counts, row_words, cap, spill, counts_h, part_done, mv, back):
+    Two ways to close it: finish(watermark) -- the host waits for this subtask's partition kernel and
+    agrees on the overflow round, the watermark and the next segment size in one host all-reduce --
+    or, with no host wait, finish_device(watermark, prev) + settle() one step later: the same three
+    values travel in one DEVICE all-reduce (RCCL), the valve's watermark stays in device memory for
+    fw_advance_device, and a step with overflow holds the watermark at the previous one until its
+    spill rows, sent by settle() before the next step's rows, are in."""
+
+    def __init__(self, ex, rows, recv_counts, row_words, cap, spill, counts_h, part_done, mv, back, counts_d=None):
         self.ex, self.rows, self.recv_counts, self.row_words = ex, rows, recv_counts, row_words
         self._cap, self._spill, self._counts_h, self._part_done = cap, spill, counts_h, part_done
-        self._mv, self._back = mv, back
+        self._mv, self._back, self._counts_d = mv, back, counts_d
+        self._agreed = None  # finish_device's all-reduced [overflow, -watermark, share] (device)
 
     def finish(self, watermark=None):
         """The overflow round and the watermark valve: waits for this subtask's partition kernel
         only (the all-to-all and whatever the caller queued after it stay in flight)."""
-        ex, w, cap = self.ex, self.row_words, self._cap
+        ex = self.ex
         if self._part_done is not None:
             self._part_done.synchronize()
         cnt = self._counts_h.tolist()
-        over = [max(0, c - cap) for c in cnt]
+        over = [max(0, c - self._cap) for c in cnt]
         # the next device-counted exchange sizes its segments from the largest share any subtask
         # sent this time: every subtask must pick the same segment size, so it rides in the same
         # all-reduce as the overflow decision and the watermark
         any_over, wm, share = ex._agree(sum(over) > 0, watermark, max(cnt) if cnt else 0)
         ex._dn_share = share
+        return self._spill_round(any_over, over), wm
+
+    def finish_device(self, watermark, prev_watermark):
+        """The device-side valve (StatusWatermarkValve.java:153: min over the input channels): this
+        subtask's overflow flag, -watermark and largest per-destination share go into ONE all-reduce
+        (MAX) on the device -- RCCL on the stream, nothing waits on the host.  Returns a one-element
+        device int64 tensor: the minimum watermark, or ``prev_watermark`` (device tensor) when any
+        subtask overflowed its segments -- its spill rows are sent by settle() at the start of the next
+        step, and the watermark must not pass them before.  settle() must be called before the next
+        exchange (it also agrees on the next device-counted segment size)."""
+        ex = self.ex
+        dev = self._counts_d.device
+        t = torch.stack([(self._counts_d > self._cap).any().to(torch.int64),
+                         torch.full((), -int(watermark), dtype=torch.int64, device=dev),
+                         self._counts_d.max() if self._counts_d.numel() else torch.zeros((), dtype=torch.int64, device=dev)])
+        if ex.world > 1:
+            if self._counts_d.is_cuda and dist.get_backend(ex.group) == "nccl":
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ex.group)
+            else:  # gloo moves host tensors (the one-GPU rehearsal and the CPU tests)
+                g = ex._cpu_group if ex._cpu_group is not None else ex.group
+                th = t.cpu()
+                dist.all_reduce(th, op=dist.ReduceOp.MAX, group=g)
+                t = th.to(dev)
+        self._agreed = t
+        if prev_watermark is None:  # nothing advanced yet: an overflowing first step holds at Long.MIN_VALUE
+            prev_watermark = torch.full((1,), -(1 << 63), dtype=torch.int64, device=dev)
+        return torch.where(t[0:1] > 0, prev_watermark, -t[1:2])
+
+    def settle(self):
+        """The host half of finish_device, one step late: reads the agreed values (waits only for this
+        step's all-reduce, long done while the next step's work is queued behind it), sets the next
+        device-counted segment size, and runs the overflow round if any subtask overflowed.  Returns the
+        spill rows for this subtask (device, packed) or None."""
+        t = self._agreed
+        if t is None:
+            return None
+        self._agreed = None
+        any_over, _, share = (int(x) for x in t.tolist())
+        self.ex._dn_share = share
+        over = None
+        if any_over:
+            cnt = self._counts_h.tolist()
+            over = [max(0, c - self._cap) for c in cnt]
+        return self._spill_round(bool(any_over), over)
+
+    def _spill_round(self, any_over, over):
+        """Rows past their destination's segment, exchanged with host-known split sizes."""
+        ex, w = self.ex, self.row_words
         out_spill = None
         if any_over:
             ex.spill_rounds += 1
@@ -330,4 +387,4 @@ class PackedExchange:
                 dst = torch.empty(sum(rin) * w, dtype=torch.int64, device=src.device)
                 dist.all_to_all_single(dst, src, [r * w for r in rin], [o * w for o in over], group=ex.group)
                 out_spill = self._back(dst) if sum(rin) else None
-        return out_spill, wm
+        return out_spill

@@ -213,6 +213,14 @@ class WindowAggHandle:
     def advance(self, wm):
         check(lib().fw_advance(self._h, int(wm)))
 
+    def advance_device(self, wm_tensor):
+        """fw_advance_device: the watermark is the first element of a device int64 tensor (e.g. the
+        device-side watermark valve of KeyByExchange); the handle's stream waits for the producer's
+        current stream first."""
+        cur = self._begin_read(wm_tensor.device)
+        check(lib().fw_advance_device(self._h, wm_tensor.data_ptr()))
+        self._end_read(cur)
+
     def flush(self):
         check(lib().fw_flush(self._h))
 

@@ -89,6 +89,40 @@ class TwoPhaseWindowAgg:
         self.glob.advance(watermark if global_watermark is None else global_watermark)
         return self.glob.results(reset=True)
 
+    def step_device_valve(self, watermark):
+        """step_device with the watermark valve on the device (PackedExchange.finish_device): no host
+        wait on this step's GPU work; the previous step's overflow round and segment-size agreement are
+        settled first (one step late).  Returns the valve's watermark as a one-element device tensor.
+        Call settle() after the last step."""
+        from ..runtime.exchange import KeyByExchange
+        if self.global_cfg.nullable_cols:
+            raise ValueError("step_device moves packed rows, which carry no NULL flags: NOT NULL inputs only")
+        if self.exchange is None:
+            self.exchange = KeyByExchange(self.global_cfg.key_hash, self.global_cfg.max_parallelism)
+        self.settle()
+        self.local.advance(watermark)
+        n, key, _, se, fields, _ = self.local.device_results_async(self.device)
+        px = self.exchange.exchange_packed_async(key, se, fields, n_dev=n)
+        self.glob.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
+        wm = px.finish_device(watermark, getattr(self, "_wm_dev", None))
+        self._wm_dev = wm
+        self._px = px
+        self.glob.advance_device(wm)
+        return wm
+
+    def settle(self):
+        """The previous device-valve step's overflow round (its spill rows reach the GLOBAL operator
+        before any later watermark)."""
+        px = getattr(self, "_px", None)
+        if px is None:
+            return
+        self._px = None
+        spill = px.settle()
+        if spill is not None:
+            n_sp = spill.numel() // px.row_words
+            self.glob.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=self.device), spill,
+                                                  px.row_words)
+
     def step_device(self, watermark):
         """One watermark interval of the plan with the partials kept on the device and no host round
         trip before the exchange: the LOCAL advance, its partial rows collected on the device

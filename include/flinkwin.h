@@ -342,6 +342,14 @@ typedef struct {
 int fw_first_element_events(fw_handle* h, fw_ordinal_events* out);
 
 int fw_advance(fw_handle* h, int64_t watermark);
+/* fw_advance with the watermark read from DEVICE memory (d_watermark[0]) by the merge launch when it
+   runs on the handle's stream: the keyBy exchange's watermark valve (StatusWatermarkValve
+   .inputWatermark, StatusWatermarkValve.java:153 -- the minimum over the input channels) is then an
+   all-reduce on the device, and a step enqueues ingest and advance without waiting for its own GPU
+   work.  The caller orders the handle's stream after the producer of d_watermark.  The host cannot
+   skip watermarks that cross no slice end here (it does not know the value): the launch finds out on
+   the device. */
+int fw_advance_device(fw_handle* h, const int64_t* d_watermark);
 int fw_flush(fw_handle* h);
 /* copy_to_host != 0: host arrays owned by the handle, valid until the next call;
    otherwise device pointers. */

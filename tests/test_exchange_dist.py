@@ -228,3 +228,73 @@ def test_gloo_two_phase_union_equals_one_phase():
     want += _rows(op.results())
     assert len(got) > 1000 and got == sorted(want)
     op.close()
+
+
+def _worker_device_valve(rank, port, n_batches, n, out_q):
+    """PackedExchange.finish_device + settle (the device-side watermark valve, here on CPU tensors):
+    every row arrives once (segment or one-step-late overflow round), the watermark is the minimum
+    proposal, held at the previous one on a step whose overflow round is still outstanding."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from flink_amd.runtime.exchange import KeyByExchange
+        from oracle.oracle import key_group, key_group_range
+
+        ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+        lo, hi = key_group_range(128, WORLD, rank)
+        got, wms, prev_px, prev_wm = [], [], None, None
+
+        def take(rows_, w):
+            sp = rows_.view(-1, w)
+            got.extend(zip(sp[:, 0].tolist(), sp[:, 1].tolist(), sp[:, 2].tolist()))
+
+        for b in range(n_batches):
+            if prev_px is not None:
+                spill = prev_px.settle()
+                if spill is not None:
+                    take(spill, prev_px.row_words)
+            k, t, v = _stream(rank, b, n)
+            cap = n // 4 if b % 2 else n  # odd steps overflow
+            px = ex.exchange_packed_async(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)], cap)
+            seg = px.rows.view(WORLD, cap, px.row_words)
+            keep = torch.arange(cap)[None, :] < px.recv_counts.clamp(max=cap)[:, None]
+            take(seg[keep].reshape(-1), px.row_words)
+            wm = px.finish_device(T0 + b * 3000 - 3000 + 500 * rank, prev_wm)
+            wms.append(int(wm.item()))
+            prev_px, prev_wm = px, wm
+        spill = prev_px.settle()
+        if spill is not None:
+            take(spill, prev_px.row_words)
+        assert all(lo <= key_group(abi.KEYHASH_BINROW_BIGINT, int(x), 128) <= hi for x in {r[0] for r in got})
+        out_q.put((rank, sorted(got), wms, ex.spill_rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_device_valve_holds_watermark_until_overflow_round():
+    from oracle.oracle import operator_indices
+    n_batches, n = 6, 2000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_device_valve, args=(r, port, n_batches, n, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # every row reached its key group's subtask exactly once
+    for r in range(WORLD):
+        want = []
+        for b in range(n_batches):
+            for src in range(WORLD):
+                k, t, v = _stream(src, b, n)
+                m = operator_indices(abi.KEYHASH_BINROW_BIGINT, k, 128, WORLD) == r
+                want += zip(k[m].tolist(), t[m].tolist(), v[m].tolist())
+        assert res[r][1] == sorted(want)
+    # the valve: rank 0's proposal (the minimum), held at the previous value on the overflowing steps
+    assert res[0][2] == res[1][2]
+    expect = [T0 + b * 3000 - 3000 if b % 2 == 0 else T0 + (b - 1) * 3000 - 3000 for b in range(n_batches)]
+    assert res[0][2] == expect
+    assert res[0][3] == n_batches // 2

@@ -66,6 +66,11 @@ SCENARIOS = {
                                             aggs=[(abi.AGG_SUM, 0, F64), (abi.AGG_AVG, 0, F64)],
                                             value_col_types=[F64])),
 }
+# the same steps with the watermark valve on the device (PackedExchange.finish_device -> one device
+# all-reduce of (overflow, watermark, share) -> fw_advance_device; overflow rounds settled one step
+# late, the watermark held at the previous one meanwhile)
+for _n in ("one_phase_hop", "one_phase_tumble_double", "two_phase_cumulate_zipf", "two_phase_hop_zipf"):
+    SCENARIOS[_n + "_device_valve"] = dict(SCENARIOS[_n], valve="device")
 N_BATCHES = 9
 N_ROWS = 24000  # per rank per batch
 
@@ -126,7 +131,38 @@ def _worker(rank, port, name, out_q):
         n_aggs = cfg.n_aggs
         ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
         rows, wms, received = [], [], 0
-        if sc["plan"] == "one":
+        device_valve = sc.get("valve") == "device"
+        if sc["plan"] == "one" and device_valve:
+            h = WindowAggHandle(cfg)
+            px_prev, wm_prev = None, None
+
+            def settle(px):
+                nonlocal received
+                spill = px.settle()
+                if spill is not None:
+                    n_sp = spill.numel() // px.row_words
+                    received += n_sp
+                    h.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=dev), spill,
+                                                  px.row_words)
+            for b in range(N_BATCHES):
+                if px_prev is not None:
+                    settle(px_prev)
+                k, t, v = (torch.from_numpy(x).to(dev) for x in _stream(sc["dist"], vt, rank, b, N_ROWS))
+                cap = ex.segment_capacity(N_ROWS, WORLD) if b % 2 == 0 else N_ROWS // (4 * WORLD)
+                px = ex.exchange_packed_async(k, t, [v], capacity=cap)
+                h.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
+                received += int(px.recv_counts.clamp(max=cap).sum())
+                wm_t = px.finish_device(_proposed_wm(b, rank), wm_prev)
+                h.advance_device(wm_t)
+                px_prev, wm_prev = px, wm_t
+                wms.append(int(wm_t.item()))  # (the test reads it back; the step itself never waits)
+                rows += _rows(h.results(), n_aggs)
+            settle(px_prev)
+            h.advance(FINAL_WM)
+            rows += _rows(h.results(), n_aggs)
+            st = h.stats()
+            h.close()
+        elif sc["plan"] == "one":
             h = WindowAggHandle(cfg)
             for b in range(N_BATCHES):
                 k, t, v = (torch.from_numpy(x).to(dev) for x in _stream(sc["dist"], vt, rank, b, N_ROWS))
@@ -155,9 +191,19 @@ def _worker(rank, port, name, out_q):
                     k, t, v = (torch.from_numpy(x).to(dev) for x in _stream(sc["dist"], vt, rank, b, N_ROWS))
                     tp.local.push_device(k, t, [v])
                 if b % 3 == 1:  # segments far below the partials' share: their overflow round runs
+                    if device_valve:
+                        tp.settle()  # (it sets the agreed share; overridden for this step)
                     ex._dn_share = 64
-                wm = tp.step_device(_proposed_wm(b, rank) if b < N_BATCHES else FINAL_WM)
+                wm_prop = _proposed_wm(b, rank) if b < N_BATCHES else FINAL_WM
+                if device_valve:
+                    wm = int(tp.step_device_valve(wm_prop).item())
+                else:
+                    wm = tp.step_device(wm_prop)
                 wms.append(wm)
+                rows += _rows(tp.glob.results(), n_aggs)
+            if device_valve:  # the last step's overflow round, then its watermark
+                tp.settle()
+                tp.glob.advance(FINAL_WM)
                 rows += _rows(tp.glob.results(), n_aggs)
             st = tp.glob.stats()
             st["error_flags"] |= tp.local.stats()["error_flags"]
@@ -245,9 +291,15 @@ def test_two_ranks_union_equals_unsharded_oracle(name):
     from oracle.oracle import key_group
     res = _run_ranks(name)
     sc = SCENARIOS[name]
-    # the ranks agreed on every watermark: the valve's minimum, rank 0's proposal
+    # the ranks agreed on every watermark: the valve's minimum, rank 0's proposal -- or, with the device
+    # valve, the previous watermark held while an overflow round is outstanding
     assert res[0]["wms"] == res[1]["wms"]
-    assert res[0]["wms"][:N_BATCHES] == [_proposed_wm(b, 0) for b in range(N_BATCHES)]
+    wms = res[0]["wms"][:N_BATCHES]
+    if sc.get("valve") == "device":
+        held = [b for b in range(N_BATCHES) if wms[b] != _proposed_wm(b, 0)]
+        assert held and all(wms[b] == (wms[b - 1] if b else -(1 << 63)) for b in held)
+    else:
+        assert wms == [_proposed_wm(b, 0) for b in range(N_BATCHES)]
     assert all(res[r]["err"] == 0 for r in range(WORLD))
     # the overflow rounds ran (the spill path is exercised), on both ranks alike
     assert res[0]["spill_rounds"] > 0 and res[0]["spill_rounds"] == res[1]["spill_rounds"]

@@ -595,12 +595,16 @@ int validate_and_plan(fw_handle* h) {
     // a fixed stride; split superbuckets (pass_log2) too.  FW_NARROW=0 switches them off (development).
     {
         const char* ne = getenv("FW_NARROW");
+        const char* ne1 = getenv("FW_NARROW1");
         const bool count_only = wd.nw == 1 && wd.op[0] == W_CNT && wd.gate[0] < 0;
-        h->narrow = (c.api == FW_API_SQL && !h->keyrow && c.agg_phase != FW_PHASE_GLOBAL && h->tz_utc.empty() &&
-                     w.fast32 && count_only && ks.pass_log2 == 0 && !(ne && atoi(ne) == 0) &&
-                     (h->chunk_rows & (h->chunk_rows - 1)) == 0)
-                        ? 2
-                        : 0;
+        // one accumulator word of a class with a compiled merge variant (MergeLayouts<1>): (key, acc)
+        // rows, 17 B instead of 24 B per partial with the rank byte
+        const bool one_word = wd.nw == 1 && !wd.has_q && !wd.has_ord && wd.gate[0] < 0 && ops_layout(wd) != OPS_ANY;
+        const bool ok = c.api == FW_API_SQL && !h->keyrow && c.agg_phase != FW_PHASE_GLOBAL && h->tz_utc.empty() &&
+                        w.fast32 && ks.pass_log2 == 0 && !(ne && atoi(ne) == 0) && (h->chunk_rows & (h->chunk_rows - 1)) == 0;
+        // (one-word MAX / MIN / SUM layouts read compact rows slower in the merge than they save in the
+        // ingest: measured 163 vs 148 us per CFG2 flush, ingest -1.6 us; FW_NARROW1=1 plans them)
+        h->narrow = !ok ? 0 : count_only ? 2 : (one_word && ne1 && atoi(ne1) == 1) ? 1 : 0;
     }
     // runs: every chunk claims its stretch of each superbucket's sub-runs, so the merge streams a
     // superbucket's rows (fw_internal.h RUN_X).  Sub-runs hold 5/4 of a uniform share of a full push
@@ -612,7 +616,12 @@ int validate_and_plan(fw_handle* h) {
         const char* re = getenv("FW_RUNS");
         const int n_isb = ks.n_sb >> ks.pass_log2;
         const int blk = ig_block(h->nw_t, ig_nv(h->nv)), rpt = ig_rpt(h->nw_t, ig_nv(h->nv));
-        if (!h->keyrow && ks.pass_log2 == 0 && ig_runs_fit(n_isb, blk, rpt, h->nw_t) && !(re && atoi(re) == 0)) {
+        // measured per step: CFG4 (TUMBLE, two words) +2-4%, CFG2 (TUMBLE, one word) within
+        // noise, CFG3 (HOP) -5%, CFG5 (CUMULATE) -3% -- the ingest's scattered stretch stores cost more
+        // than the merge saves unless the rows are wide; planned for TUMBLE with >= 2 words, FW_RUNS=1
+        // plans them everywhere
+        const bool want = re ? atoi(re) != 0 : (c.window_kind == FW_WIN_TUMBLE && c.api == FW_API_SQL && h->nw_t >= 2);
+        if (!h->keyrow && ks.pass_log2 == 0 && ig_runs_fit(n_isb, blk, rpt, h->nw_t) && want) {
             const int64_t subs = (int64_t)n_isb * RUN_X;
             const int64_t sc = ((h->cap_rows * 5 / 4 + subs - 1) / subs + 16 + 15) / 16 * 16;
             if (sc * subs < (1ll << 31)) {
@@ -1692,6 +1701,9 @@ int fw_get_kernel_times(fw_handle* h, fw_kernel_times* out) {
     if (h->ablate & AB_GSTAMPS)  // diagnostic builds only: thread 0's gather parts
         fprintf(stderr, "gather_parts cells=%llu scan=%llu loads=%llu probe=%llu fold+insert=%llu seq_miss=%llu\n", st[13],
                 st[14], st[2], st[4], st[7], st[15]);
+    if (h->ablate & AB_GSTAMPS)  // wave 0's rows: live / home empty / undecided / slow path, slow-path rounds
+        fprintf(stderr, "gather_rows live=%llu fresh=%llu undecided=%llu slow=%llu slow_rounds=%llu\n", st[8], st[9], st[10],
+                st[11], st[12]);
     if (h->ablate & AB_FSTAMPS)  // diagnostic builds only: per-lane cycles of fire_one's parts
         fprintf(stderr, "fire_parts probe+merge=%llu emit=%llu expire+next=%llu claim=%llu windows=%llu\n", st[8], st[9],
                 st[10], st[11], st[12]);

@@ -430,13 +430,6 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         wide = __syncthreads_or(wide);
     }
     uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch;
-    const int per = (n_sb + IG_BLOCK - 1) / IG_BLOCK;
-    const int sb0 = min(tid * per, n_sb), sb1 = min(sb0 + per, n_sb);
-    uint32_t seg = 0;
-    for (int i = sb0; i < sb1; i++) seg += hist[i];
-    uint32_t total;
-    const uint32_t incl = block_incl_scan<IG_BLOCK>(seg, wsum, &total);
-    uint32_t run = incl - seg;
     // runs (IngestArgs::runs): a push's run rows share one format -- compact when the push is (COUNT(*)
     // alone: PF_UNIT when no chunk folds, else PF_NARROW); a chunk that must write PF_WIDE rows in a
     // compact push keeps them all in its own region
@@ -448,6 +441,26 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                          : (!X && a.narrow == 2 && !*s_folded) ? PF_UNIT
                                                                  : PF_NARROW;
     const bool to_runs = runs && fmt == push_fmt;
+    // (runs) claim this chunk's stretch of every superbucket's sub-run now -- the counts are final --
+    // so the claims' round trip overlaps the scan and the staging of the first store window.
+    // Superbuckets strided over the threads (the host enables runs for n_sb <= RUN_KMAX * IG_BLOCK):
+    // a wave's claims hit 64 neighbouring counters.  (These reads of hist precede the scan's barriers,
+    // after which it is overwritten.)
+    const uint32_t xr = (uint32_t)c & (RUN_X - 1);
+    uint32_t pos[RUN_KMAX], cnt[RUN_KMAX];
+#pragma unroll
+    for (int k = 0; k < RUN_KMAX; k++) {
+        const int i = tid + k * IG_BLOCK;
+        cnt[k] = (runs && i < n_sb) ? hist[i] : 0u;
+        pos[k] = (to_runs && cnt[k]) ? atomicAdd(a.run_fill + ((size_t)slot * RUN_X + xr) * n_sb + i, cnt[k]) : 0u;
+    }
+    const int per = (n_sb + IG_BLOCK - 1) / IG_BLOCK;
+    const int sb0 = min(tid * per, n_sb), sb1 = min(sb0 + per, n_sb);
+    uint32_t seg = 0;
+    for (int i = sb0; i < sb1; i++) seg += hist[i];
+    uint32_t total;
+    const uint32_t incl = block_incl_scan<IG_BLOCK>(seg, wsum, &total);
+    uint32_t run = incl - seg;
     if (sort)
         for (int i = sb0; i < sb1; i++) {
             const uint32_t v = hist[i];
@@ -455,41 +468,6 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
             if (!runs) cells[cell_index(c, n_sb, i)] = run | (v << 16) | (fmt << 30);
             run += v;
         }
-    // (runs) per superbucket: chunk positions below rbound go to the run at position + roff; then
-    // every row's destination, RUN_LOCAL | position for the rows that stay in the chunk's region.
-    // They live where the fold table was; the store stage follows them.
-    const int n_sb_pad = (n_sb + 3) & ~3;
-    uint32_t* rbound = (uint32_t*)area;
-    uint32_t* roff = rbound + n_sb_pad;
-    uint32_t* sdst = roff + n_sb_pad;
-    if (runs) {
-        __syncthreads();  // hist holds every superbucket's chunk position
-        // superbuckets strided over the threads (the host enables runs for n_sb <= RUN_KMAX *
-        // IG_BLOCK): a wave's claims hit 64 neighbouring counters, all in flight before the first use
-        const uint32_t xr = (uint32_t)c & (RUN_X - 1);
-        const uint32_t scap = (uint32_t)a.sub_cap;
-        uint32_t pos[RUN_KMAX];
-#pragma unroll
-        for (int k = 0; k < RUN_KMAX; k++) {
-            const int i = tid + k * IG_BLOCK;
-            pos[k] = 0;
-            if (i < n_sb && to_runs) {
-                const uint32_t v = (i + 1 < n_sb ? hist[i + 1] : total) - hist[i];
-                if (v) pos[k] = atomicAdd(a.run_fill + ((size_t)slot * RUN_X + xr) * n_sb + i, v);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < RUN_KMAX; k++) {
-            const int i = tid + k * IG_BLOCK;
-            if (i >= n_sb) break;
-            const uint32_t st0 = hist[i], v = (i + 1 < n_sb ? hist[i + 1] : total) - st0;
-            const uint32_t n_in = to_runs ? (pos[k] >= scap ? 0u : min(v, scap - pos[k])) : 0u;
-            rbound[i] = st0 + n_in;
-            roff[i] = (uint32_t)(((size_t)i * RUN_X + xr) * scap + pos[k]) - st0;
-            cells[cell_index(c, n_sb, i)] = (st0 + n_in) | ((v - n_in) << 16) | (fmt << 30);
-            if (n_in < v) a.run_ovf[(size_t)slot * n_sb + i] = 1u;
-        }
-    }
     if (fmt != PF_WIDE)  // compact rows keep their rank instead of their slice end
         static_for<RPT>([&](auto J) {
             constexpr int j = decltype(J)::value;
@@ -503,18 +481,17 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         });
     else
         total = CH;
-    if (runs)
-        static_for<RPT>([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            if (!(valid & (1u << j))) return;
-            const uint32_t d = rdst[j];
-            const int i = rsb[j] >> PL;
-            sdst[d] = d < rbound[i] ? d + roff[i] : (RUN_LOCAL | d);
-        });
     // ---- store the partials through an LDS stage so every global store is a full line (runs:
     // word by word to each row's destination, neighbouring lanes on neighbouring words of a
     // superbucket's stretch).  The chunk's region keeps its PF_WIDE size; a compact format fills its
     // front, and its rank bytes are staged behind the rows and stored to the side array.
+    // (runs) per superbucket: chunk positions below rbound go to the run at position + roff, every
+    // row's destination in sdst (RUN_LOCAL | position for the rows that stay in the chunk's region).
+    // They live where the fold table was; the store stage follows them.
+    const int n_sb_pad = (n_sb + 3) & ~3;
+    uint32_t* rbound = (uint32_t*)area;
+    uint32_t* roff = rbound + n_sb_pad;
+    uint32_t* sdst = roff + n_sb_pad;
     const int PWX = pf_stride(fmt, NW);
     const int aoff = fmt == PF_WIDE ? 2 : 1;  // first accumulator word of a row
     uint64_t* out = a.parts + ((size_t)slot * a.cap_rows + (size_t)base) * PW;
@@ -524,33 +501,79 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                                           : (uint32_t)(stage_words * 8 / (8 * PWX + 1)) & ~15u;
     uint8_t* rstage = (uint8_t*)(stage + (size_t)wrows * PWX);
     uint64_t* rslot = runs ? a.runs + (size_t)slot * a.run_rows * PW : nullptr;
-    if (!(FW_ABL(a) & AB_NO_STORE))
+    auto stage_rows = [&](uint32_t w0) {
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const uint32_t d = rdst[j] - w0;
+            if (!(valid & (1u << j)) || d >= wrows) return;
+            uint64_t* p = stage + (size_t)d * PWX;
+            p[0] = (uint64_t)rk[j];
+            if (fmt == PF_WIDE) p[1] = (uint64_t)rs[j];
+            else rstage[d] = (uint8_t)rs[j];  // the rank (set below the format decision)
+            if (fmt != PF_UNIT)
+#pragma unroll
+                for (int w = 0; w < NW; w++) p[aoff + w] = racc[j][w];
+        });
+    };
+    const bool store = !(FW_ABL(a) & AB_NO_STORE);
+    if (runs) {
+        if (store) stage_rows(0);  // the first window, while the claims are in flight
+        const uint32_t scap = (uint32_t)a.sub_cap;
+#pragma unroll
+        for (int k = 0; k < RUN_KMAX; k++) {
+            const int i = tid + k * IG_BLOCK;
+            if (i >= n_sb) break;
+            const uint32_t st0 = hist[i], v = cnt[k];
+            const uint32_t n_in = to_runs ? (pos[k] >= scap ? 0u : min(v, scap - pos[k])) : 0u;
+            rbound[i] = st0 + n_in;
+            roff[i] = (uint32_t)(((size_t)i * RUN_X + xr) * scap + pos[k]) - st0;
+            cells[cell_index(c, n_sb, i)] = (st0 + n_in) | ((v - n_in) << 16) | (fmt << 30);
+            if (n_in < v) a.run_ovf[(size_t)slot * n_sb + i] = 1u;
+        }
+        __syncthreads();
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if (!(valid & (1u << j))) return;
+            const uint32_t d = rdst[j];
+            const int i = rsb[j] >> PL;
+            sdst[d] = d < rbound[i] ? d + roff[i] : (RUN_LOCAL | d);
+        });
+    }
+    if (store)
         for (uint32_t w0 = 0; w0 < total; w0 += wrows) {
             __syncthreads();  // fold table / previous window no longer read
-            static_for<RPT>([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                const uint32_t d = rdst[j] - w0;
-                if (!(valid & (1u << j)) || d >= wrows) return;
-                uint64_t* p = stage + (size_t)d * PWX;
-                p[0] = (uint64_t)rk[j];
-                if (fmt == PF_WIDE) p[1] = (uint64_t)rs[j];
-                else rstage[d] = (uint8_t)rs[j];  // the rank (set below the format decision)
-                if (fmt != PF_UNIT)
-#pragma unroll
-                    for (int w = 0; w < NW; w++) p[aoff + w] = racc[j][w];
-            });
+            if (!(runs && w0 == 0)) stage_rows(w0);
             __syncthreads();
             const uint32_t nr = min(wrows, total - w0);
             const uint32_t nwords = nr * PWX;
             if (runs) {
-                // word q of the window: row q / P, word q % P of it (the stride as a constant)
+                // row by row (the stride as a constant): one destination lookup per row, 16-B stores
+                // where the row's words pair up on 16-B boundaries (neighbouring lanes hold neighbouring
+                // rows of a superbucket's stretch)
                 auto copy_out = [&](auto PC) {
                     constexpr uint32_t P = decltype(PC)::value;
-                    for (uint32_t q = tid; q < nwords; q += IG_BLOCK) {
-                        const uint32_t d = q / P, w = q - d * P;
-                        const uint32_t dd = sdst[w0 + d];
-                        uint64_t* dst = (dd & RUN_LOCAL) ? out + (size_t)(dd & ~RUN_LOCAL) * P + w : rslot + (size_t)dd * P + w;
-                        *dst = stage[q];
+                    for (uint32_t r = tid; r < nr; r += IG_BLOCK) {
+                        const uint32_t dd = sdst[w0 + r];
+                        const uint64_t* src = stage + (size_t)r * P;
+                        uint64_t* dst = (dd & RUN_LOCAL) ? out + (size_t)(dd & ~RUN_LOCAL) * P : rslot + (size_t)dd * P;
+                        if constexpr (P % 2 == 0) {
+#pragma unroll
+                            for (uint32_t k = 0; k < P / 2; k++) *(ulonglong2*)(dst + 2 * k) = *(const ulonglong2*)(src + 2 * k);
+                        } else {
+                            uint64_t v[P];
+#pragma unroll
+                            for (uint32_t k = 0; k < P; k++) v[k] = src[k];
+                            if constexpr (P == 1) {
+                                dst[0] = v[0];
+                            } else {  // the lone 8-B word first or last, so the pairs are 16-B aligned
+                                const bool odd = ((uintptr_t)dst & 8) != 0;
+                                *(odd ? dst : dst + (P - 1)) = odd ? v[0] : v[P - 1];
+                                uint64_t* q = dst + (odd ? 1 : 0);
+#pragma unroll
+                                for (uint32_t k = 0; k < (P - 1) / 2; k++)
+                                    *(ulonglong2*)(q + 2 * k) = make_ulonglong2(odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
+                            }
+                        }
                     }
                 };
                 if (fmt == PF_WIDE) copy_out(std::integral_constant<uint32_t, (uint32_t)PW>{});

@@ -44,6 +44,9 @@ constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw)
 #define FW_MG_BLOCK 1024
 #endif
 constexpr int MG_BLOCK = FW_MG_BLOCK;
+// merge workgroups per CU: 512-thread workgroups share a CU two at a time (each with half the LDS:
+// half the entries per superbucket, twice the superbuckets), so one's gather overlaps the other's fire
+constexpr int MG_PER_CU = MG_BLOCK == 512 ? 2 : 1;
 constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a time per pending push (one per thread)
 // LDS slice-state capacity (entries) per superbucket by accumulator words
 // (kind: FW_WIN_* of a SQL operator, KIND_DSWIN (3) for DataStream windows).  One accumulator word
@@ -51,14 +54,14 @@ constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a t
 // window kinds that keep several slices per key (HOP, CUMULATE, DataStream panes) keep 4096 entries
 // of capacity with a 2x index.
 constexpr int mg_entries(int nw, int kind) {
-    if (kind == 4) return nw <= 1 ? 1536 : 768;  // KIND_HOPB: HB_R slots of nw words per entry
-    return nw <= 1 ? (kind == FW_WIN_TUMBLE ? 3072 : 4096) : nw <= 4 ? 2048 : 1024;
+    if (kind == 4) return (nw <= 1 ? 1536 : 768) / MG_PER_CU;  // KIND_HOPB: HB_R slots of nw words per entry
+    return (nw <= 1 ? (kind == FW_WIN_TUMBLE ? 3072 : 4096) : nw <= 4 ? 2048 : 1024) / MG_PER_CU;
 }
 // LDS index slots of a table of E entries with NW accumulator words: a power of two, 4E when it
 // fits beside the entries in a workgroup's LDS, else the largest that does
 constexpr int mg_idx_slots(int nw, int e) {
     const int entry_bytes = 8 + 8 + 4 + 8 * nw + 2;  // key, slice, flag, acc, due
-    const int room = (158 * 1024 - e * entry_bytes) / 4;
+    const int room = (158 * 1024 / MG_PER_CU - e * entry_bytes) / 4;
     int n = 1;
     while (n < 4 * e) n <<= 1;
     while (n > room) n >>= 1;

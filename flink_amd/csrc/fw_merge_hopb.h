@@ -132,7 +132,7 @@ __device__ __forceinline__ uint32_t hb_fire_entry(const MergeArgs& a, int64_t W,
 }
 
 template <int NWP, int E, uint32_t OPS, int GF>
-__global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
+__global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
     constexpr bool PS = (GF & GF_PASS) != 0;
     constexpr int NA = HB_R * NWP;  // ring words per entry
     constexpr int PW = 2 + NWP;     // partial row words
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_hopb(MergeArgs a) {
                     atomicOr(&S.flag[e], F_ACC | (1u << (HB_MASK_SHIFT + sl)));
                 });
             };
-            gather_runs<NWP, GU, GF, FW_MG_PIPE1 != 0>(a, sb, pend, fold_rows);
+            gather_runs<NWP, GU, GF, FW_MG_PIPE1 != 0 ? 2 : 1>(a, sb, pend, fold_rows);
             uint32_t ovf = run_overflow(a, sb, pend);
             while (ovf) {
                 const int pi = __ffs(ovf) - 1;

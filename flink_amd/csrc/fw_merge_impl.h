@@ -148,19 +148,20 @@ __device__ __forceinline__ int find_or_insert(StateLds<NW, E>& S, int64_t k, int
 // an insertion in flight): the caller then takes the probing path.
 template <int NW, int E, int M>
 __device__ __forceinline__ void probe_batch(StateLds<NW, E>& S, const int64_t* k, const int64_t* s, int* e,
-                                            int m = M) {
-    // only the first m (<= M, uniform) lookups are needed; the others issue no LDS reads
+                                            int m = M, uint32_t want = ~0u) {
+    // only the first m (<= M, uniform) lookups, and of those the ones set in `want`, are needed;
+    // the others issue no LDS reads (and come back -1)
     constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
     uint32_t st[M];
 #pragma unroll
     for (int j = 0; j < M; j++)
-        st[j] = j < m ? __hip_atomic_load(&S.idx[index_hash(k[j], s[j]) & MASK], __ATOMIC_RELAXED, LDS_SCOPE) : 0u;
+        st[j] = j < m && ((want >> j) & 1u) ? __hip_atomic_load(&S.idx[index_hash(k[j], s[j]) & MASK], __ATOMIC_RELAXED, LDS_SCOPE) : 0u;
     int64_t kk[M], ss[M];
 #pragma unroll
     for (int j = 0; j < M; j++) {
         kk[j] = 0;
         ss[j] = 0;
-        if (j >= m) continue;
+        if (j >= m || !((want >> j) & 1u)) continue;
         const uint32_t ei = min(st[j] - 2u, (uint32_t)(E - 1));
         kk[j] = S.key[ei];
         ss[j] = S.slice[ei];
@@ -170,6 +171,69 @@ __device__ __forceinline__ void probe_batch(StateLds<NW, E>& S, const int64_t* k
         e[j] = st[j] == 0 ? -1
                : (st[j] >= 2 && st[j] - 2 < (uint32_t)E && kk[j] == k[j] && ss[j] == s[j]) ? (int)(st[j] - 2)
                                                                                           : -2;
+}
+
+// Inserts of the rows whose home slot was empty at the first probe (ge[u] == -1, bit u of
+// `miss`), batched over the wave: each lane claims its rows' home slots (empty -> 1, in insertion)
+// with back-to-back compare-and-swaps, one LDS add reserves the wave's entries for the claims it
+// won, and each lane writes its entries and publishes them (1 -> 2 + e) -- three LDS round trips
+// for the whole batch instead of a probe / claim / allocate / publish chain per row.  Lost claims
+// (another lane took the slot, possibly for the same (key, slice)) take the probing path, which
+// waits out slots in insertion; every slot this wave claimed is published before it returns.
+template <int NW, int E, int GX, uint32_t OPS, typename Row, typename FlagsOf>
+__device__ __forceinline__ uint32_t insert_fresh(StateLds<NW, E>& S, const WordDesc& wd, const Row& row, uint32_t miss,
+                                                 const int* ge, const FlagsOf& flags_of) {
+    constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
+    uint32_t hs[GX];
+    uint32_t won = 0;
+#pragma unroll
+    for (int u = 0; u < GX; u++) {
+        hs[u] = index_hash((int64_t)row[u][0], (int64_t)row[u][1]) & MASK;
+        if (!(((miss >> u) & 1u) && ge[u] == -1)) continue;
+        uint32_t expect = 0;
+        if (__hip_atomic_compare_exchange_strong(&S.idx[hs[u]], &expect, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, LDS_SCOPE))
+            won |= 1u << u;
+    }
+    uint64_t bal[GX];
+    int total = 0;
+#pragma unroll
+    for (int u = 0; u < GX; u++) {
+        bal[u] = __ballot((won >> u) & 1u);
+        total += __popcll(bal[u]);
+    }
+    if (total == 0) return miss;
+    const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+    int base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&S.n, total);
+    base = __shfl(base, leader, 64);
+    int en[GX];
+    int pre = 0;
+#pragma unroll
+    for (int u = 0; u < GX; u++) {
+        const uint64_t b = bal[u];
+        en[u] = base + pre + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        pre += __popcll(b);
+    }
+#pragma unroll
+    for (int u = 0; u < GX; u++) {
+        if (!((won >> u) & 1u)) continue;
+        const int e = en[u];
+        if (e >= E) continue;
+        S.key[e] = (int64_t)row[u][0];
+        S.slice[e] = (int64_t)row[u][1];
+        S.flag[e] = flags_of((int64_t)row[u][1]);
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            S.acc[w][e] = word_on<OPS>(wd, w) ? reg_fold(word_op<OPS>(wd, w), word_identity(word_op<OPS>(wd, w)), row[u][2 + w]) : 0;
+    }
+    compiler_fence();
+#pragma unroll
+    for (int u = 0; u < GX; u++) {
+        if (!((won >> u) & 1u)) continue;
+        if (en[u] >= E) S.overflow = 1;
+        __hip_atomic_store(&S.idx[hs[u]], en[u] < E ? 2u + (uint32_t)en[u] : IDX_DEAD, __ATOMIC_RELAXED, LDS_SCOPE);
+    }
+    return miss & ~won;
 }
 
 // register an event-time timer on entry e; a timer that is already due at this watermark joins
@@ -687,7 +751,7 @@ __device__ __forceinline__ void merge_ticket(const MergeArgs& a, int64_t W) {
 #define FW_GU1 4
 #endif
 constexpr int mg_rows_in_flight(int nw) {
-    return MG_BLOCK <= 512 ? (nw <= 1 ? 2 * FW_GU1 : nw <= 2 ? 6 : nw <= 4 ? 4 : 2) : (nw <= 1 ? FW_GU1 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1);
+    return MG_BLOCK < 512 ? (nw <= 1 ? 2 * FW_GU1 : nw <= 2 ? 6 : nw <= 4 ? 4 : 2) : (nw <= 1 ? FW_GU1 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1);
 }
 
 #ifndef FW_MG_ROLL
@@ -782,6 +846,12 @@ __device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t 
     return live;
 }
 
+// TimeWindowUtil.isWindowFired in a shift zone, kept out of the gather's hot loop
+// (the zone table by value: a reference into the kernel arguments would copy them to scratch)
+static __device__ __noinline__ bool tz_fired_out_of_line(TzTable z, int64_t we, int64_t progress) {
+    return tz_is_fired(z, we, progress);
+}
+
 // ---- the gather over runs (IngestArgs::runs).  The pending pushes' rows of one ingest superbucket
 // lie in RUN_X contiguous sub-runs per push; lane l of every wave holds segment l = (push l / RUN_X,
 // sub-run l % RUN_X), so the 64 lanes cover FW_MAX_PENDING pushes.  A wave deals a block of 64 * G
@@ -863,7 +933,11 @@ __device__ __forceinline__ uint32_t load_run_rows(const MergeArgs& a, const RunS
         const uint32_t p = pf[u] & 15u, fmt = pf[u] >> 4;
         const uint64_t* base = a.runs + (size_t)p * a.run_rows * PW;
         if (!CR || fmt == PF_WIDE) {
-            load_words<PW>(base + (size_t)ri * PW, row[u]);
+            // plain 8-B loads straight into the row's registers: no lane-parity selects, so the
+            // wait for a block's rows is a counted s_waitcnt at its first use
+            const uint64_t* q = base + (size_t)ri * PW;
+#pragma unroll
+            for (int w = 0; w < PW; w++) row[u][w] = q[w];
         } else {
             const uint32_t rank = a.run_ranks[(size_t)p * a.run_rows + ri];
             row[u][1] = (uint64_t)(a.slot_base[p] + (int64_t)(rank * (uint32_t)a.win.interval));
@@ -886,29 +960,35 @@ __device__ __forceinline__ uint32_t load_run_rows(const MergeArgs& a, const RunS
     return live;
 }
 // every run row of superbucket sb's pending pushes through process(rows, live): waves take blocks of
-// 64 * G rows in turn; PIPE: the next block's rows are in flight while the current one is processed
-template <int NW, int G, int GF, bool PIPE, typename F>
+// 64 * G rows in turn.  D > 1: a ring of D blocks -- the loads of the next D - 1 blocks are in flight
+// while the current one is processed.  They are issued unconditionally (past the end a block re-reads
+// the last row, live bits 0), so each wait is a counted s_waitcnt that leaves the younger blocks'
+// loads in flight.
+template <int NW, int G, int GF, int D, typename F>
 __device__ __forceinline__ void gather_runs(const MergeArgs& a, int sb, int64_t pend, F&& process) {
     constexpr int PW = 2 + NW;
     constexpr uint32_t STEP = (uint32_t)MG_BLOCK * G;  // (MG_BLOCK / 64) waves x 64 lanes x G rows
     const RunSegs g = run_segs(a, sb, pend);
     uint32_t r0 = (uint32_t)(threadIdx.x >> 6) * 64u * G;
     if (r0 >= g.tot) return;  // (wave-uniform)
-    if constexpr (PIPE) {
-        // unrolled by two: the buffers alternate without copies.  The next block's loads are issued
-        // unconditionally (past the end they re-read the last row, live bits 0), so the wait for the
-        // current block's rows is a counted s_waitcnt that leaves the next block's loads in flight
-        uint64_t ra[G][PW], rb[G][PW];
-        uint32_t la = load_run_rows<NW, G, GF>(a, g, r0, ra);
-        for (;;) {
-            const uint32_t r1 = r0 + STEP;
-            const uint32_t lb = load_run_rows<NW, G, GF>(a, g, r1, rb);
-            process(ra, la);
-            if (r1 >= g.tot) break;
-            r0 = r1 + STEP;
-            la = load_run_rows<NW, G, GF>(a, g, r0, ra);
-            process(rb, lb);
-            if (r0 >= g.tot) break;
+    if constexpr (D > 1) {
+        uint64_t buf[D][G][PW];
+        uint32_t live[D];
+        static_for<D - 1>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            live[k] = load_run_rows<NW, G, GF>(a, g, r0 + (uint32_t)k * STEP, buf[k]);
+        });
+        bool done = false;
+        while (!done) {  // unrolled by D: the ring's slots rotate without copies
+            static_for<D>([&](auto K) {
+                constexpr int k = decltype(K)::value;
+                constexpr int kn = (k + D - 1) % D;
+                if (done) return;
+                live[kn] = load_run_rows<NW, G, GF>(a, g, r0 + (uint32_t)(D - 1) * STEP, buf[kn]);
+                process(buf[k], live[k]);
+                r0 += STEP;
+                done = r0 >= g.tot;
+            });
         }
     } else {
         for (; r0 < g.tot; r0 += STEP) {
@@ -960,7 +1040,7 @@ __device__ __forceinline__ void gather_cells_push(const MergeArgs& a, int sb, in
 
 // GF: gather variant (GF_PASS: KeySpace.pass_log2 > 0, GF_COMPACT: compact partial rows)
 template <int NW, int E, bool Q, int KIND, uint32_t OPS, int GF>
-__global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
+__global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
     constexpr bool PS = (GF & GF_PASS) != 0;
     constexpr int PW = 2 + NW;
     constexpr int PWE = 3 + NW;
@@ -1103,10 +1183,14 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
     if (gather && a.runs) {
         // runs (IngestArgs::runs): the superbucket's rows of every pending push as RUN_X contiguous
         // stretches per push, then the rows chunks kept in their own regions (overflow)
+        // register the window timer unless already fired (AggCombiner.java:103-110); the LOCAL phase
+        // keeps no timers (LocalAggCombiner.java:69-97).  UTC: fired <=> sliceEnd - 1 <= w_old, i.e.
+        // sliceEnd <= fired_lim (one compare per row); shift zones take the out-of-line zone rule
+        const bool utc = a.win.tz.n == 0;
+        const int64_t fired_lim = a.local ? INT64_MAX - 1 : w_old == INT64_MAX ? INT64_MAX - 1 : w_old + 1;
         auto flags_of = [&](int64_t sl) -> uint32_t {
-            // register the window timer unless already fired (AggCombiner.java:103-110); the LOCAL
-            // phase keeps no timers (LocalAggCombiner.java:69-97)
-            return (a.local || win_fired(a.win, sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
+            const bool fired = utc ? sl <= fired_lim : (a.local || tz_fired_out_of_line(a.win.tz, sl, w_old));
+            return fired ? F_ACC : (F_ACC | F_TIMER);
         };
         auto fold_rows = [&](auto& row, uint32_t live) __attribute__((always_inline)) {
             constexpr int GX = std::extent<std::remove_reference_t<decltype(row)>>::value;
@@ -1124,34 +1208,76 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         ds_add_to_windows<NW, E>(a, S, (int64_t)row[u][0], (int64_t)row[u][1], &row[u][2], w_old, false);
                 });
             } else {
+                // diagnostic (AB_GSTAMPS, thread 0): [2] rows ready + hash + first probes, [4] hit folds,
+                // [7] misses, [13] the whole gather loop (stamped in gather_runs' caller)
+                uint64_t g0 = gst ? __builtin_amdgcn_s_memtime() : 0;
+                auto gstamp = [&](int i) {
+                    if (!gst) return;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                    stm.acc[i] += g1 - g0;
+                    g0 = g1;
+                };
+                // batched first probes of the rows in `want`: folds the hits, returns the rest
                 int ge[GX];
-                {
-                    int64_t gk[GX], gs[GX];
+                auto probe_fold = [&](uint32_t want) __attribute__((always_inline)) -> uint32_t {
+                    {
+                        int64_t gk[GX], gs[GX];
 #pragma unroll
-                    for (int u = 0; u < GX; u++) {
-                        gk[u] = (int64_t)row[u][0];
-                        gs[u] = (int64_t)row[u][1];
+                        for (int u = 0; u < GX; u++) {
+                            gk[u] = (int64_t)row[u][0];
+                            gs[u] = (int64_t)row[u][1];
+                        }
+                        probe_batch<NW, E, GX>(S, gk, gs, ge, GX, want);
                     }
-                    probe_batch<NW, E, GX>(S, gk, gs, ge);
+                    uint32_t rest = 0;
+                    static_for<GX>([&](auto UU) {
+                        constexpr int u = decltype(UU)::value;
+                        if (!((want >> u) & 1u)) return;
+                        const int e = ge[u];  // -1 / -2: not decided by the batched first probe
+                        if (e < 0) {
+                            rest |= 1u << u;
+                            return;
+                        }
+                        if (FW_ABL(a) & AB_M_NO_FOLDOP) return;
+#pragma unroll
+                        for (int w = 0; w < NW; w++)
+                            if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
+                        atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
+                    });
+                    return rest;
+                };
+                uint32_t miss = probe_fold(live);
+                gstamp(4);
+                const bool gcount = (FW_ABL(a) & AB_GSTAMPS) && stm.on && (tid >> 6) == 0;  // wave 0's row census
+                if (gcount) {
+                    uint32_t lv = 0, fr = 0, ud = 0;
+#pragma unroll
+                    for (int u = 0; u < GX; u++)
+                        if ((live >> u) & 1u) {
+                            lv++;
+                            fr += ge[u] == -1;
+                            ud += ge[u] == -2;
+                        }
+                    lv = wave_sum_u32(lv);
+                    fr = wave_sum_u32(fr);
+                    ud = wave_sum_u32(ud);
+                    if (tid == 0) {
+                        stm.acc[8] += lv;
+                        stm.acc[9] += fr;
+                        stm.acc[10] += ud;
+                    }
                 }
-                uint32_t miss = 0;
-                static_for<GX>([&](auto UU) {
-                    constexpr int u = decltype(UU)::value;
-                    if (!((live >> u) & 1u)) return;
-                    const int e = ge[u];  // -1 / -2: not decided by the batched first probe
-                    if (e < 0) {
-                        miss |= 1u << u;
-                        return;
-                    }
-                    if (FW_ABL(a) & AB_M_NO_FOLDOP) return;
-#pragma unroll
-                    for (int w = 0; w < NW; w++)
-                        if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
-                    atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
-                });
+                miss = insert_fresh<NW, E, GX, OPS>(S, a.wd, row, miss, ge, flags_of);
+                if (gcount) {
+                    const uint32_t sl = wave_sum_u32((uint32_t)__popc(miss));
+                    if (tid == 0) stm.acc[11] += sl;
+                }
+                gstamp(14);
                 while (miss) {  // the wave loops max(popcount) times, not GX times
                     const int um = __ffs(miss) - 1;
                     miss &= miss - 1;
+                    if (gst) stm.acc[12]++;
                     uint64_t r[PW];
                     static_for<GX>([&](auto UU) {
                         constexpr int u = decltype(UU)::value;
@@ -1169,6 +1295,7 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
                         if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], r[2 + w]);
                     atomicOr(&S.flag[e], fl);
                 }
+                gstamp(7);
             }
         };
         // TUMBLE / CUMULATE up to 4 words: software-pipelined (two blocks in flight); the others
@@ -1177,8 +1304,13 @@ __global__ __launch_bounds__(MG_BLOCK) void k_merge_fire(MergeArgs a) {
 #ifndef FW_GR
 #define FW_GR 0  // rows per lane per pipelined block (0: half of mg_rows_in_flight)
 #endif
+#ifndef FW_GD
+#define FW_GD 2  // blocks in the pipelined gather's ring
+#endif
         constexpr int GR = RP ? (FW_GR > 0 ? FW_GR : GU / 2 > 0 ? GU / 2 : 1) : GU;
-        gather_runs<NW, GR, GF, RP>(a, sb, pend, fold_rows);
+        const uint64_t gl0 = gst ? __builtin_amdgcn_s_memtime() : 0;
+        gather_runs<NW, GR, GF, RP ? FW_GD : 1>(a, sb, pend, fold_rows);
+        if (gst) stm.acc[13] += __builtin_amdgcn_s_memtime() - gl0;
         uint32_t ovf = run_overflow(a, sb, pend);
         while (ovf) {
             const int pi = __ffs(ovf) - 1;
@@ -1611,7 +1743,7 @@ static unsigned merge_grid(int n_sb) {
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
     }
-    return (unsigned)(n_sb < n_cu ? n_sb : n_cu);
+    return (unsigned)(n_sb < n_cu * MG_PER_CU ? n_sb : n_cu * MG_PER_CU);
 }
 
 // the accumulator layouts with a compiled variant per accumulator width (the others, and every SQL
@@ -1649,8 +1781,8 @@ static bool merge_layout_launch(const MergeArgs& a, uint32_t lay, hipStream_t s)
     } else {
         constexpr uint32_t L = MergeLayouts<NW>::L[I];
         if (L != OPS_ANY && lay == L) {
-            // compact rows come only with the COUNT(*)-only layout (fw_api.hip plans narrow for it alone)
-            if constexpr (NW == 1 && L == ops_pack({W_SUM_I})) {
+            // compact rows come with the one-word layouts (fw_api.hip plans narrow for them alone)
+            if constexpr (NW == 1) {
                 if (a.compact) {
                     merge_launch<NW, false, L, GF_COMPACT>(a, s);
                     return true;

@@ -62,8 +62,13 @@ LAYOUT_CASES = [(w, a) for w in LAYOUT_WINDOWS for a in LAYOUT_AGGS
                 if w != "hop" or LAYOUT_AGGS[a][0][0] == abi.AGG_COUNT_STAR]
 
 
+# layout: the planner's choice, or the partial-row layout forced either way (FW_RUNS: superbucket
+# runs vs chunk-local cells, fw_api.hip; runs are planned only for TUMBLE with >= 2 words)
+@pytest.mark.parametrize("layout", ["planned", "runs", "cells"])
 @pytest.mark.parametrize("win,aggs", LAYOUT_CASES, ids=[f"{w}-{a}" for w, a in LAYOUT_CASES])
-def test_compiled_accumulator_layouts_match_oracle(win, aggs):
+def test_compiled_accumulator_layouts_match_oracle(win, aggs, layout, monkeypatch):
+    if layout != "planned":
+        monkeypatch.setenv("FW_RUNS", "1" if layout == "runs" else "0")
     kw = dict(LAYOUT_WINDOWS[win], aggs=LAYOUT_AGGS[aggs])
     if kw["aggs"][0][0] == abi.AGG_COUNT_STAR:
         kw["count_star_index"] = 0
@@ -371,8 +376,12 @@ def test_key_group_restore_rejects_foreign_and_mismatched_blobs():
 # checked on a key subset against the oracle (window results of a key depend only on that
 # key's records, so the oracle replays only the subset) plus size-independent properties
 # ------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("wl_name", ["cfg2", "cfg3", "cfg4", "cfg5", "cfg4_10m"])
-def test_bench_workload_full_size_key_subset(wl_name):
+@pytest.mark.parametrize("wl_name", ["cfg2", "cfg3", "cfg4", "cfg5", "cfg4_10m", "cfg2-runs", "cfg3-runs", "cfg5-runs",
+                                     "cfg4-cells"])
+def test_bench_workload_full_size_key_subset(wl_name, monkeypatch):
+    if "-" in wl_name:  # the partial-row layout the planner would not pick, forced (FW_RUNS)
+        wl_name, layout = wl_name.split("-")
+        monkeypatch.setenv("FW_RUNS", "1" if layout == "runs" else "0")
     torch = _torch_cuda()
     import ctypes as C
     import bench

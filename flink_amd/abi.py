@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 6
+FW_ABI_VERSION = 7
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -109,6 +109,15 @@ class fw_heap_state_ids(C.Structure):
     """state ids of the heap backend's key-group data (HeapSnapshotStrategy.java:171)"""
     _fields_ = [("window_state", C.c_int16), ("event_timers", C.c_int16),
                 ("processing_timers", C.c_int16), ("reserved", C.c_int16)]
+
+
+DSW_CONTENTS, DSW_TRIGGER, DSW_CLEANUP = 1, 2, 4
+
+
+class fw_ds_window(C.Structure):
+    """one (key, window) of a DataStream WindowOperator key group (flinkwin.h fw_ds_snapshot_key_group)"""
+    _fields_ = [("key", C.c_int64), ("window_end", C.c_int64), ("value", C.c_int64), ("first_ord", C.c_int64),
+                ("flags", C.c_int32), ("reserved", C.c_int32)]
 
 
 class fw_host_cols(C.Structure):

@@ -2565,6 +2565,148 @@ int fw_restore_key_group_heap(fw_handle* h, const void* buf, int64_t size, const
     return fw_restore_key_group(h, blob.data(), (int64_t)blob.size() * 8);
 }
 
+// ---- DataStream WindowOperator key-group state ---------------------------------------------
+// A heap-backend savepoint of the DataStream WindowOperator holds, per key group, the
+// "window-contents" reducing state (WindowOperatorBuilder.java:81: namespace TimeWindow, value the
+// reduced record) and the "window-timers" queues (WindowOperator.java:232).  The value is the user's
+// record type -- value1 with the aggregated field set, whose bytes only the operator shim can write
+// -- so the heap bytes are assembled there (flink_amd/datastream/heap_state.py); this pair moves
+// the device side as one fw_ds_window per (key, window) holding state or a timer.
+namespace {
+
+int ds_state_check(const fw_handle* h) {
+    if (h->cfg.api != FW_API_DATASTREAM)
+        return fail(FW_E_INVALID, "DataStream key-group windows are the DataStream WindowOperator's state");
+    if (h->cfg.key_hash != FW_KEYHASH_LONG && h->cfg.key_hash != FW_KEYHASH_INT)
+        return fail(FW_E_INVALID, "DataStream key-group windows need LONG or INT keys (a restore re-routes each key)");
+    if (h->ad.n != 1) return fail(FW_E_INVALID, "DataStream key-group windows hold one aggregated field");
+    return FW_OK;
+}
+
+// the field value of a window from its words (emit_row's DataStream branch, restated on the host)
+uint64_t ds_value_of(const fw_handle* h, const uint64_t* acc) {
+    const AggDesc& ad = h->ad;
+    const uint64_t w0 = acc[ad.w0[0]];
+    switch (ad.kind[0]) {
+        case FW_AGG_SUM: return ad.type[0] == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)w0 : w0;
+        case FW_AGG_MIN:
+        case FW_AGG_MAX: {
+            uint64_t v = ad.type[0] == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
+            if (ad.dn_hi[0] >= 0 && f64_isnan(v)) v = (acc[ad.dn_hi[0]] << 32) | (acc[ad.dn_lo[0]] & 0xFFFFFFFFull);
+            return v;
+        }
+        default: return w0;  // counts
+    }
+}
+
+// the words of a window state holding `value` whose first element has ordinal `first` (the state
+// after one element of that value, in its written-back form: NaN bits at ordinal 0)
+void ds_words_of(const fw_handle* h, uint64_t value, int64_t first, uint64_t* acc) {
+    const AggDesc& ad = h->ad;
+    const WordDesc& wd = h->wd;
+    for (int w = 0; w < h->nw_t; w++) acc[w] = w < wd.nw ? word_identity(wd.op[w]) : 0;
+    const int w0 = ad.w0[0];
+    const bool f = ad.type[0] == FW_T_F64;
+    switch (ad.kind[0]) {
+        case FW_AGG_SUM: acc[w0] = ad.type[0] == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)value : value; break;
+        case FW_AGG_MIN:
+        case FW_AGG_MAX:
+            acc[w0] = f ? (uint64_t)dkey(value) : ad.type[0] == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)value : value;
+            if (ad.dn_hi[0] >= 0 && f64_isnan(value)) {
+                acc[ad.dn_hi[0]] = value >> 32;
+                acc[ad.dn_lo[0]] = value & 0xFFFFFFFFull;
+            }
+            break;
+        default: acc[w0] = value; break;
+    }
+    // hidden counts (the sliding window's COUNT(*), a non-NULL count): only != 0 is observable
+    if (ad.count_star_word >= 0 && ad.count_star_word != w0) acc[ad.count_star_word] = 1;
+    if (ad.nn[0] >= 0 && ad.nn[0] != w0) acc[ad.nn[0]] = 1;
+    if (ad.first_word >= 0) acc[ad.first_word] = (uint64_t)first;
+}
+
+}  // namespace
+
+int fw_ds_snapshot_key_group(fw_handle* h, int32_t key_group, fw_ds_window* out, int64_t capacity, int64_t* n) {
+    if (!h || !n) return fail(FW_E_INVALID, "null argument");
+    int rc = ds_state_check(h);
+    if (rc) return rc;
+    int64_t sz = 0;
+    if ((rc = fw_snapshot_key_group(h, key_group, nullptr, 0, &sz))) return rc;  // flushes
+    std::vector<uint64_t> blob((size_t)(sz + 7) / 8);
+    if ((rc = fw_snapshot_key_group(h, key_group, blob.data(), (int64_t)blob.size() * 8, &sz))) return rc;
+    KgHeader hd;
+    memcpy(&hd, blob.data(), sizeof hd);
+    const int pwe = h->pwe;
+    const uint64_t* ent = blob.data() + sizeof hd / 8;
+    int64_t m = 0;
+    for (int64_t i = 0; i < hd.n; i++) {
+        const uint64_t* e = ent + (size_t)i * pwe;
+        const uint32_t f = (uint32_t)e[2];
+        const int32_t fl = ((f & F_ACC) ? FW_DSW_CONTENTS : 0) | ((f & F_TIMER) ? FW_DSW_TRIGGER : 0) |
+                           ((f & F_CLEAN) ? FW_DSW_CLEANUP : 0);
+        if (!fl) continue;
+        if (out && m < capacity) {
+            fw_ds_window& w = out[m];
+            w.key = (int64_t)e[0];
+            w.window_end = (int64_t)e[1];
+            w.value = (f & F_ACC) ? (int64_t)ds_value_of(h, e + 3) : 0;
+            w.first_ord = (f & F_ACC) && h->ad.first_word >= 0 ? (int64_t)e[3 + h->ad.first_word] : -1;
+            w.flags = fl;
+            w.reserved = 0;
+        }
+        m++;
+    }
+    *n = m;
+    if (out && capacity < m) return fail(FW_E_INVALID, "window buffer too small (%lld < %lld)", (long long)capacity, (long long)m);
+    return FW_OK;
+}
+
+int fw_ds_restore_key_group(fw_handle* h, int32_t key_group, const fw_ds_window* in, int64_t n, int64_t next_push_seq) {
+    if (!h || (n > 0 && !in) || n < 0) return fail(FW_E_INVALID, "null argument");
+    int rc = ds_state_check(h);
+    if (rc) return rc;
+    const WinDesc& win = h->win;
+    const int pwe = h->pwe;
+    std::vector<uint64_t> ent;
+    ent.reserve((size_t)n * pwe);
+    for (int64_t i = 0; i < n; i++) {
+        const fw_ds_window& w = in[i];
+        if (w.flags & ~(FW_DSW_CONTENTS | FW_DSW_TRIGGER | FW_DSW_CLEANUP) || !w.flags)
+            return fail(FW_E_INVALID, "window %lld: bad flags %d", (long long)i, w.flags);
+        // a window of this assigner: start = end - size on the slide grid (SlidingEventTimeWindows
+        // .assignWindows :77-90; tumbling: slide = size)
+        const int64_t st = wsub(w.window_end, win.size);
+        if (window_start(st, win.offset, win.slide_div) != st)
+            return fail(FW_E_INVALID, "window [%lld, %lld) is not a window of this assigner", (long long)st, (long long)w.window_end);
+        if ((w.flags & FW_DSW_CLEANUP) && ds_cleanup_time(win, w.window_end) == INT64_MAX)
+            return fail(FW_E_INVALID, "window %lld has no cleanup time but a cleanup timer", (long long)w.window_end);
+        const size_t at = ent.size();
+        ent.resize(at + pwe, 0);
+        uint64_t* e = ent.data() + at;
+        e[0] = (uint64_t)w.key;
+        e[1] = (uint64_t)w.window_end;
+        e[2] = ((w.flags & FW_DSW_CONTENTS) ? F_ACC : 0u) | ((w.flags & FW_DSW_TRIGGER) ? F_TIMER : 0u) |
+               ((w.flags & FW_DSW_CLEANUP) ? F_CLEAN : 0u);
+        if (w.flags & FW_DSW_CONTENTS) {
+            if (h->ad.first_word >= 0 && (w.first_ord < 0 || (w.first_ord >> 32) >= next_push_seq))
+                return fail(FW_E_INVALID, "window %lld: first element ordinal not below push %lld", (long long)i,
+                            (long long)next_push_seq);
+            ds_words_of(h, (uint64_t)w.value, w.first_ord, e + 3);
+        } else {
+            for (int x = 0; x < h->nw_t; x++) e[3 + x] = x < h->wd.nw ? word_identity(h->wd.op[x]) : 0;
+        }
+    }
+    Ctrl c;
+    if ((rc = read_ctrl(h, &c))) return rc;
+    KgHeader hd{KG_MAGIC, 3, key_group, pwe, h->wd.nw, h->ks.sb_per_kg_log2, h->cfg.key_hash, win.size, win.interval,
+                c.cur, (int64_t)(ent.size() / pwe), semantics_fingerprint(h), std::max<int64_t>(next_push_seq, 0)};
+    std::vector<uint64_t> blob(sizeof hd / 8);
+    memcpy(blob.data(), &hd, sizeof hd);
+    blob.insert(blob.end(), ent.begin(), ent.end());
+    return fw_restore_key_group(h, blob.data(), (int64_t)blob.size() * 8);
+}
+
 // ---- host-side restatements (the exact code the kernels run), for host partitioners/tests
 int32_t fw_host_key_group(int32_t key_hash_kind, int64_t key, int32_t precomputed_hash, int32_t max_parallelism) {
     return key_group_for_hash(java_key_hash(key_hash_kind, key, precomputed_hash), max_parallelism);

@@ -31,6 +31,7 @@ import numpy as np
 
 from .. import abi
 from ..runtime.handle import WindowAggHandle
+from . import heap_state
 from .windowing import EventTimeTrigger, SlidingEventTimeWindows, TumblingEventTimeWindows
 
 _AGG = {"sum": abi.AGG_SUM, "min": abi.AGG_MIN, "max": abi.AGG_MAX, "count": abi.AGG_COUNT_STAR}
@@ -59,9 +60,11 @@ class WindowOperator:
     def __init__(self, assigner, trigger, aggregation, key_type="LONG", max_parallelism=128,
                  parallelism=1, subtask_index=0, device=0, state_capacity=1 << 20,
                  max_batch_rows=1 << 22, output_capacity=1 << 22, allowed_lateness=0,
-                 late_data_output_tag=None, field=None):
+                 late_data_output_tag=None, field=None, record_serializer=None):
         """``field``: position of the aggregated field in the records (``sum(field)``, ...); given,
-        the operator emits whole records (value1.copy() with the field set), else (key, agg)."""
+        the operator emits whole records (value1.copy() with the field set), else (key, agg).
+        ``record_serializer``: the records' TypeSerializer restatement (heap_state.TupleSerializer,
+        ...), for the heap backend's key-group bytes."""
         ok, why = is_gpu_eligible(assigner, trigger, aggregation, allowed_lateness=allowed_lateness,
                                   late_data_output_tag=late_data_output_tag)
         if not ok:
@@ -82,6 +85,9 @@ class WindowOperator:
             late_side_output=late_data_output_tag is not None, ds_first_ordinals=field is not None)
         self.late_data_output_tag = late_data_output_tag
         self.field = field
+        self.key_type = key_type
+        self.allowed_lateness = allowed_lateness
+        self.record_serializer = record_serializer
         self.handle = None
         self._pending = {}   # push_seq -> records of that push (not yet flushed into state)
         self._retained = {}  # arrival ordinal -> [record, windows whose first element it is]
@@ -193,6 +199,63 @@ class WindowOperator:
         self.handle.restore(blob[8:8 + n])
         self._retained = {o: [tuple(r), c] for o, r, c in json.loads(blob[8 + n:].decode())}
         self._pending.clear()
+
+    # ---- the heap keyed-state backend's key-group bytes (heap_state.py) -------------------------
+    def _cleanup_time(self, end):
+        """WindowOperator.cleanupTime (:670-677): maxTimestamp + allowedLateness, Long.MAX_VALUE on overflow"""
+        t = end - 1 + self.allowed_lateness
+        return t if t < (1 << 63) else (1 << 63) - 1
+
+    def _heap_serializers(self, record_serializer):
+        if self.field is None:
+            raise ValueError("the heap key-group format holds records: a record-shaped operator (field=...) is needed")
+        if self.key_type not in heap_state.KEY_SERIALIZERS:
+            raise ValueError(f"the heap key-group format needs LONG or INT keys, not {self.key_type}")
+        ser = record_serializer or self.record_serializer
+        if ser is None:
+            raise ValueError("no record serializer (record_serializer=...)")
+        return heap_state.KEY_SERIALIZERS[self.key_type], ser
+
+    def snapshot_key_group_heap(self, key_group, ids=(0, 1, 2), record_serializer=None) -> bytes:
+        """Key group ``key_group`` as a heap-backend savepoint writes it: the "window-contents"
+        states (value1 with the field set) and the "window-timers" queues; ids = (window-contents,
+        event-time timers, processing-time timers) state ids."""
+        kser, vser = self._heap_serializers(record_serializer)
+        self.handle.flush()                                # prepareSnapshotPreBarrier
+        self._first_elements(np.empty(0, np.int64), True)  # the flush's retains; batches flushed
+        w = self.handle.ds_key_group_windows(key_group)
+        vals = self._field_values(w["value"])
+        f = self.field
+        recs = []
+        for row, v in zip(w, vals):
+            if int(row["flags"]) & abi.DSW_CONTENTS:
+                first = self._element(int(row["first_ord"]))
+                recs.append(tuple(first[:f]) + (v,) + tuple(first[f + 1:]))
+            else:
+                recs.append(None)
+        return heap_state.write_key_group(key_group, ids, w, recs, kser, vser, self.assigner.size, self._cleanup_time)
+
+    def restore_key_group_heap(self, blob: bytes, ids=(0, 1, 2), record_serializer=None):
+        """Adds one key group written in the heap backend's bytes (by this operator or a heap-backend
+        WindowOperator) to this subtask, which must own it.  Each restored state's record becomes
+        the window's retained first element (its field already holds the aggregate)."""
+        kser, vser = self._heap_serializers(record_serializer)
+        kg, contents, timers = heap_state.read_key_group(blob, ids, kser, vser)
+        fn, ftype = self.aggregation
+        f = self.field
+
+        def field_bits(rec):
+            v = rec[f]
+            if ftype == "DOUBLE" and fn != "count":
+                return struct.unpack("<q", struct.pack("<d", float(v)))[0]
+            return int(v)
+
+        base = self.handle.push_seq
+        w, kept = heap_state.windows_of(contents, timers, self.assigner.size, self._cleanup_time, field_bits, base << 32)
+        self.handle.ds_restore_key_group_windows(kg, w, base + 1)
+        for o, rec in kept.items():
+            self._retained[o] = [rec, 1]
+        return kg
 
     @property
     def num_late_records_dropped(self):

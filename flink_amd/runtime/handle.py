@@ -9,6 +9,10 @@ import numpy as np
 from .. import abi
 from .._native import check, lib
 
+# fw_ds_window (flinkwin.h), one (key, window) of a DataStream key group
+DS_WINDOW_DTYPE = np.dtype([("key", np.int64), ("window_end", np.int64), ("value", np.int64),
+                            ("first_ord", np.int64), ("flags", np.int32), ("reserved", np.int32)])
+
 
 def _np_view(ptr, n, dtype):
     if n == 0:
@@ -405,6 +409,26 @@ class WindowAggHandle:
         buf = C.create_string_buffer(blob, len(blob))
         check(lib().fw_restore_key_group(self._h, buf, len(blob)))
         self.push_seq = max(self.push_seq, _snapshot_push_seq(blob))
+
+    def ds_key_group_windows(self, kg: int):
+        """DataStream: the (key, window) states and timers of key group `kg` (flinkwin.h
+        fw_ds_snapshot_key_group; flushes first) as a structured numpy array."""
+        n = C.c_int64()
+        check(lib().fw_ds_snapshot_key_group(self._h, kg, None, 0, C.byref(n)))
+        arr = (abi.fw_ds_window * max(n.value, 1))()
+        check(lib().fw_ds_snapshot_key_group(self._h, kg, arr, n.value, C.byref(n)))
+        out = np.zeros(n.value, DS_WINDOW_DTYPE)
+        if n.value:
+            out[:] = np.frombuffer(bytes(arr)[:n.value * C.sizeof(abi.fw_ds_window)], DS_WINDOW_DTYPE)
+        return out
+
+    def ds_restore_key_group_windows(self, kg: int, windows, next_push_seq: int):
+        """DataStream: adds key group `kg`'s windows (DS_WINDOW_DTYPE records); first-element
+        ordinals lie below push `next_push_seq`, where this handle's ordinals then continue."""
+        w = np.ascontiguousarray(np.asarray(windows, DS_WINDOW_DTYPE))
+        arr = (abi.fw_ds_window * max(len(w), 1)).from_buffer_copy(w.tobytes() or bytes(C.sizeof(abi.fw_ds_window)))
+        check(lib().fw_ds_restore_key_group(self._h, kg, arr, len(w), next_push_seq))
+        self.push_seq = max(self.push_seq, next_push_seq)
 
     def snapshot_key_group_heap(self, kg: int, ids=(0, 1, 2)) -> bytes:
         """Key group `kg` in the heap keyed-state backend's byte format (flinkwin.h

@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 6
+#define FW_ABI_VERSION 7
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -447,6 +447,31 @@ typedef struct {
 int fw_snapshot_key_group_heap(fw_handle* h, int32_t key_group, const fw_heap_state_ids* ids, void* buf,
                                int64_t capacity, int64_t* size);
 int fw_restore_key_group_heap(fw_handle* h, const void* buf, int64_t size, const fw_heap_state_ids* ids);
+
+/* v7: the DataStream WindowOperator's keyed state of ONE key group, for a heap-backend savepoint
+   of that operator: the "window-contents" reducing state (WindowOperatorBuilder.java:81; namespace
+   TimeWindow.Serializer = start, end) and the "window-timers" event-time queue (WindowOperator.java
+   :232, InternalTimerServiceImpl.snapshotTimersForKeyGroup :360 / restoreTimersForKeyGroup :406).
+   The state's value is the user's record (value1 with the aggregated field set), so the operator
+   shim writes the heap bytes (flink_amd/datastream/heap_state.py) from one fw_ds_window per (key,
+   window end) that holds state or a timer: value = the field value (as fw_result reports it),
+   first_ord = the arrival ordinal of the window's first element (the retained record), flags:
+   CONTENTS (the window holds state), TRIGGER (timer at window.maxTimestamp()), CLEANUP (timer at
+   cleanupTime(window); with allowedLateness 0 both timers are the same one).  fw_ds_snapshot_key_group
+   flushes first; out == NULL queries *n.  fw_ds_restore_key_group adds a key group's windows to a
+   handle owning it; restored first elements carry caller-chosen ordinals below push
+   next_push_seq, after which the handle's arrival ordinals continue.  LONG / INT keys only. */
+enum { FW_DSW_CONTENTS = 1, FW_DSW_TRIGGER = 2, FW_DSW_CLEANUP = 4 };
+typedef struct {
+    int64_t key;
+    int64_t window_end;
+    int64_t value;
+    int64_t first_ord;
+    int32_t flags;
+    int32_t reserved;
+} fw_ds_window;
+int fw_ds_snapshot_key_group(fw_handle* h, int32_t key_group, fw_ds_window* out, int64_t capacity, int64_t* n);
+int fw_ds_restore_key_group(fw_handle* h, int32_t key_group, const fw_ds_window* in, int64_t n, int64_t next_push_seq);
 
 /* ---- key rows: VARCHAR / composite keys ------------------------------------------------ */
 /* A key row field, as the key projection writes it into a BinaryRowData (BinaryRowWriter,

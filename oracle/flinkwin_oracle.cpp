@@ -957,6 +957,26 @@ int64_t or_state_dump(void* h, int64_t* key, int64_t* ns, uint64_t* fields, uint
     }
     return i;
 }
+// DataStream window-contents (WindowOperatorBuilder.java:81): per (key, window end) the value the
+// window would emit (the reduced record's aggregated field) and its first element's arrival
+// ordinal (the record is value1, SumAggregator.java:66-76)
+int64_t or_ds_state_dump(void* h, int64_t* key, int64_t* end, uint64_t* value, int64_t* first, int64_t cap) {
+    Oracle* o = (Oracle*)h;
+    int64_t i = 0;
+    for (const auto& kv : o->state) {
+        if (i < cap) {
+            uint64_t v[FW_MAX_AGGS];
+            uint32_t nm = 0;
+            o->get_value(kv.second, v, &nm);
+            key[i] = kv.first.first;
+            end[i] = kv.first.second;
+            value[i] = v[0];
+            first[i] = kv.second.first;
+        }
+        i++;
+    }
+    return i;
+}
 int64_t or_timer_dump(void* h, int64_t* ts, int64_t* key, int64_t* ns, int64_t cap) {
     Oracle* o = (Oracle*)h;
     int64_t i = 0;

@@ -46,6 +46,8 @@ def lib():
         L.or_get_results.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.or_state_dump.restype = i64
         L.or_state_dump.argtypes = [vp, vp, vp, vp, vp, i64]
+        L.or_ds_state_dump.restype = i64
+        L.or_ds_state_dump.argtypes = [vp, vp, vp, vp, vp, i64]
         L.or_timer_dump.restype = i64
         L.or_timer_dump.argtypes = [vp, vp, vp, vp, i64]
         L.or_clear_results.argtypes = [vp]
@@ -152,6 +154,18 @@ class OracleOperator:
             2 if self.cfg.aggs[g].kind == abi.AGG_AVG else 1 for g in range(self.cfg.n_aggs))
         states = [(int(key[i]), int(ns[i]), [int(x) for x in fields[i, :nf]], int(nm[i])) for i in range(n)]
         timers = [(int(ts[i]), int(tk[i]), int(tn[i])) for i in range(m)]
+        return states, timers
+
+    def ds_keyed_state(self):
+        """DataStream: {(key, window end): (value bits, first element ordinal)} of every window state,
+        and the (timestamp, key, window end) event-time timers."""
+        L = lib()
+        n = L.or_ds_state_dump(self.h, None, None, None, None, 0)
+        key, end, first = np.zeros(n, np.int64), np.zeros(n, np.int64), np.zeros(n, np.int64)
+        val = np.zeros(n, np.uint64)
+        L.or_ds_state_dump(self.h, _ptr(key), _ptr(end), _ptr(val), _ptr(first), n)
+        states = {(int(key[i]), int(end[i])): (int(val[i].astype(np.int64)), int(first[i])) for i in range(n)}
+        _, timers = self.keyed_state()
         return states, timers
 
     def results(self, clear=True):

@@ -1,0 +1,204 @@
+"""GPU parity of the DataStream WindowOperator's heap key-group bytes (flink_amd/datastream/heap_state.py
+over flinkwin.h fw_ds_snapshot_key_group / fw_ds_restore_key_group).
+
+A record-shaped operator runs part of a stream; every key group is written in the heap backend's
+bytes ("window-contents": TimeWindow namespace, key, value1 with the aggregated field set;
+"window-timers": flipped timestamp, key, namespace).  Parsed back, the contents must be the oracle's
+window states at the cut -- the record is the window's first element with the window's current
+aggregate -- and the timers its timer set.  The key groups then restore into fresh operators at
+parallelism 1 or 3 and the run continues record for record against the oracle.  DoubleSerializer
+writes doubleToLongBits, so a NaN aggregate crosses the savepoint as the canonical NaN, as it does in
+the reference; NaN payloads are compared as NaN.  Byte layout: parity unpinned (no Flink build here)."""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from flink_amd import abi
+
+pytestmark = pytest.mark.gpu
+
+T0 = 1_600_000_000_000
+IDS = (4, 2, 3)  # window-contents, event-time window-timers, processing-time window-timers
+_SPECIAL = np.array([0x7FF8000000000000, 0xFFF8000000000001, 0x7FF00000DEADBEEF, 0x8000000000000000, 0],
+                    dtype=np.uint64).view(np.int64)
+
+CASES = {
+    # (window, allowed lateness, aggregation, value column)
+    "tumble_sum_long": (("tumble", 3000, 0), 0, ("sum", "LONG"), 2),
+    "tumble_min_double_lateness": (("tumble", 2000, 0), 1500, ("min", "DOUBLE"), 3),
+    "sliding_max_double_lateness": (("sliding", 3000, 1000), 2000, ("max", "DOUBLE"), 3),
+    "sliding_nondiv_sum_long": (("sliding", 3500, 1000), 0, ("sum", "LONG"), 2),
+}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _batches(seed, n_wm=16, per=1500, n_keys=400, step_ms=1000, ooo=2500):
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in range(n_wm):
+        base = T0 + b * step_ms
+        ts = (base + rng.integers(0, step_ms, per) - rng.integers(0, ooo, per)).astype(np.int64)
+        keys = rng.integers(0, n_keys, per).astype(np.int64) * 7919 - 100_000
+        iv = rng.integers(-10**6, 10**6, per).astype(np.int64)
+        dv = (rng.random(per) * 100.0).view(np.int64).copy()
+        sp = rng.random(per) < 0.2
+        dv[sp] = _SPECIAL[rng.integers(0, len(_SPECIAL), int(sp.sum()))]
+        out.append((keys, ts, iv, dv, base + step_ms - ooo // 3))
+    return out
+
+
+def _operator(case, p=1, i=0):
+    from flink_amd.datastream.heap_state import TupleSerializer
+    from flink_amd.datastream.window_operator import WindowOperator
+    from flink_amd.datastream.windowing import EventTimeTrigger, SlidingEventTimeWindows, TumblingEventTimeWindows
+    (kind, size, slide), late, agg, _ = CASES[case]
+    assigner = TumblingEventTimeWindows.of(size) if kind == "tumble" else SlidingEventTimeWindows.of(size, slide)
+    ser = TupleSerializer.of("LONG", "DOUBLE" if agg[1] == "DOUBLE" else "LONG", "STRING")
+    return WindowOperator(assigner, EventTimeTrigger(), agg, key_type="LONG", state_capacity=1 << 16,
+                          max_batch_rows=1 << 14, output_capacity=1 << 18, allowed_lateness=late, field=1,
+                          parallelism=p, subtask_index=i, record_serializer=ser).open()
+
+
+def _canon(bits, dbl):
+    """value bits as compared across a savepoint: DoubleSerializer writes doubleToLongBits"""
+    if dbl and np.isnan(np.int64(bits).view(np.float64)):
+        return 0x7FF8000000000000
+    return int(bits)
+
+
+def _field_bits(v, dbl):
+    return struct.unpack("<q", struct.pack("<d", v))[0] if dbl else int(v)
+
+
+def _kg(key):
+    from flink_amd._native import lib
+    return lib().fw_host_key_group(abi.KEYHASH_LONG, int(key), 0, 128)
+
+
+def _check_cut(case, blobs, o, elements, dbl):
+    from flink_amd.datastream.heap_state import KEY_SERIALIZERS, TupleSerializer, read_key_group
+    (kind, size, slide), late, agg, _ = CASES[case]
+    ser = TupleSerializer.of("LONG", "DOUBLE" if dbl else "LONG", "STRING")
+    want_states, want_timers = o.ds_keyed_state()
+    got_states, got_timers = {}, set()
+    for kg, blob in blobs.items():
+        k2, contents, timers = read_key_group(blob, IDS, KEY_SERIALIZERS["LONG"], ser)
+        assert k2 == kg
+        for key, st, end, rec in contents:
+            assert _kg(key) == kg, "window-contents entry in a foreign key group"
+            assert end - st == size and (key, end) not in got_states
+            got_states[(key, end)] = rec
+        for ts, key, st, end in timers:
+            assert _kg(key) == kg and end - st == size
+            got_timers.add((ts, key, end))
+    assert sorted(got_states) == sorted(want_states), "window-contents (key, window) set differs from the oracle"
+    for kw, rec in got_states.items():
+        vbits, first = want_states[kw]
+        e = elements[first]
+        assert rec[0] == e[0] and rec[2] == e[2], f"window {kw}: not value1 (the first element)"
+        assert _canon(_field_bits(rec[1], dbl), dbl) == _canon(vbits, dbl), f"window {kw}: aggregate differs"
+    assert got_timers == set(want_timers), "window-timers differ from the oracle's timer set"
+    return len(got_states), len(got_timers)
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+@pytest.mark.parametrize("p_to", [1, 3])
+def test_ds_heap_key_groups_match_oracle_and_restore(case, p_to):
+    from oracle.oracle import OracleOperator
+    vcol = CASES[case][3]
+    dbl = vcol == 3
+    ops = [_operator(case)]
+    o = OracleOperator(ops[0].cfg)
+    elements = {}  # oracle arrival ordinal -> element (key, field, tag)
+    cut, dropped = 8, 0
+    for b, (k, t, iv, dv, wm) in enumerate(_batches(zlib.crc32(case.encode()) % 1000)):
+        if b == cut:
+            blobs = {kg: ops[0].snapshot_key_group_heap(kg, IDS) for kg in range(128)}
+            n_st, n_tm = _check_cut(case, blobs, o, elements, dbl)
+            assert n_st > 100 and n_tm > 100
+            dropped = ops[0].num_late_records_dropped
+            ops[0].close()
+            ops = [_operator(case, p_to, i) for i in range(p_to)]
+            for op in ops:
+                lo, hi = op.handle.key_group_range()
+                for kg in range(lo, hi + 1):
+                    assert op.restore_key_group_heap(blobs[kg], IDS) == kg
+            o.snapshot_restore()
+        v = iv if vcol == 2 else dv
+        recs = []
+        for i in range(len(k)):
+            fv = int(v[i]) if vcol == 2 else struct.unpack("<d", struct.pack("<q", int(v[i])))[0]
+            rec = (int(k[i]), fv, f"e{b}.{i}")
+            recs.append(rec)
+            elements[(b << 32) | i] = rec
+        dest = np.array([_kg(x) * len(ops) // 128 for x in k.tolist()])
+        for i, op in enumerate(ops):
+            m = np.nonzero(dest == i)[0]
+            if len(m):
+                op.process_batch(k[m], t[m], v[m], records=[recs[j] for j in m.tolist()])
+        o.process_batch(k, t, [v])
+        got = []
+        for op in ops:
+            r = op.process_watermark(wm)
+            got += [(kk, we, _canon(val, dbl), rec[0], _canon(_field_bits(rec[1], dbl), dbl), rec[2])
+                    for kk, we, val, rec in zip(r["key"].tolist(), r["window_end"].tolist(), r["value"].tolist(),
+                                                r["records"])]
+        o.process_watermark(wm)
+        want = o.results(clear=True)
+        exp = []
+        for kk, we, val, fo in zip(want["key"].tolist(), want["window_end"].tolist(), want["values"][0].tolist(),
+                                   want["first_ord"].tolist()):
+            e = elements[fo]
+            exp.append((kk, we, _canon(val, dbl), e[0], _canon(val, dbl), e[2]))
+        assert sorted(got) == sorted(exp), f"{case} p_to={p_to} batch {b}: records differ from the oracle"
+    end = T0 + 10**9
+    for op in ops:
+        op.process_watermark(end)
+        assert op.handle.stats()["live_state_entries"] == 0
+        assert not op._retained, "first elements still retained after every window was cleared"
+    o.process_watermark(end)
+    assert dropped + sum(op.num_late_records_dropped for op in ops) == o.late_dropped
+    for op in ops:
+        op.close()
+
+
+def test_ds_heap_round_trip_and_rejects_bad_input():
+    """snapshot -> restore -> snapshot writes the same contents and timers; foreign key groups,
+    truncated bytes and non-window namespaces are refused"""
+    from flink_amd._native import FlinkWinError
+    from flink_amd.datastream.heap_state import KEY_SERIALIZERS, TupleSerializer, read_key_group
+    case = "sliding_max_double_lateness"
+    op = _operator(case)
+    for b, (k, t, iv, dv, wm) in enumerate(_batches(7, n_wm=6)):
+        recs = [(int(k[i]), float(np.int64(dv[i]).view(np.float64)), f"r{b}.{i}") for i in range(len(k))]
+        op.process_batch(k, t, dv, records=recs)
+        op.process_watermark(wm)
+    a = {kg: op.snapshot_key_group_heap(kg, IDS) for kg in range(128)}
+    op2 = _operator(case)
+    for blob in a.values():
+        op2.restore_key_group_heap(blob, IDS)
+    b2 = {kg: op2.snapshot_key_group_heap(kg, IDS) for kg in range(128)}
+    ser = TupleSerializer.of("LONG", "DOUBLE", "STRING")
+    for kg in range(128):
+        pa = read_key_group(a[kg], IDS, KEY_SERIALIZERS["LONG"], ser)
+        pb = read_key_group(b2[kg], IDS, KEY_SERIALIZERS["LONG"], ser)
+        assert sorted(map(repr, pa[1])) == sorted(map(repr, pb[1])), f"kg {kg} contents"
+        assert sorted(pa[2]) == sorted(pb[2]), f"kg {kg} timers"
+    full = max(a.items(), key=lambda kv: len(kv[1]))
+    op3 = _operator(case, 2, 0)
+    lo, hi = op3.handle.key_group_range()
+    foreign = next(kg for kg in range(128) if not lo <= kg <= hi and len(a[kg]) > 20)
+    with pytest.raises(FlinkWinError):
+        op3.restore_key_group_heap(a[foreign], IDS)  # a key group this subtask does not own
+    with pytest.raises(ValueError):
+        op3.restore_key_group_heap(full[1][:-3], IDS)  # truncated
+    for x in (op, op2, op3):
+        x.close()

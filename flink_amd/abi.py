@@ -30,6 +30,9 @@ AGG_SUM = 2
 AGG_MIN = 3
 AGG_MAX = 4
 AGG_AVG = 5
+AGG_MINBY = 6  # DataStream minBy / maxBy: the extremal element (ComparableAggregator byAggregate)
+AGG_MAXBY = 7
+AGGF_LAST = 1  # fw_agg_desc.flags: ties go to the last element (minBy / maxBy(field, first=false))
 # fw_agg_phase (TwoStageOptimizedWindowAggregateRule: one-phase, or local + global)
 PHASE_ONE = 0
 PHASE_LOCAL = 1
@@ -63,7 +66,7 @@ WINDOW_NAMES = {"TUMBLE": WIN_TUMBLE, "HOP": WIN_HOP, "CUMULATE": WIN_CUMULATE}
 
 class fw_agg_desc(C.Structure):
     _fields_ = [("kind", C.c_int32), ("input_col", C.c_int32), ("type", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("flags", C.c_int32)]
 
 
 class fw_config(C.Structure):
@@ -200,10 +203,12 @@ def make_config(*, api=API_SQL, window_kind=WIN_TUMBLE, size_ms, slide_ms=0, off
     c.offset_ms = offset_ms
     c.n_aggs = len(aggs)
     c.count_star_index = count_star_index
-    for i, (kind, col, typ) in enumerate(aggs):
+    for i, agg in enumerate(aggs):
+        kind, col, typ = agg[:3]
         c.aggs[i].kind = kind
         c.aggs[i].input_col = col
         c.aggs[i].type = typ
+        c.aggs[i].flags = agg[3] if len(agg) > 3 else 0
     c.n_value_cols = len(value_col_types)
     for i, t in enumerate(value_col_types):
         c.value_col_types[i] = t

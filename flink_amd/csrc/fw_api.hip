@@ -391,6 +391,7 @@ int validate_and_plan(fw_handle* h) {
     ad.n = c.n_aggs;
     ad.count_star_word = -1;
     ad.first_word = -1;
+    ad.by_prev = -1;
     for (int g = 0; g < FW_MAX_AGGS; g++) ad.dn_hi[g] = ad.dn_lo[g] = -1;
     if (c.ds_first_ordinals && c.api != FW_API_DATASTREAM)
         return fail(FW_E_INVALID, "ds_first_ordinals is a DataStream option (SQL output rows carry no input fields)");
@@ -401,6 +402,10 @@ int validate_and_plan(fw_handle* h) {
         ad.type[g] = d.type;
         ad.w1[g] = ad.nn[g] = ad.qf[g] = ad.qn[g] = ad.qz[g] = -1;
         if (d.type < FW_T_I64 || d.type > FW_T_I32) return fail(FW_E_INVALID, "agg %d: bad type", g);
+        const bool by = d.kind == FW_AGG_MINBY || d.kind == FW_AGG_MAXBY;
+        if (d.flags & ~(by ? FW_AGGF_LAST : 0)) return fail(FW_E_INVALID, "agg %d: bad flags %d", g, d.flags);
+        if (by && (c.api != FW_API_DATASTREAM || !c.ds_first_ordinals || c.n_aggs != 1))
+            return fail(FW_E_INVALID, "minBy / maxBy are the one aggregation of a record-shaped DataStream operator (ds_first_ordinals)");
         int slot = 0, gate = -1;
         const bool global = c.agg_phase == FW_PHASE_GLOBAL;
         if (global) {
@@ -491,6 +496,15 @@ int validate_and_plan(fw_handle* h) {
                 w0 = word_of(f ? W_SUM_F : W_SUM_I, slot, gate);
                 ad.w1[g] = word_of(cnt_op, slot, gate);
                 break;
+            case FW_AGG_MINBY:
+            case FW_AGG_MAXBY: {  // the arg's field key, its ordinal, the ordinal the host retains
+                const bool mx = d.kind == FW_AGG_MAXBY;
+                w0 = word_of(f ? (mx ? W_BYMAX_D : W_BYMIN_D) : (mx ? W_BYMAX_I : W_BYMIN_I), slot, gate);
+                ad.first_word = word_of((d.flags & FW_AGGF_LAST) ? W_BYO_LAST : W_BYO_FIRST, 0, -1);
+                ad.by_prev = word_of(W_BYPREV, 0, -1);
+                if (ad.first_word < 0 || ad.by_prev < 0) return fail(FW_E_INVALID, "too many accumulator words");
+                break;
+            }
             default: return fail(FW_E_INVALID, "agg %d: unsupported kind %d", g, d.kind);
         }
         if (w0 < 0 || (d.kind == FW_AGG_AVG && ad.w1[g] < 0)) return fail(FW_E_INVALID, "too many accumulator words");
@@ -509,12 +523,12 @@ int validate_and_plan(fw_handle* h) {
         ad.count_star_word = word_of(W_CNT, 0, -1);
         if (ad.count_star_word < 0) return fail(FW_E_INVALID, "too many accumulator words");
     }
-    if (c.ds_first_ordinals) {
+    if (c.ds_first_ordinals && ad.by_prev < 0) {
         ad.first_word = word_of(W_FIRST, 0, -1);
         if (ad.first_word < 0) return fail(FW_E_INVALID, "too many accumulator words");
     }
     wd.has_ord = wd.has_q;
-    for (int i = 0; i < wd.nw; i++) wd.has_ord |= wd.op[i] == W_FIRST || is_dnword(wd.op[i]);
+    for (int i = 0; i < wd.nw; i++) wd.has_ord |= wd.op[i] == W_FIRST || is_dnword(wd.op[i]) || is_byword(wd.op[i]);
     // NOT NULL inputs: SUM / MIN / MAX are NULL only for an entry without rows (COUNT(*) == 0),
     // which needs a COUNT(*) word to be observable; without one such an entry never fires
     int star = -1;
@@ -961,6 +975,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.row0 = o;
         a.seg_counts = seg_counts;
         a.fold_always = h->fold_always;
+        a.no_fold = h->ad.by_prev >= 0;
         a.seg_div = make_udiv((uint64_t)std::max<int64_t>(seg_len, 1));
         a.ks = h->ks;
         a.wd = h->wd;
@@ -2590,7 +2605,9 @@ uint64_t ds_value_of(const fw_handle* h, const uint64_t* acc) {
     switch (ad.kind[0]) {
         case FW_AGG_SUM: return ad.type[0] == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)w0 : w0;
         case FW_AGG_MIN:
-        case FW_AGG_MAX: {
+        case FW_AGG_MAX:
+        case FW_AGG_MINBY:
+        case FW_AGG_MAXBY: {
             uint64_t v = ad.type[0] == FW_T_F64 ? dkey_inv((int64_t)w0) : w0;
             if (ad.dn_hi[0] >= 0 && f64_isnan(v)) v = (acc[ad.dn_hi[0]] << 32) | (acc[ad.dn_lo[0]] & 0xFFFFFFFFull);
             return v;
@@ -2616,6 +2633,12 @@ void ds_words_of(const fw_handle* h, uint64_t value, int64_t first, uint64_t* ac
                 acc[ad.dn_hi[0]] = value >> 32;
                 acc[ad.dn_lo[0]] = value & 0xFFFFFFFFull;
             }
+            break;
+        case FW_AGG_MINBY:
+        case FW_AGG_MAXBY:
+            acc[w0] = f ? (uint64_t)dkey(f64_isnan(value) ? 0x7FF8000000000000ull : value)
+                        : ad.type[0] == FW_T_I32 ? (uint64_t)(int64_t)(int32_t)(uint32_t)value : value;
+            acc[ad.by_prev] = (uint64_t)first;  // the restored element is retained
             break;
         default: acc[w0] = value; break;
     }

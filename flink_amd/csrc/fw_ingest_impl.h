@@ -91,8 +91,8 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     // adaptive fold: when the LDS fold of the previous push merged < 2 % of its rows (uniform keys
     // spread over many more groups than a chunk holds), skip it -- the merge kernel folds those
     // rows anyway; every 8th push folds again to notice a skewed stream
-    const bool fold = a.fold_always || !(__hip_atomic_load(&ctrl->fold_skip, __ATOMIC_RELAXED, DEV_SCOPE) &&
-                        (__hip_atomic_load(&ctrl->push_count, __ATOMIC_RELAXED, DEV_SCOPE) & 7u) != 0);
+    const bool fold = !a.no_fold && (a.fold_always || !(__hip_atomic_load(&ctrl->fold_skip, __ATOMIC_RELAXED, DEV_SCOPE) &&
+                                     (__hip_atomic_load(&ctrl->push_count, __ATOMIC_RELAXED, DEV_SCOPE) & 7u) != 0));
     if (tid == 0) {
         *s_min = INT64_MAX;
         *s_drop = 0;

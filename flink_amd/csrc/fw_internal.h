@@ -154,7 +154,20 @@ enum WordOp : int32_t {
     // that arrived last, split in halves, each with the 32-bit arrival ordinal within the flush
     // (state from earlier flushes keeps ordinal 0):
     W_DNHI = 14,   // unsigned max of ord << 32 | (isNaN ? bits >> 32 : 0) over NaN values (0: none)
-    W_DNLO = 15    // unsigned max of ord << 32 | (bits & 0xffffffff) over NaN values
+    W_DNLO = 15,   // unsigned max of ord << 32 | (bits & 0xffffffff) over NaN values
+    // DataStream minBy / maxBy (ComparableAggregator byAggregate, ComparableAggregator.java:89-96):
+    // the element with the extremal field, ties to the first (or last) arrival.  That is the
+    // lexicographic extremum of (field under compareTo, arrival ordinal), one commutative fold of
+    // a word PAIR: the field key and the arg's global ordinal change together (by_fold, under the
+    // entry's lock bit in LDS; ingest partials are not pre-folded).  The third word keeps the
+    // ordinal the host retains the element for (write-back retain / release events).
+    W_BYMAX_I = 16,   // field key of the arg: the value (Long / Integer.compareTo)
+    W_BYMIN_I = 17,
+    W_BYMAX_D = 18,   // dkey of the value with NaN canonical (Double.compareTo: -0.0 < 0.0 < NaN)
+    W_BYMIN_D = 19,
+    W_BYO_FIRST = 20, // global arrival ordinal of the arg; ties to the smaller ordinal
+    W_BYO_LAST = 21,  //   ... ties to the larger ordinal
+    W_BYPREV = 22     // the arg ordinal as of the last write-back (~0: none), never folded
 };
 
 FW_HD uint64_t word_identity(int32_t op) {
@@ -169,8 +182,24 @@ FW_HD uint64_t word_identity(int32_t op) {
         case W_QNANLO:
         case W_QZERO:
         case W_FIRST: return ~0ull;
-        default: return 0;  // counts, integer sums, +0.0 for double sums; W_DNHI / W_DNLO: no NaN yet
+        case W_BYMAX_I:
+        case W_BYMAX_D: return (uint64_t)INT64_MIN;
+        case W_BYMIN_I:
+        case W_BYMIN_D: return (uint64_t)INT64_MAX;
+        case W_BYO_FIRST:
+        case W_BYPREV: return ~0ull;
+        default: return 0;  // counts, integer sums, +0.0 for double sums; W_DNHI / W_DNLO: no NaN yet;
+                            // W_BYO_LAST: earlier than any element
     }
+}
+FW_HD bool is_byword(int32_t op) { return op >= W_BYMAX_I && op <= W_BYPREV; }
+// does the element (v, o) replace the arg (cv, co) of a minBy / maxBy pair: strictly extremal
+// field key, or an equal key and the tie rule's ordinal (MaxByComparator / MinByComparator,
+// Comparator.java:58-101, then `first ? value1 : value2` on c == 0)
+FW_HD bool by_better(int32_t vop, int32_t oop, uint64_t v, uint64_t o, uint64_t cv, uint64_t co) {
+    const bool mx = vop == W_BYMAX_I || vop == W_BYMAX_D;
+    if (v != cv) return mx ? (int64_t)v > (int64_t)cv : (int64_t)v < (int64_t)cv;
+    return oop == W_BYO_FIRST ? o < co : o > co;
 }
 FW_HD bool is_qword(int32_t op) { return op >= W_QMIN && op <= W_QZERO; }
 FW_HD bool is_dnword(int32_t op) { return op == W_DNHI || op == W_DNLO; }
@@ -436,7 +465,9 @@ struct AggDesc {
     int32_t count_star_word;  // word of the SQL indexOfCountStar aggregate, -1 if none
     int32_t dn_hi[FW_MAX_AGGS];  // DataStream MIN/MAX(DOUBLE): the W_DNHI / W_DNLO words (else -1)
     int32_t dn_lo[FW_MAX_AGGS];
-    int32_t first_word;       // DataStream: the W_FIRST word (-1: the first element is not tracked)
+    int32_t first_word;       // DataStream: the W_FIRST word (-1: the first element is not tracked);
+                              // minBy / maxBy: the arg's W_BYO_* word
+    int32_t by_prev;          // minBy / maxBy: the W_BYPREV word (-1: not a minBy / maxBy layout)
 };
 
 constexpr int CS_WORDS = 8;  // IngestArgs::chunk_stats words per chunk
@@ -479,6 +510,7 @@ struct IngestArgs {
     int32_t push_seq;      // fw_commit / fw_push_device call number (side-output rows)
     int64_t row0;          // row offset of this launch within its call
     int32_t fold_always;   // development (FW_FOLD=1): fold every push (no adaptive skip)
+    int32_t no_fold;       // minBy / maxBy: word pairs do not fold per word -- partials stay per element
     const int64_t* seg_counts;  // padded exchange buffer: valid rows per segment (nullptr: all valid)
     UDiv seg_div;          // divisor = segment length
     unsigned long long* kt;  // launch timing (fw_set_profiling FW_PROF_DEVICE): KtSlot of this kernel class

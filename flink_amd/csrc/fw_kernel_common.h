@@ -59,7 +59,12 @@ __device__ __forceinline__ uint64_t record_word(int32_t op, uint64_t v, uint32_t
         case W_FIRST: return gord;
         case W_DNHI: return f64_isnan(v) ? (((uint64_t)ord << 32) | (v >> 32)) : 0ull;
         case W_DNLO: return f64_isnan(v) ? (((uint64_t)ord << 32) | (v & 0xFFFFFFFFull)) : 0ull;
-        default: return v;  // SUM_I, SUM_F (bits), MIN_I, MAX_I, CNTV
+        case W_BYMAX_D:
+        case W_BYMIN_D: return (uint64_t)dkey(f64_isnan(v) ? 0x7FF8000000000000ull : v);
+        case W_BYO_FIRST:
+        case W_BYO_LAST: return gord;
+        case W_BYPREV: return ~0ull;
+        default: return v;  // SUM_I, SUM_F (bits), MIN_I, MAX_I, CNTV, BYMAX_I, BYMIN_I
     }
 }
 // a record's word, honouring the word's NULL gate (null_slots: bit s = value slot s is NULL)
@@ -86,6 +91,13 @@ __device__ __forceinline__ void lds_fold(int32_t op, uint64_t* slot, uint64_t v)
         case W_FIRST: __hip_atomic_fetch_min(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
         case W_DNHI:
         case W_DNLO: __hip_atomic_fetch_max(slot, v, __ATOMIC_RELAXED, LDS_SCOPE); break;
+        case W_BYMAX_I:
+        case W_BYMIN_I:
+        case W_BYMAX_D:
+        case W_BYMIN_D:
+        case W_BYO_FIRST:
+        case W_BYO_LAST:
+        case W_BYPREV: break;  // pair words: by_fold (fw_merge_impl.h)
         default: __hip_atomic_fetch_max((int64_t*)slot, (int64_t)v, __ATOMIC_RELAXED, LDS_SCOPE); break;
     }
 }
@@ -106,7 +118,13 @@ __device__ __forceinline__ uint64_t reg_fold(int32_t op, uint64_t a, uint64_t b)
         case W_FIRST: return a < b ? a : b;
         case W_DNHI:
         case W_DNLO: return a > b ? a : b;
-        default: return (int64_t)a > (int64_t)b ? a : b;
+        // pair words (by_fold): folded only onto their identity, when an entry is created
+        case W_BYMIN_I:
+        case W_BYMIN_D: return (int64_t)a < (int64_t)b ? a : b;
+        case W_BYO_FIRST:
+        case W_BYO_LAST: return b;
+        case W_BYPREV: return a;
+        default: return (int64_t)a > (int64_t)b ? a : b;  // also W_BYMAX_*
     }
 }
 

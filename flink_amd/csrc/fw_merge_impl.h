@@ -289,6 +289,8 @@ __device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_
                 break;
             case FW_AGG_MIN:
             case FW_AGG_MAX:
+            case FW_AGG_MINBY:  // the arg's field: its key decoded (a NaN as the canonical NaN)
+            case FW_AGG_MAXBY:
                 if (Q && a.ad.qf[g] >= 0) {
                     bool isnull;
                     v = q_result(a.ad, g, acc, &isnull);
@@ -607,6 +609,31 @@ __device__ __forceinline__ void mark_hop_successor(const MergeArgs& a, int64_t W
 // gets its maxTimestamp timer (EventTimeTrigger.onElement) and its cleanup timer
 // (registerCleanupTimer).  Windows the watermark already fired are not reached here: their rows
 // took the late-fire path.
+// minBy / maxBy: folds the element (v = field key, o = arrival ordinal) into entry e's pair.  The
+// two words change together, so lanes take the entry's lock bit in turn.  The retry loop is
+// wave-uniform (it runs until no active lane is left): a lane that wins the bit runs its critical
+// section and releases it in the same pass, so neither a lane of the same wave spinning on the bit
+// nor the compiler moving the section out of the loop can stall the holder.
+constexpr uint32_t F_BYLOCK = 1u << 30;
+template <int NW, int E>
+__device__ __forceinline__ void by_fold(const MergeArgs& a, StateLds<NW, E>& S, int e, uint64_t v, uint64_t o) {
+    const int wv = a.ad.w0[0], wo = a.ad.first_word;
+    const int32_t vop = a.wd.op[wv], oop = a.wd.op[wo];
+    bool done = false;
+    do {
+        if (!done && !(atomicOr(&S.flag[e], F_BYLOCK) & F_BYLOCK)) {
+            compiler_fence();
+            if (by_better(vop, oop, v, o, S.acc[wv][e], S.acc[wo][e])) {
+                S.acc[wv][e] = v;
+                S.acc[wo][e] = o;
+            }
+            compiler_fence();
+            atomicAnd(&S.flag[e], ~F_BYLOCK);
+            done = true;
+        }
+    } while (__ballot(!done) != 0);
+}
+
 template <int NW, int E>
 __device__ __forceinline__ void ds_add_to_windows(const MergeArgs& a, StateLds<NW, E>& S, int64_t k, int64_t pe, const uint64_t* v,
                                   int64_t w_old, bool late_rows) {
@@ -625,7 +652,8 @@ __device__ __forceinline__ void ds_add_to_windows(const MergeArgs& a, StateLds<N
         if (en < 0 || ins) continue;
 #pragma unroll
         for (int q = 0; q < NW; q++)
-            if (q < a.wd.nw) lds_fold(a.wd.op[q], &S.acc[q][en], v[q]);
+            if (q < a.wd.nw) lds_fold(a.wd.op[q], &S.acc[q][en], v[q]);  // (pair words: no-op)
+        if (a.ad.by_prev >= 0) by_fold<NW, E>(a, S, en, v[a.ad.w0[0]], v[a.ad.first_word]);
         atomicOr(&S.flag[en], fl);
     }
 }
@@ -656,8 +684,13 @@ __device__ __forceinline__ uint32_t fire_ds(const MergeArgs& a, int64_t W, State
     }
     S.flag[e] = f & ~((fire ? F_TIMER : 0u) | (clean ? (F_ACC | F_TIMER | F_CLEAN) : 0u));
     // clearAllState: a window state retained by an earlier launch releases its first element
-    if (clean && (f & F_ACC) && !(f & F_NEW) && a.ad.first_word >= 0)
+    // (minBy / maxBy: the arg retained at the last write-back, if any)
+    if (clean && (f & F_ACC) && a.ad.by_prev >= 0) {
+        const uint64_t pv = S.acc[a.ad.by_prev][e];
+        if (pv != ~0ull) push_ordev(a, ORDEV_RELEASE | (int64_t)pv);
+    } else if (clean && (f & F_ACC) && !(f & F_NEW) && a.ad.first_word >= 0) {
         push_ordev(a, ORDEV_RELEASE | (int64_t)S.acc[a.ad.first_word][e]);
+    }
     return fire ? 1u : 0u;
 }
 
@@ -1598,7 +1631,21 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                     if (!ds_pane_in_window(w, (int64_t)o[1], e)) continue;
 #pragma unroll
                     for (int q = 0; q < NW; q++)
-                        if (q < a.wd.nw) acc[q] = reg_fold(a.wd.op[q], acc[q], o[3 + q]);
+                        if (q < a.wd.nw && !is_byword(a.wd.op[q])) acc[q] = reg_fold(a.wd.op[q], acc[q], o[3 + q]);
+                    if (a.ad.by_prev >= 0) {  // minBy / maxBy pair (by_fold in registers)
+                        const int wv = a.ad.w0[0], wo = a.ad.first_word;
+                        uint64_t cv = 0, co = 0;
+#pragma unroll
+                        for (int q = 0; q < NW; q++) {
+                            if (q == wv) cv = acc[q];
+                            if (q == wo) co = acc[q];
+                        }
+                        if (by_better(a.wd.op[wv], a.wd.op[wo], o[3 + wv], o[3 + wo], cv, co)) {
+#pragma unroll
+                            for (int q = 0; q < NW; q++)
+                                if (q == wv || q == wo) acc[q] = o[3 + q];
+                        }
+                    }
                 }
                 emit_row<NW, false>(a, sb, &s_emit, k, e, acc);
             }
@@ -1703,9 +1750,18 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                 for (int w = 0; w < NW; w++) v[w] = S.acc[w][e];
 #pragma unroll
                 for (int w = 0; w < NW; w++) p[3 + w] = w < a.wd.nw ? q_normalise(a.wd, w, v) : v[w];
-                // a new DataStream window state: its first element is retained by the host shim
-                if (KIND == KIND_DSWIN && (f0 & F_NEW) && (f & F_ACC) && a.ad.first_word >= 0)
+                // a new DataStream window state: its first element is retained by the host shim;
+                // minBy / maxBy: a changed arg is retained, the one it replaced released
+                if (KIND == KIND_DSWIN && (f & F_ACC) && a.ad.by_prev >= 0) {
+                    const uint64_t o = v[a.ad.first_word], pv = v[a.ad.by_prev];
+                    if (o != pv) {
+                        push_ordev(a, (int64_t)o);
+                        if (pv != ~0ull) push_ordev(a, ORDEV_RELEASE | (int64_t)pv);
+                        p[3 + a.ad.by_prev] = o;
+                    }
+                } else if (KIND == KIND_DSWIN && (f0 & F_NEW) && (f & F_ACC) && a.ad.first_word >= 0) {
                     push_ordev(a, (int64_t)v[a.ad.first_word]);
+                }
             } else {
 #pragma unroll
                 for (int w = 0; w < NW; w++) p[3 + w] = S.acc[w][e];

@@ -4,7 +4,8 @@ WindowOperatorBuilder.buildWindowOperator (flink-runtime/.../windowing/WindowOpe
 would return this operator iff: the assigner is TumblingEventTimeWindows or
 SlidingEventTimeWindows (any size and slide), the trigger is EventTimeTrigger, there is no
 evictor, and the function is a built-in field aggregation (SumAggregator / ComparableAggregator
-for min/max, WindowedStream.java:660-880) on a numeric field.  Any allowedLateness and a
+for min/max and -- record-shaped -- minBy/maxBy with either tie rule, WindowedStream.java:660-880)
+on a numeric field.  Any allowedLateness and a
 late-data side output (sideOutputLateData) are supported.  Anything else stays on the reference
 WindowOperator.
 
@@ -34,9 +35,21 @@ from ..runtime.handle import WindowAggHandle
 from . import heap_state
 from .windowing import EventTimeTrigger, SlidingEventTimeWindows, TumblingEventTimeWindows
 
-_AGG = {"sum": abi.AGG_SUM, "min": abi.AGG_MIN, "max": abi.AGG_MAX, "count": abi.AGG_COUNT_STAR}
+_AGG = {"sum": abi.AGG_SUM, "min": abi.AGG_MIN, "max": abi.AGG_MAX, "count": abi.AGG_COUNT_STAR,
+        "minBy": abi.AGG_MINBY, "maxBy": abi.AGG_MAXBY}
+_BY = ("minBy", "maxBy")
 _KEY = {"LONG": abi.KEYHASH_LONG, "INT": abi.KEYHASH_INT, "HOST_HASHED": abi.KEYHASH_PRECOMPUTED}
 _TYPE = {"LONG": abi.T_I64, "INT": abi.T_I32, "DOUBLE": abi.T_F64}
+
+
+def _enc_field(x):
+    """a record field for the snapshot's JSON side: floats by their bits (a NaN keeps its payload,
+    which minBy / maxBy hand back inside the element)"""
+    return {"f64": struct.unpack("<q", struct.pack("<d", x))[0]} if isinstance(x, float) else x
+
+
+def _dec_field(x):
+    return struct.unpack("<d", struct.pack("<q", x["f64"]))[0] if isinstance(x, dict) and "f64" in x else x
 
 
 def is_gpu_eligible(assigner, trigger, aggregation, *, evictor=None, allowed_lateness=0,
@@ -53,6 +66,8 @@ def is_gpu_eligible(assigner, trigger, aggregation, *, evictor=None, allowed_lat
         return False, "The allowed lateness cannot be negative."
     if aggregation[0] not in _AGG or aggregation[1] not in _TYPE:
         return False, "not a built-in field aggregation"
+    if len(aggregation) > 2 and (aggregation[0] not in _BY or not isinstance(aggregation[2], bool)):
+        return False, "only minBy / maxBy take a first/last flag"
     return True, ""
 
 
@@ -69,7 +84,11 @@ class WindowOperator:
                                   late_data_output_tag=late_data_output_tag)
         if not ok:
             raise ValueError(f"not eligible for the GPU window operator: {why}")
-        fn, ftype = aggregation
+        fn, ftype = aggregation[:2]
+        if fn in _BY and field is None:
+            raise ValueError("minBy / maxBy emit whole elements: a record-shaped operator (field=...) is needed")
+        # minBy / maxBy(field, first): ties go to the first element unless first is False
+        by_flags = abi.AGGF_LAST if fn in _BY and len(aggregation) > 2 and not aggregation[2] else 0
         sliding = isinstance(assigner, SlidingEventTimeWindows)
         self.assigner = assigner
         self.aggregation = aggregation
@@ -77,7 +96,7 @@ class WindowOperator:
         self.cfg = abi.make_config(
             api=abi.API_DATASTREAM, window_kind=abi.WIN_HOP if sliding else abi.WIN_TUMBLE,
             size_ms=assigner.size, slide_ms=assigner.slide if sliding else 0,
-            offset_ms=assigner.offset, aggs=[(_AGG[fn], 0, t)], count_star_index=-1,
+            offset_ms=assigner.offset, aggs=[(_AGG[fn], 0, t, by_flags)], count_star_index=-1,
             value_col_types=[t], key_hash=_KEY[key_type], max_parallelism=max_parallelism,
             parallelism=parallelism, subtask_index=subtask_index, device=device,
             state_capacity=state_capacity, max_batch_rows=max_batch_rows,
@@ -160,13 +179,16 @@ class WindowOperator:
             flushed = watermark > self._wm
             out["first_ord"] = r["first_ord"]
             firsts = self._first_elements(r["first_ord"], flushed)
-            vals = self._field_values(r["values"][0])
-            out["records"] = [tuple(f[:self.field]) + (v,) + tuple(f[self.field + 1:]) for f, v in zip(firsts, vals)]
+            if self.aggregation[0] in _BY:  # the extremal element itself
+                out["records"] = firsts
+            else:
+                vals = self._field_values(r["values"][0])
+                out["records"] = [tuple(f[:self.field]) + (v,) + tuple(f[self.field + 1:]) for f, v in zip(firsts, vals)]
         self._wm = max(self._wm, watermark)
         return out
 
     def _field_values(self, words):
-        fn, ftype = self.aggregation
+        fn, ftype = self.aggregation[:2]
         if ftype == "DOUBLE" and fn != "count":
             return [struct.unpack("<d", struct.pack("<q", int(w)))[0] for w in words]
         if ftype == "INT" and fn != "count":
@@ -188,7 +210,7 @@ class WindowOperator:
         self.handle.flush()                          # prepareSnapshotPreBarrier
         self._first_elements(np.empty(0, np.int64), True)  # the flush's retains; batches flushed
         blob = self.handle.snapshot()
-        side = json.dumps([[o, list(r), c] for o, (r, c) in self._retained.items()]).encode()
+        side = json.dumps([[o, [_enc_field(x) for x in r], c] for o, (r, c) in self._retained.items()]).encode()
         return struct.pack("<q", len(blob)) + blob + side
 
     def initialize_state(self, blob: bytes):
@@ -197,7 +219,7 @@ class WindowOperator:
             return
         n = struct.unpack_from("<q", blob, 0)[0]
         self.handle.restore(blob[8:8 + n])
-        self._retained = {o: [tuple(r), c] for o, r, c in json.loads(blob[8 + n:].decode())}
+        self._retained = {o: [tuple(_dec_field(x) for x in r), c] for o, r, c in json.loads(blob[8 + n:].decode())}
         self._pending.clear()
 
     # ---- the heap keyed-state backend's key-group bytes (heap_state.py) -------------------------
@@ -230,7 +252,8 @@ class WindowOperator:
         for row, v in zip(w, vals):
             if int(row["flags"]) & abi.DSW_CONTENTS:
                 first = self._element(int(row["first_ord"]))
-                recs.append(tuple(first[:f]) + (v,) + tuple(first[f + 1:]))
+                by = self.aggregation[0] in _BY  # minBy / maxBy: the state holds the element itself
+                recs.append(first if by else tuple(first[:f]) + (v,) + tuple(first[f + 1:]))
             else:
                 recs.append(None)
         return heap_state.write_key_group(key_group, ids, w, recs, kser, vser, self.assigner.size, self._cleanup_time)
@@ -241,7 +264,7 @@ class WindowOperator:
         the window's retained first element (its field already holds the aggregate)."""
         kser, vser = self._heap_serializers(record_serializer)
         kg, contents, timers = heap_state.read_key_group(blob, ids, kser, vser)
-        fn, ftype = self.aggregation
+        fn, ftype = self.aggregation[:2]
         f = self.field
 
         def field_bits(rec):
@@ -262,7 +285,7 @@ class WindowOperator:
         return self.handle.stats()["num_late_records_dropped"]
 
     def output_records(self, res):
-        fn, ftype = self.aggregation
+        fn, ftype = self.aggregation[:2]
         vals = res["value"]
         if ftype == "DOUBLE" and fn != "count":
             vals = vals.view(np.float64)

@@ -96,8 +96,17 @@ typedef enum {
     FW_AGG_SUM = 2,         /* SUM(col)            SumAggFunction / SumAggregator        */
     FW_AGG_MIN = 3,         /* MIN(col)            MinAggFunction / ComparableAggregator */
     FW_AGG_MAX = 4,         /* MAX(col)            MaxAggFunction / ComparableAggregator */
-    FW_AGG_AVG = 5          /* AVG(col)            AvgAggFunction                        */
+    FW_AGG_AVG = 5,         /* AVG(col)            AvgAggFunction                        */
+    /* v7, DataStream only (record-shaped operators, ds_first_ordinals = 1): the ELEMENT with the
+       extremal field (WindowedStream.minBy / maxBy :725-790, ComparableAggregator byAggregate
+       :89-96, MinByComparator / MaxByComparator: Comparable.compareTo, Double.compareTo for
+       DOUBLE); ties go to the first element, or to the last with FW_AGGF_LAST in flags.  The
+       result's value column is the field (a NaN as the canonical NaN), fw_result.first_ord the
+       element's arrival ordinal. */
+    FW_AGG_MINBY = 6,
+    FW_AGG_MAXBY = 7
 } fw_agg_kind;
+enum { FW_AGGF_LAST = 1 };  /* fw_agg_desc.flags: minBy / maxBy(field, first = false) */
 
 /* Aggregation phase (TwoStageOptimizedWindowAggregateRule.java:80-109).  ONE: the slicing
    WindowAggOperator with AggCombiner.  LOCAL: LocalSlicingWindowAggOperator + LocalAggCombiner
@@ -136,7 +145,7 @@ typedef struct {
     int32_t kind;        /* fw_agg_kind                                   */
     int32_t input_col;   /* value column index (ignored for COUNT_STAR)   */
     int32_t type;        /* fw_value_type of the input column             */
-    int32_t reserved;
+    int32_t flags;       /* v7: FW_AGGF_LAST for MINBY / MAXBY, else 0    */
 } fw_agg_desc;
 
 typedef struct {

@@ -407,6 +407,33 @@ struct Oracle {
         }
     }
 
+    // DataStream minBy / maxBy (WindowedStream.java:725-790): the reducing state holds an ELEMENT;
+    // ComparableAggregator.reduce (:83-104) with byAggregate keeps value1 (the state) when
+    // MaxByComparator / MinByComparator (Comparator.java:58-101) says it is strictly extremal, and
+    // on c == 0 keeps value1 iff `first`.  Row::first is the kept element's arrival ordinal and the
+    // aggregate its field.
+    bool is_by() const {
+        return ds && cfg.c.n_aggs == 1 && (cfg.c.aggs[0].kind == FW_AGG_MINBY || cfg.c.aggs[0].kind == FW_AGG_MAXBY);
+    }
+    void by_reduce(Row& r, const uint64_t* vals, int64_t ord, bool fresh) const {
+        const fw_agg_desc& g = cfg.c.aggs[0];
+        AggState& s = r.a[0];
+        const uint64_t raw = vals[g.input_col];
+        const bool isf = g.type == FW_T_F64;
+        if (!fresh) {
+            // o1 = the state's field, o2 = the new element's: c = sign of o1.compareTo(o2), flipped for minBy
+            int c;
+            if (isf) c = java_double_compare(s.d, bits_to_double(raw));
+            else c = s.i < (int64_t)raw ? -1 : s.i > (int64_t)raw ? 1 : 0;
+            if (g.kind == FW_AGG_MINBY) c = -c;
+            const bool first = !(g.flags & FW_AGGF_LAST);
+            if (c > 0 || (c == 0 && first)) return;  // value1 stays
+        }
+        if (isf) s.d = bits_to_double(raw); else s.i = (int64_t)raw;
+        s.is_null = false;
+        r.first = ord;
+    }
+
     // mergeExpressions of the same functions
     void merge(Row& r, const Row& o) const {
         for (int a = 0; a < cfg.c.n_aggs; a++) {
@@ -517,6 +544,10 @@ struct Oracle {
                 case FW_AGG_MAX:
                 case FW_AGG_MIN:
                     if (s.is_null) { *nm |= 1u << a; break; }
+                    v[a] = isf ? double_to_bits(s.d) : (uint64_t)s.i;
+                    break;
+                case FW_AGG_MINBY:  // the kept element's field (its element: Row::first)
+                case FW_AGG_MAXBY:
                     v[a] = isf ? double_to_bits(s.d) : (uint64_t)s.i;
                     break;
                 case FW_AGG_AVG:  // count == 0 ? null : cast(sum / count)
@@ -806,8 +837,10 @@ struct Oracle {
             auto sk = std::make_pair(key, end);
             auto it = state.find(sk);
             Row acc = it == state.end() ? create_accumulators() : it->second;
-            if (it == state.end()) acc.first = (int64_t)(((uint64_t)push_seq << 32) | (uint64_t)row);
-            accumulate(acc, vals, no_nulls);  // HeapReducingState.add / HeapAggregatingState.add
+            const int64_t ord = (int64_t)(((uint64_t)push_seq << 32) | (uint64_t)row);
+            if (it == state.end()) acc.first = ord;
+            if (is_by()) by_reduce(acc, vals, ord, it == state.end());
+            else accumulate(acc, vals, no_nulls);  // HeapReducingState.add / HeapAggregatingState.add
             state[sk] = acc;
             // EventTimeTrigger.onElement (:37-45): a window whose maxTimestamp the watermark has
             // passed FIRES at once (emitWindowContents), else its timer is registered

@@ -55,7 +55,19 @@ CASES = {
     "sliding_min_double_nan": (("sliding", 4000, 1000), 0, False, ("min", "DOUBLE"), 3),
     "sliding_max_double_lateness": (("sliding", 3000, 1000), 2000, False, ("max", "DOUBLE"), 3),
     "tumble_min_long_lateness_side": (("tumble", 2000, 0), 1500, True, ("min", "LONG"), 2),
+    # minBy / maxBy (WindowedStream.java:725-790): the extremal ELEMENT, ties to the first (default)
+    # or the last; LONG fields are taken mod 5 so ties are common, DOUBLE ones hold NaNs and +-0.0
+    "tumble_maxby_long_first": (("tumble", 3000, 0), 0, False, ("maxBy", "LONG"), 2),
+    "tumble_minby_long_last_lateness_side": (("tumble", 2000, 0), 1500, True, ("minBy", "LONG", False), 2),
+    "tumble_maxby_double_nan_last": (("tumble", 2000, 0), 0, False, ("maxBy", "DOUBLE", False), 3),
+    "sliding_minby_double_first_lateness": (("sliding", 3000, 1000), 2000, False, ("minBy", "DOUBLE"), 3),
+    "sliding_nondiv_maxby_long_last": (("sliding", 3500, 1000), 1000, False, ("maxBy", "LONG", False), 2),
 }
+_CANON_NAN = 0x7FF8000000000000
+
+
+def _canon(bits, dbl):
+    return _CANON_NAN if dbl and np.isnan(np.int64(bits).view(np.float64)) else int(bits)
 
 
 def _operator(case):
@@ -80,8 +92,10 @@ def test_datastream_records_match_reference_shape(case):
     vcol = CASES[case][4]
     elements = {}  # arrival ordinal -> element (key, field, tag)
     snap_at = 9
+    by = CASES[case][3][0] in ("minBy", "maxBy")
+    dbl = vcol == 3
     for b, (k, t, iv, dv, wm) in enumerate(_batches(zlib.crc32(case.encode()) % 1000)):
-        v = iv if vcol == 2 else dv
+        v = (iv % 5 if by else iv) if vcol == 2 else dv
         seq = op.handle.push_seq
         recs = []
         for i in range(len(k)):
@@ -98,10 +112,16 @@ def test_datastream_records_match_reference_shape(case):
                        [(r[0], _bits(r[1]), r[2]) for r in got["records"]]))
         w = sorted(zip(want["key"].tolist(), want["window_end"].tolist(), want["values"][0].tolist(),
                        want["first_ord"].tolist()))
+        if by:  # the value column is the field's key decoded: a NaN as the canonical NaN
+            g = [(x[0], x[1], _canon(x[2], dbl)) + tuple(x[3:]) for x in g]
+            w = [(x[0], x[1], _canon(x[2], dbl)) + tuple(x[3:]) for x in w]
         assert [x[:4] for x in g] == w, f"batch {b}: value bits / first element differ from the oracle"
-        for key, we, val, fo, rec in g:  # value1.copy() with the field set
+        for key, we, val, fo, rec in g:
             first = elements[fo]
-            assert rec == (first[0], val, first[2]), f"batch {b}: record of window ({key}, {we})"
+            if by:  # the extremal element itself
+                assert rec == (first[0], _bits(first[1]), first[2]), f"batch {b}: element of window ({key}, {we})"
+            else:  # value1.copy() with the field set
+                assert rec == (first[0], val, first[2]), f"batch {b}: record of window ({key}, {we})"
         if CASES[case][2]:
             sg, so = op.side_output(), o.side_output()
             assert sorted(zip(sg["push_seq"].tolist(), sg["row"].tolist())) == \

@@ -30,6 +30,9 @@ CASES = {
     "tumble_min_double_lateness": (("tumble", 2000, 0), 1500, ("min", "DOUBLE"), 3),
     "sliding_max_double_lateness": (("sliding", 3000, 1000), 2000, ("max", "DOUBLE"), 3),
     "sliding_nondiv_sum_long": (("sliding", 3500, 1000), 0, ("sum", "LONG"), 2),
+    # minBy / maxBy: the state holds the extremal element itself
+    "sliding_maxby_long_last": (("sliding", 3000, 1000), 1000, ("maxBy", "LONG", False), 2),
+    "tumble_minby_double_first": (("tumble", 2000, 0), 0, ("minBy", "DOUBLE"), 3),
 }
 
 

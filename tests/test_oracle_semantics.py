@@ -18,6 +18,7 @@ import math
 import struct
 
 import numpy as np
+import pytest
 
 from flink_amd import abi
 from oracle.oracle import OracleOperator
@@ -171,3 +172,35 @@ def test_datastream_sliding_windows_slide_not_dividing_size():
     got = {(int(k), int(e)): int(v) for k, e, v in zip(r["key"], r["window_end"], r["values"][0])}
     o.close()
     assert got == want
+
+
+@pytest.mark.parametrize("fn,last,vals,want_row", [
+    # maxBy: 7 arrives at rows 1 and 2 -- the first (default) keeps row 1, first=false takes row 2
+    ("MAXBY", False, [5, 7, 7, 2], 1),
+    ("MAXBY", True, [5, 7, 7, 2], 2),
+    ("MINBY", False, [5, 2, 9, 2], 1),
+    ("MINBY", True, [5, 2, 9, 2], 3),
+    # Double.compareTo: -0.0 < 0.0, NaN above everything and every NaN equal to every other
+    ("MINBY_D", False, [0.0, -0.0, 1.0, -0.0], 1),
+    ("MAXBY_D", False, [1.0, float("nan"), 5.0, float("nan")], 1),
+    ("MAXBY_D", True, [1.0, float("nan"), 5.0, float("nan")], 3),
+])
+def test_datastream_minby_maxby_tie_rules(fn, last, vals, want_row):
+    """ComparableAggregator.reduce with byAggregate (:89-96): value1 (the state) stays when it is
+    strictly extremal (MaxByComparator / MinByComparator, Comparator.java:58-101), and on a tie iff
+    `first`; the window emits that ELEMENT (its arrival ordinal is the result's first_ord)."""
+    dbl = fn.endswith("_D")
+    kind = abi.AGG_MAXBY if fn.startswith("MAXBY") else abi.AGG_MINBY
+    t = abi.T_F64 if dbl else abi.T_I64
+    cfg = abi.make_config(api=abi.API_DATASTREAM, window_kind=abi.WIN_TUMBLE, size_ms=10_000,
+                          aggs=[(kind, 0, t, abi.AGGF_LAST if last else 0)], value_col_types=[t],
+                          key_hash=abi.KEYHASH_LONG, ds_first_ordinals=1)
+    o = OracleOperator(cfg)
+    n = len(vals)
+    v = np.array(vals, np.float64).view(np.int64) if dbl else np.array(vals, np.int64)
+    o.process_batch(np.full(n, 3, np.int64), np.arange(T0, T0 + n, dtype=np.int64), [v])
+    o.process_watermark(T0 + 20_000)
+    r = o.results()
+    o.close()
+    assert r["first_ord"].tolist() == [want_row]  # push 0, row want_row
+    assert r["values"][0].tolist() == [int(v[want_row])]

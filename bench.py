@@ -50,9 +50,8 @@ WORKLOADS = {
                  window=("TUMBLE", 10_000, 0), aggs=[("SUM", 0, "DOUBLE"), ("AVG", 0, "DOUBLE")],
                  count_star=-1, keys=1_250_000, key_base=0, rate=1_000_000, value_kind=1, dist=0, w_in=24,
                  value_cols=["DOUBLE"], nw=2, state_per_key=2),
-    # CFG4's full key space on ONE GPU (10^7 keys, sharded over 8 GPUs in cfg4): the state
-    # outgrows the 8192 superbuckets the ingest histogram partitions into, so two merge passes share
-    # each ingest superbucket (KeySpace.pass_log2 = 1)
+    # CFG4's full key space on ONE GPU (10^7 keys, sharded over 8 GPUs in cfg4): 16384
+    # superbuckets, the most the ingest histogram partitions into (one merge pass each)
     "cfg4_10m": dict(desc="TUMBLE(10 s) SUM(v), AVG(v) DOUBLE over 10^7 keys on one GPU",
                      window=("TUMBLE", 10_000, 0), aggs=[("SUM", 0, "DOUBLE"), ("AVG", 0, "DOUBLE")],
                      count_star=-1, keys=10_000_000, key_base=0, rate=1_000_000, value_kind=1, dist=0, w_in=24,

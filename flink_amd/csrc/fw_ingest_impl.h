@@ -61,7 +61,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int SL = ig_slots(NW);
     constexpr bool CAN_COMPACT = NW == 1;  // compact partial rows (PF_NARROW / PF_UNIT)
     static_assert(RPT % IG_SRPT == 0, "fold sub-tiles must tile the chunk");
-    // dynamic LDS only (16-B aligned base, G17): [header 16 words][hist: n_sb u32, padded to
+    // dynamic LDS only (16-B aligned base, G17): [header 16 words][hist: n_sb u16, padded to
     // 16 B][area: fold table, later the store stage]
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     int64_t* s_min = (int64_t*)&lds[0];
@@ -72,7 +72,11 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     const int PL = a.ks.pass_log2;
     const int n_sb = a.ks.n_sb >> PL;  // ingest superbuckets: the histogram and the cells
     const int n_units = a.ks.n_sb;     // state superbuckets (route_key's result)
-    uint32_t* hist = (uint32_t*)(lds + IG_HDR_WORDS);  // partials per superbucket -> cell start
+    // partials per superbucket -> cell start: 16-bit (a chunk holds < 2^16 rows), so the histogram of
+    // IG_MAX_SB superbuckets takes 32 KiB; counted with 32-bit LDS adds on the counter's half
+    static_assert(IG_BLOCK * RPT < (1 << 16), "16-bit superbucket counters");
+    uint16_t* hist = (uint16_t*)(lds + IG_HDR_WORDS);
+    uint32_t* hist2 = (uint32_t*)hist;
     uint64_t* area = lds + IG_HDR_WORDS + ig_hist_words(n_sb);
     const int area_words = (a.lds_bytes >> 3) - IG_HDR_WORDS - ig_hist_words(n_sb);
     uint32_t* claim = (uint32_t*)area;                   // [SL]
@@ -99,7 +103,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         *s_rows = 0;
         *s_folded = 0;
     }
-    for (int s = tid; s < n_sb; s += IG_BLOCK) hist[s] = 0;
+    for (int s = tid; s < (n_sb + 1) >> 1; s += IG_BLOCK) hist2[s] = 0;
 
     // ---- coalesced column loads of the whole chunk (all in flight before the first use)
     const int64_t base = c * CH;
@@ -413,7 +417,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     const bool sort = !(FW_ABL(a) & AB_NO_SORT);
     static_for<RPT>([&](auto J) {
         constexpr int j = decltype(J)::value;
-        rdst[j] = (sort && (valid & (1u << j))) ? atomicAdd(&hist[rsb[j] >> PL], 1u) : (uint32_t)(j * IG_BLOCK + tid);
+        const uint32_t i = (uint32_t)(rsb[j] >> PL), sh = (i & 1u) << 4;
+        rdst[j] = (sort && (valid & (1u << j))) ? (atomicAdd(&hist2[i >> 1], 1u << sh) >> sh) & 0xFFFFu
+                                                : (uint32_t)(j * IG_BLOCK + tid);
     });
     __syncthreads();
     // ---- the chunk's partial-row format (PF_*): compact unless a row kept its own slice end or

@@ -24,10 +24,10 @@ constexpr int IG_BLOCK = 512;  // the 512-thread variant (and the default LDS bu
 constexpr int IG_SRPT = 2;                      // rows per thread per fold sub-tile
 constexpr int IG_SUB = IG_BLOCK * IG_SRPT;      // rows per fold sub-tile (1024)
 constexpr int IG_LDS = 78 * 1024;               // dynamic LDS per workgroup: histogram + fold/stage area
-constexpr int IG_MAX_SB = 8192;                 // superbuckets the ingest histogram holds (32 KiB)
+constexpr int IG_MAX_SB = 16384;                // superbuckets the ingest histogram holds (16-bit counters, 32 KiB)
 constexpr int MAX_PASS_LOG2 = 3;                // state superbuckets per ingest superbucket, log2 (KeySpace)
 constexpr int IG_HDR_WORDS = 16;                // 8-B words of per-chunk counters at the LDS base
-constexpr int ig_hist_words(int n_sb) { return ((n_sb + 3) >> 2) << 1; }  // 16-B multiple
+constexpr int ig_hist_words(int n_sb) { return ((n_sb + 7) >> 3) << 1; }  // u16 counters, 16-B multiple
 // rows per thread by accumulator words and loaded value columns (template NV): the chunk's rows
 // and partials stay in registers (<= 128 VGPRs)
 constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }

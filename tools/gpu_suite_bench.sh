@@ -1,3 +1,6 @@
+#!/bin/bash
+# GPU box: the full -m gpu suite, then short bench lines (WLS, default cfg4_10m cfg2 cfg5):
+#   bash tools/gpu_suite_bench.sh
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/gpu_tests.log | head -20; exit $rc; }

@@ -623,9 +623,8 @@ int validate_and_plan(fw_handle* h) {
     // runs: every chunk claims its stretch of each superbucket's sub-runs, so the merge streams a
     // superbucket's rows (fw_internal.h RUN_X).  Sub-runs hold 5/4 of a uniform share of a full push
     // (+16 rows); skew beyond that stays in the chunks' regions (overflow flags).  Off for key-row
-    // handles (their collector reads the chunk regions), split superbuckets (pass_log2: several
-    // readers per ingest superbucket) and superbucket counts the ingest LDS cannot book-keep;
-    // FW_RUNS=0 switches them off (development A/B).
+    // handles (their collector reads the chunk regions) and split superbuckets (pass_log2: several
+    // readers per ingest superbucket); FW_RUNS=1 / 0 forces them on / off (development A/B).
     {
         const char* re = getenv("FW_RUNS");
         const int n_isb = ks.n_sb >> ks.pass_log2;

@@ -30,8 +30,14 @@ constexpr int IG_HDR_WORDS = 16;                // 8-B words of per-chunk counte
 constexpr int ig_hist_words(int n_sb) { return ((n_sb + 7) >> 3) << 1; }  // u16 counters, 16-B multiple
 // rows per thread by accumulator words and loaded value columns (template NV): the chunk's rows
 // and partials stay in registers (<= 128 VGPRs)
-constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
-constexpr int ig_block(int nw, int nv) { return (nv > 4 || nw > 2) ? 1024 : 512; }
+#ifndef FW_IG_RPT2
+#define FW_IG_RPT2 8    // rows per thread, <= 2 words (development A/B builds override)
+#endif
+#ifndef FW_IG_BLK2
+#define FW_IG_BLK2 512  // workgroup size, <= 2 words
+#endif
+constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? FW_IG_RPT2 : nw <= 4 ? 4 : 2; }
+constexpr int ig_block(int nw, int nv) { return (nv > 4 || nw > 2) ? 1024 : FW_IG_BLK2; }
 constexpr int ig_lds(int block) { return block == 1024 ? 156 * 1024 : 78 * 1024; }
 // the template NV of a count of loaded value columns
 constexpr int ig_nv(int nv) { return nv <= 2 ? nv : nv <= 4 ? 4 : 8; }

@@ -178,6 +178,11 @@ def main():
                     help="N>1: the watermark valve / overflow agreement as one device all-reduce read by "
                          "fw_advance_device (no host wait per step), or on the host (gloo all-reduce after "
                          "waiting for the partition kernel)")
+    ap.add_argument("--sink", default="segments", choices=["segments", "compact", "discard"],
+                    help="each watermark's result rows, consumed on the device: where the merge wrote them "
+                         "(fw_results_device_segments: per-superbucket segments, no copy), compacted into "
+                         "contiguous device columns (fw_results_device: one more read and write of every row), "
+                         "or dropped (fw_results_reset)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
                          "one-GPU box: ranks share the GPUs round robin and the exchange is staged "
@@ -298,7 +303,7 @@ def main():
 
         def step(self, b):
             self.tp.local.push_device(gk[b], gt[b], [gv[b]] if nv else [])
-            self.tp.glob.reset_results()  # blackhole sink
+            sink(self.tp.glob)
             if args.valve == "device":
                 self.tp.step_device_valve(watermark(b, wl["rate"]))
             else:
@@ -335,13 +340,25 @@ def main():
     def make_op(cfg):
         return TwoPhaseOp(cfg) if two_phase else WindowAggHandle(cfg)
 
+    sink_res, sink_dn, sink_seg = abi.fw_result(), C.c_void_p(), abi.fw_result_segments()
+
+    def sink(h):
+        """the previous watermark's rows, consumed on the device through the C-ABI call itself (no
+        torch views): as segments in place, compacted, or dropped"""
+        if args.sink == "segments":
+            _native.check(L.fw_results_device_segments(h._h, C.byref(sink_seg)))
+        elif args.sink == "compact":
+            _native.check(L.fw_results_device(h._h, C.byref(sink_res), C.byref(sink_dn)))
+        else:
+            h.reset_results()
+
     def run(first, nsteps, handle):
         for b in range(first, first + nsteps):
             if two_phase:
                 handle.step(b)
                 continue
             wm = push_step(b, handle)
-            handle.reset_results()       # blackhole sink: results of the previous watermark consumed
+            sink(handle)
             if torch.is_tensor(wm):
                 handle.advance_device(wm)
             else:
@@ -572,6 +589,11 @@ def main():
                            "" if world == 1 else " + RCCL all-to-all" if args.dist_backend == "nccl"
                            else " + gloo all-to-all (rehearsal, shared GPU)"),
                        "max_parallelism": 128, "superbuckets": st["num_superbuckets"],
+                       "result_sink": {"segments": "each watermark's rows consumed where the merge wrote them "
+                                                   "(fw_results_device_segments: per-superbucket device segments)",
+                                       "compact": "each watermark's rows compacted into contiguous device columns "
+                                                  "(fw_results_device)",
+                                       "discard": "dropped (fw_results_reset)"}[args.sink],
                        "exchange": None if world == 1 else {
                            "kind": "packed padded all-to-all, segments of the batch's even share + 25 %",
                            "watermark_valve": ("device all-reduce (overflow, watermark, share) -> fw_advance_device"

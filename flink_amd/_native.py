@@ -69,6 +69,7 @@ def lib():
         "fw_snapshot_key_group_heap": (i32, [vp, i32, P(abi.fw_heap_state_ids), vp, i64, P(i64)]),
         "fw_restore_key_group_heap": (i32, [vp, vp, i64, P(abi.fw_heap_state_ids)]),
         "fw_ds_snapshot_key_group": (i32, [vp, i32, vp, i64, P(i64)]),
+        "fw_results_device_segments": (i32, [vp, P(abi.fw_result_segments)]),
         "fw_ds_restore_key_group": (i32, [vp, i32, vp, i64, i64]),
         "fw_assign_key_groups": (i32, [vp, vp, i64, i32, i32, i32, vp, vp, vp]),
         "fw_partition_by_dest": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, vp, vp, vp, vp, vp, i64, vp]),
@@ -104,7 +105,7 @@ EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_ge
             "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance", "fw_advance_device",
             "fw_flush", "fw_results", "fw_results_reset", "fw_results_async", "fw_results_ready", "fw_results_device", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
-            "fw_snapshot_key_group_heap", "fw_restore_key_group_heap", "fw_ds_snapshot_key_group", "fw_ds_restore_key_group", "fw_key_row_hash", "fw_host_key_row_hash",
+            "fw_snapshot_key_group_heap", "fw_restore_key_group_heap", "fw_ds_snapshot_key_group", "fw_ds_restore_key_group", "fw_results_device_segments", "fw_key_row_hash", "fw_host_key_row_hash",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_packed_spill", "fw_partition_packed_spill_dn", "fw_partition_workspace_bytes",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
             "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records", "fw_first_element_events",

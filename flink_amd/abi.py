@@ -141,6 +141,12 @@ class fw_result(C.Structure):
                 ("key_row_stride", C.c_int64)]
 
 
+class fw_result_segments(C.Structure):
+    """flinkwin.h fw_results_device_segments: per-superbucket result slabs, no copy"""
+    _fields_ = [("n_segments", C.c_int64), ("seg_cap", C.c_int64), ("counts", C.c_void_p),
+                ("cols", fw_result)]
+
+
 class fw_ordinal_events(C.Structure):
     _fields_ = [("n_retain", C.c_int64), ("retain", C.POINTER(C.c_int64)),
                 ("n_release", C.c_int64), ("release", C.POINTER(C.c_int64))]

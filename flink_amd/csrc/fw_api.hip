@@ -735,7 +735,7 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->res_null, h->out_cap))) return rc;
     for (int g = 0; g < h->n_out; g++)
         if ((rc = dalloc(&h->res_val[g], h->out_cap))) return rc;
-    if ((rc = dalloc(&h->sb_out, h->ks.n_sb))) return rc;
+    if ((rc = dalloc(&h->sb_out, h->ks.n_sb + 1))) return rc;  // + the overflow region's rows
     if ((rc = dalloc(&h->sb_fired, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->coff, h->ks.n_sb + 2))) return rc;
     if ((rc = dalloc(&h->chunk_stats, CS_WORDS * (h->max_nch + 1)))) return rc;
@@ -748,7 +748,7 @@ int allocate(fw_handle* h) {
     HIP_TRY(hipMemsetAsync(h->tickets, 0, sizeof(Tickets), h->stream));
     HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(unsigned long long) * N_STAMPS, h->stream));
     HIP_TRY(hipMemsetAsync(h->kt_dev, 0, sizeof(unsigned long long) * FW_KT_N * KT_WORDS, h->stream));
-    HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
+    HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * (h->ks.n_sb + 1), h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_fired, 0, sizeof(uint32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->state_count, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
     std::vector<int64_t> inf(h->ks.n_sb, INT64_MAX);
@@ -1512,6 +1512,27 @@ int fw_results_async(fw_handle* h) {
     HIP_TRY(launch_compact(ca, h->stream, h->timer));
     HIP_TRY(hipEventRecord(h->ar_ev[b], h->stream));
     h->reset_pending = true;  // the rows are collected: the next merge launch starts the slabs afresh
+    return FW_OK;
+}
+
+int fw_results_device_segments(fw_handle* h, fw_result_segments* out) {
+    if (!h || !out) return fail(FW_E_INVALID, "null argument");
+    if (h->keyrow) return fail(FW_E_INVALID, "key-row operators return their rows through fw_results");
+    memset(out, 0, sizeof *out);
+    const int na = h->n_out;
+    const int nv = h->ad.first_word >= 0 ? na - 1 : na;
+    out->seg_cap = h->slab_cap;
+    out->counts = h->sb_out;
+    out->cols.n = (int64_t)h->ks.n_sb * h->slab_cap + h->out_cap;
+    out->cols.key = h->out_key;
+    out->cols.window_start = h->out_ws;
+    out->cols.window_end = h->out_we;
+    for (int g = 0; g < nv; g++) out->cols.values[g] = (int64_t*)h->out_val[g];
+    if (nv < na) out->cols.first_ord = (int64_t*)h->out_val[nv];
+    out->cols.null_mask = h->out_null;
+    // consumed and nothing emitted since: no segments (the counts are those of consumed rows)
+    out->n_segments = h->reset_pending ? 0 : (int64_t)h->ks.n_sb + 1;
+    h->reset_pending = true;  // consumed: the next merge launch starts the slabs afresh
     return FW_OK;
 }
 

@@ -52,8 +52,11 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, 
 }
 
 // X: the configuration has nullable columns or words that read arrival ordinals (gates, ordinals)
+#ifndef FW_IG_MINW
+#define FW_IG_MINW 4  // waves per SIMD the register budget must allow (development A/B builds override)
+#endif
 template <int NV, int NW, int RPT, bool X, int IG_BLOCK>
-__global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
+__global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
     constexpr int CH = IG_BLOCK * RPT;
     constexpr int NSUB = RPT / IG_SRPT;
     constexpr int NVR = NV > 0 ? NV : 1;

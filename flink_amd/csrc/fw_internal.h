@@ -38,7 +38,10 @@ constexpr int ig_hist_words(int n_sb) { return ((n_sb + 7) >> 3) << 1; }  // u16
 #endif
 constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? FW_IG_RPT2 : nw <= 4 ? 4 : 2; }
 constexpr int ig_block(int nw, int nv) { return (nv > 4 || nw > 2) ? 1024 : FW_IG_BLK2; }
-constexpr int ig_lds(int block) { return block == 1024 ? 156 * 1024 : 78 * 1024; }
+#ifndef FW_IG_LDS2_KB
+#define FW_IG_LDS2_KB 78  // LDS of a 512-thread ingest workgroup (two per CU)
+#endif
+constexpr int ig_lds(int block) { return block == 1024 ? 156 * 1024 : FW_IG_LDS2_KB * 1024; }
 // the template NV of a count of loaded value columns
 constexpr int ig_nv(int nv) { return nv <= 2 ? nv : nv <= 4 ? 4 : 8; }
 // LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)

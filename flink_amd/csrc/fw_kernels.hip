@@ -40,57 +40,51 @@ extern template hipError_t merge_nw<4>(const MergeArgs&, hipStream_t);
 extern template hipError_t merge_nw<8>(const MergeArgs&, hipStream_t);
 
 // ---- result compaction: slabs (+ overflow) -> one contiguous result set ----------------------
-__global__ __launch_bounds__(BLOCK) void k_compact_scan(const int32_t* sb_out, int32_t n_sb, int64_t* off, Ctrl* ctrl,
-                                                        int64_t out_cap, int64_t* host_n) {
-    __shared__ int64_t tmp[BLOCK];
-    __shared__ int64_t carry;
-    if (threadIdx.x == 0) carry = 0;
+// One launch: block b copies the slabs of superbuckets [b·R, (b+1)·R) in order; its first output row
+// is the sum of the slab counts before its range (a block-wide reduction over sb_out, read from L2:
+// at most 512 blocks, so <= n_sb / 2 reads each on average).  The last block also copies the shared
+// overflow region and publishes the totals (off[n_sb] = slab rows, off[n_sb + 1] = all rows).
+__device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* tmp) {
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    if ((threadIdx.x & 63) == 0) tmp[threadIdx.x >> 6] = v;
     __syncthreads();
-    for (int base = 0; base < n_sb; base += BLOCK) {
-        const int i = base + threadIdx.x;
-        const int64_t v = i < n_sb ? sb_out[i] : 0;
-        tmp[threadIdx.x] = v;
-        __syncthreads();
-        for (int d = 1; d < BLOCK; d <<= 1) {
-            const int64_t x = threadIdx.x >= d ? tmp[threadIdx.x - d] : 0;
-            __syncthreads();
-            tmp[threadIdx.x] += x;
-            __syncthreads();
-        }
-        if (i < n_sb) off[i] = carry + tmp[threadIdx.x] - v;
-        __syncthreads();
-        if (threadIdx.x == BLOCK - 1) carry += tmp[BLOCK - 1];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const int64_t ovf = (int64_t)min(ctrl->out_count[ctrl->ovf_sel & 1], (uint64_t)out_cap);
-        off[n_sb] = carry;          // slab rows
-        off[n_sb + 1] = carry + ovf;  // total rows
-        if (host_n)  // fw_results_async: the count, next to the rows in mapped host memory (vector store)
-            __hip_atomic_store(host_n, carry + ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    int64_t t = 0;
+    for (int w = 0; w < BLOCK / 64; w++) t += tmp[w];
+    __syncthreads();
+    return t;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_compact_copy(CompactArgs a) {
-    const int sb = blockIdx.x;
-    int64_t src0, dst0, n;
-    if (sb < a.n_sb) {
-        src0 = (int64_t)sb * a.slab_cap;
-        dst0 = a.off[sb];
-        n = a.sb_out[sb];
-    } else {  // overflow region
-        src0 = (int64_t)a.n_sb * a.slab_cap;
-        dst0 = a.off[a.n_sb];
-        n = a.off[a.n_sb + 1] - a.off[a.n_sb];
+__global__ __launch_bounds__(BLOCK) void k_compact(CompactArgs a, int32_t R) {
+    __shared__ int64_t tmp[BLOCK / 64];
+    const int s0 = blockIdx.x * R, s1 = min(s0 + R, a.n_sb);
+    int64_t part = 0;
+    for (int i = threadIdx.x; i < s0; i += BLOCK) part += a.sb_out[i];
+    int64_t base = block_sum_i64(part, tmp);
+    auto copy = [&](int64_t src0, int64_t dst0, int64_t n) {
+        for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
+            const int64_t d = dst0 + i, sidx = src0 + i;
+            if (d >= a.res_cap) break;
+            a.res_key[d] = a.out_key[sidx];
+            a.res_ws[d] = a.out_ws[sidx];
+            a.res_we[d] = a.out_we[sidx];
+            a.res_null[d] = a.out_null[sidx];
+            for (int g = 0; g < a.n_aggs; g++) a.res_val[g][d] = a.out_val[g][sidx];
+        }
+    };
+    for (int sb = s0; sb < s1; sb++) {
+        const int64_t n = a.sb_out[sb];
+        if (threadIdx.x == 0) a.off[sb] = base;
+        copy((int64_t)sb * a.slab_cap, base, n);
+        base += n;
     }
-    for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
-        const int64_t d = dst0 + i, sidx = src0 + i;
-        if (d >= a.res_cap) break;
-        a.res_key[d] = a.out_key[sidx];
-        a.res_ws[d] = a.out_ws[sidx];
-        a.res_we[d] = a.out_we[sidx];
-        a.res_null[d] = a.out_null[sidx];
-        for (int g = 0; g < a.n_aggs; g++) a.res_val[g][d] = a.out_val[g][sidx];
+    if (blockIdx.x != gridDim.x - 1) return;
+    const int64_t ovf = (int64_t)min(a.ctrl->out_count[a.ctrl->ovf_sel & 1], (uint64_t)a.res_cap);
+    copy((int64_t)a.n_sb * a.slab_cap, base, ovf);
+    if (threadIdx.x == 0) {
+        a.off[a.n_sb] = base;          // slab rows
+        a.off[a.n_sb + 1] = base + ovf;  // total rows
+        if (a.host_n)  // fw_results_async: the count, next to the rows in mapped host memory (vector store)
+            __hip_atomic_store(a.host_n, base + ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -133,8 +127,9 @@ __global__ void k_init_ctrl(Ctrl* c) {
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t) {
     kt_mark(t, FW_KT_OTHER, false, s);
-    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(BLOCK), 0, s, a.sb_out, a.n_sb, a.off, a.ctrl, a.res_cap, a.host_n);
-    hipLaunchKernelGGL(k_compact_copy, dim3(a.n_sb + 1), dim3(BLOCK), 0, s, a);
+    const int R = (a.n_sb + 511) / 512;  // superbuckets per block: at most 512 blocks
+    const int nb = (a.n_sb + R - 1) / R;
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)nb), dim3(BLOCK), 0, s, a, (int32_t)R);
     kt_mark(t, FW_KT_OTHER, true, s);
     return hipGetLastError();
 }

@@ -759,6 +759,8 @@ __device__ void merge_finalize(const MergeArgs& a, int64_t W) {
     const int sel = (c->ovf_sel ^ a.reset_out) & 1;
     c->ovf_sel = sel;
     __hip_atomic_store(&c->out_count[sel ^ 1], 0ull, __ATOMIC_RELAXED, DEV_SCOPE);
+    // the overflow region's rows, beside the slab counts (fw_results_device_segments)
+    a.sb_out[a.n_sb] = (int32_t)min((int64_t)__hip_atomic_load(&c->out_count[sel], __ATOMIC_RELAXED, DEV_SCOPE), a.out_cap);
     if (a.host_mirror)  // vector store to host-mapped memory (system scope)
         __hip_atomic_store(a.host_mirror, (unsigned long long)((a.merge_seq << 8) | (uint64_t)(do_flush ? 0 : pend)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -250,6 +250,50 @@ class WindowAggHandle:
             self.reset_results()
         return out
 
+    def result_segments(self):
+        """fw_results_device_segments: the rows emitted since the last collection where the merge
+        wrote them (no compaction), consumed.  Returns the device description (n_segments, seg_cap,
+        counts pointer, column pointers) as the ABI struct; segments_to_host() reads it back."""
+        seg = abi.fw_result_segments()
+        check(lib().fw_results_device_segments(self._h, C.byref(seg)))
+        return seg
+
+    def segments_to_host(self, seg):
+        """The rows of a result_segments() description as the dict results() returns (host copies,
+        after the handle's stream drains; for tests and tools -- a device consumer reads the
+        segments in place)."""
+        self.sync()
+        cols = {"key": seg.cols.key, "window_start": seg.cols.window_start, "window_end": seg.cols.window_end}
+        out = {k: [] for k in cols}
+        out["values"] = [[] for _ in range(self.n_aggs)]
+        out["null_mask"] = []
+        ds = bool(self.cfg.ds_first_ordinals)
+        if ds:
+            out["first_ord"] = []
+        if seg.n_segments:
+            counts = _np_view(seg.counts, int(seg.n_segments), np.int32).copy()
+            total = int(seg.cols.n)
+            for sidx, c in enumerate(counts.tolist()):
+                if c <= 0:
+                    continue
+                r0 = sidx * int(seg.seg_cap)
+                for k, ptr in cols.items():
+                    out[k].append(_np_view(ptr, total, np.int64)[r0:r0 + c].copy())
+                for a in range(self.n_aggs):
+                    out["values"][a].append(_np_view(seg.cols.values[a], total, np.int64)[r0:r0 + c].copy())
+                out["null_mask"].append(_np_view(seg.cols.null_mask, total, np.uint32)[r0:r0 + c].copy())
+                if ds:
+                    out["first_ord"].append(_np_view(seg.cols.first_ord, total, np.int64)[r0:r0 + c].copy())
+
+        def cat(xs, dt):
+            return np.concatenate(xs) if xs else np.empty(0, dt)
+        res = {k: cat(out[k], np.int64) for k in cols}
+        res["values"] = [cat(v, np.int64) for v in out["values"]]
+        res["null_mask"] = cat(out["null_mask"], np.uint32)
+        if ds:
+            res["first_ord"] = cat(out["first_ord"], np.int64)
+        return res
+
     def results_async(self):
         """Queue the collection of the rows emitted since the last collection into pinned host
         memory (fw_results_async); they count as consumed.  results_ready() returns them."""

@@ -380,6 +380,22 @@ int fw_results_ready(fw_handle* h, fw_result* out);
    out->n is only its bound (output_capacity).  The rows count as consumed; read them on the
    handle's stream (fw_get_stream) or after it, before the next call that collects results. */
 int fw_results_device(fw_handle* h, fw_result* out, int64_t** d_n);
+/* v7, device-side consumers without a copy: the rows emitted since the last collection where the
+   merge wrote them.  Segment s < n_segments - 1 (superbucket s) holds counts[s] rows at rows
+   [s * seg_cap, s * seg_cap + counts[s]) of the columns in cols (device pointers; cols.n bounds
+   the row index); the last segment, the shared overflow region, holds counts[n_segments - 1] rows
+   from row (n_segments - 1) * seg_cap.  counts is a device int32 array written by the merge
+   kernels, so read it (and the rows) on the handle's stream (fw_get_stream) or after it, before
+   the next fw_advance / fw_flush.  n_segments = 0 when nothing was emitted since the last
+   collection.  The rows count as consumed.  fw_results / fw_results_device compact the same rows
+   into one contiguous set (a copy of every row). */
+typedef struct {
+    int64_t n_segments;
+    int64_t seg_cap;
+    const int32_t* counts;
+    fw_result cols;
+} fw_result_segments;
+int fw_results_device_segments(fw_handle* h, fw_result_segments* out);
 int fw_get_stats(fw_handle* h, fw_stats* out);
 
 /* ---- per-kernel device timing (in-kernel clock stamps, or hipEvents around each launch) --- */

@@ -62,8 +62,9 @@ def _stream(seed, n, n_keys, ooo, step_ms, n_wm, dup_wm=False):
     return batches
 
 
-def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None, stats=None):
-    """nulls: per batch {column: flags} (or None); stats: a dict that receives the handle's final fw_stats."""
+def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None, stats=None, collect="compact"):
+    """nulls: per batch {column: flags} (or None); stats: a dict that receives the handle's final fw_stats;
+    collect: "compact" (fw_results) or "segments" (fw_results_device_segments, read back per segment)."""
     from flink_amd.runtime.handle import WindowAggHandle
     from oracle.oracle import OracleOperator
     o = OracleOperator(cfg)
@@ -78,7 +79,8 @@ def _run_both(cfg, batches, double_cols, split=1, snapshot_at=None, nulls=None, 
         o.process_watermark(wm)
         g.advance(wm)
         want = _rows(o.results(clear=True), cfg, double_cols)
-        got = _rows(g.results(reset=True), cfg, double_cols)
+        got = _rows(g.results(reset=True) if collect == "compact" else g.segments_to_host(g.result_segments()), cfg,
+                    double_cols)
         _compare(got, want, double_cols, f"batch {bi} wm {wm}")
         if snapshot_at is not None and bi == snapshot_at:
             o.snapshot_restore()

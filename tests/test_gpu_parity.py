@@ -62,6 +62,21 @@ LAYOUT_CASES = [(w, a) for w in LAYOUT_WINDOWS for a in LAYOUT_AGGS
                 if w != "hop" or LAYOUT_AGGS[a][0][0] == abi.AGG_COUNT_STAR]
 
 
+# The rows where the merge wrote them (fw_results_device_segments: per-superbucket slabs and the
+# shared overflow region, no compaction) are the oracle's rows -- with an output capacity small
+# enough that the slabs overflow into the shared region.
+@pytest.mark.parametrize("name,out_cap,n,n_keys", [
+    ("sql_tumble_int_aggs", 1 << 20, 30000, 2000), ("sql_hop", 1 << 20, 30000, 2000),
+    ("sql_cumulate_countstar", 1 << 20, 30000, 2000), ("ds_sliding_max", 1 << 20, 30000, 2000),
+    # ~11 700 rows per firing over 128 superbuckets of 64-row slabs: ~3 500 rows in the overflow region
+    ("sql_tumble_int_aggs", 1 << 12, 140000, 12000)])
+def test_result_segments_match_oracle(name, out_cap, n, n_keys):
+    kw = CASES[name]
+    _run_both(_cfg(kw, output_capacity=out_cap), _stream(zlib.crc32(name.encode()) % 997, n, n_keys,
+                                                         ooo=2 * kw["size_ms"] + 1500, step_ms=1500, n_wm=14),
+              _double_cols(kw), collect="segments")
+
+
 # layout: the planner's choice, or the partial-row layout forced either way (FW_RUNS: superbucket
 # runs vs chunk-local cells, fw_api.hip; runs are planned only for TUMBLE with >= 2 words)
 @pytest.mark.parametrize("layout", ["planned", "runs", "cells"])

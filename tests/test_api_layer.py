@@ -119,6 +119,21 @@ def test_datastream_eligible():
     assert dso.is_gpu_eligible(SlidingEventTimeWindows.of(6000, 2000), EventTimeTrigger(), ("max", "DOUBLE"))[0]
     # slide need not divide size (SlidingEventTimeWindows.java:77-90): panes of gcd(size, slide)
     assert dso.is_gpu_eligible(SlidingEventTimeWindows.of(5000, 2000), EventTimeTrigger(), ("sum", "LONG"))[0]
+    # minBy / maxBy (WindowedStream.java:725-790), first (default) or last element on ties
+    assert dso.is_gpu_eligible(**dict(DS_OK, aggregation=("maxBy", "DOUBLE")))[0]
+    assert dso.is_gpu_eligible(**dict(DS_OK, aggregation=("minBy", "LONG", False)))[0]
+
+
+def test_datastream_minby_maxby_planning():
+    """minBy / maxBy emit whole elements: a record-shaped operator (field=...) is required, and the
+    first/last flag becomes fw_agg_desc.flags (FW_AGGF_LAST)"""
+    with pytest.raises(ValueError):
+        dso.WindowOperator(TumblingEventTimeWindows.of(5000), EventTimeTrigger(), ("maxBy", "LONG"))
+    op = dso.WindowOperator(TumblingEventTimeWindows.of(5000), EventTimeTrigger(), ("minBy", "LONG", False), field=1)
+    assert op.cfg.aggs[0].kind == abi.AGG_MINBY and op.cfg.aggs[0].flags == abi.AGGF_LAST
+    assert op.cfg.ds_first_ordinals == 1
+    op = dso.WindowOperator(TumblingEventTimeWindows.of(5000), EventTimeTrigger(), ("maxBy", "DOUBLE"), field=0)
+    assert op.cfg.aggs[0].kind == abi.AGG_MAXBY and op.cfg.aggs[0].flags == 0
 
 
 class _CountTrigger:  # a custom trigger (CountTrigger, ContinuousEventTimeTrigger, ...)
@@ -137,6 +152,7 @@ class _Sessions:  # a merging assigner (EventTimeSessionWindows)
     (dict(assigner=SlidingEventTimeWindows.of(2000, 5000)), "size < slide"),
     (dict(aggregation=("reduce", "LONG")), "built-in field aggregation"),
     (dict(aggregation=("sum", "FLOAT")), "built-in field aggregation"),
+    (dict(aggregation=("sum", "LONG", False)), "first/last flag"),
 ])
 def test_datastream_fallback_reasons(change, reason):
     kw = dict(DS_OK)

@@ -782,11 +782,20 @@ __device__ __forceinline__ void merge_ticket(const MergeArgs& a, int64_t W) {
 #ifndef FW_MG_PIPE1
 #define FW_MG_PIPE1 0  // ... also for one-word layouts and HOP block state (A/B: CFG2 slower with half blocks)
 #endif
+// (measured against the round-3 sizes: one word 3 rows per lane instead of 4 -- CFG2 flush 176 ->
+// 167 us, CFG3 274 -> 266 us; two words 2 instead of 3 -- CFG4 203 -> 191 us; four words stay at 2)
 #ifndef FW_GU1
-#define FW_GU1 4
+#define FW_GU1 3
+#endif
+#ifndef FW_GU2
+#define FW_GU2 2
+#endif
+#ifndef FW_GU4
+#define FW_GU4 2
 #endif
 constexpr int mg_rows_in_flight(int nw) {
-    return MG_BLOCK < 512 ? (nw <= 1 ? 2 * FW_GU1 : nw <= 2 ? 6 : nw <= 4 ? 4 : 2) : (nw <= 1 ? FW_GU1 : nw <= 2 ? 3 : nw <= 4 ? 2 : 1);
+    return MG_BLOCK < 512 ? (nw <= 1 ? 2 * FW_GU1 : nw <= 2 ? 2 * FW_GU2 : nw <= 4 ? 2 * FW_GU4 : 2)
+                          : (nw <= 1 ? FW_GU1 : nw <= 2 ? FW_GU2 : nw <= 4 ? FW_GU4 : 1);
 }
 
 #ifndef FW_MG_ROLL

@@ -71,8 +71,11 @@ constexpr int mg_entries(int nw, int kind) {
 constexpr int mg_idx_slots(int nw, int e) {
     const int entry_bytes = 8 + 8 + 4 + 8 * nw + 2;  // key, slice, flag, acc, due
     const int room = (158 * 1024 / MG_PER_CU - e * entry_bytes) / 4;
+#ifndef FW_IDX_MULT
+#define FW_IDX_MULT 4  // index slots per entry aimed at (development A/B builds override)
+#endif
     int n = 1;
-    while (n < 4 * e) n <<= 1;
+    while (n < FW_IDX_MULT * e) n <<= 1;
     while (n > room) n >>= 1;
     return n;
 }

@@ -12,8 +12,9 @@ N > 1 (torchrun, one rank per GPU, RCCL): every rank generates its slice of each
 routes rows to the key-group owner with fw_partition_packed + one packed padded all-to-all over
 xGMI (the keyBy exchange; the row counts stay on the device and the operator reads the packed rows
 in place, skipping the padding itself),
-min-reduces the watermark on the host (gloo), then runs its own operator subtask -- no host
-synchronisation inside a step.  Weak scaling: per-GPU events, keys and event rate stay fixed as
+min-reduces the watermark on the device (--valve device, the default: one RCCL all-reduce whose
+result fw_advance_device reads from device memory; --valve host keeps a host gloo all-reduce for
+A/B), then runs its own operator subtask -- no host synchronisation inside a step.  Weak scaling: per-GPU events, keys and event rate stay fixed as
 N grows.
 """
 import argparse
@@ -179,10 +180,10 @@ def main():
                          "fw_advance_device (no host wait per step), or on the host (gloo all-reduce after "
                          "waiting for the partition kernel)")
     ap.add_argument("--sink", default="segments", choices=["segments", "compact", "discard"],
-                    help="each watermark's result rows, consumed on the device: where the merge wrote them "
-                         "(fw_results_device_segments: per-superbucket segments, no copy), compacted into "
-                         "contiguous device columns (fw_results_device: one more read and write of every row), "
-                         "or dropped (fw_results_reset)")
+                    help="each watermark's result rows: handed over as per-superbucket device segments where "
+                         "the merge wrote them (fw_results_device_segments; the timed loop reads no row, so this "
+                         "costs what dropping them costs), compacted into contiguous device columns "
+                         "(fw_results_device: one more read and write of every row), or dropped (fw_results_reset)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, one rank per GPU).  gloo is a rehearsal of the N>1 path on a "
                          "one-GPU box: ranks share the GPUs round robin and the exchange is staged "
@@ -589,8 +590,9 @@ def main():
                            "" if world == 1 else " + RCCL all-to-all" if args.dist_backend == "nccl"
                            else " + gloo all-to-all (rehearsal, shared GPU)"),
                        "max_parallelism": 128, "superbuckets": st["num_superbuckets"],
-                       "result_sink": {"segments": "each watermark's rows consumed where the merge wrote them "
-                                                   "(fw_results_device_segments: per-superbucket device segments)",
+                       "result_sink": {"segments": "each watermark's rows left in the merge's device slabs and "
+                                                   "handed over as per-superbucket segments "
+                                                   "(fw_results_device_segments); no row is read in the timed loop",
                                        "compact": "each watermark's rows compacted into contiguous device columns "
                                                   "(fw_results_device)",
                                        "discard": "dropped (fw_results_reset)"}[args.sink],

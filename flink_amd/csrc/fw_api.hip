@@ -1981,6 +1981,15 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
     HIP_TRY(hipMemcpy(&c, h->ctrl, sizeof c, hipMemcpyDeviceToHost));  // the key-row allocator survives
     const Ctrl keep = c;
     HIP_TRY(launch_init_ctrl(h->ctrl, h->stream));
+    // the restore drops the pending pushes: with runs, their fill counters, overflow flags and formats
+    // go too (as allocate() starts them), or the next push would add onto the dropped push's fills and
+    // the next flush would fold its stale rows
+    if (h->run_rows) {
+        const size_t n_isb = (size_t)(h->ks.n_sb >> h->ks.pass_log2);
+        HIP_TRY(hipMemsetAsync(h->run_fill, 0, sizeof(uint32_t) * FW_MAX_PENDING * RUN_X * n_isb, h->stream));
+        HIP_TRY(hipMemsetAsync(h->run_ovf, 0, sizeof(uint32_t) * FW_MAX_PENDING * n_isb, h->stream));
+        HIP_TRY(hipMemsetAsync(h->slot_fmt, 0, sizeof(int32_t) * FW_MAX_PENDING, h->stream));
+    }
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(&c, h->ctrl, sizeof c, hipMemcpyDeviceToHost));
     // SQL: union-list watermark state (WindowAggOperator.initializeState :183-206).  DataStream:

@@ -8,9 +8,10 @@ namespace fw {
 // K1+K2+K3: single-pass ingest = slice/key-group assignment + LDS segmented reduce + a
 // chunk-local counting sort of the partials by superbucket.
 //
-// One 1024-thread workgroup owns a chunk of CH = 1024*RPT rows and keeps all of them in
-// registers (row j*1024 + tid, coalesced column loads, every load of the chunk in flight at
-// once).  The chunk is folded in fold sub-tiles of 2048 rows: rows with equal (key, slice) meet
+// One workgroup of ig_block(nw, nv) threads (512 for <= 2 accumulator words, two per CU; 1024 for
+// wider accumulators, one per CU) owns a chunk of CH = block*RPT rows (4096 either way) and keeps
+// all of them in registers (row j*block + tid, coalesced column loads, every load of the chunk in
+// flight at once).  The chunk is folded in fold sub-tiles of IG_SUB rows: rows with equal (key, slice) meet
 // in an LDS slot table whose owner is the lowest row index hashing to the slot (so a hot key,
 // which occurs early, keeps its slot); the owner ends up holding the folded partial in its
 // registers.  The surviving partials are then ranked per superbucket with LDS atomics, the

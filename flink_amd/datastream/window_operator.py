@@ -32,6 +32,7 @@ import numpy as np
 
 from .. import abi
 from ..runtime.handle import WindowAggHandle
+from ..runtime.options import gpu_enabled
 from . import heap_state
 from .windowing import EventTimeTrigger, SlidingEventTimeWindows, TumblingEventTimeWindows
 
@@ -53,7 +54,11 @@ def _dec_field(x):
 
 
 def is_gpu_eligible(assigner, trigger, aggregation, *, evictor=None, allowed_lateness=0,
-                    late_data_output_tag=None):
+                    late_data_output_tag=None, conf=None):
+    """WindowOperatorBuilder.buildWindowOperator's seam.  ``conf``: the job configuration
+    (runtime/options.py): ``gpu.window-agg.enabled`` must be true; None = the GPU operator was chosen."""
+    if conf is not None and not gpu_enabled(conf):
+        return False, "gpu.window-agg.enabled is false"
     if not isinstance(assigner, (TumblingEventTimeWindows, SlidingEventTimeWindows)):
         return False, "assigner is not Tumbling/SlidingEventTimeWindows"
     if isinstance(assigner, SlidingEventTimeWindows) and assigner.size < assigner.slide:

@@ -13,6 +13,7 @@ import numpy as np
 
 from .. import abi
 from ..runtime.handle import WindowAggHandle
+from ..runtime.options import gpu_enabled
 from .key_rows import KeyRowColumns, decode_key_row
 from .slice_assigners import SliceAssigner
 
@@ -23,11 +24,14 @@ KEY_HASH = {"BIGINT": abi.KEYHASH_BINROW_BIGINT, "INT": abi.KEYHASH_BINROW_INT,
 
 
 def is_gpu_eligible(assigner, aggs, value_types, *, is_event_time=True, shift_time_zone="UTC",
-                    has_distinct=False, needs_retraction=False, key_type="BIGINT"):
+                    has_distinct=False, needs_retraction=False, key_type="BIGINT", conf=None):
     """The builder-seam eligibility rule: rowtime (TIMESTAMP, or TIMESTAMP_LTZ with
     any shift time zone), built-in SUM/COUNT/COUNT(*)/MIN/MAX/AVG on numeric columns, no DISTINCT /
-    retraction / UDAF.  Returns (ok, reason); callers fall back to the reference processor when
-    not ok."""
+    retraction / UDAF.  ``conf``: the job configuration the builder passes (runtime/options.py):
+    ``gpu.window-agg.enabled`` must be true (default false); None = the caller already chose the
+    GPU operator.  Returns (ok, reason); callers fall back to the reference processor when not ok."""
+    if conf is not None and not gpu_enabled(conf):
+        return False, "gpu.window-agg.enabled is false"
     if not isinstance(assigner, SliceAssigner):
         return False, "not a slicing assigner"
     if not is_event_time or not assigner.is_event_time():

@@ -167,3 +167,18 @@ def test_assigner_mirrors_match_the_reference_window_assignment():
     assert TumblingEventTimeWindows.of(5000, 1000).assign_windows(7500) == [(6000, 11000)]
     assert sorted(SlidingEventTimeWindows.of(10000, 2000).assign_windows(7500)) == \
         [(-2000, 8000), (0, 10000), (2000, 12000), (4000, 14000), (6000, 16000)]
+
+
+def test_gpu_window_agg_options_gate_both_seams():
+    """gpu.window-agg.enabled (default false) gates both builder seams; gpu.window-agg.device picks
+    the handle's device (SURVEY.md 5 Config/flags)."""
+    from flink_amd.runtime import options
+    assert not sqlo.is_gpu_eligible(**SQL_OK, conf={})[0]
+    assert sqlo.is_gpu_eligible(**SQL_OK, conf={"gpu.window-agg.enabled": "false"})[1] == "gpu.window-agg.enabled is false"
+    assert sqlo.is_gpu_eligible(**SQL_OK, conf={"gpu.window-agg.enabled": "true"}) == (True, "")
+    assert not dso.is_gpu_eligible(**DS_OK, conf={})[0]
+    assert dso.is_gpu_eligible(**DS_OK, conf={"gpu.window-agg.enabled": True}) == (True, "")
+    with pytest.raises(ValueError):
+        options.gpu_enabled({"gpu.window-agg.enabled": "maybe"})
+    assert options.gpu_device({}, 5, 8) == 5 and options.gpu_device({}, 13, 8) == 5
+    assert options.gpu_device({"gpu.window-agg.device": "2"}, 13, 8) == 2

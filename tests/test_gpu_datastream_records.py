@@ -139,3 +139,40 @@ def test_datastream_records_match_reference_shape(case):
     assert not op._retained, "first elements still retained after every window was cleared"
     assert op.num_late_records_dropped == o.late_dropped
     op.close()
+
+
+@pytest.mark.parametrize("agg,vcol", [(("maxBy", "LONG"), 2), (("minBy", "LONG", False), 2),
+                                      (("maxBy", "DOUBLE", False), 3), (("minBy", "DOUBLE"), 3)],
+                         ids=["maxby_long_first", "minby_long_last", "maxby_double_last", "minby_double_first"])
+def test_by_lock_worst_case_one_key_one_window(agg, vcol):
+    """minBy / maxBy's entry lock at its worst (ComparableAggregator.java:89-96): 2^20 elements of ONE
+    key in ONE window, values with heavy ties (and NaN / +-0.0 for DOUBLE), so every lane of every
+    wave of the merge contends for one LDS entry's lock bit.  The extremal element and its arrival
+    ordinal must equal the oracle's."""
+    from flink_amd.datastream.window_operator import WindowOperator
+    from flink_amd.datastream.windowing import EventTimeTrigger, TumblingEventTimeWindows
+    from oracle.oracle import OracleOperator
+    n = 1 << 20
+    op = WindowOperator(TumblingEventTimeWindows.of(10_000), EventTimeTrigger(), agg, key_type="LONG",
+                        state_capacity=1 << 12, max_batch_rows=n, output_capacity=1 << 12, field=1).open()
+    o = OracleOperator(op.cfg)
+    rng = np.random.default_rng(20 + vcol)
+    k = np.full(n, 4242, dtype=np.int64)
+    t = (T0 + rng.integers(0, 10_000, n)).astype(np.int64)
+    if vcol == 2:
+        v = rng.integers(0, 3, n).astype(np.int64)
+    else:
+        pool = np.array([1.0, 1.0, 2.0, np.nan, 0.0, -0.0, -5.0], dtype=np.float64).view(np.int64)
+        v = pool[rng.integers(0, len(pool), n)]
+    seq = op.handle.push_seq
+    recs = [(4242, int(v[i]) if vcol == 2 else float(np.int64(v[i]).view(np.float64)), i) for i in range(n)]
+    op.process_batch(k, t, v, records=recs)
+    o.process_batch(k, t, [v])
+    got = op.process_watermark(T0 + 10_000)
+    o.process_watermark(T0 + 10_000)
+    want = o.results(clear=True)
+    assert len(got["key"]) == 1 and len(want["key"]) == 1
+    assert got["first_ord"].tolist() == want["first_ord"].tolist(), "arg element's arrival ordinal"
+    assert _canon(got["value"][0], vcol == 3) == _canon(want["values"][0][0], vcol == 3)
+    assert got["records"][0][2] == int(want["first_ord"][0]) - (seq << 32), "the record is the arg element"
+    op.close()

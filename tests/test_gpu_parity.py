@@ -890,3 +890,43 @@ def test_skipped_advance_keeps_watermark_through_snapshot():
     assert wm == t0 + 12_345
     for x in (g, h):
         x.close()
+
+
+@pytest.mark.parametrize("layout", ["runs", "cells"])
+def test_restore_into_same_handle_drops_pending_pushes(layout, monkeypatch):
+    """A restore drops the pushes still pending in the handle (the reference restores into a fresh
+    operator: nothing buffered survives).  With runs, the dropped push's sub-run fill counters must
+    go too, or the next flush folds its stale rows."""
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    monkeypatch.setenv("FW_RUNS", "1" if layout == "runs" else "0")
+    kw = CASES["sql_tumble_int_aggs"]
+    cfg = _cfg(kw)
+    batches = _stream(4242, 120_000, 3000, ooo=2500, step_ms=3000, n_wm=6)
+    o, g = OracleOperator(cfg), WindowAggHandle(cfg)
+
+    def step(bi, push_oracle=True):
+        k, t, iv, dv, wm = batches[bi]
+        vals = [iv, dv.view(np.int64)]
+        g.push_host(k, t, vals)
+        if push_oracle:
+            o.process_batch(k, t, vals)
+
+    for bi in range(3):
+        step(bi)
+        wm = batches[bi][4]
+        o.process_watermark(wm)
+        g.advance(wm)
+        _compare(_rows(g.results(reset=True), cfg, set()), _rows(o.results(clear=True), cfg, set()), set(), f"batch {bi}")
+    blob = g.snapshot()
+    o.snapshot_restore()
+    step(3, push_oracle=False)  # pending in the handle, then dropped by the restore
+    g.restore(blob)
+    for bi in range(4, 6):
+        step(bi)
+        wm = batches[bi][4]
+        o.process_watermark(wm)
+        g.advance(wm)
+        _compare(_rows(g.results(reset=True), cfg, set()), _rows(o.results(clear=True), cfg, set()), set(), f"batch {bi}")
+    assert g.stats()["error_flags"] == 0
+    g.close()

@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 7
+FW_ABI_VERSION = 8
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -120,7 +120,7 @@ DSW_CONTENTS, DSW_TRIGGER, DSW_CLEANUP = 1, 2, 4
 class fw_ds_window(C.Structure):
     """one (key, window) of a DataStream WindowOperator key group (flinkwin.h fw_ds_snapshot_key_group)"""
     _fields_ = [("key", C.c_int64), ("window_end", C.c_int64), ("value", C.c_int64), ("first_ord", C.c_int64),
-                ("flags", C.c_int32), ("reserved", C.c_int32)]
+                ("flags", C.c_int32), ("key_hash", C.c_int32)]
 
 
 class fw_host_cols(C.Structure):

@@ -2621,8 +2621,10 @@ namespace {
 int ds_state_check(const fw_handle* h) {
     if (h->cfg.api != FW_API_DATASTREAM)
         return fail(FW_E_INVALID, "DataStream key-group windows are the DataStream WindowOperator's state");
-    if (h->cfg.key_hash != FW_KEYHASH_LONG && h->cfg.key_hash != FW_KEYHASH_INT)
-        return fail(FW_E_INVALID, "DataStream key-group windows need LONG or INT keys (a restore re-routes each key)");
+    // LONG / INT keys are re-routed from the key itself; precomputed-hash keys (interned String keys)
+    // from the hash the shim passes with each restored window (fw_ds_window.key_hash)
+    if (h->cfg.key_hash != FW_KEYHASH_LONG && h->cfg.key_hash != FW_KEYHASH_INT && h->cfg.key_hash != FW_KEYHASH_PRECOMPUTED)
+        return fail(FW_E_INVALID, "DataStream key-group windows need LONG, INT or precomputed-hash keys");
     if (h->ad.n != 1) return fail(FW_E_INVALID, "DataStream key-group windows hold one aggregated field");
     return FW_OK;
 }
@@ -2705,7 +2707,7 @@ int fw_ds_snapshot_key_group(fw_handle* h, int32_t key_group, fw_ds_window* out,
             w.value = (f & F_ACC) ? (int64_t)ds_value_of(h, e + 3) : 0;
             w.first_ord = (f & F_ACC) && h->ad.first_word >= 0 ? (int64_t)e[3 + h->ad.first_word] : -1;
             w.flags = fl;
-            w.reserved = 0;
+            w.key_hash = 0;
         }
         m++;
     }
@@ -2720,6 +2722,8 @@ int fw_ds_restore_key_group(fw_handle* h, int32_t key_group, const fw_ds_window*
     if (rc) return rc;
     const WinDesc& win = h->win;
     const int pwe = h->pwe;
+    if (key_group < h->ks.kg_start || key_group >= h->ks.kg_start + h->ks.n_kg)
+        return fail(FW_E_INVALID, "key group %d is not owned by this subtask", key_group);
     std::vector<uint64_t> ent;
     ent.reserve((size_t)n * pwe);
     for (int64_t i = 0; i < n; i++) {
@@ -2733,13 +2737,24 @@ int fw_ds_restore_key_group(fw_handle* h, int32_t key_group, const fw_ds_window*
             return fail(FW_E_INVALID, "window [%lld, %lld) is not a window of this assigner", (long long)st, (long long)w.window_end);
         if ((w.flags & FW_DSW_CLEANUP) && ds_cleanup_time(win, w.window_end) == INT64_MAX)
             return fail(FW_E_INVALID, "window %lld has no cleanup time but a cleanup timer", (long long)w.window_end);
+        // precomputed-hash keys (a shim's interned String keys): the window's superbucket comes from
+        // the key's hash, routed as the ingest routes the key's records; the sub-bucket rides in the
+        // high half of the flags word like a key-group blob's (fw_restore_key_group)
+        uint64_t sub = 0;
+        if (h->ks.hash_kind == KH_PRE && !h->keyrow) {
+            uint32_t m;
+            const int sb = route_key(h->ks, w.key, w.key_hash, &m);
+            if ((sb >> h->ks.sb_per_kg_log2) != key_group - h->ks.kg_start)
+                return fail(FW_E_INVALID, "window %lld: key hash %d is not in key group %d", (long long)i, w.key_hash, key_group);
+            sub = (uint64_t)(sb & ((1 << h->ks.sb_per_kg_log2) - 1));
+        }
         const size_t at = ent.size();
         ent.resize(at + pwe, 0);
         uint64_t* e = ent.data() + at;
         e[0] = (uint64_t)w.key;
         e[1] = (uint64_t)w.window_end;
         e[2] = ((w.flags & FW_DSW_CONTENTS) ? F_ACC : 0u) | ((w.flags & FW_DSW_TRIGGER) ? F_TIMER : 0u) |
-               ((w.flags & FW_DSW_CLEANUP) ? F_CLEAN : 0u);
+               ((w.flags & FW_DSW_CLEANUP) ? F_CLEAN : 0u) | (sub << 32);
         if (w.flags & FW_DSW_CONTENTS) {
             if (h->ad.first_word >= 0 && (w.first_ord < 0 || (w.first_ord >> 32) >= next_push_seq))
                 return fail(FW_E_INVALID, "window %lld: first element ordinal not below push %lld", (long long)i,

@@ -17,8 +17,11 @@ then per registered state in id order writeShort(stateId) and that state's key-g
 The device side (flinkwin.h fw_ds_snapshot_key_group / fw_ds_restore_key_group) moves one record per
 (key, window): its field value, its first element's arrival ordinal and which timers it holds; the
 operator shim keeps the first elements themselves (window_operator.py), so the bytes are assembled
-here.  No Flink build runs in this image: the byte layout follows the Java writers cited above and is
-parity unpinned; tests check the contents against the oracle's keyed state and the restore.
+here.  Byte parity is pinned by the reference's own heap-backend snapshot of this operator
+(WindowOperatorMigrationTest.java:365-443, String keys, Tuple2<String, Integer> records;
+tests/golden/heap_ds_reduce_event_time_flink2.2.json): parsed, then written back byte for byte
+(tests/test_ds_heap_format.py), and restored into the GPU operator, which continues with the
+reference test's own expected records (tests/test_gpu_ds_heap_key_group.py).
 """
 import struct
 
@@ -167,47 +170,72 @@ class TupleSerializer:       # TupleSerializer.serialize (:135-144): the fields 
         return TupleSerializer([m[t]() for t in types])
 
 
-KEY_SERIALIZERS = {"LONG": LongSerializer(), "INT": IntSerializer()}
+# StringSerializer keys: WindowedStream over keyBy(String field), e.g. the reference's own
+# WindowOperatorMigrationTest (Tuple2<String, Integer> keyed by f0)
+KEY_SERIALIZERS = {"LONG": LongSerializer(), "INT": IntSerializer(), "STRING": StringSerializer()}
+
+
+def java_string_hash(s):
+    """String.hashCode (JLS): s[0]*31^(n-1) + ... + s[n-1] over the UTF-16 code units, int32 wrap"""
+    h = 0
+    for u in np.frombuffer(str(s).encode("utf-16-le"), np.uint16).tolist():
+        h = (31 * h + u) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= 1 << 31 else h
 
 
 # ---- key-group bytes ----------------------------------------------------------------------------
-def write_key_group(kg, ids, windows, records, key_ser, value_ser, size, cleanup_time):
-    """windows: DS_WINDOW_DTYPE rows; records[i]: the state value (record) of windows[i] when it holds
-    contents.  ids = (window-contents, event window-timers, processing window-timers) state ids."""
+def write_key_group_entries(kg, ids, contents, timers, key_ser, value_ser, state_order=None):
+    """The key group's bytes from explicit entry lists, written in list order: contents [(key, start,
+    end, record)] and event timers [(ts, key, start, end)].  The reference writes its states in the
+    iteration order of a HashMap over StateUID (HeapSnapshotStrategy.java:161-172: the order varies with
+    the JVM's enum identity hashes), the window-contents entries in CopyOnWriteStateMap bucket order and
+    the timers in heap-array order; none of those orders carries meaning (the restore reads any), so
+    ``state_order`` (default: id order) and the list orders are the caller's choice."""
     out = _Out()
     out.i32(kg)
-    contents = [(int(w["key"]), int(w["window_end"]), r) for w, r in zip(windows, records)
-                if int(w["flags"]) & abi.DSW_CONTENTS]
-    timers = set()
-    for w in windows:
-        key, end, fl = int(w["key"]), int(w["window_end"]), int(w["flags"])
-        if fl & abi.DSW_TRIGGER:
-            timers.add((end - 1, key, end))
-        if fl & abi.DSW_CLEANUP:
-            timers.add((cleanup_time(end), key, end))
-    for sid in sorted(ids):
+    for sid in (state_order if state_order is not None else sorted(ids)):
         out.i16(sid)
         if sid == ids[0]:
             out.i32(len(contents))
-            for key, end, rec in contents:
-                out.i64(end - size)
+            for key, start, end, rec in contents:
+                out.i64(start)
                 out.i64(end)
                 key_ser.serialize(key, out)
                 value_ser.serialize(rec, out)
         elif sid == ids[1]:
             out.i32(len(timers))
-            for ts, key, end in sorted(timers):
+            for ts, key, start, end in timers:
                 out.u64(ts ^ _FLIP)  # MathUtils.flipSignBit
                 key_ser.serialize(key, out)
-                out.i64(end - size)
+                out.i64(start)
                 out.i64(end)
-        else:
+        elif sid == ids[2]:
             out.i32(0)  # event-time windows register no processing-time timers
+        else:
+            raise ValueError(f"state id {sid} is not one of {ids}")
     return bytes(out.b)
 
 
-def read_key_group(blob, ids, key_ser, value_ser):
-    """-> (key_group, contents [(key, start, end, record)], event timers [(ts, key, start, end)])"""
+def write_key_group(kg, ids, windows, records, key_ser, value_ser, size, cleanup_time, key_of=None):
+    """windows: DS_WINDOW_DTYPE rows; records[i]: the state value (record) of windows[i] when it holds
+    contents.  ids = (window-contents, event window-timers, processing window-timers) state ids.
+    key_of: the key object of a device key (a String key's interned id -> the String; default int)."""
+    key_of = key_of or int
+    contents = [(key_of(int(w["key"])), int(w["window_end"]) - size, int(w["window_end"]), r)
+                for w, r in zip(windows, records) if int(w["flags"]) & abi.DSW_CONTENTS]
+    timers = set()
+    for w in windows:
+        key, end, fl = key_of(int(w["key"])), int(w["window_end"]), int(w["flags"])
+        if fl & abi.DSW_TRIGGER:
+            timers.add((end - 1, key, end - size, end))
+        if fl & abi.DSW_CLEANUP:
+            timers.add((cleanup_time(end), key, end - size, end))
+    return write_key_group_entries(kg, ids, contents, sorted(timers), key_ser, value_ser)
+
+
+def read_key_group(blob, ids, key_ser, value_ser, order=None):
+    """-> (key_group, contents [(key, start, end, record)], event timers [(ts, key, start, end)]), each
+    in the blob's order; ``order`` (a list) receives the state ids in the order the blob holds them"""
     inp = _In(blob)
     kg = inp.i32()
     contents, timers, seen = [], [], set()
@@ -217,6 +245,8 @@ def read_key_group(blob, ids, key_ser, value_ser):
         if sid in seen or sid not in ids:
             raise ValueError(f"unexpected state id {sid} in key group {kg}")
         seen.add(sid)
+        if order is not None:
+            order.append(sid)
         for _ in range(n):
             if sid == ids[0]:
                 st, end = inp.i64(), inp.i64()
@@ -233,9 +263,10 @@ def read_key_group(blob, ids, key_ser, value_ser):
     return kg, contents, timers
 
 
-def windows_of(contents, timers, size, cleanup_time, field_bits, first_ord0):
+def windows_of(contents, timers, size, cleanup_time, field_bits, first_ord0, key_id=None):
     """heap contents + timers -> DS_WINDOW_DTYPE rows (first elements numbered from first_ord0) and
-    the records they retain"""
+    the records they retain.  key_id: key object -> (device key, key hash) for keys the device does not
+    hash itself (a String key: its interned id and String.hashCode); default: the key is the device key."""
     rows = {}
     for key, st, end, rec in contents:
         if end - st != size:
@@ -256,7 +287,8 @@ def windows_of(contents, timers, size, cleanup_time, field_bits, first_ord0):
     out = np.zeros(len(rows), DS_WINDOW_DTYPE)
     kept = {}
     for i, ((key, end), (fl, rec)) in enumerate(sorted(rows.items(), key=lambda kv: kv[0])):
-        out[i]["key"], out[i]["window_end"], out[i]["flags"] = key, end, fl
+        dk, kh = key_id(key) if key_id is not None else (key, 0)
+        out[i]["key"], out[i]["key_hash"], out[i]["window_end"], out[i]["flags"] = dk, kh, end, fl
         out[i]["first_ord"] = -1
         if rec is not None:
             o = first_ord0 + len(kept)

@@ -39,7 +39,11 @@ from .windowing import EventTimeTrigger, SlidingEventTimeWindows, TumblingEventT
 _AGG = {"sum": abi.AGG_SUM, "min": abi.AGG_MIN, "max": abi.AGG_MAX, "count": abi.AGG_COUNT_STAR,
         "minBy": abi.AGG_MINBY, "maxBy": abi.AGG_MAXBY}
 _BY = ("minBy", "maxBy")
-_KEY = {"LONG": abi.KEYHASH_LONG, "INT": abi.KEYHASH_INT, "HOST_HASHED": abi.KEYHASH_PRECOMPUTED}
+# STRING keys (keyBy a String field): the operator interns each String to a dense int64 id -- the
+# device key -- and hands the device its String.hashCode, which routes it exactly as
+# KeyGroupRangeAssignment.assignToKeyGroup(key) does (FW_KEYHASH_PRECOMPUTED)
+_KEY = {"LONG": abi.KEYHASH_LONG, "INT": abi.KEYHASH_INT, "HOST_HASHED": abi.KEYHASH_PRECOMPUTED,
+        "STRING": abi.KEYHASH_PRECOMPUTED}
 _TYPE = {"LONG": abi.T_I64, "INT": abi.T_I32, "DOUBLE": abi.T_F64}
 
 
@@ -116,6 +120,7 @@ class WindowOperator:
         self._pending = {}   # push_seq -> records of that push (not yet flushed into state)
         self._retained = {}  # arrival ordinal -> [record, windows whose first element it is]
         self._wm = -(1 << 63)
+        self._kid, self._kstr, self._khash = {}, [], []  # STRING keys: String <-> device id, hashCode
 
     def open(self):
         self.handle = WindowAggHandle(self.cfg)
@@ -126,14 +131,36 @@ class WindowOperator:
             self.handle.close()
             self.handle = None
 
+    def _intern(self, key):
+        """STRING key -> (device id, String.hashCode)"""
+        i = self._kid.get(key)
+        if i is None:
+            i = self._kid[key] = len(self._kstr)
+            self._kstr.append(key)
+            self._khash.append(heap_state.java_string_hash(key))
+        return i, self._khash[i]
+
+    def _key_objects(self, ids):
+        """device keys -> the operator's keys (the Strings of a STRING-keyed operator)"""
+        if self.key_type != "STRING":
+            return ids
+        return np.array([self._kstr[int(i)] for i in ids], dtype=object)
+
     def process_batch(self, keys, timestamps, values, key_hashes=None, records=None):
         """processElement for a batch; ``records``: the elements themselves (record-shaped
-        operator), kept until the device says which ones are first elements of a window."""
+        operator), kept until the device says which ones are first elements of a window.  A
+        STRING-keyed operator takes its keys as Python strings."""
         seq0 = self.handle.push_seq
+        if self.key_type == "STRING":
+            pairs = [self._intern(str(k)) for k in keys]
+            keys = np.array([p[0] for p in pairs], dtype=np.int64)
+            key_hashes = np.array([p[1] for p in pairs], dtype=np.int32)
         self.handle.push_host(keys, timestamps, [values], key_hashes)
         self._keep(seq0, records, len(keys))
 
     def process_batch_device(self, keys, timestamps, values, key_hashes=None, records=None):
+        if self.key_type == "STRING":
+            raise ValueError("a STRING-keyed operator interns its keys on the host (process_batch)")
         seq0 = self.handle.push_seq
         self.handle.push_device(keys, timestamps, [values], key_hashes)
         self._keep(seq0, records, keys.numel())
@@ -177,7 +204,7 @@ class WindowOperator:
         a record-shaped operator, "records": value1.copy() with the aggregated field set)."""
         self.handle.advance(watermark)
         r = self.handle.results(reset=True)
-        out = {"key": r["key"], "value": r["values"][0], "timestamp": r["window_end"] - 1,
+        out = {"key": self._key_objects(r["key"]), "value": r["values"][0], "timestamp": r["window_end"] - 1,
                "window_start": r["window_start"], "window_end": r["window_end"],
                "values": r["values"], "null_mask": r["null_mask"]}
         if self.field is not None:
@@ -204,7 +231,7 @@ class WindowOperator:
         """Records routed to the late-data side output since the last call
         (WindowOperator.sideOutput): {key, timestamp, value, push_seq, row}."""
         r = self.handle.late_records()
-        return {"key": r["key"], "timestamp": r["ts"], "value": r["values"][0], "push_seq": r["push_seq"],
+        return {"key": self._key_objects(r["key"]), "timestamp": r["ts"], "value": r["values"][0], "push_seq": r["push_seq"],
                 "row": r["row"]}
 
     def snapshot_state(self) -> bytes:
@@ -237,7 +264,7 @@ class WindowOperator:
         if self.field is None:
             raise ValueError("the heap key-group format holds records: a record-shaped operator (field=...) is needed")
         if self.key_type not in heap_state.KEY_SERIALIZERS:
-            raise ValueError(f"the heap key-group format needs LONG or INT keys, not {self.key_type}")
+            raise ValueError(f"the heap key-group format needs LONG, INT or STRING keys, not {self.key_type}")
         ser = record_serializer or self.record_serializer
         if ser is None:
             raise ValueError("no record serializer (record_serializer=...)")
@@ -261,7 +288,9 @@ class WindowOperator:
                 recs.append(first if by else tuple(first[:f]) + (v,) + tuple(first[f + 1:]))
             else:
                 recs.append(None)
-        return heap_state.write_key_group(key_group, ids, w, recs, kser, vser, self.assigner.size, self._cleanup_time)
+        key_of = (lambda i: self._kstr[i]) if self.key_type == "STRING" else None
+        return heap_state.write_key_group(key_group, ids, w, recs, kser, vser, self.assigner.size, self._cleanup_time,
+                                          key_of=key_of)
 
     def restore_key_group_heap(self, blob: bytes, ids=(0, 1, 2), record_serializer=None):
         """Adds one key group written in the heap backend's bytes (by this operator or a heap-backend
@@ -279,7 +308,9 @@ class WindowOperator:
             return int(v)
 
         base = self.handle.push_seq
-        w, kept = heap_state.windows_of(contents, timers, self.assigner.size, self._cleanup_time, field_bits, base << 32)
+        key_id = (lambda k: self._intern(str(k))) if self.key_type == "STRING" else None
+        w, kept = heap_state.windows_of(contents, timers, self.assigner.size, self._cleanup_time, field_bits, base << 32,
+                                        key_id=key_id)
         self.handle.ds_restore_key_group_windows(kg, w, base + 1)
         for o, rec in kept.items():
             self._retained[o] = [rec, 1]
@@ -296,4 +327,4 @@ class WindowOperator:
             vals = vals.view(np.float64)
         elif ftype == "INT" and fn != "count":
             vals = vals.astype(np.int32)
-        return [(int(k), v.item(), int(t)) for k, v, t in zip(res["key"], vals, res["timestamp"])]
+        return [(k if isinstance(k, str) else int(k), v.item(), int(t)) for k, v, t in zip(res["key"], vals, res["timestamp"])]

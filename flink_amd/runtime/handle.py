@@ -11,7 +11,7 @@ from .._native import check, lib
 
 # fw_ds_window (flinkwin.h), one (key, window) of a DataStream key group
 DS_WINDOW_DTYPE = np.dtype([("key", np.int64), ("window_end", np.int64), ("value", np.int64),
-                            ("first_ord", np.int64), ("flags", np.int32), ("reserved", np.int32)])
+                            ("first_ord", np.int64), ("flags", np.int32), ("key_hash", np.int32)])
 
 
 def _np_view(ptr, n, dtype):

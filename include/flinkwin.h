@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 7
+#define FW_ABI_VERSION 8
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -485,7 +485,11 @@ int fw_restore_key_group_heap(fw_handle* h, const void* buf, int64_t size, const
    cleanupTime(window); with allowedLateness 0 both timers are the same one).  fw_ds_snapshot_key_group
    flushes first; out == NULL queries *n.  fw_ds_restore_key_group adds a key group's windows to a
    handle owning it; restored first elements carry caller-chosen ordinals below push
-   next_push_seq, after which the handle's arrival ordinals continue.  LONG / INT keys only. */
+   next_push_seq, after which the handle's arrival ordinals continue.  v8: key_hash -- for a
+   FW_KEYHASH_PRECOMPUTED handle (keys the shim interns, e.g. String keys: key = the interned id,
+   key_hash = String.hashCode) the key's hash, which routes the restored window exactly as the
+   ingest routes the key's records; ignored for LONG / INT keys; 0 on snapshot (the shim knows its
+   keys' hashes). */
 enum { FW_DSW_CONTENTS = 1, FW_DSW_TRIGGER = 2, FW_DSW_CLEANUP = 4 };
 typedef struct {
     int64_t key;
@@ -493,7 +497,7 @@ typedef struct {
     int64_t value;
     int64_t first_ord;
     int32_t flags;
-    int32_t reserved;
+    int32_t key_hash;     /* v8 (was reserved): FW_KEYHASH_PRECOMPUTED handles: the key's hash on restore */
 } fw_ds_window;
 int fw_ds_snapshot_key_group(fw_handle* h, int32_t key_group, fw_ds_window* out, int64_t capacity, int64_t* n);
 int fw_ds_restore_key_group(fw_handle* h, int32_t key_group, const fw_ds_window* in, int64_t n, int64_t next_push_seq);

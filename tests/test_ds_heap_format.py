@@ -2,8 +2,9 @@
 the basic serializers' bytes as the Java writers produce them (LongSerializer / IntSerializer
 big-endian, DoubleSerializer doubleToLongBits, StringValue.writeString's variable-length lengths and
 UTF-16 code units, TupleSerializer's fields in order), TimerSerializer's flipped timestamps, and a
-write -> read round trip of one key group.  Byte layout restated from the Java writers: parity
-unpinned (no Flink build in this image)."""
+write -> read round trip of one key group.  Byte parity is pinned by the reference's own heap-backend
+snapshot of a WindowOperator (tests/golden/heap_ds_reduce_event_time_flink2.2.json, extracted by
+tests/golden/make_heap_golden.py): parsed, and written back byte for byte.""" 
 import struct
 
 import numpy as np
@@ -85,3 +86,56 @@ def test_key_group_write_read_round_trip():
         hs.read_key_group(blob, (6, 1, 2), hs.LongSerializer(), ser)  # unknown state id
     with pytest.raises(ValueError):  # a timer that is neither the trigger nor the cleanup time
         hs.windows_of([], [(1234, 7, 0, 3000)], size, cleanup, lambda r: 0, 0)
+
+
+def _reference_fixture():
+    import json
+    import os
+    p = os.path.join(os.path.dirname(__file__), "golden", "heap_ds_reduce_event_time_flink2.2.json")
+    with open(p) as f:
+        fx = json.load(f)
+    ids = fx["state_ids"]
+    # (window-contents, event-time window-timers, processing-time window-timers)
+    order = (ids["window-contents"], ids["_timer_state/event_window-timers"], ids["_timer_state/processing_window-timers"])
+    return fx, order, bytes.fromhex(fx["key_groups"][0]["hex"])
+
+
+def test_reference_heap_snapshot_parses_and_writes_back_byte_for_byte():
+    """The reference's own heap-backend bytes (WindowOperatorMigrationTest.java:365-443, extracted by
+    tests/golden/make_heap_golden.py): a tumbling 3 s WindowOperator whose ReducingState holds
+    Tuple2<String, Integer> sums keyed by the String f0.  read_key_group must find exactly the state the
+    writer left after watermark 1999 (elements of WindowOperatorMigrationTest.java:411-418), and writing
+    those entries back in the blob's own order must reproduce the reference bytes byte for byte -- the
+    StringSerializer keys and records, IntSerializer, TimeWindow.Serializer namespaces, flipped timer
+    timestamps and the per-state framing."""
+    fx, ids, blob = _reference_fixture()
+    kser, vser = hs.KEY_SERIALIZERS["STRING"], hs.TupleSerializer.of("STRING", "INT")
+    order = []
+    kg, contents, timers = hs.read_key_group(blob, ids, kser, vser, order=order)
+    assert kg == fx["key_groups"][0]["key_group"] == 0
+    assert sorted(contents) == [("key1", 0, 3000, ("key1", 3)), ("key2", 0, 3000, ("key2", 3)),
+                                ("key2", 3000, 6000, ("key2", 2))]
+    assert sorted(timers) == [(2999, "key1", 0, 3000), (2999, "key2", 0, 3000), (5999, "key2", 3000, 6000)]
+    assert sorted(order) == sorted(ids)
+    assert hs.write_key_group_entries(kg, ids, contents, timers, kser, vser, state_order=order) == blob
+    # as device windows (String keys interned to ids, routed by String.hashCode), then written back in
+    # the library's canonical order (ids ascending, timers sorted): the same state
+    names = sorted({k for k, *_ in contents})
+    key_id = lambda k: (names.index(k), hs.java_string_hash(k))  # noqa: E731
+    w, kept = hs.windows_of(contents, timers, 3000, lambda end: end - 1, lambda r: r[1], 7 << 32, key_id=key_id)
+    full = abi.DSW_CONTENTS | abi.DSW_TRIGGER | abi.DSW_CLEANUP  # allowedLateness 0: one timer is both
+    assert [(names[int(r["key"])], int(r["window_end"]), int(r["flags"]), int(r["key_hash"])) for r in w] == \
+        [("key1", 3000, full, 3288498), ("key2", 3000, full, 3288499), ("key2", 6000, full, 3288499)]
+    recs = [kept.get(int(r["first_ord"])) for r in w]
+    canon = hs.write_key_group(kg, ids, w, recs, kser, vser, 3000, lambda end: end - 1, key_of=lambda i: names[i])
+    assert len(canon) == len(blob)
+    kg2, c2, t2 = hs.read_key_group(canon, ids, kser, vser)
+    assert (kg2, sorted(c2), sorted(t2)) == (kg, sorted(contents), sorted(timers))
+
+
+def test_java_string_hash():
+    # String.hashCode (JLS 15.8 / java.lang.String): "" -> 0, "a" -> 97, "key1", surrogate pairs as units
+    assert hs.java_string_hash("") == 0 and hs.java_string_hash("a") == 97
+    assert hs.java_string_hash("key1") == 3288498
+    assert hs.java_string_hash("polygenelubricants") == -2147483648  # the classic Integer.MIN_VALUE hash
+    assert hs.java_string_hash("\U0001F600") == 0xD83D * 31 + 0xDE00

@@ -205,3 +205,100 @@ def test_ds_heap_round_trip_and_rejects_bad_input():
         op3.restore_key_group_heap(full[1][:-3], IDS)  # truncated
     for x in (op, op2, op3):
         x.close()
+
+
+def _reference_heap_fixture():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "heap_ds_reduce_event_time_flink2.2.json")) as f:
+        fx = json.load(f)
+    sid = fx["state_ids"]
+    ids = (sid["window-contents"], sid["_timer_state/event_window-timers"], sid["_timer_state/processing_window-timers"])
+    return fx, ids, bytes.fromhex(fx["key_groups"][0]["hex"])
+
+
+def _string_operator(max_p):
+    from flink_amd.datastream.heap_state import TupleSerializer
+    from flink_amd.datastream.window_operator import WindowOperator
+    from flink_amd.datastream.windowing import EventTimeTrigger, TumblingEventTimeWindows
+    return WindowOperator(TumblingEventTimeWindows.of(3000), EventTimeTrigger(), ("sum", "INT"), key_type="STRING",
+                          max_parallelism=max_p, state_capacity=1 << 12, max_batch_rows=1 << 12,
+                          output_capacity=1 << 12, field=1, record_serializer=TupleSerializer.of("STRING", "INT")).open()
+
+
+@pytest.mark.parametrize("extra", [False, True], ids=["reference_continuation", "plus_new_string_key"])
+def test_reference_heap_snapshot_restores_into_gpu_operator(extra):
+    """The reference's own heap-backend key group (WindowOperatorMigrationTest.writeReducingEventTimeWindowsSnapshot
+    :365-443: String keys, Tuple2<String, Integer> sums, max parallelism 1) restored into the GPU operator
+    continues exactly as testRestoreReducingEventTimeWindows (:445-514) asserts: (key1, 3) and (key2, 3) at
+    watermark 2999, nothing at 3999 / 4999, (key2, 2) at 5999.  With ``extra`` a new String key's element
+    arrives after the restore (routed by String.hashCode like the restored windows) and fires with key2's
+    window.  Writing the state back after the first watermark reproduces the reference's remaining entry."""
+    from flink_amd.datastream import heap_state as hs
+    fx, ids, blob = _reference_heap_fixture()
+    op = _string_operator(fx["operator"]["max_parallelism"])
+    assert op.restore_key_group_heap(blob, ids) == 0
+    if extra:
+        op.process_batch(["key3"], np.array([4500], np.int64), np.array([1], np.int64), records=[("key3", 1)])
+    for wm, want in fx["continuation"]:
+        got = op.process_watermark(wm)
+        recs = sorted((r[0], r[1], int(t)) for r, t in zip(got["records"], got["timestamp"]))
+        want = sorted(tuple(x) for x in want) + ([("key3", 1, 5999)] if extra and wm == 5999 else [])
+        assert recs == sorted(want), f"watermark {wm}"
+        assert all(isinstance(k, str) for k in got["key"])
+        if wm == 2999 and not extra:  # left: key2's [3000, 6000) with its timer, as the reference holds it
+            kser, vser = hs.KEY_SERIALIZERS["STRING"], hs.TupleSerializer.of("STRING", "INT")
+            _, contents, timers = hs.read_key_group(op.snapshot_key_group_heap(0, ids), ids, kser, vser)
+            assert contents == [("key2", 3000, 6000, ("key2", 2))]
+            assert timers == [(5999, "key2", 3000, 6000)]
+    assert op.handle.stats()["live_state_entries"] == 0
+    assert not op._retained
+    op.close()
+
+
+def test_string_keys_route_by_java_hash_across_subtasks():
+    """STRING keys at max parallelism 128 over 3 subtasks: a key group written by one STRING-keyed operator
+    restores only into the subtask owning it (computeKeyGroupRangeForOperatorIndex), where the keys' windows
+    land by String.hashCode and fire with their sums."""
+    from flink_amd.datastream.heap_state import TupleSerializer, java_string_hash
+    from flink_amd.datastream.window_operator import WindowOperator
+    from flink_amd.datastream.windowing import EventTimeTrigger, TumblingEventTimeWindows
+    from flink_amd import _native
+    import ctypes as C
+
+    def op(p=1, i=0):
+        return WindowOperator(TumblingEventTimeWindows.of(3000), EventTimeTrigger(), ("sum", "INT"), key_type="STRING",
+                              parallelism=p, subtask_index=i, state_capacity=1 << 14, max_batch_rows=1 << 14,
+                              output_capacity=1 << 14, field=1, record_serializer=TupleSerializer.of("STRING", "INT")).open()
+    rng = np.random.default_rng(5)
+    names = [f"user-{i}-é" for i in range(300)]
+    keys = [names[j] for j in rng.integers(0, len(names), 4000)]
+    ts = (T0 + rng.integers(0, 3000, 4000)).astype(np.int64)
+    vals = rng.integers(0, 100, 4000).astype(np.int64)
+    a = op()
+    a.process_batch(keys, ts, vals, records=[(k, int(v)) for k, v in zip(keys, vals)])
+    a.process_watermark(T0 - 1)
+    kg_of = {}
+    for n in set(keys):
+        kg_of[n] = _native.lib().fw_host_key_group(abi.KEYHASH_PRECOMPUTED, 0, java_string_hash(n), 128)
+    want = {}
+    for k, v in zip(keys, vals):
+        want[k] = want.get(k, 0) + int(v)
+    blobs = {kg: a.snapshot_key_group_heap(kg) for kg in sorted(set(kg_of.values()))}
+    got = {}
+    for i in range(3):
+        b = op(3, i)
+        for kg, blob in blobs.items():
+            lo, hi = (i * 128 + 2) // 3, ((i + 1) * 128 - 1) // 3
+            if lo <= kg <= hi:
+                b.restore_key_group_heap(blob)
+            else:
+                with pytest.raises(Exception):
+                    b.restore_key_group_heap(blob)
+        r = b.process_watermark(T0 + 2999)
+        for rec in r["records"]:
+            assert rec[0] not in got
+            got[rec[0]] = rec[1]
+        b.close()
+    a.close()
+    assert got == want

@@ -245,9 +245,10 @@ def main():
         k, t, v = ex.exchange(gk[b], gt[b], [gv[b]] if nv else [])
         return k, t, (v[0] if nv else None)
 
-    # the timed keyBy exchange is the packed padded one: segments of the batch's even share + 25 %
-    # (KeyByExchange.segment_capacity, from the batch itself), rows past a segment in an overflow
-    # round; the overflow decision and the watermark valve share one host all-reduce per step
+    # the timed keyBy exchange is the packed padded one: segments of the previous step's agreed
+    # largest per-destination share + 3 % (KeyByExchange.headroom; the first step: the batch's even
+    # share + 25 %), rows past a segment in an overflow round; the overflow decision, the next share
+    # and the watermark valve share one all-reduce per step
     def push_step(b, handle):
         """Ingest step b; returns the watermark to advance to (the valve's minimum over subtasks)."""
         if world == 1:
@@ -597,10 +598,12 @@ def main():
                                                   "(fw_results_device)",
                                        "discard": "dropped (fw_results_reset)"}[args.sink],
                        "exchange": None if world == 1 else {
-                           "kind": "packed padded all-to-all, segments of the batch's even share + 25 %",
+                           "kind": "packed padded all-to-all, segments of the previous step's agreed largest "
+                                   "share + 3 % (first step: even share + 25 %)",
                            "watermark_valve": ("device all-reduce (overflow, watermark, share) -> fw_advance_device"
                                                if args.valve == "device" else "host gloo all-reduce"),
-                           "segment_rows": ex.segment_capacity(B, world),
+                           "segment_rows_first_step": ex.segment_capacity(B, world),
+                           "agreed_share_rows": ex._dn_share if ex._share_known else None,
                            "overflow_rounds": ex.spill_rounds}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,

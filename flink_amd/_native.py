@@ -40,6 +40,7 @@ def lib():
         "fw_destroy": (i32, [vp]),
         "fw_last_error": (C.c_char_p, []),
         "fw_abi_version": (i32, []),
+        "fw_device_count": (i32, []),
         "fw_get_stream": (vp, [vp]),
         "fw_sync": (i32, [vp]),
         "fw_initialize_watermark": (i32, [vp, i64]),
@@ -101,7 +102,7 @@ def lib():
 
 
 # every symbol the public header declares (tests check they are exported)
-EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_get_stream", "fw_sync",
+EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_device_count", "fw_get_stream", "fw_sync",
             "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance", "fw_advance_device",
             "fw_flush", "fw_results", "fw_results_reset", "fw_results_async", "fw_results_ready", "fw_results_device", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",

@@ -49,6 +49,9 @@ KEYHASH_BINROW_INT = 3
 KEYHASH_PRECOMPUTED = 4
 KEYHASH_KEYROW = 5
 
+# fw_stats.error_flags bits (FW_ERRF_*)
+ERRF = {"CHUNKS": 1, "STATE": 2, "OUTPUT": 4, "TREQ": 8, "KEYGROUP": 16, "LATE": 32, "ORDEV": 64, "KEYROW": 128}
+
 # fw_key_field_kind (key-row fields for fw_key_row_hash)
 KF_STRING, KF_FIXED1, KF_FIXED2, KF_FIXED4, KF_FIXED8 = 0, 1, 2, 4, 8
 FW_MAX_KEY_FIELDS = 8

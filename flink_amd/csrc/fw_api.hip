@@ -211,8 +211,15 @@ struct fw_handle {
     uint8_t* d_nul[2][FW_MAX_COLS] = {};
     int64_t reserved = -1;
 
-    // asynchronous result delivery (fw_results_async / fw_results_ready): rows compacted straight
-    // into one of two pinned, device-mapped host buffers
+    // asynchronous result delivery (fw_results_async / fw_results_ready): rows compacted on the
+    // device into one of two device buffers (ard_*), then moved by DMA (hipMemcpyAsync on the D2H
+    // stream) into pinned host buffers (ar_*); only the row count goes through mapped memory
+    int64_t* ard_key[2] = {};
+    int64_t* ard_ws[2] = {};
+    int64_t* ard_we[2] = {};
+    uint64_t* ard_val[2][FW_MAX_AGGS] = {};
+    uint32_t* ard_null[2] = {};
+    hipStream_t d2h_stream = nullptr;
     int64_t* ar_key[2] = {};
     int64_t* ar_ws[2] = {};
     int64_t* ar_we[2] = {};
@@ -220,6 +227,7 @@ struct fw_handle {
     uint32_t* ar_null[2] = {};
     int64_t* ar_n[2] = {};          // row count (written by the compaction kernel)
     hipEvent_t ar_ev[2] = {};
+    bool ar_copied[2] = {};         // fw_results_ready already moved buffer b's rows to the host
     int ar_cur = 0;                 // buffer of the next fw_results_async
     int ar_last = -1;               // buffer of the last one (-1: none)
     bool ar_empty[2] = {};          // that call had nothing to collect
@@ -629,11 +637,11 @@ int validate_and_plan(fw_handle* h) {
         const char* re = getenv("FW_RUNS");
         const int n_isb = ks.n_sb >> ks.pass_log2;
         const int blk = ig_block(h->nw_t, ig_nv(h->nv)), rpt = ig_rpt(h->nw_t, ig_nv(h->nv));
-        // measured per step: CFG4 (TUMBLE, two words) +2-4%, CFG2 (TUMBLE, one word) within
-        // noise, CFG3 (HOP) -5%, CFG5 (CUMULATE) -3% -- the ingest's scattered stretch stores cost more
-        // than the merge saves unless the rows are wide; planned for TUMBLE with >= 2 words, FW_RUNS=1
-        // plans them everywhere
-        const bool want = re ? atoi(re) != 0 : (c.window_kind == FW_WIN_TUMBLE && c.api == FW_API_SQL && h->nw_t >= 2);
+        // measured per step: CFG4 (TUMBLE, two words) +2-4%, CFG2 (TUMBLE, one word) +1.5%
+        // with its one-block runs gather (round 5: ingest +11 us, merge -14 us), CFG3 (HOP) -5%, CFG5
+        // (CUMULATE) -3% -- the ingest's scattered stretch stores cost more than the merge saves there;
+        // planned for SQL TUMBLE, FW_RUNS=1 plans them everywhere
+        const bool want = re ? atoi(re) != 0 : (c.window_kind == FW_WIN_TUMBLE && c.api == FW_API_SQL);
         if (!h->keyrow && ks.pass_log2 == 0 && ig_runs_fit(n_isb, blk, rpt, h->nw_t) && want) {
             const int64_t subs = (int64_t)n_isb * RUN_X;
             const int64_t sc = ((h->cap_rows * 5 / 4 + subs - 1) / subs + 16 + 15) / 16 * 16;
@@ -687,9 +695,25 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->slot_base, FW_MAX_PENDING))) return rc;
     if (h->narrow && (rc = dalloc(&h->ranks, (size_t)FW_MAX_PENDING * h->cap_rows))) return rc;
     if (h->run_rows) {
+        // the runs layout is a plan, not a requirement: FW_MAX_PENDING * run_rows partial rows (about
+        // 1.25x the partial buffer) on top of it.  When the device cannot hold them the handle keeps
+        // the cell layout instead of failing fw_create.
         const size_t n_isb = (size_t)(h->ks.n_sb >> h->ks.pass_log2);
-        if ((rc = dalloc(&h->runs, (size_t)FW_MAX_PENDING * h->run_rows * PW))) return rc;
-        if (h->narrow && (rc = dalloc(&h->run_ranks, (size_t)FW_MAX_PENDING * h->run_rows))) return rc;
+        void* r = nullptr;
+        void* rr = nullptr;
+        if (hipMalloc(&r, (size_t)FW_MAX_PENDING * h->run_rows * PW * sizeof(uint64_t)) != hipSuccess ||
+            (h->narrow && hipMalloc(&rr, (size_t)FW_MAX_PENDING * h->run_rows) != hipSuccess)) {
+            (void)hipGetLastError();
+            if (r) hipFree(r);
+            h->run_rows = 0;
+            h->sub_cap = 0;
+        } else {
+            h->runs = (uint64_t*)r;
+            h->run_ranks = (uint8_t*)rr;
+        }
+    }
+    if (h->run_rows) {
+        const size_t n_isb = (size_t)(h->ks.n_sb >> h->ks.pass_log2);
         if ((rc = dalloc(&h->run_fill, (size_t)FW_MAX_PENDING * RUN_X * n_isb))) return rc;
         if ((rc = dalloc(&h->run_ovf, (size_t)FW_MAX_PENDING * n_isb))) return rc;
         if ((rc = dalloc(&h->slot_fmt, FW_MAX_PENDING))) return rc;
@@ -798,15 +822,23 @@ int alloc_staging(fw_handle* h) {
 int alloc_async_results(fw_handle* h) {
     if (h->ar_n[0]) return FW_OK;
     const size_t n = (size_t)h->out_cap;
-    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    int rc;
+    HIP_TRY(hipStreamCreateWithFlags(&h->d2h_stream, hipStreamNonBlocking));
     for (int b = 0; b < 2; b++) {
-        HIP_TRY(hipHostMalloc((void**)&h->ar_key[b], n * 8, fl));
-        HIP_TRY(hipHostMalloc((void**)&h->ar_ws[b], n * 8, fl));
-        HIP_TRY(hipHostMalloc((void**)&h->ar_we[b], n * 8, fl));
-        HIP_TRY(hipHostMalloc((void**)&h->ar_null[b], n * 4, fl));
-        for (int g = 0; g < h->n_out; g++) HIP_TRY(hipHostMalloc((void**)&h->ar_val[b][g], n * 8, fl));
-        HIP_TRY(hipHostMalloc((void**)&h->ar_n[b], 8, fl));
+        // plain pinned buffers: the rows arrive by DMA, not by kernel stores over PCIe
+        HIP_TRY(hipHostMalloc((void**)&h->ar_key[b], n * 8, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_ws[b], n * 8, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_we[b], n * 8, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_null[b], n * 4, hipHostMallocDefault));
+        for (int g = 0; g < h->n_out; g++) HIP_TRY(hipHostMalloc((void**)&h->ar_val[b][g], n * 8, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_n[b], 8, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipEventCreateWithFlags(&h->ar_ev[b], hipEventDisableTiming));
+        if ((rc = dalloc(&h->ard_key[b], n))) return rc;
+        if ((rc = dalloc(&h->ard_ws[b], n))) return rc;
+        if ((rc = dalloc(&h->ard_we[b], n))) return rc;
+        if ((rc = dalloc(&h->ard_null[b], n))) return rc;
+        for (int g = 0; g < h->n_out; g++)
+            if ((rc = dalloc(&h->ard_val[b][g], n))) return rc;
     }
     return FW_OK;
 }
@@ -1061,6 +1093,12 @@ extern "C" {
 const char* fw_last_error(void) { return g_err.c_str(); }
 int fw_abi_version(void) { return FW_ABI_VERSION; }
 
+int fw_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
 int fw_create(const fw_config* cfg, fw_handle** out) {
     if (!cfg || !out) return fail(FW_E_INVALID, "null argument");
     *out = nullptr;
@@ -1162,7 +1200,13 @@ int fw_destroy(fw_handle* h) {
         for (int g = 0; g < FW_MAX_AGGS; g++) hipHostFree(h->ar_val[b][g]);
         hipHostFree(h->ar_n[b]);
         if (h->ar_ev[b]) hipEventDestroy(h->ar_ev[b]);
+        hipFree(h->ard_key[b]);
+        hipFree(h->ard_ws[b]);
+        hipFree(h->ard_we[b]);
+        hipFree(h->ard_null[b]);
+        for (int g = 0; g < FW_MAX_AGGS; g++) hipFree(h->ard_val[b][g]);
     }
+    if (h->d2h_stream) hipStreamDestroy(h->d2h_stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
     delete h->timer;
     if (h->stream) hipStreamDestroy(h->stream);
@@ -1485,6 +1529,7 @@ int fw_results_async(fw_handle* h) {
     h->ar_cur ^= 1;
     h->ar_last = b;
     h->ar_empty[b] = h->reset_pending;  // consumed and nothing emitted since
+    h->ar_copied[b] = false;
     if (h->ar_empty[b]) return FW_OK;
     CompactArgs ca{};
     ca.ctrl = h->ctrl;
@@ -1499,16 +1544,15 @@ int fw_results_async(fw_handle* h) {
     ca.out_null = h->out_null;
     for (int g = 0; g < h->n_out; g++) {
         ca.out_val[g] = h->out_val[g];
-        ca.res_val[g] = mapped(h->ar_val[b][g]);
+        ca.res_val[g] = h->ard_val[b][g];
     }
-    ca.res_key = mapped(h->ar_key[b]);
-    ca.res_ws = mapped(h->ar_ws[b]);
-    ca.res_we = mapped(h->ar_we[b]);
-    ca.res_null = mapped(h->ar_null[b]);
+    ca.res_key = h->ard_key[b];
+    ca.res_ws = h->ard_ws[b];
+    ca.res_we = h->ard_we[b];
+    ca.res_null = h->ard_null[b];
     ca.res_cap = h->out_cap;
     ca.host_n = mapped(h->ar_n[b]);
-    if (!ca.res_key || !ca.res_ws || !ca.res_we || !ca.res_null || !ca.host_n)
-        return fail(FW_E_DEVICE, "mapped result buffers unavailable");
+    if (!ca.host_n) return fail(FW_E_DEVICE, "mapped result count unavailable");
     HIP_TRY(launch_compact(ca, h->stream, h->timer));
     HIP_TRY(hipEventRecord(h->ar_ev[b], h->stream));
     h->reset_pending = true;  // the rows are collected: the next merge launch starts the slabs afresh
@@ -1585,13 +1629,24 @@ int fw_results_ready(fw_handle* h, fw_result* out) {
     const int b = h->ar_last;
     if (b < 0) return fail(FW_E_STATE, "fw_results_ready without fw_results_async");
     if (h->ar_empty[b]) return FW_OK;
-    HIP_TRY(hipEventSynchronize(h->ar_ev[b]));
+    HIP_TRY(hipEventSynchronize(h->ar_ev[b]));  // the compaction (long done: it ran a step ago)
     const int64_t n = __atomic_load_n(h->ar_n[b], __ATOMIC_ACQUIRE);
     if (n > h->out_cap)
         return fail(FW_E_CAPACITY, "%lld result rows exceed output_capacity %lld (read results more often)",
                     (long long)n, (long long)h->out_cap);
     const int na = h->n_out;
     const int nv = h->ad.first_word >= 0 ? na - 1 : na;
+    if (n > 0 && !h->ar_copied[b]) {  // the rows by DMA on the D2H stream (no CU time, no operator-stream slot)
+        hipStream_t ds = h->d2h_stream;
+        HIP_TRY(hipMemcpyAsync(h->ar_key[b], h->ard_key[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+        HIP_TRY(hipMemcpyAsync(h->ar_ws[b], h->ard_ws[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+        HIP_TRY(hipMemcpyAsync(h->ar_we[b], h->ard_we[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+        HIP_TRY(hipMemcpyAsync(h->ar_null[b], h->ard_null[b], (size_t)n * 4, hipMemcpyDeviceToHost, ds));
+        for (int g = 0; g < na; g++)
+            HIP_TRY(hipMemcpyAsync(h->ar_val[b][g], h->ard_val[b][g], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+        HIP_TRY(hipStreamSynchronize(ds));
+        h->ar_copied[b] = true;
+    }
     out->n = n;
     out->key = h->ar_key[b];
     out->window_start = h->ar_ws[b];

@@ -568,20 +568,23 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
                         uint64_t* dst = (dd & RUN_LOCAL) ? out + (size_t)(dd & ~RUN_LOCAL) * P : rslot + (size_t)dd * P;
                         if constexpr (P % 2 == 0) {
 #pragma unroll
-                            for (uint32_t k = 0; k < P / 2; k++) *(ulonglong2*)(dst + 2 * k) = *(const ulonglong2*)(src + 2 * k);
+                            for (uint32_t k = 0; k < P / 2; k++) {
+                                const ulonglong2 x = *(const ulonglong2*)(src + 2 * k);
+                                st_wt16(dst + 2 * k, x.x, x.y);
+                            }
                         } else {
                             uint64_t v[P];
 #pragma unroll
                             for (uint32_t k = 0; k < P; k++) v[k] = src[k];
                             if constexpr (P == 1) {
-                                dst[0] = v[0];
+                                st_wt8(dst, v[0]);
                             } else {  // the lone 8-B word first or last, so the pairs are 16-B aligned
                                 const bool odd = ((uintptr_t)dst & 8) != 0;
-                                *(odd ? dst : dst + (P - 1)) = odd ? v[0] : v[P - 1];
+                                st_wt8(odd ? dst : dst + (P - 1), odd ? v[0] : v[P - 1]);
                                 uint64_t* q = dst + (odd ? 1 : 0);
 #pragma unroll
                                 for (uint32_t k = 0; k < (P - 1) / 2; k++)
-                                    *(ulonglong2*)(q + 2 * k) = make_ulonglong2(odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
+                                    st_wt16(q + 2 * k, odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
                             }
                         }
                     }
@@ -601,9 +604,10 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
             uint64_t* dst = out + (size_t)w0 * PWX;  // 16-B aligned: slot, chunk and window bases are 16-row multiples
             for (uint32_t q = 2 * tid; q < nwords; q += 2 * IG_BLOCK) {
                 if (q + 1 < nwords) {
-                    *(ulonglong2*)(dst + q) = *(const ulonglong2*)(stage + q);
+                    const ulonglong2 x = *(const ulonglong2*)(stage + q);
+                    st_wt16(dst + q, x.x, x.y);
                 } else {
-                    dst[q] = stage[q];
+                    st_wt8(dst + q, stage[q]);
                 }
             }
             if (fmt != PF_WIDE) {

@@ -70,7 +70,11 @@ constexpr int mg_entries(int nw, int kind) {
 // fits beside the entries in a workgroup's LDS, else the largest that does
 constexpr int mg_idx_slots(int nw, int e) {
     const int entry_bytes = 8 + 8 + 4 + 8 * nw + 2;  // key, slice, flag, acc, due
-    const int room = (158 * 1024 / MG_PER_CU - e * entry_bytes) / 4;
+#ifndef FW_LEAN
+#define FW_LEAN 0
+#endif
+    const int spare_bytes = FW_LEAN ? 64 * (4 + 8 * nw) : 0;  // the per-lane spare flag / acc columns (StateLds)
+    const int room = (158 * 1024 / MG_PER_CU - e * entry_bytes - spare_bytes) / 4;
 #ifndef FW_IDX_MULT
 #define FW_IDX_MULT 4  // index slots per entry aimed at (development A/B builds override)
 #endif
@@ -226,7 +230,7 @@ constexpr uint32_t F_TIMER = 2u;  // event-time timer registered for (key, windo
 // cleanup timer at cleanupTime (WindowOperator.registerCleanupTimer :616-628)
 constexpr uint32_t F_CLEAN = 32u;
 
-// Error bits reported through Ctrl::error.
+// Error bits reported through Ctrl::error (= fw_stats.error_flags, FW_ERRF_* in flinkwin.h).
 constexpr uint32_t ERR_CHUNKS = 1u;
 constexpr uint32_t ERR_STATE = 2u;
 constexpr uint32_t ERR_OUTPUT = 4u;
@@ -235,6 +239,10 @@ constexpr uint32_t ERR_KEYGROUP = 16u;  // a record's key group is outside this 
 constexpr uint32_t ERR_LATE = 32u;      // late-fire rows or late side-output rows over capacity
 constexpr uint32_t ERR_ORDEV = 64u;     // first-element retain / release events over capacity
 constexpr uint32_t ERR_KEYROW = 128u;   // key-row table full, or a key row over key_row_max_bytes / misaligned
+static_assert(ERR_CHUNKS == FW_ERRF_CHUNKS && ERR_STATE == FW_ERRF_STATE && ERR_OUTPUT == FW_ERRF_OUTPUT &&
+                  ERR_TREQ == FW_ERRF_TREQ && ERR_KEYGROUP == FW_ERRF_KEYGROUP && ERR_LATE == FW_ERRF_LATE &&
+                  ERR_ORDEV == FW_ERRF_ORDEV && ERR_KEYROW == FW_ERRF_KEYROW,
+              "error bits and the public FW_ERRF_* values");
 
 // FW_KEYHASH_KEYROW: the key-row intern table in HBM.  The window state keys on a dense int64 id per
 // distinct key row; the id's image (the key row's BinaryRowData bytes, what BinaryRowData.equals

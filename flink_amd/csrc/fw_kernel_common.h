@@ -250,6 +250,40 @@ __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
     return h ^ (h >> 13);
 }
 
+// Write-through stores for the bulk outputs a later kernel reads (partial rows, state write-back):
+// global_store ... sc1 leaves no dirty line in the XCD's L2 (MI355X_MICROARCH.md, store flavours:
+// sc1 drops the line, a 16-B sc1 store costs what a plain one does), so the kernel boundary that
+// follows has no ~100 MB of dirty lines to write back before the next kernel starts.  Off: measured
+// (round 5, CFG2/CFG4) the sc1 stores made the ingest store phase 1.1-2x slower (CFG2 runs ingest 67 ->
+// 116 us, CFG4 78 -> 152 us) and the step gaps did not shrink; kept as an A/B knob.
+#ifndef FW_WT
+#define FW_WT 0
+#endif
+typedef unsigned int fw_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int fw_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_wt16(void* p, uint64_t lo, uint64_t hi) {
+#if FW_WT
+    fw_u32x4 w;
+    w.x = (unsigned)lo;
+    w.y = (unsigned)(lo >> 32);
+    w.z = (unsigned)hi;
+    w.w = (unsigned)(hi >> 32);
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+#else
+    *(ulonglong2*)p = make_ulonglong2(lo, hi);
+#endif
+}
+__device__ __forceinline__ void st_wt8(void* p, uint64_t v) {
+#if FW_WT
+    fw_u32x2 w;
+    w.x = (unsigned)v;
+    w.y = (unsigned)(v >> 32);
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+#else
+    *(uint64_t*)p = v;
+#endif
+}
+
 // wave-level reductions: one LDS atomic per wave instead of one per lane (same-address LDS
 // atomics serialise lane by lane)
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {

@@ -9,14 +9,21 @@ namespace fw {
 // ======================================================================================
 // K4+K5: merge pending partials into the HBM slice-state table, fire due timers
 // ======================================================================================
+#ifndef FW_LEAN
+#define FW_LEAN 0  // branch-free first probes and folds in the SQL gathers (fold_block; A/B, off: measured
+                   // neutral on CFG2 / CFG4 and 3 % slower on CFG5 -- DESIGN.md 4)
+#endif
+// One spare accumulator / flag column per lane beyond the E entries (MG_SPARE): the branch-free fold
+// (fold_block) sends a lane's row that is not a first-probe hit there instead of masking the lane off.
+constexpr int MG_SPARE = FW_LEAN ? 64 : 0;
 template <int NW, int E>
 struct StateLds {
     static constexpr int NI = mg_idx_slots(NW, E);  // 4E slots where they fit (mg_idx_slots)
     uint32_t idx[NI];      // open-addressing index: 0 empty, 1 claiming, 2+e entry e
     int64_t key[E];
     int64_t slice[E];
-    uint32_t flag[E];
-    uint64_t acc[NW][E];
+    uint32_t flag[E + MG_SPARE];
+    uint64_t acc[NW][E + MG_SPARE];
     uint16_t due[E];       // entries whose timer is due at this watermark (each fires once)
     int32_t ndue;
     int32_t n;             // entries in use
@@ -60,18 +67,18 @@ __device__ __forceinline__ void load_words(const uint64_t* p, uint64_t (&o)[W]) 
         }
     }
 }
+// (write-through: the state rows are read by the next flush, not by this kernel -- st_wt16)
 template <int W>
 __device__ __forceinline__ void store_words(uint64_t* p, const uint64_t (&v)[W]) {
     if constexpr (W % 2 == 0) {
 #pragma unroll
-        for (int k = 0; k < W / 2; k++) *(ulonglong2*)(p + 2 * k) = make_ulonglong2(v[2 * k], v[2 * k + 1]);
+        for (int k = 0; k < W / 2; k++) st_wt16(p + 2 * k, v[2 * k], v[2 * k + 1]);
     } else {
         const bool odd = ((uintptr_t)p & 8) != 0;
-        *(odd ? p : p + (W - 1)) = odd ? v[0] : v[W - 1];
+        st_wt8(odd ? p : p + (W - 1), odd ? v[0] : v[W - 1]);
         uint64_t* q = p + (odd ? 1 : 0);
 #pragma unroll
-        for (int k = 0; k < (W - 1) / 2; k++)
-            *(ulonglong2*)(q + 2 * k) = make_ulonglong2(odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
+        for (int k = 0; k < (W - 1) / 2; k++) st_wt16(q + 2 * k, odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
     }
 }
 
@@ -236,6 +243,48 @@ __device__ __forceinline__ uint32_t insert_fresh(StateLds<NW, E>& S, const WordD
     return miss & ~won;
 }
 
+// Branch-free first probes and folds of a block of GX rows per lane (SQL TUMBLE / CUMULATE / HOP
+// slices; not DataStream windows): every lane issues the index reads of all its rows, then the entry
+// reads, then folds each row -- a first-probe hit into its entry, any other row (not live, home slot
+// empty, collision, insertion in flight) into the lane's spare column, so no row masks a lane off
+// and the hot path runs without exec-mask branches.  Returns the live rows the first probe did not
+// decide (bit u) with ge[u] = -1 (home slot empty: insert_fresh may claim it) or -2 (probe further).
+template <int NW, int E, int GX, uint32_t OPS, typename Row, typename FlagsOf>
+__device__ __forceinline__ uint32_t fold_block(StateLds<NW, E>& S, const WordDesc& wd, const Row& row, uint32_t live,
+                                               int* ge, const FlagsOf& flags_of) {
+    static_assert(MG_SPARE >= 64 || GX < 0, "fold_block needs the spare columns (FW_LEAN)");
+    constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
+    const uint32_t spare = (uint32_t)E + (uint32_t)(threadIdx.x & 63);
+    uint32_t st[GX];
+#pragma unroll
+    for (int u = 0; u < GX; u++)
+        st[u] = __hip_atomic_load(&S.idx[index_hash((int64_t)row[u][0], (int64_t)row[u][1]) & MASK], __ATOMIC_RELAXED,
+                                  LDS_SCOPE);
+    int64_t kk[GX], ss[GX];
+    uint32_t ei[GX];
+#pragma unroll
+    for (int u = 0; u < GX; u++) {
+        ei[u] = min(st[u] - 2u, (uint32_t)(E - 1));
+        kk[u] = S.key[ei[u]];
+        ss[u] = S.slice[ei[u]];
+    }
+    uint32_t miss = 0;
+#pragma unroll
+    for (int u = 0; u < GX; u++) {
+        const bool lv = (live >> u) & 1u;
+        const bool hit = lv && st[u] >= 2u && st[u] - 2u < (uint32_t)E && kk[u] == (int64_t)row[u][0] &&
+                         ss[u] == (int64_t)row[u][1];
+        const uint32_t t = hit ? ei[u] : spare;
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            if (word_on<OPS>(wd, w)) lds_fold(word_op<OPS>(wd, w), &S.acc[w][t], row[u][2 + w]);
+        atomicOr(&S.flag[t], flags_of((int64_t)row[u][1]));
+        ge[u] = hit ? (int)ei[u] : st[u] == 0u ? -1 : -2;
+        miss |= (uint32_t)(lv && !hit) << u;
+    }
+    return miss;
+}
+
 // register an event-time timer on entry e; a timer that is already due at this watermark joins
 // the due list (an entry's timer fires at most once per advance: its timestamp is its slice end)
 template <int NW, int E>
@@ -270,9 +319,9 @@ __device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_
     if (FW_ABL(a) & AB_M_NO_EMIT) return;
     const int64_t i = claim_out_row(a, sb, s_emit);
     if (i < 0) return;
-    a.out_key[i] = key;
-    a.out_ws[i] = window_start_of(a.win, we);
-    a.out_we[i] = we;
+    st_wt8(&a.out_key[i], (uint64_t)key);
+    st_wt8(&a.out_ws[i], (uint64_t)window_start_of(a.win, we));
+    st_wt8(&a.out_we[i], (uint64_t)we);
     uint32_t nm = 0;
     for (int g = 0; g < a.ad.n; g++) {
         const int32_t kind = a.ad.kind[g], type = a.ad.type[g];
@@ -315,9 +364,9 @@ __device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_
                 break;
             }
         }
-        a.out_val[g][i] = ((nm >> g) & 1u) ? 0ull : v;  // a NULL's value word is 0
+        st_wt8(&a.out_val[g][i], ((nm >> g) & 1u) ? 0ull : v);  // a NULL's value word is 0
     }
-    if (a.ad.first_word >= 0) a.out_val[a.ad.n][i] = acc[a.ad.first_word];  // value1's arrival ordinal
+    if (a.ad.first_word >= 0) st_wt8(&a.out_val[a.ad.n][i], acc[a.ad.first_word]);  // value1's arrival ordinal
     a.out_null[i] = nm;
 }
 
@@ -1231,9 +1280,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
         // keeps no timers (LocalAggCombiner.java:69-97).  UTC: fired <=> sliceEnd - 1 <= w_old, i.e.
         // sliceEnd <= fired_lim (one compare per row); shift zones take the out-of-line zone rule
         const bool utc = a.win.tz.n == 0;
-        const int64_t fired_lim = a.local ? INT64_MAX - 1 : w_old == INT64_MAX ? INT64_MAX - 1 : w_old + 1;
         auto flags_of = [&](int64_t sl) -> uint32_t {
-            const bool fired = utc ? sl <= fired_lim : (a.local || tz_fired_out_of_line(a.win.tz, sl, w_old));
+            const bool fired = a.local || (utc ? is_fired(sl, w_old) : tz_fired_out_of_line(a.win.tz, sl, w_old));
             return fired ? F_ACC : (F_ACC | F_TIMER);
         };
         auto fold_rows = [&](auto& row, uint32_t live) __attribute__((always_inline)) {
@@ -1291,7 +1339,12 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                     });
                     return rest;
                 };
+#if FW_LEAN
+                uint32_t miss = fold_block<NW, E, GX, OPS>(S, a.wd, row, live, ge, flags_of);
+                (void)probe_fold;
+#else
                 uint32_t miss = probe_fold(live);
+#endif
                 gstamp(4);
                 const bool gcount = (FW_ABL(a) & AB_GSTAMPS) && stm.on && (tid >> 6) == 0;  // wave 0's row census
                 if (gcount) {
@@ -1346,14 +1399,19 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
         // (HOP chains, DataStream windows) leave no registers for a second block
         constexpr bool RP = FW_MG_PIPE && NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
 #ifndef FW_GR
-#define FW_GR 0  // rows per lane per pipelined block (0: half of mg_rows_in_flight)
+#define FW_GR 0  // rows per lane per pipelined block (0: planned below)
 #endif
 #ifndef FW_GD
-#define FW_GD 2  // blocks in the pipelined gather's ring
+#define FW_GD 0  // blocks in the pipelined gather's ring (0: planned below)
 #endif
-        constexpr int GR = RP ? (FW_GR > 0 ? FW_GR : GU / 2 > 0 ? GU / 2 : 1) : GU;
+        // one-word TUMBLE: one block of 3 rows per lane (measured round 5, CFG2 runs flush 144.5 ->
+        // 131.8 us; the freed registers go to the probe loop); CFG4 (two words, 197 -> 201 us) and CFG5
+        // (CUMULATE, 322 -> 370 us) keep two blocks of half of mg_rows_in_flight
+        constexpr bool ONE_BLOCK = NW == 1 && KIND == FW_WIN_TUMBLE;
+        constexpr int GR = !RP ? GU : FW_GR > 0 ? FW_GR : ONE_BLOCK ? 3 : GU / 2 > 0 ? GU / 2 : 1;
+        constexpr int GD = !RP ? 1 : FW_GD > 0 ? FW_GD : ONE_BLOCK ? 1 : 2;
         const uint64_t gl0 = gst ? __builtin_amdgcn_s_memtime() : 0;
-        gather_runs<NW, GR, GF, RP ? FW_GD : 1>(a, sb, pend, fold_rows);
+        gather_runs<NW, GR, GF, GD>(a, sb, pend, fold_rows);
         if (gst) stm.acc[13] += __builtin_amdgcn_s_memtime() - gl0;
         uint32_t ovf = run_overflow(a, sb, pend);
         while (ovf) {
@@ -1363,8 +1421,12 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
         }
     } else if (PIPE && gather) {
         constexpr int GP = NW == 1 ? GU : GU / 2 > 0 ? GU / 2 : 1;  // one word: two full blocks fit
+        // register the window timer unless already fired (AggCombiner.java:103-110); the LOCAL phase
+        // keeps no timers; shift zones take the out-of-line zone rule
+        const bool utc = a.win.tz.n == 0;
         auto flags_of = [&](int64_t sl) -> uint32_t {
-            return (a.local || win_fired(a.win, sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
+            const bool fired = a.local || (utc ? is_fired(sl, w_old) : tz_fired_out_of_line(a.win.tz, sl, w_old));
+            return fired ? F_ACC : (F_ACC | F_TIMER);
         };
         auto ngroups_of = [&](int64_t p) {
             const int nc = (int)cell_pad(a.slot_nch[p]);
@@ -1415,6 +1477,9 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                 return;
             }
             int ge[GX];
+#if FW_LEAN
+            uint32_t miss = fold_block<NW, E, GX, OPS>(S, a.wd, row, live, ge, flags_of);
+#else
             {
                 int64_t gk[GX], gs[GX];
 #pragma unroll
@@ -1439,6 +1504,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                     if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
                 atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
             });
+#endif
             while (miss) {
                 const int um = __ffs(miss) - 1;
                 miss &= miss - 1;
@@ -1523,7 +1589,24 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                         });
                         continue;
                     }
+                    // register the window timer unless already fired (AggCombiner.java:103-110);
+                    // the LOCAL phase keeps no timers (LocalAggCombiner.java:69-97); shift zones take
+                    // the out-of-line zone rule
+                    const bool utc = a.win.tz.n == 0;
+                    auto flags_of = [&](int64_t sl) -> uint32_t {
+                        const bool fired = a.local || (utc ? is_fired(sl, w_old) : tz_fired_out_of_line(a.win.tz, sl, w_old));
+                        return fired ? F_ACC : (F_ACC | F_TIMER);
+                    };
                     int ge[GU];
+#if FW_LEAN
+                    uint32_t miss = fold_block<NW, E, GU, OPS>(S, a.wd, row, live, ge, flags_of);
+                    if (gst) {
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        const uint64_t g1 = __builtin_amdgcn_s_memtime();
+                        stm.acc[4] += g1 - g0;
+                        g0 = g1;
+                    }
+#else
                     {
                         int64_t gk[GU], gs[GU];
 #pragma unroll
@@ -1539,11 +1622,6 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                         stm.acc[4] += g1 - g0;
                         g0 = g1;
                     }
-                    // register the window timer unless already fired (AggCombiner.java:103-110);
-                    // the LOCAL phase keeps no timers (LocalAggCombiner.java:69-97)
-                    auto flags_of = [&](int64_t sl) -> uint32_t {
-                        return (a.local || win_fired(a.win, sl, w_old)) ? F_ACC : (F_ACC | F_TIMER);
-                    };
                     uint32_t miss = 0;
                     static_for<GU>([&](auto UU) {
                         constexpr int u = decltype(UU)::value;
@@ -1559,6 +1637,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                             if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
                         atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
                     });
+#endif
                     const uint64_t gm0 = gst ? __builtin_amdgcn_s_memtime() : 0;
                     while (miss) {  // the wave loops max(popcount) times, not GU times
                         const int um = __ffs(miss) - 1;

@@ -53,7 +53,11 @@ class KeyByExchange:
             self._cpu_group = dist.new_group(ranks=ranks, backend="gloo")
         self._max_count = None  # running max of rows per destination (padded exchanges), on the device
         self.spill_rounds = 0
-        self._dn_share = 1 << 16  # largest per-destination share of the last device-counted exchange
+        self._dn_share = 1 << 16  # largest per-destination share of the last exchange, agreed by all subtasks
+        self._share_known = False  # _dn_share comes from an agreed exchange (not the initial guess)
+        # packed segments: the previous exchange's agreed largest share plus this headroom (rows past a
+        # segment take the overflow round, so a tight headroom costs a spill round, never rows)
+        self.headroom = 0.03
 
     # ---- routing ------------------------------------------------------------------------
     def partition(self, key, ts, values, key_hash=None):
@@ -191,6 +195,8 @@ class KeyByExchange:
         w = 2 + len(values)
         if capacity is not None:
             cap = int(capacity)
+        elif self._share_known:  # the last agreed share + headroom: padding is ~3 %, not 25 % + 1024 rows
+            cap = max(int(self._dn_share * (1.0 + self.headroom)) + 64, 64)
         elif n_dev is not None:
             cap = int(self._dn_share * 1.25) + 1024
         else:
@@ -255,9 +261,10 @@ class KeyByExchange:
         if self.world == 1:
             return overflow, wm, int(share)
         g = self.group if self._cpu_group is None else self._cpu_group
-        t = torch.tensor([1 if overflow else 0, -wm if wm is not None else 0, int(share)], dtype=torch.int64)
+        # ~w (= -w - 1) reverses the int64 order with no overflow (-Long.MIN_VALUE would): MAX of ~w is ~MIN
+        t = torch.tensor([1 if overflow else 0, ~wm if wm is not None else 0, int(share)], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
-        return bool(t[0].item()), (None if wm is None else -int(t[1].item())), int(t[2].item())
+        return bool(t[0].item()), (None if wm is None else ~int(t[1].item())), int(t[2].item())
 
     def _note_counts(self, counts, cap):
         """Keep the running max of rows per destination on the device (check_capacity)."""
@@ -308,7 +315,9 @@ class PackedExchange:
         self.ex, self.rows, self.recv_counts, self.row_words = ex, rows, recv_counts, row_words
         self._cap, self._spill, self._counts_h, self._part_done = cap, spill, counts_h, part_done
         self._mv, self._back, self._counts_d = mv, back, counts_d
-        self._agreed = None  # finish_device's all-reduced [overflow, -watermark, share] (device)
+        self._agreed = None  # finish_device's all-reduced [overflow, ~watermark, share] (device)
+        self.agreed_watermark = None  # settle(): the valve's minimum watermark of this step (host)
+        self._agreed_h = self._agreed_ev = None  # its pinned host mirror and the event that fills it
 
     def finish(self, watermark=None):
         """The overflow round and the watermark valve: waits for this subtask's partition kernel
@@ -322,12 +331,12 @@ class PackedExchange:
         # sent this time: every subtask must pick the same segment size, so it rides in the same
         # all-reduce as the overflow decision and the watermark
         any_over, wm, share = ex._agree(sum(over) > 0, watermark, max(cnt) if cnt else 0)
-        ex._dn_share = share
+        ex._dn_share, ex._share_known = share, True
         return self._spill_round(any_over, over), wm
 
     def finish_device(self, watermark, prev_watermark):
         """The device-side valve (StatusWatermarkValve.java:153: min over the input channels): this
-        subtask's overflow flag, -watermark and largest per-destination share go into ONE all-reduce
+        subtask's overflow flag, ~watermark and largest per-destination share go into ONE all-reduce
         (MAX) on the device -- RCCL on the stream, nothing waits on the host.  Returns a one-element
         device int64 tensor: the minimum watermark, or ``prev_watermark`` (device tensor) when any
         subtask overflowed its segments -- its spill rows are sent by settle() at the start of the next
@@ -336,7 +345,7 @@ class PackedExchange:
         ex = self.ex
         dev = self._counts_d.device
         t = torch.stack([(self._counts_d > self._cap).any().to(torch.int64),
-                         torch.full((), -int(watermark), dtype=torch.int64, device=dev),
+                         torch.full((), ~int(watermark), dtype=torch.int64, device=dev),
                          self._counts_d.max() if self._counts_d.numel() else torch.zeros((), dtype=torch.int64, device=dev)])
         if ex.world > 1:
             if self._counts_d.is_cuda and dist.get_backend(ex.group) == "nccl":
@@ -347,21 +356,33 @@ class PackedExchange:
                 dist.all_reduce(th, op=dist.ReduceOp.MAX, group=g)
                 t = th.to(dev)
         self._agreed = t
+        self._agreed_h = self._agreed_ev = None
+        if t.is_cuda:  # settle() reads a pinned mirror behind an event: no stream-wide sync
+            self._agreed_h = torch.empty(3, dtype=torch.int64, pin_memory=True)
+            self._agreed_h.copy_(t, non_blocking=True)
+            self._agreed_ev = torch.cuda.Event()
+            self._agreed_ev.record(torch.cuda.current_stream(dev))
         if prev_watermark is None:  # nothing advanced yet: an overflowing first step holds at Long.MIN_VALUE
             prev_watermark = torch.full((1,), -(1 << 63), dtype=torch.int64, device=dev)
-        return torch.where(t[0:1] > 0, prev_watermark, -t[1:2])
+        return torch.where(t[0:1] > 0, prev_watermark, torch.bitwise_not(t[1:2]))
 
     def settle(self):
         """The host half of finish_device, one step late: reads the agreed values (waits only for this
         step's all-reduce, long done while the next step's work is queued behind it), sets the next
         device-counted segment size, and runs the overflow round if any subtask overflowed.  Returns the
-        spill rows for this subtask (device, packed) or None."""
+        spill rows for this subtask (device, packed) or None.  When it returns spill rows, the step's
+        watermark was held at the previous one: the caller pushes the rows, then advances to
+        ``agreed_watermark`` (TwoPhaseWindowAgg.settle does)."""
         t = self._agreed
         if t is None:
             return None
         self._agreed = None
-        any_over, _, share = (int(x) for x in t.tolist())
-        self.ex._dn_share = share
+        if self._agreed_ev is not None:  # waits for this step's all-reduce only (the stream runs on)
+            self._agreed_ev.synchronize()
+            t = self._agreed_h
+        any_over, nwm, share = (int(x) for x in t.tolist())
+        self.agreed_watermark = ~nwm
+        self.ex._dn_share, self.ex._share_known = share, True
         over = None
         if any_over:
             cnt = self._counts_h.tolist()

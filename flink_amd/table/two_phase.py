@@ -111,8 +111,10 @@ class TwoPhaseWindowAgg:
         return wm
 
     def settle(self):
-        """The previous device-valve step's overflow round (its spill rows reach the GLOBAL operator
-        before any later watermark)."""
+        """The previous device-valve step's overflow round: its spill rows reach the GLOBAL operator
+        before any later watermark, and the watermark that step held back (finish_device keeps the
+        previous one while rows are in flight) is issued after them, so the last step needs no extra
+        advance from the caller."""
         px = getattr(self, "_px", None)
         if px is None:
             return
@@ -122,6 +124,7 @@ class TwoPhaseWindowAgg:
             n_sp = spill.numel() // px.row_words
             self.glob.push_device_packed_segments(torch.tensor([n_sp], dtype=torch.int64, device=self.device), spill,
                                                   px.row_words)
+            self.glob.advance(px.agreed_watermark)
 
     def step_device(self, watermark):
         """One watermark interval of the plan with the partials kept on the device and no host round

@@ -249,7 +249,7 @@ typedef struct {
     int64_t results_available;
     int64_t num_fired_windows;         /* numFiredTimers analogue                       */
     int64_t partials_emitted;          /* partial (key, slice) aggregates written by ingest */
-    int32_t error_flags;
+    int32_t error_flags;               /* FW_ERRF_* bits raised by the device since create / restore */
     int32_t num_superbuckets;
     /* v5: merge traffic counters (cumulative, device-side): measurement of the flush kernel */
     int64_t flush_launches;            /* fw_advance / flush launches that merged pending partials */
@@ -269,6 +269,9 @@ int fw_create(const fw_config* cfg, fw_handle** out);
 int fw_destroy(fw_handle* h);
 const char* fw_last_error(void);
 int fw_abi_version(void);
+/* Number of visible HIP devices (hipGetDeviceCount); 0 when the runtime finds none or fails.  The
+ * JNI binding's FlinkWin.deviceCount() uses it for available(). */
+int fw_device_count(void);
 /* hipStream_t of the handle, as void* (so a caller can order its own work with it). */
 void* fw_get_stream(fw_handle* h);
 int fw_sync(fw_handle* h);
@@ -367,11 +370,13 @@ int fw_results_reset(fw_handle* h);
 /* v6, pipelined emission (the shim's collector side of WindowAggOperator.onTimer ->
    output.collect, WindowAggOperator.java:227-238, and WindowOperator.emitWindowContents :568-575):
    fw_results_async queues the collection of every result row emitted since the last collection
-   straight into one of two pinned host buffers of the handle and returns at once (the rows count as
-   consumed, as after fw_results_reset); fw_results_ready waits for the LAST fw_results_async's rows
-   and returns them as host arrays, valid until the second fw_results_async after it.  So a caller
-   emits watermark b's rows while batch b + 1 is ingested.  Not for FW_KEYHASH_KEYROW operators
-   (fw_results returns their key rows). */
+   (compacted on the device into one of two device buffers of the handle; only the row count goes to
+   mapped host memory) and returns at once (the rows count as consumed, as after fw_results_reset);
+   fw_results_ready waits for the LAST fw_results_async's compaction, moves its rows into pinned host
+   memory by DMA (v8: hipMemcpyAsync on the handle's D2H stream, no CU time) and returns them as host
+   arrays, valid until the second fw_results_async after it.  So a caller emits watermark b's rows
+   while batch b + 1 is ingested.  Not for FW_KEYHASH_KEYROW operators (fw_results returns their key
+   rows). */
 int fw_results_async(fw_handle* h);
 int fw_results_ready(fw_handle* h, fw_result* out);
 /* v6, device-side consumers (the two-phase plan's LOCAL -> GLOBAL exchange): queues the collection
@@ -386,7 +391,7 @@ int fw_results_device(fw_handle* h, fw_result* out, int64_t** d_n);
    the row index); the last segment, the shared overflow region, holds counts[n_segments - 1] rows
    from row (n_segments - 1) * seg_cap.  counts is a device int32 array written by the merge
    kernels, so read it (and the rows) on the handle's stream (fw_get_stream) or after it, before
-   the next fw_advance / fw_flush.  n_segments = 0 when nothing was emitted since the last
+   the next call that can run a merge (see FW_ERRF_OUTPUT below).  n_segments = 0 when nothing was emitted since the last
    collection.  The rows count as consumed.  fw_results / fw_results_device compact the same rows
    into one contiguous set (a copy of every row). */
 typedef struct {
@@ -396,6 +401,20 @@ typedef struct {
     fw_result cols;
 } fw_result_segments;
 int fw_results_device_segments(fw_handle* h, fw_result_segments* out);
+/* fw_stats.error_flags bits.  fw_results / fw_results_device turn FW_ERRF_OUTPUT into FW_E_CAPACITY;
+   fw_results_device_segments returns the rows it has (the overflow region's count is clamped to the
+   output capacity), so a segments consumer checks error_flags (fw_get_stats) for FW_ERRF_OUTPUT.
+   A segments consumer also finishes with the rows before ANY call that can run a merge: fw_advance,
+   fw_advance_device, fw_flush, and every push (a push starts a flush by itself once the pending
+   pushes fill the handle's FW_MAX_PENDING slots). */
+#define FW_ERRF_CHUNKS 1      /* ingest chunk table over capacity                          */
+#define FW_ERRF_STATE 2       /* state table full (FW_E_CAPACITY)                          */
+#define FW_ERRF_OUTPUT 4      /* emitted rows over output_capacity: rows past it dropped  */
+#define FW_ERRF_TREQ 8        /* timer request buffer over capacity                        */
+#define FW_ERRF_KEYGROUP 16   /* a record's key group is outside this subtask's range      */
+#define FW_ERRF_LATE 32       /* late-fire rows or late side-output rows over capacity     */
+#define FW_ERRF_ORDEV 64      /* first-element retain / release events over capacity       */
+#define FW_ERRF_KEYROW 128    /* key-row table full, or a key row over key_row_max_bytes   */
 int fw_get_stats(fw_handle* h, fw_stats* out);
 
 /* ---- per-kernel device timing (in-kernel clock stamps, or hipEvents around each launch) --- */

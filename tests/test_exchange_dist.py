@@ -242,7 +242,8 @@ def _worker_device_valve(rank, port, n_batches, n, out_q):
 
         ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
         lo, hi = key_group_range(128, WORLD, rank)
-        got, wms, prev_px, prev_wm = [], [], None, None
+        got, wms, agreed, prev_px, prev_wm = [], [], [], None, None
+        LMIN = -(1 << 63)
 
         def take(rows_, w):
             sp = rows_.view(-1, w)
@@ -251,6 +252,7 @@ def _worker_device_valve(rank, port, n_batches, n, out_q):
         for b in range(n_batches):
             if prev_px is not None:
                 spill = prev_px.settle()
+                agreed.append(prev_px.agreed_watermark)
                 if spill is not None:
                     take(spill, prev_px.row_words)
             k, t, v = _stream(rank, b, n)
@@ -259,12 +261,15 @@ def _worker_device_valve(rank, port, n_batches, n, out_q):
             seg = px.rows.view(WORLD, cap, px.row_words)
             keep = torch.arange(cap)[None, :] < px.recv_counts.clamp(max=cap)[:, None]
             take(seg[keep].reshape(-1), px.row_words)
-            wm = px.finish_device(T0 + b * 3000 - 3000 + 500 * rank, prev_wm)
+            # step 0: rank 0 proposes Long.MIN_VALUE (no watermark yet), which the valve must carry
+            wm = px.finish_device(LMIN if b == 0 and rank == 0 else T0 + b * 3000 - 3000 + 500 * rank, prev_wm)
             wms.append(int(wm.item()))
             prev_px, prev_wm = px, wm
         spill = prev_px.settle()
+        agreed.append(prev_px.agreed_watermark)
         if spill is not None:
             take(spill, prev_px.row_words)
+        assert agreed == [LMIN] + [T0 + b * 3000 - 3000 for b in range(1, n_batches)]
         assert all(lo <= key_group(abi.KEYHASH_BINROW_BIGINT, int(x), 128) <= hi for x in {r[0] for r in got})
         out_q.put((rank, sorted(got), wms, ex.spill_rounds))
     finally:
@@ -296,5 +301,6 @@ def test_gloo_device_valve_holds_watermark_until_overflow_round():
     # the valve: rank 0's proposal (the minimum), held at the previous value on the overflowing steps
     assert res[0][2] == res[1][2]
     expect = [T0 + b * 3000 - 3000 if b % 2 == 0 else T0 + (b - 1) * 3000 - 3000 for b in range(n_batches)]
+    expect[0] = expect[1] = -(1 << 63)  # step 0 is Long.MIN_VALUE; step 1 overflows and holds it
     assert res[0][2] == expect
     assert res[0][3] == n_batches // 2

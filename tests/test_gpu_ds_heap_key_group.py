@@ -273,11 +273,12 @@ def test_string_keys_route_by_java_hash_across_subtasks():
     rng = np.random.default_rng(5)
     names = [f"user-{i}-é" for i in range(300)]
     keys = [names[j] for j in rng.integers(0, len(names), 4000)]
-    ts = (T0 + rng.integers(0, 3000, 4000)).astype(np.int64)
+    t3 = 1_599_999_999_000  # a multiple of the 3 s window: one window holds every element
+    ts = (t3 + rng.integers(0, 3000, 4000)).astype(np.int64)
     vals = rng.integers(0, 100, 4000).astype(np.int64)
     a = op()
     a.process_batch(keys, ts, vals, records=[(k, int(v)) for k, v in zip(keys, vals)])
-    a.process_watermark(T0 - 1)
+    a.process_watermark(t3 - 1)
     kg_of = {}
     for n in set(keys):
         kg_of[n] = _native.lib().fw_host_key_group(abi.KEYHASH_PRECOMPUTED, 0, java_string_hash(n), 128)
@@ -295,7 +296,7 @@ def test_string_keys_route_by_java_hash_across_subtasks():
             else:
                 with pytest.raises(Exception):
                     b.restore_key_group_heap(blob)
-        r = b.process_watermark(T0 + 2999)
+        r = b.process_watermark(t3 + 2999)
         for rec in r["records"]:
             assert rec[0] not in got
             got[rec[0]] = rec[1]

@@ -71,6 +71,12 @@ SCENARIOS = {
 # late, the watermark held at the previous one meanwhile)
 for _n in ("one_phase_hop", "one_phase_tumble_double", "two_phase_cumulate_zipf", "two_phase_hop_zipf"):
     SCENARIOS[_n + "_device_valve"] = dict(SCENARIOS[_n], valve="device")
+# segments sized as the bench sizes them -- the previous step's agreed largest share plus a headroom
+# (KeyByExchange.headroom) -- with the headroom negative, so every step after the first overflows its
+# segments and the overflow round carries the rest (host and device valves)
+for _n, _v in (("one_phase_hop_share_sizing", "host"), ("one_phase_tumble_double_share_sizing_device_valve", "device")):
+    SCENARIOS[_n] = dict(SCENARIOS["one_phase_hop" if "hop" in _n else "one_phase_tumble_double"], valve=_v,
+                         cap="share", headroom=-0.15)
 N_BATCHES = 9
 N_ROWS = 24000  # per rank per batch
 
@@ -130,6 +136,9 @@ def _worker(rank, port, name, out_q):
         cfg = _cfg(kw, WORLD, rank)
         n_aggs = cfg.n_aggs
         ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+        share_sizing = sc.get("cap") == "share"
+        if share_sizing:
+            ex.headroom = sc["headroom"]
         rows, wms, received = [], [], 0
         device_valve = sc.get("valve") == "device"
         if sc["plan"] == "one" and device_valve:
@@ -148,10 +157,10 @@ def _worker(rank, port, name, out_q):
                 if px_prev is not None:
                     settle(px_prev)
                 k, t, v = (torch.from_numpy(x).to(dev) for x in _stream(sc["dist"], vt, rank, b, N_ROWS))
-                cap = ex.segment_capacity(N_ROWS, WORLD) if b % 2 == 0 else N_ROWS // (4 * WORLD)
+                cap = None if share_sizing else ex.segment_capacity(N_ROWS, WORLD) if b % 2 == 0 else N_ROWS // (4 * WORLD)
                 px = ex.exchange_packed_async(k, t, [v], capacity=cap)
                 h.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
-                received += int(px.recv_counts.clamp(max=cap).sum())
+                received += int(px.recv_counts.clamp(max=px._cap).sum())
                 wm_t = px.finish_device(_proposed_wm(b, rank), wm_prev)
                 h.advance_device(wm_t)
                 px_prev, wm_prev = px, wm_t
@@ -167,11 +176,11 @@ def _worker(rank, port, name, out_q):
             for b in range(N_BATCHES):
                 k, t, v = (torch.from_numpy(x).to(dev) for x in _stream(sc["dist"], vt, rank, b, N_ROWS))
                 # odd steps: segments of a quarter of the even share -> the overflow round carries the rest
-                cap = ex.segment_capacity(N_ROWS, WORLD) if b % 2 == 0 else N_ROWS // (4 * WORLD)
+                cap = None if share_sizing else ex.segment_capacity(N_ROWS, WORLD) if b % 2 == 0 else N_ROWS // (4 * WORLD)
                 px = ex.exchange_packed_async(k, t, [v], capacity=cap)
                 h.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
                 spill, wm = px.finish(watermark=_proposed_wm(b, rank))
-                received += int(px.recv_counts.clamp(max=cap).sum())  # rows past a segment come in the spill
+                received += int(px.recv_counts.clamp(max=px._cap).sum())  # rows past a segment come in the spill
                 if spill is not None:
                     n_sp = spill.numel() // px.row_words
                     received += n_sp

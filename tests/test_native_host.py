@@ -89,3 +89,19 @@ def test_invalid_configs_fail_without_device():
     with pytest.raises(_native.FlinkWinError, match="integral multiple"):
         WindowAggHandle(abi.make_config(window_kind=abi.WIN_CUMULATE, size_ms=3000, slide_ms=700,
                                         aggs=[(abi.AGG_SUM, 0, abi.T_I64)], value_col_types=[abi.T_I64]))
+
+
+def test_device_count_without_gpu_is_zero_not_an_error():
+    # fw_device_count never throws: on a host without a visible HIP device it reports 0, which is
+    # what FlinkWin.available() relies on to keep the Java path.
+    import torch
+    n = _native.lib().fw_device_count()
+    assert n >= 0
+    if not torch.cuda.is_available():
+        assert n == 0
+
+
+def test_error_flag_bits_match_header():
+    text = open(HEADER).read()
+    declared = {m[0]: int(m[1]) for m in re.findall(r"#define FW_ERRF_(\w+) (\d+)", text)}
+    assert declared == abi.ERRF

@@ -698,7 +698,6 @@ int allocate(fw_handle* h) {
         // the runs layout is a plan, not a requirement: FW_MAX_PENDING * run_rows partial rows (about
         // 1.25x the partial buffer) on top of it.  When the device cannot hold them the handle keeps
         // the cell layout instead of failing fw_create.
-        const size_t n_isb = (size_t)(h->ks.n_sb >> h->ks.pass_log2);
         void* r = nullptr;
         void* rr = nullptr;
         if (hipMalloc(&r, (size_t)FW_MAX_PENDING * h->run_rows * PW * sizeof(uint64_t)) != hipSuccess ||

@@ -96,6 +96,7 @@ __device__ __forceinline__ uint32_t hb_fire_entry(const MergeArgs& a, int64_t W,
     if (!mask) return 0;
     // candidate window ends: slot j's slice end, j in [0, HB_R + n - 1)
     int prev = -2, next = -2;  // neighbouring blocks' entries, looked up on first need
+    if (FW_ABL(a) & AB_M_NO_HASH) prev = next = -1;  // (diagnostic: fire without neighbour lookups)
     uint32_t nf = 0;
     for (int j = 0; j < HB_R + n - 1; j++) {
         const int64_t we = wadd(bs, (int64_t)(j + 1) * w.interval);
@@ -213,7 +214,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         }
         __syncthreads();
         const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
-        for (int e = tid; e < n0; e += MG_BLOCK) {
+        if ((FW_ABL(a) & AB_M_NO_LOAD) && tid == 0) S.n = 0;  // (diagnostic ablations: timing only)
+        if (!(FW_ABL(a) & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
             uint64_t p[PWE];
             load_words<PWE>(st + (size_t)e * PWE, p);
             const int64_t k = (int64_t)p[0], bs = (int64_t)p[1];
@@ -236,7 +238,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         // accumulator word (COUNT(*)): software-pipelined over the wave's blocks of rows, as in
         // k_merge_fire (the next block's rows in flight while the current one folds)
         constexpr bool PIPE = FW_MG_PIPE && FW_MG_PIPE1 && NWP == 1;
-        if (do_flush && a.runs) {  // runs (IngestArgs::runs), then the rows chunks kept in their regions
+        const bool gather = do_flush && !(FW_ABL(a) & AB_M_NO_GATHER);
+        if (gather && a.runs) {  // runs (IngestArgs::runs), then the rows chunks kept in their regions
             auto fold_rows = [&](auto& row, uint32_t live) __attribute__((always_inline)) {
                 constexpr int GX = std::extent<std::remove_reference_t<decltype(row)>>::value;
                 int ge[GX], slot[GX];
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
                 ovf &= ovf - 1;
                 gather_cells_push<NWP, GU, GF>(a, sb, pi, fold_rows);
             }
-        } else if (PIPE && do_flush) {
+        } else if (PIPE && gather) {
             constexpr int GP = GU;  // two full blocks fit beside the block-state code
             auto ngroups_of = [&](int64_t p) {
                 const int nc = (int)cell_pad(a.slot_nch[p]);
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
                 if (ha) la = load_group_rows<NWP, GP, GF>(a, cp, cg, r0, sb, ra);
                 process(rb, lb);
             }
-        } else if (do_flush) {
+        } else if (gather) {
             for (int64_t pi = 0; pi < pend; pi++) {
                 const int ncell = (int)cell_pad(a.slot_nch[pi]);
                 const int G = gather_group(ncell);
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         __syncthreads();
         if (do_flush && a.runs) run_release(a, sb, pend);
         // ---- fire: every due window that holds data, each by exactly one block entry
-        if (do_fire) {
+        if (do_fire && !(FW_ABL(a) & AB_M_NO_FIRE)) {
             const int n = min(S.n, E);
             uint32_t nf = 0;
             const int qlane = (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
             p[0] = (uint64_t)S.key[e];
             p[1] = (uint64_t)bs;
             p[2] = (uint64_t)(F_ACC | (mask << HB_MASK_SHIFT));
-            store_words<PWE>(so + (size_t)pos * PWE, p);
+            if (!(FW_ABL(a) & AB_M_NO_WB)) store_words<PWE>(so + (size_t)pos * PWE, p);
             lnm = min(lnm, max(first, e_min));  // no window of this entry is due before it
         }
         lnm = wave_min_i64(lnm);

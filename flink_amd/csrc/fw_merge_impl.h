@@ -1404,11 +1404,12 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
 #ifndef FW_GD
 #define FW_GD 0  // blocks in the pipelined gather's ring (0: planned below)
 #endif
-        // one-word TUMBLE: one block of 3 rows per lane (measured round 5, CFG2 runs flush 144.5 ->
-        // 131.8 us; the freed registers go to the probe loop); CFG4 (two words, 197 -> 201 us) and CFG5
-        // (CUMULATE, 322 -> 370 us) keep two blocks of half of mg_rows_in_flight
+        // one-word TUMBLE: one block of 4 rows per lane (measured round 5, CFG2 runs flush 144.5 ->
+        // 128.7 us; 3 rows: 131.8, 2 rows: 133.3; the freed registers go to the probe loop); CFG4 (two
+        // words, 197 -> 201 us) and CFG5 (CUMULATE, 322 -> 370 us) keep two blocks of half of
+        // mg_rows_in_flight
         constexpr bool ONE_BLOCK = NW == 1 && KIND == FW_WIN_TUMBLE;
-        constexpr int GR = !RP ? GU : FW_GR > 0 ? FW_GR : ONE_BLOCK ? 3 : GU / 2 > 0 ? GU / 2 : 1;
+        constexpr int GR = !RP ? GU : FW_GR > 0 ? FW_GR : ONE_BLOCK ? 4 : GU / 2 > 0 ? GU / 2 : 1;
         constexpr int GD = !RP ? 1 : FW_GD > 0 ? FW_GD : ONE_BLOCK ? 1 : 2;
         const uint64_t gl0 = gst ? __builtin_amdgcn_s_memtime() : 0;
         gather_runs<NW, GR, GF, GD>(a, sb, pend, fold_rows);
@@ -1768,7 +1769,10 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
         // due entries are dealt lane-major over the waves (lane l of wave w takes l * 16 + w):
         // fewer due entries than threads then still keep every wave busy, so each SIMD has four
         // waves of dependent LDS chains to interleave instead of two
-        const int qlane = (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
+#ifndef FW_QLANE
+#define FW_QLANE 1  // 1: lane-major dealing of the due entries; 0: lane-consecutive (A/B)
+#endif
+        const int qlane = FW_QLANE ? (tid & 63) * (MG_BLOCK / 64) + (tid >> 6) : tid;
         if (KIND == FW_WIN_CUMULATE || KIND == FW_WIN_HOP) {
             for (int q = qlane; q < nd; q += MG_BLOCK) {
                 if (KIND == FW_WIN_CUMULATE) mark_cumulate_successor<NW, E>(a, W, S, S.due[q]);

@@ -407,8 +407,10 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         if (do_fire && !(FW_ABL(a) & AB_M_NO_FIRE)) {
             const int n = min(S.n, E);
             uint32_t nf = 0;
-            const int qlane = FW_QLANE ? (tid & 63) * (MG_BLOCK / 64) + (tid >> 6) : tid;
-            for (int e = qlane; e < n; e += MG_BLOCK) nf += hb_fire_entry<NWP, E, OPS>(a, W, S, e, w_old, sb, &s_emit);
+            for (int b0 = 0; b0 < n; b0 += MG_BLOCK) {
+                const int e = fire_deal(b0, n, tid);
+                if (e < n) nf += hb_fire_entry<NWP, E, OPS>(a, W, S, e, w_old, sb, &s_emit);
+            }
             nf = wave_sum_u32(nf);
             if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
         }

@@ -296,6 +296,30 @@ __device__ __forceinline__ void set_timer(StateLds<NW, E>& S, int e, int64_t W, 
     }
 }
 
+// The fire passes deal n items (due entries, HOP block entries) to the 1024 threads in passes of
+// 1024, in thread order: the lanes of a wave take consecutive items, and consecutive entries sit in
+// consecutive LDS words, so the fire's entry reads are bank-conflict free.  Round 4's lane-major
+// dealing (l * 16 + w, FW_QLANE 1: every wave busy when fewer items than threads) put a wave's lanes
+// 16 entries apart, 32-way conflicts on every 8-byte entry read; measured round 5: thread order
+// CFG3 merge 267 -> 248 us, CFG5 317 -> 300, CFG4 196 -> 187, CFG2 131 -> 127 us per flush; blocks
+// of consecutive items for every wave (FW_QLANE 2) landed in between.
+#ifndef FW_QLANE
+#define FW_QLANE 0  // 0: thread order; 1: lane-major; 2: blocks of consecutive items per wave (A/B)
+#endif
+__device__ __forceinline__ int fire_deal(int b0, int n, int tid) {
+#if FW_QLANE == 2
+    const int rem = n - b0;
+    if (rem >= MG_BLOCK) return b0 + tid;
+    const int per = (rem + MG_BLOCK / 64 - 1) / (MG_BLOCK / 64);
+    const int l = tid & 63;
+    return l < per ? b0 + (tid >> 6) * per + l : n;
+#elif FW_QLANE == 1
+    return b0 + (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
+#else
+    return b0 + tid;
+#endif
+}
+
 // Emission is atomic-free at device scope: each superbucket appends to its own output slab
 // (LDS cursor); only slab overflow falls back to a shared overflow region.  fw_results compacts
 // slabs + overflow into one contiguous result set on demand (k_compact_*).
@@ -1766,15 +1790,11 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
             }
         __syncthreads();
         const int nd = min(S.ndue, E);
-        // due entries are dealt lane-major over the waves (lane l of wave w takes l * 16 + w):
-        // fewer due entries than threads then still keep every wave busy, so each SIMD has four
-        // waves of dependent LDS chains to interleave instead of two
-#ifndef FW_QLANE
-#define FW_QLANE 1  // 1: lane-major dealing of the due entries; 0: lane-consecutive (A/B)
-#endif
-        const int qlane = FW_QLANE ? (tid & 63) * (MG_BLOCK / 64) + (tid >> 6) : tid;
+        // due entries are dealt to every wave (fire_deal)
         if (KIND == FW_WIN_CUMULATE || KIND == FW_WIN_HOP) {
-            for (int q = qlane; q < nd; q += MG_BLOCK) {
+            for (int b0 = 0; b0 < nd; b0 += MG_BLOCK) {
+                const int q = fire_deal(b0, nd, tid);
+                if (q >= nd) continue;
                 if (KIND == FW_WIN_CUMULATE) mark_cumulate_successor<NW, E>(a, W, S, S.due[q]);
                 else mark_hop_successor<NW, E>(a, W, S, S.due[q]);
             }
@@ -1784,7 +1804,9 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
         uint32_t nf = 0;
         uint64_t fst[4] = {0, 0, 0, 0};
         const bool fs = (FW_ABL(a) & AB_FSTAMPS) != 0;
-        for (int q = qlane; q < nd; q += MG_BLOCK) {
+        for (int b0 = 0; b0 < nd; b0 += MG_BLOCK) {
+            const int q = fire_deal(b0, nd, tid);
+            if (q >= nd) continue;
             const int e = S.due[q];
             if (KIND == KIND_DSWIN) {
                 nf += fire_ds<NW, E>(a, W, S, e, sb, &s_emit);

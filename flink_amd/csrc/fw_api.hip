@@ -227,7 +227,14 @@ struct fw_handle {
     uint32_t* ar_null[2] = {};
     int64_t* ar_n[2] = {};          // row count (written by the compaction kernel)
     hipEvent_t ar_ev[2] = {};
+    hipEvent_t ar_dma_ev[2] = {};   // the DMA of buffer b's rows (started early by ar_kick)
     bool ar_copied[2] = {};         // fw_results_ready already moved buffer b's rows to the host
+    bool ar_inflight[2] = {};       // buffer b's DMA is queued (ar_kick), fw_results_ready waits for it
+    // async result delivery: CU stores of the compacted rows into mapped pinned host memory (1, the
+    // default), or DMA on the D2H stream (FW_AR_KERNEL=0).  Measured round 5 (CFG2 end to end):
+    // the DMA queues behind the next batch's H2D on the copy engine, so fw_results_ready waited
+    // 2.2 ms per step (1.18 G ev/s); the kernel stores run beside that H2D: 1.1 ms (1.64 G ev/s)
+    int ar_kernel = 1;
     int ar_cur = 0;                 // buffer of the next fw_results_async
     int ar_last = -1;               // buffer of the last one (-1: none)
     bool ar_empty[2] = {};          // that call had nothing to collect
@@ -674,6 +681,40 @@ int validate_and_plan(fw_handle* h) {
     return FW_OK;
 }
 
+// queues the DMA of async result buffer b's n rows into its pinned host buffers on the D2H stream
+int ar_enqueue_copy(fw_handle* h, int b, int64_t n) {
+    hipStream_t ds = h->d2h_stream;
+    HIP_TRY(hipMemcpyAsync(h->ar_key[b], h->ard_key[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+    HIP_TRY(hipMemcpyAsync(h->ar_ws[b], h->ard_ws[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+    HIP_TRY(hipMemcpyAsync(h->ar_we[b], h->ard_we[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+    HIP_TRY(hipMemcpyAsync(h->ar_null[b], h->ard_null[b], (size_t)n * 4, hipMemcpyDeviceToHost, ds));
+    for (int g = 0; g < h->n_out; g++)
+        HIP_TRY(hipMemcpyAsync(h->ar_val[b][g], h->ard_val[b][g], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
+    HIP_TRY(hipEventRecord(h->ar_dma_ev[b], ds));
+    return FW_OK;
+}
+
+// Starts the DMA of the last fw_results_async's rows as soon as its compaction has finished, from
+// the calls a pipelined caller makes between fw_results_async and fw_results_ready (the next batch's
+// fw_commit / push, fw_advance): the copy then runs beside that batch's kernels and
+// fw_results_ready finds it done.  Never blocks; any failure is left for fw_results_ready.
+void ar_kick(fw_handle* h) {
+    if (h->ar_kernel) return;
+    const int b = h->ar_last;
+    if (b < 0 || !h->d2h_stream || h->ar_empty[b] || h->ar_copied[b] || h->ar_inflight[b]) return;
+    if (hipEventQuery(h->ar_ev[b]) != hipSuccess) {  // compaction still queued: try at the next call
+        (void)hipGetLastError();
+        return;
+    }
+    const int64_t n = __atomic_load_n(h->ar_n[b], __ATOMIC_ACQUIRE);
+    if (n <= 0 || n > h->out_cap) return;
+    if (ar_enqueue_copy(h, b, n) != FW_OK) {
+        (void)hipGetLastError();
+        return;
+    }
+    h->ar_inflight[b] = true;
+}
+
 template <typename T>
 int dalloc(T** p, size_t count) {
     void* v = nullptr;
@@ -824,14 +865,16 @@ int alloc_async_results(fw_handle* h) {
     int rc;
     HIP_TRY(hipStreamCreateWithFlags(&h->d2h_stream, hipStreamNonBlocking));
     for (int b = 0; b < 2; b++) {
-        // plain pinned buffers: the rows arrive by DMA, not by kernel stores over PCIe
-        HIP_TRY(hipHostMalloc((void**)&h->ar_key[b], n * 8, hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc((void**)&h->ar_ws[b], n * 8, hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc((void**)&h->ar_we[b], n * 8, hipHostMallocDefault));
-        HIP_TRY(hipHostMalloc((void**)&h->ar_null[b], n * 4, hipHostMallocDefault));
-        for (int g = 0; g < h->n_out; g++) HIP_TRY(hipHostMalloc((void**)&h->ar_val[b][g], n * 8, hipHostMallocDefault));
+        // pinned host buffers: mapped for the kernel delivery, plain for the DMA
+        const unsigned fl = h->ar_kernel ? hipHostMallocMapped : hipHostMallocDefault;
+        HIP_TRY(hipHostMalloc((void**)&h->ar_key[b], n * 8, fl));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_ws[b], n * 8, fl));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_we[b], n * 8, fl));
+        HIP_TRY(hipHostMalloc((void**)&h->ar_null[b], n * 4, fl));
+        for (int g = 0; g < h->n_out; g++) HIP_TRY(hipHostMalloc((void**)&h->ar_val[b][g], n * 8, fl));
         HIP_TRY(hipHostMalloc((void**)&h->ar_n[b], 8, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(hipEventCreateWithFlags(&h->ar_ev[b], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h->ar_dma_ev[b], hipEventDisableTiming));
         if ((rc = dalloc(&h->ard_key[b], n))) return rc;
         if ((rc = dalloc(&h->ard_ws[b], n))) return rc;
         if ((rc = dalloc(&h->ard_we[b], n))) return rc;
@@ -1105,6 +1148,7 @@ int fw_create(const fw_config* cfg, fw_handle** out) {
     h->cfg = *cfg;
     if (const char* ab = getenv("FW_ABLATE")) h->ablate = atoi(ab);
     if (const char* fo = getenv("FW_FOLD")) h->fold_always = atoi(fo);
+    if (const char* ak = getenv("FW_AR_KERNEL")) h->ar_kernel = atoi(ak);
     if (const char* fp = getenv("FW_FILL_PCT")) h->fill_pct = std::min(95, std::max(10, atoi(fp)));
     if (const char* si = getenv("FW_SKIP_IDLE")) h->skip_idle = atoi(si) != 0;
     int rc = validate_and_plan(h);
@@ -1199,13 +1243,17 @@ int fw_destroy(fw_handle* h) {
         for (int g = 0; g < FW_MAX_AGGS; g++) hipHostFree(h->ar_val[b][g]);
         hipHostFree(h->ar_n[b]);
         if (h->ar_ev[b]) hipEventDestroy(h->ar_ev[b]);
+        if (h->ar_dma_ev[b]) hipEventDestroy(h->ar_dma_ev[b]);
         hipFree(h->ard_key[b]);
         hipFree(h->ard_ws[b]);
         hipFree(h->ard_we[b]);
         hipFree(h->ard_null[b]);
         for (int g = 0; g < FW_MAX_AGGS; g++) hipFree(h->ard_val[b][g]);
     }
-    if (h->d2h_stream) hipStreamDestroy(h->d2h_stream);
+    if (h->d2h_stream) {
+        hipStreamSynchronize(h->d2h_stream);  // an early DMA (ar_kick) may still be reading the buffers
+        hipStreamDestroy(h->d2h_stream);
+    }
     if (h->cstream) hipStreamDestroy(h->cstream);
     delete h->timer;
     if (h->stream) hipStreamDestroy(h->stream);
@@ -1257,6 +1305,7 @@ int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out) {
 
 int fw_commit(fw_handle* h, int64_t n) {
     if (!h) return fail(FW_E_INVALID, "null handle");
+    ar_kick(h);
     if (h->reserved < 0 || n > h->reserved || n < 0) return fail(FW_E_STATE, "commit without matching reserve");
     h->reserved = -1;
     const int b = h->stage_cur;
@@ -1272,19 +1321,23 @@ int fw_commit(fw_handle* h, int64_t n) {
     // operator stream waits for the copies.  The previous batch's ingest and merge overlap them.
     hipStream_t cs = h->cstream;
     HIP_TRY(hipStreamWaitEvent(cs, h->dstage_free[b], 0));
+    // (a second copy stream for the upper half of every column was measured slower: CFG2 end to end
+    // 1.76 -> 1.26 G ev/s, its enqueue blocking the host 0.9 ms per batch)
+    auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs);
+    };
     if (h->keyrow) {
-        HIP_TRY(hipMemcpyAsync(h->d_kro[b], h->h_kro[b], (n + 1) * 8, hipMemcpyHostToDevice, cs));
-        HIP_TRY(hipMemcpyAsync(h->d_krb[b], h->h_krb[b], (size_t)krb_n, hipMemcpyHostToDevice, cs));
+        HIP_TRY(h2d(h->d_kro[b], h->h_kro[b], (n + 1) * 8));
+        HIP_TRY(h2d(h->d_krb[b], h->h_krb[b], (size_t)krb_n));
     } else {
-        HIP_TRY(hipMemcpyAsync(h->d_key[b], h->h_key[b], n * 8, hipMemcpyHostToDevice, cs));
+        HIP_TRY(h2d(h->d_key[b], h->h_key[b], n * 8));
     }
-    HIP_TRY(hipMemcpyAsync(h->d_ts[b], h->h_ts[b], n * 8, hipMemcpyHostToDevice, cs));
-    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED)
-        HIP_TRY(hipMemcpyAsync(h->d_kh[b], h->h_kh[b], n * 4, hipMemcpyHostToDevice, cs));
+    HIP_TRY(h2d(h->d_ts[b], h->h_ts[b], n * 8));
+    if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED) HIP_TRY(h2d(h->d_kh[b], h->h_kh[b], n * 4));
     for (int s = 0; s < h->nv; s++) {
         const int v = h->slot_col[s];
-        HIP_TRY(hipMemcpyAsync(h->d_val[b][v], h->h_val[b][v], n * 8, hipMemcpyHostToDevice, cs));
-        if (h->d_nul[b][v]) HIP_TRY(hipMemcpyAsync(h->d_nul[b][v], h->h_nul[b][v], n, hipMemcpyHostToDevice, cs));
+        HIP_TRY(h2d(h->d_val[b][v], h->h_val[b][v], n * 8));
+        if (h->d_nul[b][v]) HIP_TRY(h2d(h->d_nul[b][v], h->h_nul[b][v], n));
     }
     HIP_TRY(hipEventRecord(h->stage_ev[b], cs));
     HIP_TRY(hipStreamWaitEvent(h->stream, h->stage_ev[b], 0));
@@ -1322,6 +1375,7 @@ int fw_push_device(fw_handle* h, int64_t n, const int64_t* d_key, const int64_t*
                    const void* const* d_values, const uint8_t* const* d_nulls) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     if (n < 0) return fail(FW_E_INVALID, "negative n");
+    ar_kick(h);
     if (n == 0) return FW_OK;
     if (!d_key || !d_ts) return fail(FW_E_INVALID, "null key/ts column");
     if (h->keyrow) return fail(FW_E_INVALID, "a FW_KEYHASH_KEYROW operator takes key rows (fw_push_device_key_rows)");
@@ -1373,6 +1427,7 @@ int fw_push_device_packed_segments(fw_handle* h, int32_t n_segs, int64_t seg_len
 
 int fw_advance(fw_handle* h, int64_t watermark) {
     if (!h) return fail(FW_E_INVALID, "null handle");
+    ar_kick(h);
     // A SQL watermark below the next trigger watermark crosses no slice end: no window fires, no
     // buffer flush is due (AbstractSliceSyncStateWindowAggProcessor.advanceProgress :139-153 only
     // flushes at a trigger) and lateness is unchanged (no window end lies between the old and the
@@ -1529,6 +1584,10 @@ int fw_results_async(fw_handle* h) {
     h->ar_last = b;
     h->ar_empty[b] = h->reset_pending;  // consumed and nothing emitted since
     h->ar_copied[b] = false;
+    if (h->ar_inflight[b]) {  // an early DMA of this buffer's previous rows: the compaction waits for it
+        HIP_TRY(hipStreamWaitEvent(h->stream, h->ar_dma_ev[b], 0));
+        h->ar_inflight[b] = false;
+    }
     if (h->ar_empty[b]) return FW_OK;
     CompactArgs ca{};
     ca.ctrl = h->ctrl;
@@ -1553,6 +1612,28 @@ int fw_results_async(fw_handle* h) {
     ca.host_n = mapped(h->ar_n[b]);
     if (!ca.host_n) return fail(FW_E_DEVICE, "mapped result count unavailable");
     HIP_TRY(launch_compact(ca, h->stream, h->timer));
+    if (h->ar_kernel) {
+        CopyOutArgs co{};
+        co.d_n = h->coff + h->ks.n_sb + 1;
+        co.n_aggs = h->n_out;
+        co.cap = h->out_cap;
+        co.src_key = h->ard_key[b];
+        co.src_ws = h->ard_ws[b];
+        co.src_we = h->ard_we[b];
+        co.src_null = h->ard_null[b];
+        co.dst_key = mapped(h->ar_key[b]);
+        co.dst_ws = mapped(h->ar_ws[b]);
+        co.dst_we = mapped(h->ar_we[b]);
+        co.dst_null = mapped(h->ar_null[b]);
+        for (int g = 0; g < h->n_out; g++) {
+            co.src_val[g] = h->ard_val[b][g];
+            co.dst_val[g] = mapped(h->ar_val[b][g]);
+            if (!co.dst_val[g]) return fail(FW_E_DEVICE, "mapped result buffer unavailable");
+        }
+        if (!co.dst_key || !co.dst_ws || !co.dst_we || !co.dst_null) return fail(FW_E_DEVICE, "mapped result buffer unavailable");
+        HIP_TRY(launch_copy_out(co, h->stream));
+        h->ar_copied[b] = true;  // the rows are in host memory once ar_ev[b] has fired
+    }
     HIP_TRY(hipEventRecord(h->ar_ev[b], h->stream));
     h->reset_pending = true;  // the rows are collected: the next merge launch starts the slabs afresh
     return FW_OK;
@@ -1636,14 +1717,12 @@ int fw_results_ready(fw_handle* h, fw_result* out) {
     const int na = h->n_out;
     const int nv = h->ad.first_word >= 0 ? na - 1 : na;
     if (n > 0 && !h->ar_copied[b]) {  // the rows by DMA on the D2H stream (no CU time, no operator-stream slot)
-        hipStream_t ds = h->d2h_stream;
-        HIP_TRY(hipMemcpyAsync(h->ar_key[b], h->ard_key[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
-        HIP_TRY(hipMemcpyAsync(h->ar_ws[b], h->ard_ws[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
-        HIP_TRY(hipMemcpyAsync(h->ar_we[b], h->ard_we[b], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
-        HIP_TRY(hipMemcpyAsync(h->ar_null[b], h->ard_null[b], (size_t)n * 4, hipMemcpyDeviceToHost, ds));
-        for (int g = 0; g < na; g++)
-            HIP_TRY(hipMemcpyAsync(h->ar_val[b][g], h->ard_val[b][g], (size_t)n * 8, hipMemcpyDeviceToHost, ds));
-        HIP_TRY(hipStreamSynchronize(ds));
+        if (!h->ar_inflight[b]) {  // not started early by ar_kick
+            int rc = ar_enqueue_copy(h, b, n);
+            if (rc) return rc;
+            h->ar_inflight[b] = true;
+        }
+        HIP_TRY(hipEventSynchronize(h->ar_dma_ev[b]));
         h->ar_copied[b] = true;
     }
     out->n = n;

@@ -658,6 +658,25 @@ struct CompactArgs {
     int64_t* host_n;         // fw_results_async: also store the row count here (mapped host memory)
 };
 
+// fw_results_async with kernel delivery (FW_AR_KERNEL=1): the compacted rows copied by CU stores into
+// mapped pinned host memory (runs beside the H2D of the next batch, which occupies the DMA engine)
+struct CopyOutArgs {
+    const int64_t* d_n;      // rows (the compaction's total, device)
+    int32_t n_aggs;
+    int64_t cap;
+    const int64_t* src_key;
+    const int64_t* src_ws;
+    const int64_t* src_we;
+    const uint64_t* src_val[FW_MAX_AGGS];
+    const uint32_t* src_null;
+    int64_t* dst_key;
+    int64_t* dst_ws;
+    int64_t* dst_we;
+    uint64_t* dst_val[FW_MAX_AGGS];
+    uint32_t* dst_null;
+};
+hipError_t launch_copy_out(const CopyOutArgs& a, hipStream_t s);
+
 // In-kernel launch timing (fw_set_profiling FW_PROF_DEVICE): per kernel class 4 words -- the
 // constant-rate device clock (s_memrealtime) when block 0 started the current launch, the summed
 // launch durations, the launch count, spare.  Block 0 stamps the start; the last workgroup of the

@@ -134,6 +134,22 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s, KTimer* t) {
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(BLOCK) void k_copy_out(CopyOutArgs a) {
+    const int64_t n = min(*a.d_n, a.cap);
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * BLOCK) {
+        a.dst_key[i] = a.src_key[i];
+        a.dst_ws[i] = a.src_ws[i];
+        a.dst_we[i] = a.src_we[i];
+        a.dst_null[i] = a.src_null[i];
+        for (int g = 0; g < a.n_aggs; g++) a.dst_val[g][i] = a.src_val[g][i];
+    }
+}
+
+hipError_t launch_copy_out(const CopyOutArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
     hipLaunchKernelGGL(k_init_ctrl, dim3(1), dim3(64), 0, s, c);
     return hipGetLastError();

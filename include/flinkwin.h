@@ -372,9 +372,10 @@ int fw_results_reset(fw_handle* h);
    fw_results_async queues the collection of every result row emitted since the last collection
    (compacted on the device into one of two device buffers of the handle; only the row count goes to
    mapped host memory) and returns at once (the rows count as consumed, as after fw_results_reset);
-   fw_results_ready waits for the LAST fw_results_async's compaction, moves its rows into pinned host
-   memory by DMA (v8: hipMemcpyAsync on the handle's D2H stream, no CU time) and returns them as host
-   arrays, valid until the second fw_results_async after it.  So a caller emits watermark b's rows
+   fw_results_ready waits for the LAST fw_results_async's rows to reach pinned host memory (v8: a
+   copy kernel queued behind the compaction stores them into mapped host memory, beside the next
+   batch's H2D on the copy engine; FW_AR_KERNEL=0 moves them by hipMemcpyAsync on a D2H stream
+   instead) and returns them as host arrays, valid until the second fw_results_async after it.  So a caller emits watermark b's rows
    while batch b + 1 is ingested.  Not for FW_KEYHASH_KEYROW operators (fw_results returns their key
    rows). */
 int fw_results_async(fw_handle* h);

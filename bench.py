@@ -170,6 +170,10 @@ def main():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: time the steps without the per-launch hipEvents (no roofline)")
     ap.add_argument("--e2e-steps", type=int, default=8)
+    ap.add_argument("--e2e-depth", type=int, default=2, choices=[1, 2],
+                    help="end-to-end leg: read each watermark's rows 1 or 2 watermarks after collecting them "
+                         "(fw_results_ready returns the oldest outstanding collection; 2 keeps the collection "
+                         "off the host's critical path)")
     ap.add_argument("--kernel-timing", default="device", choices=["device", "events"],
                     help="per-launch kernel timing: in-kernel device-clock stamps (default) or hipEvents")
     ap.add_argument("--plan", default="auto", choices=["auto", "one", "two"],
@@ -516,6 +520,7 @@ def main():
         _native.check(L.fw_commit(he._h, 0))
         he.results_async()  # allocates the pinned result buffers (untimed); nothing to collect yet
         he.results_ready(copy=False)
+        depth = args.e2e_depth
         rows_out = 0
         t_reserve = t_fill = t_ready = t_commit = t_adv = t_async = 0.0
         te0 = time.perf_counter()
@@ -532,18 +537,19 @@ def main():
             t3c = time.perf_counter()
             he.advance(watermark(b, wl["rate"]))
             t4 = time.perf_counter()
-            if b:
-                rows_out += len(he.results_ready(copy=False)["key"])  # watermark b - 1's rows
+            he.results_async()  # watermark b's rows, collected while the next batches are ingested
             t5 = time.perf_counter()
-            he.results_async()
+            if b >= depth:
+                rows_out += len(he.results_ready(copy=False)["key"])  # watermark b - depth's rows
             t_reserve += t2 - t1
             t_fill += t3 - t2
             t_commit += t3c - t3
             t_adv += t4 - t3c
-            t_ready += t5 - t4
-            t_async += time.perf_counter() - t5
+            t_async += t5 - t4
+            t_ready += time.perf_counter() - t5
         t6 = time.perf_counter()
-        rows_out += len(he.results_ready(copy=False)["key"])
+        for _ in range(min(depth, ns)):
+            rows_out += len(he.results_ready(copy=False)["key"])
         he.sync()
         te = time.perf_counter() - te0
         t_ready += time.perf_counter() - t6
@@ -560,7 +566,8 @@ def main():
                "fill_GBps": ns * B * wl["w_in"] / max(t_fill, 1e-9) / 1e9,
                "path": "numpy batch -> pinned staging (fw_reserve, 8 fill threads) -> H2D on the copy stream, "
                        "overlapping the previous batch's ingest (fw_commit) -> advance -> rows into pinned host "
-                       "memory (fw_results_async), read one watermark later (fw_results_ready)"}
+                       f"memory (fw_results_async), read {depth} watermark(s) later (fw_results_ready)",
+               "results_depth": depth}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -212,32 +212,34 @@ struct fw_handle {
     int64_t reserved = -1;
 
     // asynchronous result delivery (fw_results_async / fw_results_ready): rows compacted on the
-    // device into one of two device buffers (ard_*), then moved by DMA (hipMemcpyAsync on the D2H
-    // stream) into pinned host buffers (ar_*); only the row count goes through mapped memory
-    int64_t* ard_key[2] = {};
-    int64_t* ard_ws[2] = {};
-    int64_t* ard_we[2] = {};
-    uint64_t* ard_val[2][FW_MAX_AGGS] = {};
-    uint32_t* ard_null[2] = {};
+    // device into one of FW_AR_BUFS device buffers (ard_*), then moved into pinned host buffers
+    // (ar_*); only the row count goes through mapped memory.  Up to FW_AR_BUFS collections are
+    // outstanding; fw_results_ready returns the oldest (ar_q, a FIFO of buffer indices)
+    int64_t* ard_key[FW_AR_BUFS] = {};
+    int64_t* ard_ws[FW_AR_BUFS] = {};
+    int64_t* ard_we[FW_AR_BUFS] = {};
+    uint64_t* ard_val[FW_AR_BUFS][FW_MAX_AGGS] = {};
+    uint32_t* ard_null[FW_AR_BUFS] = {};
     hipStream_t d2h_stream = nullptr;
-    int64_t* ar_key[2] = {};
-    int64_t* ar_ws[2] = {};
-    int64_t* ar_we[2] = {};
-    uint64_t* ar_val[2][FW_MAX_AGGS] = {};
-    uint32_t* ar_null[2] = {};
-    int64_t* ar_n[2] = {};          // row count (written by the compaction kernel)
-    hipEvent_t ar_ev[2] = {};
-    hipEvent_t ar_dma_ev[2] = {};   // the DMA of buffer b's rows (started early by ar_kick)
-    bool ar_copied[2] = {};         // fw_results_ready already moved buffer b's rows to the host
-    bool ar_inflight[2] = {};       // buffer b's DMA is queued (ar_kick), fw_results_ready waits for it
+    int64_t* ar_key[FW_AR_BUFS] = {};
+    int64_t* ar_ws[FW_AR_BUFS] = {};
+    int64_t* ar_we[FW_AR_BUFS] = {};
+    uint64_t* ar_val[FW_AR_BUFS][FW_MAX_AGGS] = {};
+    uint32_t* ar_null[FW_AR_BUFS] = {};
+    int64_t* ar_n[FW_AR_BUFS] = {};          // row count (written by the compaction kernel)
+    hipEvent_t ar_ev[FW_AR_BUFS] = {};
+    hipEvent_t ar_dma_ev[FW_AR_BUFS] = {};   // the DMA of buffer b's rows (started early by ar_kick)
+    bool ar_copied[FW_AR_BUFS] = {};         // buffer b's rows are (or are queued to be) in host memory
+    bool ar_inflight[FW_AR_BUFS] = {};       // buffer b's DMA is queued (ar_kick), fw_results_ready waits for it
     // async result delivery: CU stores of the compacted rows into mapped pinned host memory (1, the
     // default), or DMA on the D2H stream (FW_AR_KERNEL=0).  Measured round 5 (CFG2 end to end):
     // the DMA queues behind the next batch's H2D on the copy engine, so fw_results_ready waited
     // 2.2 ms per step (1.18 G ev/s); the kernel stores run beside that H2D: 1.1 ms (1.64 G ev/s)
     int ar_kernel = 1;
     int ar_cur = 0;                 // buffer of the next fw_results_async
-    int ar_last = -1;               // buffer of the last one (-1: none)
-    bool ar_empty[2] = {};          // that call had nothing to collect
+    int ar_q[FW_AR_BUFS] = {};      // outstanding collections, oldest first
+    int ar_qhead = 0, ar_qn = 0;
+    bool ar_empty[FW_AR_BUFS] = {}; // that call had nothing to collect
 
     // FW_KEYHASH_KEYROW: the key-row intern table, per-push intern output, key-row staging
     bool keyrow = false;
@@ -699,20 +701,22 @@ int ar_enqueue_copy(fw_handle* h, int b, int64_t n) {
 // fw_commit / push, fw_advance): the copy then runs beside that batch's kernels and
 // fw_results_ready finds it done.  Never blocks; any failure is left for fw_results_ready.
 void ar_kick(fw_handle* h) {
-    if (h->ar_kernel) return;
-    const int b = h->ar_last;
-    if (b < 0 || !h->d2h_stream || h->ar_empty[b] || h->ar_copied[b] || h->ar_inflight[b]) return;
-    if (hipEventQuery(h->ar_ev[b]) != hipSuccess) {  // compaction still queued: try at the next call
-        (void)hipGetLastError();
-        return;
+    if (h->ar_kernel || !h->d2h_stream) return;
+    for (int i = 0; i < h->ar_qn; i++) {  // outstanding collections, oldest first
+        const int b = h->ar_q[(h->ar_qhead + i) % FW_AR_BUFS];
+        if (h->ar_empty[b] || h->ar_copied[b] || h->ar_inflight[b]) continue;
+        if (hipEventQuery(h->ar_ev[b]) != hipSuccess) {  // compaction still queued: try at the next call
+            (void)hipGetLastError();
+            return;
+        }
+        const int64_t n = __atomic_load_n(h->ar_n[b], __ATOMIC_ACQUIRE);
+        if (n <= 0 || n > h->out_cap) continue;
+        if (ar_enqueue_copy(h, b, n) != FW_OK) {
+            (void)hipGetLastError();
+            return;
+        }
+        h->ar_inflight[b] = true;
     }
-    const int64_t n = __atomic_load_n(h->ar_n[b], __ATOMIC_ACQUIRE);
-    if (n <= 0 || n > h->out_cap) return;
-    if (ar_enqueue_copy(h, b, n) != FW_OK) {
-        (void)hipGetLastError();
-        return;
-    }
-    h->ar_inflight[b] = true;
 }
 
 template <typename T>
@@ -864,7 +868,7 @@ int alloc_async_results(fw_handle* h) {
     const size_t n = (size_t)h->out_cap;
     int rc;
     HIP_TRY(hipStreamCreateWithFlags(&h->d2h_stream, hipStreamNonBlocking));
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < FW_AR_BUFS; b++) {
         // pinned host buffers: mapped for the kernel delivery, plain for the DMA
         const unsigned fl = h->ar_kernel ? hipHostMallocMapped : hipHostMallocDefault;
         HIP_TRY(hipHostMalloc((void**)&h->ar_key[b], n * 8, fl));
@@ -1236,6 +1240,9 @@ int fw_destroy(fw_handle* h) {
             hipFree(h->d_val[b][v]);
             hipFree(h->d_nul[b][v]);
         }
+    }
+    if (h->d2h_stream) hipStreamSynchronize(h->d2h_stream);  // an early DMA (ar_kick) may still be reading the buffers
+    for (int b = 0; b < FW_AR_BUFS; b++) {
         hipHostFree(h->ar_key[b]);
         hipHostFree(h->ar_ws[b]);
         hipHostFree(h->ar_we[b]);
@@ -1250,10 +1257,7 @@ int fw_destroy(fw_handle* h) {
         hipFree(h->ard_null[b]);
         for (int g = 0; g < FW_MAX_AGGS; g++) hipFree(h->ard_val[b][g]);
     }
-    if (h->d2h_stream) {
-        hipStreamSynchronize(h->d2h_stream);  // an early DMA (ar_kick) may still be reading the buffers
-        hipStreamDestroy(h->d2h_stream);
-    }
+    if (h->d2h_stream) hipStreamDestroy(h->d2h_stream);
     if (h->cstream) hipStreamDestroy(h->cstream);
     delete h->timer;
     if (h->stream) hipStreamDestroy(h->stream);
@@ -1579,9 +1583,12 @@ int fw_results_async(fw_handle* h) {
     if (h->keyrow) return fail(FW_E_INVALID, "key-row operators return their rows through fw_results");
     int rc = alloc_async_results(h);
     if (rc) return rc;
+    if (h->ar_qn == FW_AR_BUFS)
+        return fail(FW_E_STATE, "%d result collections outstanding: fw_results_ready first", FW_AR_BUFS);
     const int b = h->ar_cur;
-    h->ar_cur ^= 1;
-    h->ar_last = b;
+    h->ar_cur = (b + 1) % FW_AR_BUFS;
+    h->ar_q[(h->ar_qhead + h->ar_qn) % FW_AR_BUFS] = b;
+    h->ar_qn++;
     h->ar_empty[b] = h->reset_pending;  // consumed and nothing emitted since
     h->ar_copied[b] = false;
     if (h->ar_inflight[b]) {  // an early DMA of this buffer's previous rows: the compaction waits for it
@@ -1706,8 +1713,10 @@ int fw_results_device(fw_handle* h, fw_result* out, int64_t** d_n) {
 int fw_results_ready(fw_handle* h, fw_result* out) {
     if (!h || !out) return fail(FW_E_INVALID, "null argument");
     memset(out, 0, sizeof *out);
-    const int b = h->ar_last;
-    if (b < 0) return fail(FW_E_STATE, "fw_results_ready without fw_results_async");
+    if (h->ar_qn == 0) return fail(FW_E_STATE, "fw_results_ready without an outstanding fw_results_async");
+    const int b = h->ar_q[h->ar_qhead];  // the oldest outstanding collection
+    h->ar_qhead = (h->ar_qhead + 1) % FW_AR_BUFS;
+    h->ar_qn--;
     if (h->ar_empty[b]) return FW_OK;
     HIP_TRY(hipEventSynchronize(h->ar_ev[b]));  // the compaction (long done: it ran a step ago)
     const int64_t n = __atomic_load_n(h->ar_n[b], __ATOMIC_ACQUIRE);

@@ -658,6 +658,10 @@ struct CompactArgs {
     int64_t* host_n;         // fw_results_async: also store the row count here (mapped host memory)
 };
 
+// fw_results_async buffers: up to this many collections outstanding (fw_results_ready reads the
+// oldest), so a caller can read watermark b - 2's rows while b - 1's and b's are still in flight
+constexpr int FW_AR_BUFS = 3;
+
 // fw_results_async with kernel delivery (FW_AR_KERNEL=1): the compacted rows copied by CU stores into
 // mapped pinned host memory (runs beside the H2D of the next batch, which occupies the DMA engine)
 struct CopyOutArgs {

@@ -300,9 +300,9 @@ class WindowAggHandle:
         check(lib().fw_results_async(self._h))
 
     def results_ready(self, copy=True):
-        """The rows of the last results_async() (waits for them): the dict results() returns.  With
-        copy=False the arrays are views of the handle's pinned buffers, valid until the second
-        results_async() after that one."""
+        """The rows of the OLDEST outstanding results_async() (waits for them; up to three may be
+        outstanding): the dict results() returns.  With copy=False the arrays are views of the
+        handle's pinned buffers, valid until the third results_async() after that one."""
         r = abi.fw_result()
         check(lib().fw_results_ready(self._h, C.byref(r)))
         n = r.n

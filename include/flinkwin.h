@@ -370,14 +370,17 @@ int fw_results_reset(fw_handle* h);
 /* v6, pipelined emission (the shim's collector side of WindowAggOperator.onTimer ->
    output.collect, WindowAggOperator.java:227-238, and WindowOperator.emitWindowContents :568-575):
    fw_results_async queues the collection of every result row emitted since the last collection
-   (compacted on the device into one of two device buffers of the handle; only the row count goes to
-   mapped host memory) and returns at once (the rows count as consumed, as after fw_results_reset);
-   fw_results_ready waits for the LAST fw_results_async's rows to reach pinned host memory (v8: a
-   copy kernel queued behind the compaction stores them into mapped host memory, beside the next
-   batch's H2D on the copy engine; FW_AR_KERNEL=0 moves them by hipMemcpyAsync on a D2H stream
-   instead) and returns them as host arrays, valid until the second fw_results_async after it.  So a caller emits watermark b's rows
-   while batch b + 1 is ingested.  Not for FW_KEYHASH_KEYROW operators (fw_results returns their key
-   rows). */
+   (compacted on the device into one of the handle's FW_AR_BUFS = 3 device buffers; only the row
+   count goes to mapped host memory) and returns at once (the rows count as consumed, as after
+   fw_results_reset); at most 3 collections may be outstanding (a 4th call fails with FW_E_STATE).
+   fw_results_ready returns the OLDEST outstanding collection (v8; with one outstanding, as before,
+   the last one): it waits for its rows to reach pinned host memory (a copy kernel queued behind the
+   compaction stores them into mapped host memory, beside the next batch's H2D on the copy engine;
+   FW_AR_KERNEL=0 moves them by hipMemcpyAsync on a D2H stream instead) and returns them as host
+   arrays, valid until the third fw_results_async after their own.  So a caller emits watermark b's
+   rows while batch b + 1 is ingested, or -- reading two collections behind -- while batches b + 1
+   and b + 2 are ingested, which takes the collection off the caller's critical path.  Not for
+   FW_KEYHASH_KEYROW operators (fw_results returns their key rows). */
 int fw_results_async(fw_handle* h);
 int fw_results_ready(fw_handle* h, fw_result* out);
 /* v6, device-side consumers (the two-phase plan's LOCAL -> GLOBAL exchange): queues the collection

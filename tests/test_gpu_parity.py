@@ -753,18 +753,20 @@ def test_partition_packed_equals_partition_by_dest():
         o += int(cnt[d])
 
 
+@pytest.mark.parametrize("depth", [1, 2])
 @pytest.mark.parametrize("name", ["sql_tumble_int_aggs", "sql_hop", "sql_tumble_double", "ds_sliding_max"])
-def test_async_results_pipeline_matches_oracle(name):
+def test_async_results_pipeline_matches_oracle(name, depth):
     """fw_results_async / fw_results_ready: watermark b's rows are collected into pinned host memory
     while batch b + 1 is pushed (three pushes per watermark through the double-buffered staging)
-    and read one step later -- the same rows as the oracle's, watermark by watermark."""
+    and read ``depth`` steps later (the oldest outstanding collection first) -- the same rows as
+    the oracle's, watermark by watermark.  A fourth outstanding collection is refused."""
     from flink_amd.runtime.handle import WindowAggHandle
     from oracle.oracle import OracleOperator
     kw = CASES[name]
     cfg = _cfg(kw)
     dc = _double_cols(kw)
     o, g = OracleOperator(cfg), WindowAggHandle(cfg)
-    pending = None
+    pending = []
     for bi, (k, t, iv, dv, wm) in enumerate(_stream(zlib.crc32(name.encode()) % 997, 30000, 500, ooo=2 * kw["size_ms"],
                                                     step_ms=1500, n_wm=16)):
         vals = [iv, dv.view(np.int64)]
@@ -774,11 +776,25 @@ def test_async_results_pipeline_matches_oracle(name):
         o.process_watermark(wm)
         g.advance(wm)
         want = _rows(o.results(clear=True), cfg, dc)
-        if pending is not None:
-            _compare(_rows(g.results_ready(), cfg, dc), pending, dc, f"watermark before batch {bi}")
+        if depth == 1 and pending:
+            _compare(_rows(g.results_ready(), cfg, dc), pending.pop(0), dc, f"watermark before batch {bi}")
         g.results_async()
-        pending = want
-    _compare(_rows(g.results_ready(), cfg, dc), pending, dc, "last watermark")
+        pending.append(want)
+        if depth == 2 and len(pending) > 2:
+            _compare(_rows(g.results_ready(), cfg, dc), pending.pop(0), dc, f"watermark two before batch {bi}")
+    if depth == 2:
+        from flink_amd._native import FlinkWinError
+        g.results_async()  # a third outstanding collection is allowed (nothing emitted since: no rows)
+        with pytest.raises(FlinkWinError):
+            g.results_async()
+        pending.append(None)
+    while pending:
+        want = pending.pop(0)
+        rows = _rows(g.results_ready(), cfg, dc)
+        if want is None:
+            assert len(rows) == 0
+        else:
+            _compare(rows, want, dc, "last watermarks")
     assert g.stats()["error_flags"] == 0 and g.stats()["num_late_records_dropped"] == o.late_dropped
     g.close()
 

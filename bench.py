@@ -495,9 +495,9 @@ def main():
     # What the JNI shim does, pipelined the way the handle allows: the host fills
     # the operator's pinned staging columns (fw_reserve; 8 threads copying slices of the numpy
     # batch, standing for the shim's record serialisation), fw_commit moves them over PCIe on the
-    # copy stream while the previous batch is still being ingested (double-buffered device staging),
-    # and each watermark's rows are collected into pinned host memory by fw_results_async and read
-    # one step later (fw_results_ready).  Reported beside the device-resident `value`, never as it.
+    # copy stream while the previous batch is still being ingested (two staging sets), and each
+    # watermark's rows are collected into pinned host memory by fw_results_async and read
+    # --e2e-depth steps later (fw_results_ready).  Reported beside the device-resident `value`, never as it.
     e2e = None
     if world == 1 and not args.no_e2e and args.e2e_steps > 0:
         from concurrent.futures import ThreadPoolExecutor

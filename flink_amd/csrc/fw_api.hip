@@ -191,24 +191,24 @@ struct fw_handle {
     uint64_t* res_val[FW_MAX_AGGS] = {};
     uint32_t* res_null = nullptr;
 
-    // host-staged ingest (double-buffered pinned columns)
+    // host-staged ingest (FW_STAGE_BUFS pinned column sets)
     int64_t stage_cap = 0;
     int stage_cur = 0;
-    int64_t* h_key[2] = {};
-    int64_t* h_ts[2] = {};
-    int32_t* h_kh[2] = {};
-    int64_t* h_val[2][FW_MAX_COLS] = {};
-    uint8_t* h_nul[2][FW_MAX_COLS] = {};
-    hipEvent_t stage_ev[2] = {};   // H2D from host buffer b done (copy stream)
-    // device staging, double-buffered: batch b+1 crosses PCIe on the copy stream while batch b is
-    // ingested on the operator stream
+    int64_t* h_key[FW_STAGE_BUFS] = {};
+    int64_t* h_ts[FW_STAGE_BUFS] = {};
+    int32_t* h_kh[FW_STAGE_BUFS] = {};
+    int64_t* h_val[FW_STAGE_BUFS][FW_MAX_COLS] = {};
+    uint8_t* h_nul[FW_STAGE_BUFS][FW_MAX_COLS] = {};
+    hipEvent_t stage_ev[FW_STAGE_BUFS] = {};   // H2D from host buffer b done (copy stream)
+    // device staging, one set per host set: batch b+1 crosses PCIe on the copy stream while batch b
+    // is ingested on the operator stream
     hipStream_t cstream = nullptr;
-    hipEvent_t dstage_free[2] = {};  // the ingest that read device buffer b has run (operator stream)
-    int64_t* d_key[2] = {};
-    int64_t* d_ts[2] = {};
-    int32_t* d_kh[2] = {};
-    int64_t* d_val[2][FW_MAX_COLS] = {};
-    uint8_t* d_nul[2][FW_MAX_COLS] = {};
+    hipEvent_t dstage_free[FW_STAGE_BUFS] = {};  // the ingest that read device buffer b has run (operator stream)
+    int64_t* d_key[FW_STAGE_BUFS] = {};
+    int64_t* d_ts[FW_STAGE_BUFS] = {};
+    int32_t* d_kh[FW_STAGE_BUFS] = {};
+    int64_t* d_val[FW_STAGE_BUFS][FW_MAX_COLS] = {};
+    uint8_t* d_nul[FW_STAGE_BUFS][FW_MAX_COLS] = {};
     int64_t reserved = -1;
 
     // asynchronous result delivery (fw_results_async / fw_results_ready): rows compacted on the
@@ -247,11 +247,11 @@ struct fw_handle {
     int64_t kr_scratch_n = 0;
     int64_t* d_kid = nullptr;       // interned ids of the push being ingested
     int32_t* d_khash = nullptr;     // their hashCodes
-    int64_t* h_kro[2] = {};         // pinned staging: key row offsets / bytes (fw_reserve)
-    uint8_t* h_krb[2] = {};
+    int64_t* h_kro[FW_STAGE_BUFS] = {};         // pinned staging: key row offsets / bytes (fw_reserve)
+    uint8_t* h_krb[FW_STAGE_BUFS] = {};
     int64_t krb_cap = 0;            // staging bytes per batch
-    int64_t* d_kro[2] = {};
-    uint8_t* d_krb[2] = {};
+    int64_t* d_kro[FW_STAGE_BUFS] = {};
+    uint8_t* d_krb[FW_STAGE_BUFS] = {};
     int32_t* res_kr_len = nullptr;  // result key rows (fw_results)
     uint64_t* res_kr_img = nullptr;
     std::vector<int32_t> r_kr_len;
@@ -832,7 +832,7 @@ int alloc_staging(fw_handle* h) {
     const size_t n = (size_t)h->stage_cap;
     HIP_TRY(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
     int rc;
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < FW_STAGE_BUFS; b++) {
         HIP_TRY(hipHostMalloc((void**)&h->h_key[b], n * 8, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc((void**)&h->h_ts[b], n * 8, hipHostMallocDefault));
         HIP_TRY(hipHostMalloc((void**)&h->h_kh[b], n * 4, hipHostMallocDefault));
@@ -1196,7 +1196,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->d_khash);
     hipFree(h->res_kr_len);
     hipFree(h->res_kr_img);
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < FW_STAGE_BUFS; b++) {
         hipHostFree(h->h_kro[b]);
         hipHostFree(h->h_krb[b]);
     }
@@ -1221,7 +1221,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->tickets);
     hipFree(h->stamps);
     hipFree(h->kt_dev);
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < FW_STAGE_BUFS; b++) {
         hipHostFree(h->h_key[b]);
         hipHostFree(h->h_ts[b]);
         hipHostFree(h->h_kh[b]);
@@ -1313,7 +1313,7 @@ int fw_commit(fw_handle* h, int64_t n) {
     if (h->reserved < 0 || n > h->reserved || n < 0) return fail(FW_E_STATE, "commit without matching reserve");
     h->reserved = -1;
     const int b = h->stage_cur;
-    h->stage_cur ^= 1;
+    h->stage_cur = (b + 1) % FW_STAGE_BUFS;
     if (n == 0) return FW_OK;
     int64_t krb_n = 0;
     if (h->keyrow) {

@@ -658,6 +658,11 @@ struct CompactArgs {
     int64_t* host_n;         // fw_results_async: also store the row count here (mapped host memory)
 };
 
+// host staging buffers of fw_reserve / fw_commit (pinned host + device): batch b + 1 is filled while
+// batch b crosses PCIe.  (3 measured neutral on the end-to-end leg, which is PCIe-bound: CFG2 2.25 ->
+// 2.27 ms per step, the wait for the staging buffer moving to the wait for the rows)
+constexpr int FW_STAGE_BUFS = 2;
+
 // fw_results_async buffers: up to this many collections outstanding (fw_results_ready reads the
 // oldest), so a caller can read watermark b - 2's rows while b - 1's and b's are still in flight
 constexpr int FW_AR_BUFS = 3;

@@ -170,6 +170,8 @@ def main():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: time the steps without the per-launch hipEvents (no roofline)")
     ap.add_argument("--e2e-steps", type=int, default=8)
+    ap.add_argument("--state-per-key", type=float, default=None,
+                    help="capacity hint override: (key, slice) entries per key at a flush's peak")
     ap.add_argument("--e2e-depth", type=int, default=2, choices=[1, 2],
                     help="end-to-end leg: read each watermark's rows 1 or 2 watermarks after collecting them "
                          "(fw_results_ready returns the oldest outstanding collection; 2 keeps the collection "
@@ -217,7 +219,9 @@ def main():
     from flink_amd import _native, abi
     from flink_amd.runtime.handle import WindowAggHandle
     L = _native.lib()
-    wl = WORKLOADS[args.workload]
+    wl = dict(WORKLOADS[args.workload])
+    if args.state_per_key is not None:
+        wl["state_per_key"] = args.state_per_key
     nv = len(wl["value_cols"])
 
     # ---------------- synthetic input, resident in HBM before timing --------------------
@@ -594,6 +598,7 @@ def main():
             "config": {"workload": f"{args.workload}: {wl['desc']}", "events_per_gpu_per_step": B,
                        "plan": "two-phase (LOCAL -> partials on the device exchange -> GLOBAL)" if two_phase else "one-phase",
                        "keys_total": keys_total, "rate_per_gpu_ev_s": wl["rate"],
+                       "state_per_key_hint": wl["state_per_key"],
                        "parallelism": f"key-group sharded x{world}" + (
                            "" if world == 1 else " + RCCL all-to-all" if args.dist_backend == "nccl"
                            else " + gloo all-to-all (rehearsal, shared GPU)"),
@@ -637,6 +642,9 @@ def main():
                                    "state_entries_moved_w_entry": st["state_entries_moved"] * w_entry / max(mg_n, 1),
                                    "F_w_out": fired_total * w_out / max(mg_n, 1)},
                                "flush_launches": st["flush_launches"], "live_state_entries_end": live,
+                               "superbuckets": st["num_superbuckets"],
+                               "peak_superbucket_entries": st["peak_superbucket_entries"],
+                               "superbucket_capacity": st["superbucket_capacity"],
                                "partial_bytes_read_per_launch": st["partial_bytes_merged"] / max(mg_n, 1),
                                "design_bytes_per_launch": merge_read_total / max(mg_n, 1),
                                "avg_launch_us": avg_merge_s * 1e6, "launches": mg_n, "traffic": traffic_m,

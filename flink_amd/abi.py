@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 8
+FW_ABI_VERSION = 9
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 
@@ -172,7 +172,9 @@ class fw_stats(C.Structure):
                 ("state_entries_moved", C.c_int64), ("key_rows", C.c_int64),
                 ("key_row_collections", C.c_int64),
                 ("partial_bytes_written", C.c_int64), ("partial_bytes_merged", C.c_int64),
-                ("compact_chunks", C.c_int64)]
+                ("compact_chunks", C.c_int64),
+                ("peak_superbucket_entries", C.c_int64), ("superbucket_capacity", C.c_int32),
+                ("reserved_stats0", C.c_int32)]
 
 
 KT_PARTITION, KT_SCAN, KT_REDUCE, KT_MERGE, KT_OTHER = 0, 1, 2, 3, 4

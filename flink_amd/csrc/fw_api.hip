@@ -1845,6 +1845,8 @@ int fw_get_stats(fw_handle* h, fw_stats* out) {
     out->partial_bytes_written = (int64_t)c.part_bytes;
     out->partial_bytes_merged = (int64_t)c.part_bytes_merged;
     out->compact_chunks = (int64_t)c.compact_chunks;
+    out->peak_superbucket_entries = (int64_t)c.peak_entries;
+    out->superbucket_capacity = h->cap_e;
     out->key_rows = h->keyrow ? c.kr_next_id - std::max<int64_t>(0, c.kr_free_count - std::min(c.kr_free_cursor, c.kr_free_count)) : 0;
     out->key_row_collections = c.kr_collections;
     return FW_OK;

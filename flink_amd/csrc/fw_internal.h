@@ -302,6 +302,7 @@ struct Ctrl {
     uint64_t part_bytes_merged;  // of those, the bytes flushes read (cumulative)
     uint64_t compact_chunks; // chunks written in a compact partial-row format (cumulative)
     uint64_t state_moved;    // state entries the merge launches loaded + wrote back (cumulative)
+    uint64_t peak_entries;   // most entries one superbucket's LDS table held in a merge (since create / restore)
     // FW_KEYHASH_KEYROW: the key-row intern table's allocator (KeyRowTable)
     int64_t kr_next_id;      // ids handed out fresh so far (ids < kr_next_id exist)
     int64_t kr_free_count;   // ids in the free list (rebuilt by each collection)

@@ -116,6 +116,7 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->part_bytes_merged = 0;
         c->compact_chunks = 0;
         c->state_moved = 0;
+        c->peak_entries = 0;
         c->kr_next_id = 0;
         c->kr_free_count = 0;
         c->kr_free_cursor = 0;

@@ -1897,6 +1897,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
         if (s_fired) a.sb_fired[sb] += s_fired;
         // state traffic of this superbucket: entries loaded + entries written back
         __hip_atomic_fetch_add(&c->state_moved, (uint64_t)(n0 + (a.local ? 0 : s_nlive)), __ATOMIC_RELAXED, DEV_SCOPE);
+        __hip_atomic_fetch_max(&c->peak_entries, (uint64_t)max(S.n, 0), __ATOMIC_RELAXED, DEV_SCOPE);
         if (S.overflow) __hip_atomic_fetch_or(&c->error, ERR_STATE, __ATOMIC_RELAXED, DEV_SCOPE);
     }
     __syncthreads();

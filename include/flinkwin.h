@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 8
+#define FW_ABI_VERSION 9
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -262,6 +262,12 @@ typedef struct {
     int64_t partial_bytes_written;     /* bytes of partial rows (+ rank bytes) the ingest wrote */
     int64_t partial_bytes_merged;      /* of those, the bytes flushes have read          */
     int64_t compact_chunks;            /* ingest chunks written in a compact row format  */
+    /* v9: state sizing -- the most (key, slice) entries one superbucket held in a merge since create /
+       restore, against the entries a superbucket's table holds (FW_ERRF_STATE beyond it).  The peak
+       over the capacity hint's superbuckets tells how much of the hint a stream really uses. */
+    int64_t peak_superbucket_entries;
+    int32_t superbucket_capacity;
+    int32_t reserved_stats0;
 } fw_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------- */

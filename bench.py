@@ -38,7 +38,10 @@ WORKLOADS = {
     # name: (description, window, aggs, keys per GPU, rate per GPU, value kind, key dist, input B/event)
     # state_per_key: the operator's capacity hint, (key, slice) entries per key at the PEAK of a
     # flush (live entries plus the batch's new slices before firing expires the old ones; live after
-    # a step: CFG2 0.94, CFG3 5.3, CFG4 0.90, CFG5 1.24); a step that outgrows it fails loudly
+    # a step: CFG2 0.94, CFG3 5.3, CFG4 0.90, CFG5 1.24); a step that outgrows it fails loudly.  The
+    # planner fills 75 % of a superbucket's table at the hint; the fullest superbucket's peak
+    # (fw_stats.peak_superbucket_entries, round 5) lands at 72 % (CFG2), 76 % (CFG3), 69 % (CFG4), 94 %
+    # (CFG5) and 74 % (cfg4_10m) of its table
     "cfg2": dict(desc="Nexmark Q7-style TUMBLE(10 s) MAX(price) GROUP BY auction",
                  window=("TUMBLE", 10_000, 0), aggs=[("MAX", 0, "BIGINT")], count_star=-1,
                  keys=1_000_000, key_base=1000, rate=1_000_000, value_kind=0, dist=0, w_in=24,
@@ -51,12 +54,15 @@ WORKLOADS = {
                  window=("TUMBLE", 10_000, 0), aggs=[("SUM", 0, "DOUBLE"), ("AVG", 0, "DOUBLE")],
                  count_star=-1, keys=1_250_000, key_base=0, rate=1_000_000, value_kind=1, dist=0, w_in=24,
                  value_cols=["DOUBLE"], nw=2, state_per_key=2),
-    # CFG4's full key space on ONE GPU (10^7 keys, sharded over 8 GPUs in cfg4): 16384
-    # superbuckets, the most the ingest histogram partitions into (one merge pass each)
+    # CFG4's full key space on ONE GPU (10^7 keys, sharded over 8 GPUs in cfg4).  At 10^6
+    # events/s a 10 s window sees ~63 % of the 10^7 keys, so a flush's peak is ~1.24 entries per key
+    # (the fired window + the next one's first seconds; measured: 1508 entries in the fullest of 8192
+    # superbuckets), not CFG4's ~2.3 (1.25 M keys: every key in both windows).  Hint 1.25: 8192
+    # superbuckets (hint 2 planned 16384 at 39 % of their tables: merge 1070 -> 639 us per flush)
     "cfg4_10m": dict(desc="TUMBLE(10 s) SUM(v), AVG(v) DOUBLE over 10^7 keys on one GPU",
                      window=("TUMBLE", 10_000, 0), aggs=[("SUM", 0, "DOUBLE"), ("AVG", 0, "DOUBLE")],
                      count_star=-1, keys=10_000_000, key_base=0, rate=1_000_000, value_kind=1, dist=0, w_in=24,
-                     keys_fixed=True, value_cols=["DOUBLE"], nw=2, state_per_key=2),
+                     keys_fixed=True, value_cols=["DOUBLE"], nw=2, state_per_key=1.25),
     "cfg5": dict(desc="CUMULATE(1 min step, 1 h) COUNT(*), SUM, MIN, MAX, Zipf(1.1) keys",
                  window=("CUMULATE", 3_600_000, 60_000),
                  aggs=[("COUNT_STAR", 0, "BIGINT"), ("SUM", 0, "BIGINT"), ("MIN", 0, "BIGINT"), ("MAX", 0, "BIGINT")],

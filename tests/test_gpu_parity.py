@@ -391,19 +391,23 @@ def test_key_group_restore_rejects_foreign_and_mismatched_blobs():
 # checked on a key subset against the oracle (window results of a key depend only on that
 # key's records, so the oracle replays only the subset) plus size-independent properties
 # ------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("wl_name", ["cfg2", "cfg3", "cfg4", "cfg5", "cfg4_10m", "cfg2-runs", "cfg3-runs", "cfg5-runs",
-                                     "cfg4-cells"])
+@pytest.mark.parametrize("wl_name", ["cfg2", "cfg3", "cfg4", "cfg5", "cfg4_10m", "cfg4_10m-h2", "cfg2-runs", "cfg3-runs",
+                                     "cfg5-runs", "cfg4-cells"])
 def test_bench_workload_full_size_key_subset(wl_name, monkeypatch):
-    if "-" in wl_name:  # the partial-row layout the planner would not pick, forced (FW_RUNS)
-        wl_name, layout = wl_name.split("-")
-        monkeypatch.setenv("FW_RUNS", "1" if layout == "runs" else "0")
+    variant = None
+    if "-" in wl_name:
+        wl_name, variant = wl_name.split("-")
+    if variant in ("runs", "cells"):  # the partial-row layout the planner would not pick, forced (FW_RUNS)
+        monkeypatch.setenv("FW_RUNS", "1" if variant == "runs" else "0")
     torch = _torch_cuda()
     import ctypes as C
     import bench
     from flink_amd import _native
     from flink_amd.runtime.handle import WindowAggHandle
     from oracle.oracle import OracleOperator
-    wl = bench.WORKLOADS[wl_name]
+    wl = dict(bench.WORKLOADS[wl_name])
+    if variant == "h2":  # capacity hint 2: 16384 superbuckets, the ingest histogram's limit
+        wl["state_per_key"] = 2
     # CFG5: 27 steps = 4077 s of event time at 27 778 ev/s, past the 1 h CUMULATE window's last step
     # (its final slice fires and the window's first-slice state is cleared, SliceAssigners.java:398-453)
     steps, B, MOD, PICK = (27 if wl_name == "cfg5" else 6), bench.B, 97, 13
@@ -416,8 +420,8 @@ def test_bench_workload_full_size_key_subset(wl_name, monkeypatch):
     gp, keys_total = bench.gen_params(wl, 1, zipf_t.data_ptr() if zipf_t is not None else None)
     cfg = bench.build_config(wl, 1, 0, keys_total, (8 if keys_total <= 2_000_000 else 2) * keys_total + (1 << 20))
     g, o = WindowAggHandle(cfg), OracleOperator(cfg)
-    if wl_name == "cfg4_10m":  # 16384 superbuckets: the ingest histogram's limit, one merge pass each
-        assert g.stats()["num_superbuckets"] == 16384
+    if wl_name == "cfg4_10m":  # bench hint 1.25: 8192 superbuckets; hint 2: 16384 (one merge pass each)
+        assert g.stats()["num_superbuckets"] == (16384 if variant == "h2" else 8192)
     k = torch.empty(B, dtype=torch.int64, device="cuda")
     t, v = torch.empty_like(k), torch.empty_like(k)
     s = torch.cuda.current_stream().cuda_stream
@@ -455,6 +459,8 @@ def test_bench_workload_full_size_key_subset(wl_name, monkeypatch):
         got += got_b
     st = g.stats()
     assert st["error_flags"] == 0 and st["num_late_records_dropped"] == 0 == o.late_dropped
+    # the superbucket peak (fw_stats v9): some table held entries, none beyond its capacity
+    assert 0 < st["peak_superbucket_entries"] <= st["superbucket_capacity"]
     assert n_sub > 1000 and len(got) > 100 and total_rows > len(got)
     kind = wl["window"][0]
     if kind == "HOP" and cs >= 0:       # every event is counted in size/slide windows

@@ -1429,7 +1429,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
 #define FW_GD 0  // blocks in the pipelined gather's ring (0: planned below)
 #endif
         // one-word TUMBLE: one block of 4 rows per lane (measured round 5, CFG2 runs flush 144.5 ->
-        // 128.7 us; 3 rows: 131.8, 2 rows: 133.3; the freed registers go to the probe loop); CFG4 (two
+        // 128.7 us; 3 rows: 131.8, 2 rows: 133.3, 5 rows: 130.1, 6 rows: 141.7; the freed registers go to the probe loop); CFG4 (two
         // words, 197 -> 201 us) and CFG5 (CUMULATE, 322 -> 370 us) keep two blocks of half of
         // mg_rows_in_flight
         constexpr bool ONE_BLOCK = NW == 1 && KIND == FW_WIN_TUMBLE;

@@ -176,6 +176,9 @@ def main():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: time the steps without the per-launch hipEvents (no roofline)")
     ap.add_argument("--e2e-steps", type=int, default=8)
+    ap.add_argument("--e2e-transfer", default="delta32", choices=["delta32", "words"],
+                    help="end-to-end leg: columns spanning < 2^32 per batch cross PCIe as 32-bit deltas "
+                         "(fw_commit_delta32), or every column as 8-byte words (fw_commit)")
     ap.add_argument("--state-per-key", type=float, default=None,
                     help="capacity hint override: (key, slice) entries per key at a flush's peak")
     ap.add_argument("--e2e-depth", type=int, default=2, choices=[1, 2],
@@ -525,6 +528,27 @@ def main():
             d = C.cast(dst, C.c_void_p).value
             return [pool.submit(C.memmove, d + 8 * a, src.ctypes.data + 8 * a, 8 * (e - a)) for a, e in parts]
 
+        def span(s):
+            return int(s.min()), int(s.max())
+
+        def fill_delta32(items):
+            # the shim's per-record range check (slice min / max, numpy releases the GIL), then every
+            # column of the batch that spans < 2^32 written as 32-bit deltas from its minimum
+            mm = [[pool.submit(span, src[a:e]) for a, e in parts] for _, _, src in items]
+            mask, bases, fs = 0, (C.c_int64 * (2 + abi.FW_MAX_COLS))(), []
+            for (slot, dst, src), f in zip(items, mm):
+                r = [x.result() for x in f]
+                lo, hi = min(x[0] for x in r), max(x[1] for x in r)
+                if hi - lo < (1 << 32):
+                    mask |= 1 << slot
+                    bases[slot] = lo
+                    d32 = _np_view(dst, B, np.uint32)
+                    fs += [pool.submit(np.subtract, src[a:e], np.int64(lo), out=d32[a:e], casting="unsafe")
+                           for a, e in parts]
+                else:
+                    fs += fill(dst, src)
+            return mask, bases, fs
+
         cols = abi.fw_host_cols()
         _native.check(L.fw_reserve(he._h, 0, C.byref(cols)))  # allocates the staging (untimed)
         _native.check(L.fw_commit(he._h, 0))
@@ -532,6 +556,7 @@ def main():
         he.results_ready(copy=False)
         depth = args.e2e_depth
         rows_out = 0
+        delta_cols = 0
         t_reserve = t_fill = t_ready = t_commit = t_adv = t_async = 0.0
         te0 = time.perf_counter()
         for b in range(ns):
@@ -539,11 +564,19 @@ def main():
             cols = abi.fw_host_cols()
             _native.check(L.fw_reserve(he._h, B, C.byref(cols)))  # waits for the H2D two commits back
             t2 = time.perf_counter()
-            fs = fill(cols.key, hk[b]) + fill(cols.ts, ht[b]) + (fill(cols.values[0], hv[b]) if nv else [])
+            if args.e2e_transfer == "delta32":
+                mask, bases, fs = fill_delta32([(0, cols.key, hk[b]), (1, cols.ts, ht[b])] +
+                                               ([(2, cols.values[0], hv[b])] if nv else []))
+            else:
+                mask, fs = 0, fill(cols.key, hk[b]) + fill(cols.ts, ht[b]) + (fill(cols.values[0], hv[b]) if nv else [])
             for f in fs:
                 f.result()
             t3 = time.perf_counter()
-            _native.check(L.fw_commit(he._h, B))
+            if mask:
+                _native.check(L.fw_commit_delta32(he._h, B, mask, bases))
+                delta_cols |= mask
+            else:
+                _native.check(L.fw_commit(he._h, B))
             t3c = time.perf_counter()
             he.advance(watermark(b, wl["rate"]))
             t4 = time.perf_counter()
@@ -575,9 +608,10 @@ def main():
                                     "results_async_enqueue": t_async / ns * 1e3},
                "fill_GBps": ns * B * wl["w_in"] / max(t_fill, 1e-9) / 1e9,
                "path": "numpy batch -> pinned staging (fw_reserve, 8 fill threads) -> H2D on the copy stream, "
-                       "overlapping the previous batch's ingest (fw_commit) -> advance -> rows into pinned host "
+                       "overlapping the previous batch's ingest (fw_commit, or fw_commit_delta32 for columns spanning < 2^32) -> advance -> rows into pinned host "
                        f"memory (fw_results_async), read {depth} watermark(s) later (fw_results_ready)",
-               "results_depth": depth}
+               "results_depth": depth, "transfer": args.e2e_transfer,
+               "delta32_columns": [n for i, n in enumerate(["key", "ts", "value"]) if delta_cols >> i & 1]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

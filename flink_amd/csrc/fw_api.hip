@@ -209,6 +209,9 @@ struct fw_handle {
     int32_t* d_kh[FW_STAGE_BUFS] = {};
     int64_t* d_val[FW_STAGE_BUFS][FW_MAX_COLS] = {};
     uint8_t* d_nul[FW_STAGE_BUFS][FW_MAX_COLS] = {};
+    // fw_commit_delta32: the 32-bit delta columns of staging set b, FW_PACK_COLS slices of pack_stride
+    uint32_t* d_pack[FW_STAGE_BUFS] = {};
+    int64_t pack_stride = 0;
     int64_t reserved = -1;
 
     // asynchronous result delivery (fw_results_async / fw_results_ready): rows compacted on the
@@ -1235,6 +1238,7 @@ int fw_destroy(fw_handle* h) {
         hipFree(h->d_krb[b]);
         hipFree(h->d_key[b]);
         hipFree(h->d_ts[b]);
+        hipFree(h->d_pack[b]);
         hipFree(h->d_kh[b]);
         for (int v = 0; v < FW_MAX_COLS; v++) {
             hipFree(h->d_val[b][v]);
@@ -1307,8 +1311,23 @@ int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out) {
     return FW_OK;
 }
 
+static int commit_impl(fw_handle* h, int64_t n, uint32_t packed, const int64_t* bases);
+
 int fw_commit(fw_handle* h, int64_t n) {
     if (!h) return fail(FW_E_INVALID, "null handle");
+    return commit_impl(h, n, 0u, nullptr);
+}
+
+int fw_commit_delta32(fw_handle* h, int64_t n, uint32_t delta_cols, const int64_t* bases) {
+    if (!h) return fail(FW_E_INVALID, "null handle");
+    const uint32_t valid = FW_DELTA_KEY | FW_DELTA_TS | (((1u << h->cfg.n_value_cols) - 1u) << 2);
+    if (delta_cols & ~valid) return fail(FW_E_INVALID, "delta_cols 0x%x names a column the operator does not have", delta_cols);
+    if ((delta_cols & FW_DELTA_KEY) && h->keyrow) return fail(FW_E_INVALID, "key-row operators have no key column to pack");
+    if (delta_cols && !bases) return fail(FW_E_INVALID, "packed columns need their bases");
+    return commit_impl(h, n, delta_cols, bases);
+}
+
+static int commit_impl(fw_handle* h, int64_t n, uint32_t packed, const int64_t* bases) {
     ar_kick(h);
     if (h->reserved < 0 || n > h->reserved || n < 0) return fail(FW_E_STATE, "commit without matching reserve");
     h->reserved = -1;
@@ -1330,19 +1349,38 @@ int fw_commit(fw_handle* h, int64_t n) {
     auto h2d = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs);
     };
+    if (packed && !h->d_pack[b]) {  // first packed commit into this set (allocation outside any timed loop of the caller's)
+        h->pack_stride = (h->stage_cap + 3) & ~3ll;
+        HIP_TRY(hipMalloc((void**)&h->d_pack[b], (size_t)FW_PACK_COLS * h->pack_stride * 4));
+    }
+    // an 8-byte word column: a packed one crosses PCIe as n 32-bit deltas (the first 4n bytes of its
+    // staging column) and is widened on the copy stream, behind its copy
+    WidenArgs wa{};
+    wa.n = n;
+    int nw = 0;
+    auto col = [&](int slot, void* dst, const void* src) -> hipError_t {
+        if (!((packed >> slot) & 1u)) return h2d(dst, src, (size_t)n * 8);
+        uint32_t* p = h->d_pack[b] + (size_t)slot * h->pack_stride;
+        wa.src[nw] = p;
+        wa.dst[nw] = (uint64_t*)dst;
+        wa.base[nw] = (uint64_t)bases[slot];
+        nw++;
+        return h2d(p, src, (size_t)n * 4);
+    };
     if (h->keyrow) {
         HIP_TRY(h2d(h->d_kro[b], h->h_kro[b], (n + 1) * 8));
         HIP_TRY(h2d(h->d_krb[b], h->h_krb[b], (size_t)krb_n));
     } else {
-        HIP_TRY(h2d(h->d_key[b], h->h_key[b], n * 8));
+        HIP_TRY(col(0, h->d_key[b], h->h_key[b]));
     }
-    HIP_TRY(h2d(h->d_ts[b], h->h_ts[b], n * 8));
+    HIP_TRY(col(1, h->d_ts[b], h->h_ts[b]));
     if (h->cfg.key_hash == FW_KEYHASH_PRECOMPUTED) HIP_TRY(h2d(h->d_kh[b], h->h_kh[b], n * 4));
     for (int s = 0; s < h->nv; s++) {
         const int v = h->slot_col[s];
-        HIP_TRY(h2d(h->d_val[b][v], h->h_val[b][v], n * 8));
+        HIP_TRY(col(2 + v, h->d_val[b][v], h->h_val[b][v]));
         if (h->d_nul[b][v]) HIP_TRY(h2d(h->d_nul[b][v], h->h_nul[b][v], n));
     }
+    HIP_TRY(launch_widen(wa, nw, cs));
     HIP_TRY(hipEventRecord(h->stage_ev[b], cs));
     HIP_TRY(hipStreamWaitEvent(h->stream, h->stage_ev[b], 0));
     const void* vals[FW_MAX_COLS];

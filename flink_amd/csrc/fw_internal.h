@@ -687,6 +687,17 @@ struct CopyOutArgs {
 };
 hipError_t launch_copy_out(const CopyOutArgs& a, hipStream_t s);
 
+// fw_commit_delta32: transfer columns of 32-bit deltas widened on the device into the 8-byte words the
+// ingest reads (word = base + delta, modulo 2^64).  Column slot c of a launch: src[c] -> dst[c].
+constexpr int FW_PACK_COLS = 2 + FW_MAX_COLS;  // key, ts, value columns
+struct WidenArgs {
+    int64_t n;
+    const uint32_t* src[FW_PACK_COLS];
+    uint64_t* dst[FW_PACK_COLS];
+    uint64_t base[FW_PACK_COLS];
+};
+hipError_t launch_widen(const WidenArgs& a, int n_cols, hipStream_t s);
+
 // In-kernel launch timing (fw_set_profiling FW_PROF_DEVICE): per kernel class 4 words -- the
 // constant-rate device clock (s_memrealtime) when block 0 started the current launch, the summed
 // launch durations, the launch count, spare.  Block 0 stamps the start; the last workgroup of the

@@ -151,6 +151,33 @@ hipError_t launch_copy_out(const CopyOutArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// one column per grid row: 16-B loads of four deltas, two 16-B stores of their words
+__global__ __launch_bounds__(BLOCK) void k_widen(WidenArgs a) {
+    const int c = blockIdx.y;
+    const uint32_t* s = a.src[c];
+    uint64_t* d = a.dst[c];
+    const uint64_t b = a.base[c];
+    const int64_t n4 = a.n >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n4; i += (int64_t)gridDim.x * BLOCK) {
+        const uint4 v = ((const uint4*)s)[i];
+        ulonglong2* q = (ulonglong2*)(d + 4 * i);
+        q[0] = make_ulonglong2(b + v.x, b + v.y);
+        q[1] = make_ulonglong2(b + v.z, b + v.w);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
+        const int64_t i = 4 * n4 + threadIdx.x;
+        d[i] = b + s[i];
+    }
+}
+
+hipError_t launch_widen(const WidenArgs& a, int n_cols, hipStream_t s) {
+    if (n_cols <= 0 || a.n <= 0) return hipSuccess;
+    const int64_t n4 = (a.n + 3) >> 2;
+    const unsigned gx = (unsigned)std::min<int64_t>(1024, (n4 + BLOCK - 1) / BLOCK);
+    hipLaunchKernelGGL(k_widen, dim3(gx, (unsigned)n_cols), dim3(BLOCK), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_init_ctrl(Ctrl* c, hipStream_t s) {
     hipLaunchKernelGGL(k_init_ctrl, dim3(1), dim3(64), 0, s, c);
     return hipGetLastError();

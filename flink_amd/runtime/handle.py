@@ -73,9 +73,12 @@ class WindowAggHandle:
         check(lib().fw_initialize_watermark(self._h, int(wm)))
 
     # ---- ingest
-    def push_host(self, keys, ts, values=(), key_hashes=None, nulls=None):
+    def push_host(self, keys, ts, values=(), key_hashes=None, nulls=None, delta32=True):
         """Host columns -> pinned staging -> device (fw_reserve / fw_commit).  ``nulls`` maps a
-        nullable value column to its per-row null flags (bool / uint8, non-zero = SQL NULL)."""
+        nullable value column to its per-row null flags (bool / uint8, non-zero = SQL NULL).
+        ``delta32``: a column whose batch values span < 2^32 crosses PCIe as 32-bit deltas from its
+        minimum (fw_commit_delta32, as the JNI shim packs event times and bounded ids); the device
+        sees the same 8-byte words either way."""
         keys = np.asarray(keys, dtype=np.int64)
         n = len(keys)
         cap = self.cfg.max_batch_rows
@@ -83,22 +86,37 @@ class WindowAggHandle:
             m = min(cap, n - o)
             cols = abi.fw_host_cols()
             check(lib().fw_reserve(self._h, m, C.byref(cols)))
+            mask, bases = 0, (C.c_int64 * (2 + abi.FW_MAX_COLS))()
+
+            def put(slot, ptr, col):
+                nonlocal mask
+                if delta32:
+                    lo, hi = int(col.min()), int(col.max())
+                    if hi - lo < (1 << 32):
+                        np.subtract(col, np.int64(lo), out=_np_view(ptr, m, np.uint32), casting="unsafe")
+                        mask |= 1 << slot
+                        bases[slot] = lo
+                        return
+                _np_view(ptr, m, np.int64)[:] = col
             if m:
-                _np_view(cols.key, m, np.int64)[:] = keys[o:o + m]
-                _np_view(cols.ts, m, np.int64)[:] = np.asarray(ts, dtype=np.int64)[o:o + m]
+                put(0, cols.key, keys[o:o + m])
+                put(1, cols.ts, np.asarray(ts, dtype=np.int64)[o:o + m])
                 if key_hashes is not None:
                     _np_view(cols.key_hash, m, np.int32)[:] = np.asarray(key_hashes, dtype=np.int32)[o:o + m]
                 for c, v in enumerate(values):
                     v = np.asarray(v)
                     if v.dtype == np.float64:
                         v = v.view(np.int64)
-                    _np_view(cols.values[c], m, np.int64)[:] = v.astype(np.int64, copy=False)[o:o + m]
+                    put(2 + c, cols.values[c], v.astype(np.int64, copy=False)[o:o + m])
                 for c in range(self.cfg.n_value_cols):
                     if self.cfg.nullable_cols >> c & 1:
                         nf = np.zeros(n, np.uint8) if nulls is None or c not in nulls else \
                             np.asarray(nulls[c]).astype(np.uint8, copy=False)
                         _np_view(cols.nulls[c], m, np.uint8)[:] = nf[o:o + m]
-            check(lib().fw_commit(self._h, m))
+            if mask:
+                check(lib().fw_commit_delta32(self._h, m, mask, bases))
+            else:
+                check(lib().fw_commit(self._h, m))
             self.push_seq += 1
 
     def push_host_key_rows(self, offsets, images, ts, values=(), nulls=None):

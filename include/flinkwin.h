@@ -22,7 +22,7 @@
  *   fw_initialize_watermark
  *                    WindowProcessor.initializeWatermark (WindowProcessor.java:48) /
  *                    InternalTimerServiceImpl.initializeWatermark
- *   fw_reserve/fw_commit, fw_push_device
+ *   fw_reserve/fw_commit(_delta32), fw_push_device
  *                    SyncStateWindowProcessor.processElement(key,row) -> dropped
  *                    (TR/operators/window/tvf/common/SyncStateWindowProcessor.java:37),
  *                    i.e. AbstractSliceSyncStateWindowAggProcessor.processElement :96-126
@@ -287,6 +287,18 @@ int fw_initialize_watermark(fw_handle* h, int64_t watermark);
 /* ---- ingest ------------------------------------------------------------------------ */
 int fw_reserve(fw_handle* h, int64_t n, fw_host_cols* out);
 int fw_commit(fw_handle* h, int64_t n);
+/* v9: fw_commit with narrow transfer columns.  For each column named in delta_cols the caller wrote n
+   uint32 deltas into the first 4n bytes of its fw_reserve staging column; the column's 8-byte word of
+   row i is bases[slot] + delta_i (modulo 2^64), slot 0 the key, 1 the ts, 2 + c value column c.  The
+   deltas cross PCIe (half the bytes) and a device kernel widens them behind the copy, so the ingest
+   sees the same words as fw_commit's.  A JNI shim packs a column of a batch whose values span
+   < 2^32 (event times of one watermark interval; INT keys; bounded BIGINT ids) with bases[slot] its
+   minimum, and writes the others as words.  Returns FW_E_INVALID for a slot the operator does not
+   have (key-row operators have no key column). */
+#define FW_DELTA_KEY 1u
+#define FW_DELTA_TS 2u
+#define FW_DELTA_VALUE(c) (4u << (c))
+int fw_commit_delta32(fw_handle* h, int64_t n, uint32_t delta_cols, const int64_t* bases);
 /* Device-resident columns (caller-owned device memory, ordered on the handle stream).
    d_values[c] points at n 8-byte words of value column c; d_key_hash may be NULL unless
    key_hash == FW_KEYHASH_PRECOMPUTED; d_nulls may be NULL unless nullable_cols != 0, and then

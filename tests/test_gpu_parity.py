@@ -805,6 +805,49 @@ def test_async_results_pipeline_matches_oracle(name, depth):
     g.close()
 
 
+@pytest.mark.parametrize("name", ["sql_tumble_int_aggs", "sql_tumble_double", "ds_sliding_max"])
+def test_delta32_transfer_matches_words(name):
+    """fw_commit_delta32: columns whose batch values span < 2^32 cross PCIe as 32-bit deltas and are
+    widened on the device -- the same rows as 8-byte words through fw_commit, and the oracle's.  Odd
+    push sizes (the widening's tail), and batches whose value column spans more (not packed): the
+    mask changes from push to push."""
+    import ctypes as C
+    from flink_amd import _native, abi
+    from flink_amd.runtime.handle import WindowAggHandle
+    from oracle.oracle import OracleOperator
+    kw = CASES[name]
+    cfg = _cfg(kw)
+    dc = _double_cols(kw)
+    o, gw, gd = OracleOperator(cfg), WindowAggHandle(cfg), WindowAggHandle(cfg)
+    for bi, (k, t, iv, dv, wm) in enumerate(_stream(zlib.crc32(name.encode()) % 991, 20000, 400, ooo=2 * kw["size_ms"],
+                                                    step_ms=1500, n_wm=10)):
+        if bi % 3 == 1:  # this batch's BIGINT values span > 2^32: that column goes as words
+            iv = iv * (1 << 30) - (1 << 40)
+        vals = [iv, dv.view(np.int64)]
+        o.process_batch(k, t, vals)
+        for part in np.split(np.arange(len(k)), [len(k) // 3 + 1, len(k) // 2 + 3]):
+            gw.push_host(k[part], t[part], [v[part] for v in vals], delta32=False)
+            gd.push_host(k[part], t[part], [v[part] for v in vals])
+        o.process_watermark(wm)
+        gw.advance(wm)
+        gd.advance(wm)
+        want = _rows(o.results(clear=True), cfg, dc)
+        _compare(_rows(gw.results(reset=True), cfg, dc), want, dc, f"words, watermark {bi}")
+        _compare(_rows(gd.results(reset=True), cfg, dc), want, dc, f"delta32, watermark {bi}")
+    for g in (gw, gd):
+        assert g.stats()["error_flags"] == 0 and g.stats()["num_late_records_dropped"] == o.late_dropped
+    # a slot the operator does not have, or packed columns without bases: refused
+    L = _native.lib()
+    cols = abi.fw_host_cols()
+    _native.check(L.fw_reserve(gd._h, 16, C.byref(cols)))
+    bases = (C.c_int64 * (2 + abi.FW_MAX_COLS))()
+    assert L.fw_commit_delta32(gd._h, 16, 1 << (2 + cfg.n_value_cols), bases) != 0
+    assert L.fw_commit_delta32(gd._h, 16, 2, None) != 0
+    _native.check(L.fw_commit(gd._h, 0))
+    gw.close()
+    gd.close()
+
+
 @pytest.mark.parametrize("name", ["sql_tumble_int_aggs", "sql_hop", "sql_cumulate_countstar", "ds_sliding_max",
                                   "sql_tumble_double"])
 def test_state_beyond_ingest_superbuckets_matches_oracle(name):

@@ -528,23 +528,24 @@ def main():
             d = C.cast(dst, C.c_void_p).value
             return [pool.submit(C.memmove, d + 8 * a, src.ctypes.data + 8 * a, 8 * (e - a)) for a, e in parts]
 
-        def span(s):
-            return int(s.min()), int(s.max())
-
         def fill_delta32(items):
-            # the shim's per-record range check (slice min / max, numpy releases the GIL), then every
-            # column of the batch that spans < 2^32 written as 32-bit deltas from its minimum
-            mm = [[pool.submit(span, src[a:e]) for a, e in parts] for _, _, src in items]
-            mask, bases, fs = 0, (C.c_int64 * (2 + abi.FW_MAX_COLS))(), []
-            for (slot, dst, src), f in zip(items, mm):
-                r = [x.result() for x in f]
-                lo, hi = min(x[0] for x in r), max(x[1] for x in r)
-                if hi - lo < (1 << 32):
+            # as the shim serialises records: each column as 32-bit deltas from (its first value - 2^31),
+            # range-checked in the same pass (fw_delta32_encode, 8 threads); a column with a value
+            # outside that 2^32 window is written again as words
+            mask, bases, pend = 0, (C.c_int64 * (2 + abi.FW_MAX_COLS))(), []
+            for slot, dst, src in items:
+                base = int(src[0]) - (1 << 31)
+                if base < -(1 << 63):
+                    pend.append((slot, dst, src, None))
+                    continue
+                d = C.cast(dst, C.c_void_p).value
+                pend.append((slot, dst, src, base, [pool.submit(L.fw_delta32_encode, src.ctypes.data + 8 * a, e - a, base,
+                                                                d + 4 * a) for a, e in parts]))
+            fs = []
+            for slot, dst, src, base, *f in pend:
+                if base is not None and not any(x.result() for x in f[0]):
                     mask |= 1 << slot
-                    bases[slot] = lo
-                    d32 = _np_view(dst, B, np.uint32)
-                    fs += [pool.submit(np.subtract, src[a:e], np.int64(lo), out=d32[a:e], casting="unsafe")
-                           for a, e in parts]
+                    bases[slot] = base
                 else:
                     fs += fill(dst, src)
             return mask, bases, fs

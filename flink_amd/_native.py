@@ -47,6 +47,7 @@ def lib():
         "fw_reserve": (i32, [vp, i64, P(abi.fw_host_cols)]),
         "fw_commit": (i32, [vp, i64]),
         "fw_commit_delta32": (i32, [vp, i64, C.c_uint32, P(C.c_int64)]),
+        "fw_delta32_encode": (i32, [vp, i64, i64, vp]),
         "fw_push_device": (i32, [vp, i64, vp, vp, vp, vp, vp]),
         "fw_push_device_segments": (i32, [vp, i32, i64, vp, vp, vp, vp, vp, vp]),
         "fw_push_device_packed_segments": (i32, [vp, i32, i64, vp, vp, i32]),
@@ -104,7 +105,7 @@ def lib():
 
 # every symbol the public header declares (tests check they are exported)
 EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_device_count", "fw_get_stream", "fw_sync",
-            "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_commit_delta32", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance", "fw_advance_device",
+            "fw_initialize_watermark", "fw_reserve", "fw_commit", "fw_commit_delta32", "fw_delta32_encode", "fw_push_device", "fw_push_device_segments", "fw_push_device_packed_segments", "fw_advance", "fw_advance_device",
             "fw_flush", "fw_results", "fw_results_reset", "fw_results_async", "fw_results_ready", "fw_results_device", "fw_get_stats", "fw_set_profiling",
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_snapshot_key_group_heap", "fw_restore_key_group_heap", "fw_ds_snapshot_key_group", "fw_ds_restore_key_group", "fw_results_device_segments", "fw_key_row_hash", "fw_host_key_row_hash",

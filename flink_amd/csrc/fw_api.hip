@@ -1318,6 +1318,17 @@ int fw_commit(fw_handle* h, int64_t n) {
     return commit_impl(h, n, 0u, nullptr);
 }
 
+int fw_delta32_encode(const int64_t* src, int64_t n, int64_t base, uint32_t* dst) {
+    if (n <= 0) return 0;
+    uint64_t out = 0;  // any high bits: a value outside the column's 2^32 window
+    for (int64_t i = 0; i < n; i++) {
+        const uint64_t d = (uint64_t)src[i] - (uint64_t)base;
+        out |= d >> 32;
+        dst[i] = (uint32_t)d;
+    }
+    return out ? 1 : 0;
+}
+
 int fw_commit_delta32(fw_handle* h, int64_t n, uint32_t delta_cols, const int64_t* bases) {
     if (!h) return fail(FW_E_INVALID, "null handle");
     const uint32_t valid = FW_DELTA_KEY | FW_DELTA_TS | (((1u << h->cfg.n_value_cols) - 1u) << 2);

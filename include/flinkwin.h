@@ -299,6 +299,10 @@ int fw_commit(fw_handle* h, int64_t n);
 #define FW_DELTA_TS 2u
 #define FW_DELTA_VALUE(c) (4u << (c))
 int fw_commit_delta32(fw_handle* h, int64_t n, uint32_t delta_cols, const int64_t* bases);
+/* v9, host helper (no device work): dst[i] = src[i] - base as uint32, for a shim that packs a column
+   in bulk; returns 1 if some value lies outside [base, base + 2^32) (that column then goes as
+   words), else 0.  Slices of one column may be encoded from several threads with the same base. */
+int fw_delta32_encode(const int64_t* src, int64_t n, int64_t base, uint32_t* dst);
 /* Device-resident columns (caller-owned device memory, ordered on the handle stream).
    d_values[c] points at n 8-byte words of value column c; d_key_hash may be NULL unless
    key_hash == FW_KEYHASH_PRECOMPUTED; d_nulls may be NULL unless nullable_cols != 0, and then

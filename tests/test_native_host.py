@@ -105,3 +105,27 @@ def test_error_flag_bits_match_header():
     text = open(HEADER).read()
     declared = {m[0]: int(m[1]) for m in re.findall(r"#define FW_ERRF_(\w+) (\d+)", text)}
     assert declared == abi.ERRF
+
+
+def test_delta32_encode_round_trip_and_range_flag():
+    """fw_delta32_encode (host helper of fw_commit_delta32): the deltas widen back to the words
+    (base + delta, the device kernel's rule), and a value outside [base, base + 2^32) is flagged."""
+    L = _native.lib()
+    rng = np.random.default_rng(7)
+    src = rng.integers(-(1 << 40), 1 << 40, 1001, dtype=np.int64)
+    src = (src % (1 << 31)) + 1_599_998_400_000  # event times within 2^31 ms of a base
+    base = int(src[0]) - (1 << 31)
+    dst = np.zeros(len(src), np.uint32)
+    assert L.fw_delta32_encode(src.ctypes.data, len(src), base, dst.ctypes.data) == 0
+    assert np.array_equal(dst.astype(np.int64) + base, src)
+    # INT64 extremes wrap modulo 2^64 on both sides
+    ext = np.array([np.iinfo(np.int64).max, np.iinfo(np.int64).max - 5], np.int64)
+    d2 = np.zeros(2, np.uint32)
+    assert L.fw_delta32_encode(ext.ctypes.data, 2, int(ext[1]), d2.ctypes.data) == 0
+    assert list(d2) == [5, 0]
+    bad = src.copy()
+    bad[500] = base + (1 << 32)
+    assert L.fw_delta32_encode(bad.ctypes.data, len(bad), base, dst.ctypes.data) == 1
+    bad[500] = base - 1
+    assert L.fw_delta32_encode(bad.ctypes.data, len(bad), base, dst.ctypes.data) == 1
+    assert L.fw_delta32_encode(src.ctypes.data, 0, base, dst.ctypes.data) == 0

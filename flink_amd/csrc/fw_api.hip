@@ -1318,6 +1318,8 @@ int fw_commit(fw_handle* h, int64_t n) {
     return commit_impl(h, n, 0u, nullptr);
 }
 
+// the loop vectorises; the wider x86 units where the host has them (chosen at load time)
+__attribute__((target_clones("avx512f", "avx2", "default")))
 int fw_delta32_encode(const int64_t* src, int64_t n, int64_t base, uint32_t* dst) {
     if (n <= 0) return 0;
     uint64_t out = 0;  // any high bits: a value outside the column's 2^32 window

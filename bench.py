@@ -155,6 +155,28 @@ def cpu_baseline(wl, sample_events, threads=1):
     return steps * B / dt, steps * B, dt, sum(n_out)
 
 
+def rank_load(owned, elapsed_s, partials, world):
+    """N > 1 per-rank load, collective over the job's process group (after the timed region).
+    owned: int64 tensor [world] of THIS rank's timed rows by destination subtask (its share of the
+    keyBy), on the collective's device; returns the job-wide per-subtask event counts, their max/mean
+    (the key-group imbalance that bounds linear scaling), every rank's timed wall clock and the
+    partial rows its operator ingested."""
+    import torch
+    import torch.distributed as dist
+    dist.all_reduce(owned)
+    mine = torch.tensor([float(elapsed_s), float(partials)], dtype=torch.float64, device=owned.device)
+    allr = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    ev = [int(x) for x in owned.cpu().tolist()]
+    mean = sum(ev) / world
+    return {"events_owned_per_rank": ev, "events_total": sum(ev),
+            "key_group_imbalance_max_over_mean": max(ev) / mean if mean else None,
+            "rank_elapsed_s": [float(x[0]) for x in allr],
+            "partials_ingested_per_rank": [int(x[1]) for x in allr],
+            "note": "events owned = rows of the timed batches whose key group the subtask owns "
+                    "(computeKeyGroupRangeForOperatorIndex); gathered after the timed region"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -446,6 +468,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    elapsed_own = elapsed
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -454,6 +477,23 @@ def main():
     kt = h.kernel_times()
     if st["error_flags"]:
         raise SystemExit(f"device error flags {st['error_flags']}")
+
+    # ---------------- N > 1: per-rank load (after the timed region) ---------------------------
+    # key-group skew limits linearity, so the line reports each subtask's share of the
+    # timed events -- the rows whose key group it owns (KeyGroupRangeAssignment
+    # .computeKeyGroupRangeForOperatorIndex :93-106, as KeyGroupStreamPartitioner.selectChannel routes
+    # them) -- and every rank's own timed wall clock; the shares sum to N * B * steps
+    ranks = None
+    if world > 1:
+        cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        owned = torch.zeros(world, dtype=torch.int64, device=dev)
+        kg_b = torch.empty(B, dtype=torch.int32, device=dev)
+        dst_b = torch.empty(B, dtype=torch.int32, device=dev)
+        for b in range(args.warmup, total_steps):
+            _native.check(L.fw_assign_key_groups(gk[b].data_ptr(), None, B, abi.KEYHASH_BINROW_BIGINT, 128, world,
+                                                 kg_b.data_ptr(), dst_b.data_ptr(), s))
+            owned += torch.bincount(dst_b.long(), minlength=world)
+        ranks = rank_load(owned.to(cdev), elapsed_own, st["partials_emitted"], world)
 
     n_total = args.steps * B * world
     value = n_total / elapsed
@@ -498,11 +538,17 @@ def main():
         import glob
         found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"traffic_{args.workload}.json")))
         tpath = found[-1] if found else ""
+    plan_name = "two-phase" if two_phase else "one-phase"
+    traffic_src = None
     if tpath and os.path.exists(tpath):
         tj = json.load(open(tpath))
-        if tj.get("workload") == args.workload:
+        # counters measured on this exact run shape only: same workload, GPU count and plan (files
+        # written before round 6 carry neither field: tools/measure.sh ran them at N = 1, one-phase)
+        if (tj.get("workload") == args.workload and tj.get("n_gpus", 1) == world
+                and tj.get("plan", "one-phase") == plan_name):
             traffic = tj.get("k_ingest_hbm_bytes_per_launch")
             traffic_m = tj.get("k_merge_fire_hbm_bytes_per_launch")
+            traffic_src = os.path.relpath(tpath, ROOT) if tpath.startswith(ROOT) else tpath
 
     # ---------------- end-to-end leg (N = 1): host-staged, pipelined --------------------------
     # What the JNI shim does, pipelined the way the handle allows: the host fills
@@ -664,7 +710,7 @@ def main():
                            "agreed_share_rows": ex._dn_share if ex._share_known else None,
                            "overflow_rounds": ex.spill_rounds}},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "fw::k_ingest (K1 key group + K2 slice assign + K3 LDS segmented reduce, "
                                    "chunk-local superbucket sort)",
                          "algorithmic_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_reduce_s * 1e6,
@@ -698,6 +744,7 @@ def main():
                                "traffic_over_algorithmic": (traffic_m / merge_bytes) if traffic_m else None},
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "per_rank": ranks,
             "device_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
             "host_issue_ms_per_step": t_issued / args.steps * 1e3,
         }

@@ -144,6 +144,7 @@ struct fw_handle {
     Ctrl* ctrl = nullptr;
     uint64_t* parts = nullptr;
     int32_t narrow = 0;          // compact partial rows (IngestArgs::narrow)
+    int32_t pack = 0;            // PF_PACK run rows (IngestArgs::pack)
     int64_t* slot_base = nullptr;  // [FW_MAX_PENDING] rank base of each pending push
     uint8_t* ranks = nullptr;      // [FW_MAX_PENDING][cap_rows] rank bytes of compact rows
     int64_t cell_cols = 0;       // cell_pad(max_nch): cells per superbucket per slot
@@ -663,6 +664,19 @@ int validate_and_plan(fw_handle* h) {
             }
         }
     }
+    // PF_PACK run rows: one 8-B word per partial (key and accumulator offsets, slice rank) for the
+    // one-word integer layouts on the compact rows' conditions (COUNT / SUM / MIN / MAX of BIGINT or
+    // INT, no NULLs); 24 -> 8 B per partial on the ingest's stores and the merge's reads.  FW_PACK=0
+    // switches them off (A/B).
+    {
+        const char* pe = getenv("FW_PACK");
+        const int32_t op = wd.op[0];
+        const bool int_word = wd.nw == 1 && !wd.has_q && !wd.has_ord && wd.gate[0] < 0 &&
+                              (op == W_CNT || op == W_SUM_I || op == W_MIN_I || op == W_MAX_I) && ops_layout(wd) != OPS_ANY;
+        const bool ok = c.api == FW_API_SQL && !h->keyrow && c.agg_phase != FW_PHASE_GLOBAL && h->tz_utc.empty() &&
+                        w.fast32 && ks.pass_log2 == 0 && (h->chunk_rows & (h->chunk_rows - 1)) == 0;
+        h->pack = ok && int_word && h->run_rows > 0 && !(pe && atoi(pe) == 0);
+    }
     h->treq_cap = std::max<int64_t>(c.max_batch_rows * 2, 1 << 16);
     if (c.api == FW_API_DATASTREAM) {
         if (c.allowed_lateness_ms > 0 && (int64_t)FW_MAX_PENDING * h->cap_rows >= (1ll << 32) - 1)
@@ -754,6 +768,7 @@ int allocate(fw_handle* h) {
             if (r) hipFree(r);
             h->run_rows = 0;
             h->sub_cap = 0;
+            h->pack = 0;
         } else {
             h->runs = (uint64_t*)r;
             h->run_ranks = (uint8_t*)rr;
@@ -969,7 +984,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.ordev_cap = h->ordev_cap;
     a.slot_base = h->slot_base;
     a.ranks = h->ranks;
-    a.compact = h->narrow != 0;
+    a.compact = h->narrow != 0 || h->pack != 0;
     a.runs = h->runs;
     a.run_ranks = h->run_ranks;
     a.run_fill = h->run_fill;
@@ -1088,6 +1103,7 @@ int push(fw_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const i
         a.slot_fmt = h->slot_fmt;
         a.run_rows = h->run_rows;
         a.sub_cap = h->sub_cap;
+        a.pack = h->pack;
         HIP_TRY(launch_ingest(a, h->stream, h->timer));
         h->pushes_ub++;
         h->pushes_total++;

@@ -73,6 +73,7 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
     unsigned long long* s_rows = (unsigned long long*)&lds[2];
     uint32_t* s_folded = (uint32_t*)&lds[3] + 1;  // a row of the chunk was folded into another
     uint32_t* wsum = (uint32_t*)&lds[4];  // IG_BLOCK / 64 words
+    int64_t* s_pk = (int64_t*)&lds[12];   // PF_PACK ranges of the chunk: key min / max, accumulator min / max
     const int PL = a.ks.pass_log2;
     const int n_sb = a.ks.n_sb >> PL;  // ingest superbuckets: the histogram and the cells
     const int n_units = a.ks.n_sb;     // state superbuckets (route_key's result)
@@ -106,6 +107,8 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
         *s_drop = 0;
         *s_rows = 0;
         *s_folded = 0;
+        s_pk[0] = s_pk[2] = INT64_MAX;
+        s_pk[1] = s_pk[3] = INT64_MIN;
     }
     for (int s = tid; s < (n_sb + 1) >> 1; s += IG_BLOCK) hist2[s] = 0;
 
@@ -416,6 +419,36 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
     });
     // PF_UNIT needs a chunk in which no row folded into another: one LDS flag store per wave that folded
     if (a.narrow == 2 && do_fold && __ballot(valid != valid_unfolded) && (tid & 63) == 0) *s_folded = 1u;
+    // ---- PF_PACK (runs, one integer word, no NULLs / ordinals): every push measures the key and
+    // accumulator ranges of its partials for the next flush epoch; the epoch's first push (slot 0)
+    // takes the parameters the previous push measured, the others the epoch's
+    const bool pk_stats = CAN_COMPACT && !X && a.pack != 0;
+    int64_t pk_k = 0, pk_v = 0;
+    uint32_t pk_bits = 0;
+    if (pk_stats) {
+        pk_k = __hip_atomic_load(slot == 0 ? &ctrl->pk_next_k : &ctrl->pk_cur_k, __ATOMIC_RELAXED, DEV_SCOPE);
+        pk_v = __hip_atomic_load(slot == 0 ? &ctrl->pk_next_v : &ctrl->pk_cur_v, __ATOMIC_RELAXED, DEV_SCOPE);
+        pk_bits = __hip_atomic_load(slot == 0 ? &ctrl->pk_next_bits : &ctrl->pk_cur_bits, __ATOMIC_RELAXED, DEV_SCOPE);
+        int64_t kmn = INT64_MAX, kmx = INT64_MIN, vmn = INT64_MAX, vmx = INT64_MIN;
+        static_for<RPT>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const bool v = (valid >> j) & 1u;
+            kmn = v ? min(kmn, rk[j]) : kmn;
+            kmx = v ? max(kmx, rk[j]) : kmx;
+            vmn = v ? min(vmn, (int64_t)racc[j][0]) : vmn;
+            vmx = v ? max(vmx, (int64_t)racc[j][0]) : vmx;
+        });
+        kmn = wred_min_i64(kmn);
+        kmx = wred_max_i64(kmx);
+        vmn = wred_min_i64(vmn);
+        vmx = wred_max_i64(vmx);
+        if ((tid & 63) == 0 && kmn <= kmx) {
+            __hip_atomic_fetch_min(&s_pk[0], kmn, __ATOMIC_RELAXED, LDS_SCOPE);
+            __hip_atomic_fetch_max(&s_pk[1], kmx, __ATOMIC_RELAXED, LDS_SCOPE);
+            __hip_atomic_fetch_min(&s_pk[2], vmn, __ATOMIC_RELAXED, LDS_SCOPE);
+            __hip_atomic_fetch_max(&s_pk[3], vmx, __ATOMIC_RELAXED, LDS_SCOPE);
+        }
+    }
     // ---- rank the partials per superbucket, scan, publish the cells
     uint32_t rdst[RPT];
     const bool sort = !(FW_ABL(a) & AB_NO_SORT);
@@ -429,9 +462,27 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
     // ---- the chunk's partial-row format (PF_*): compact unless a row kept its own slice end or
     // the chunk's slice ends spread over more than rank_lim slices
     bool wide = wide_row || !nar;
-    // (re-read here rather than kept live through the fold: the watermark does not change during a push)
-    const int64_t nbase = nar ? slice_end_of(a.win, wadd(__hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE), 1)) : 0;
-    if (nar) {  // uniform: the block-wide vote only when compact rows are possible
+    const bool runs = a.runs != nullptr && sort;
+    // PF_PACK push: runs, the epoch's parameters valid, every row on the common path's slice grid
+    const bool pk = pk_stats && runs && (pk_bits & PK_OK) && simple && cur_wm != INT64_MIN;
+    const uint32_t pk_kb = pk_bits & 255u, pk_rb = (pk_bits >> 8) & 255u, pk_vb = (pk_bits >> 16) & 255u;
+    // (re-read here rather than kept live through the fold: the watermark does not change during a push);
+    // a PF_PACK push counts ranks from the epoch's rank base (slot 0's, every later row's slice end is >= it)
+    const int64_t nbase = (pk && slot > 0) ? a.slot_base[0]
+                          : (nar || pk) ? slice_end_of(a.win, wadd(__hip_atomic_load(&ctrl->cur, __ATOMIC_RELAXED, DEV_SCOPE), 1))
+                                        : 0;
+    if (pk) {  // uniform: does every row of the chunk fit the epoch's bit fields?
+        const uint64_t rlim = min((uint64_t)a.rank_lim, (uint64_t)a.win.interval << pk_rb);
+        bool fit = !wide_row;
+        if (fit)
+            static_for<RPT>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                if ((valid & (1u << j)) && ((uint64_t)(rs[j] - nbase) >= rlim || ((uint64_t)(rk[j] - pk_k) >> pk_kb) != 0 ||
+                                            ((uint64_t)((int64_t)racc[j][0] - pk_v) >> pk_vb) != 0))
+                    fit = false;
+            });
+        wide = !__syncthreads_and(fit);
+    } else if (nar) {  // uniform: the block-wide vote only when compact rows are possible
         if (!wide)
             static_for<RPT>([&](auto J) {
                 constexpr int j = decltype(J)::value;
@@ -440,11 +491,12 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
         wide = __syncthreads_or(wide);
     }
     uint32_t* cells = a.cells + (size_t)slot * n_sb * a.max_nch;
-    // runs (IngestArgs::runs): a push's run rows share one format -- compact when the push is (COUNT(*)
-    // alone: PF_UNIT when no chunk folds, else PF_NARROW); a chunk that must write PF_WIDE rows in a
-    // compact push keeps them all in its own region
-    const bool runs = a.runs != nullptr && sort;
-    const uint32_t push_fmt = (runs && CAN_COMPACT && nar) ? ((!X && a.narrow == 2 && !do_fold) ? PF_UNIT : PF_NARROW) : PF_WIDE;
+    // runs (IngestArgs::runs): a push's run rows share one format -- PF_PACK, else compact when the
+    // push is (COUNT(*) alone: PF_UNIT when no chunk folds, else PF_NARROW); a chunk that must write
+    // PF_WIDE rows in a compact push keeps them all in its own region
+    const uint32_t push_fmt = pk ? PF_PACK
+                              : (runs && CAN_COMPACT && nar) ? ((!X && a.narrow == 2 && !do_fold) ? PF_UNIT : PF_NARROW)
+                                                             : PF_WIDE;
     // COUNT(*) alone and nothing folded in this chunk: every row counts 1
     const uint32_t fmt = runs ? (wide ? PF_WIDE : push_fmt)
                          : (!CAN_COMPACT || wide || !sort) ? PF_WIDE
@@ -517,6 +569,11 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
             const uint32_t d = rdst[j] - w0;
             if (!(valid & (1u << j)) || d >= wrows) return;
             uint64_t* p = stage + (size_t)d * PWX;
+            if (CAN_COMPACT && fmt == PF_PACK) {  // rs is the rank here
+                p[0] = ((uint64_t)(rk[j] - pk_k) << (64 - pk_kb)) | ((uint64_t)rs[j] << pk_vb) |
+                       (uint64_t)((int64_t)racc[j][0] - pk_v);
+                return;
+            }
             p[0] = (uint64_t)rk[j];
             if (fmt == PF_WIDE) p[1] = (uint64_t)rs[j];
             else rstage[d] = (uint8_t)rs[j];  // the rank (set below the format decision)
@@ -563,9 +620,13 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
                 auto copy_out = [&](auto PC) {
                     constexpr uint32_t P = decltype(PC)::value;
                     for (uint32_t r = tid; r < nr; r += IG_BLOCK) {
-                        const uint32_t dd = sdst[w0 + r];
+                        const uint32_t dd = (FW_ABL(a) & AB_IG_LINEAR) ? (RUN_LOCAL | (w0 + r)) : sdst[w0 + r];
                         const uint64_t* src = stage + (size_t)r * P;
                         uint64_t* dst = (dd & RUN_LOCAL) ? out + (size_t)(dd & ~RUN_LOCAL) * P : rslot + (size_t)dd * P;
+                        if (FW_ABL(a) & AB_IG_NO_GSTORE) {
+                            asm volatile("" ::"v"(src[0]), "v"(dst));
+                            continue;
+                        }
                         if constexpr (P % 2 == 0) {
 #pragma unroll
                             for (uint32_t k = 0; k < P / 2; k++) {
@@ -592,7 +653,7 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
                 if (fmt == PF_WIDE) copy_out(std::integral_constant<uint32_t, (uint32_t)PW>{});
                 else if (fmt == PF_NARROW) copy_out(std::integral_constant<uint32_t, (uint32_t)(1 + NW)>{});
                 else copy_out(std::integral_constant<uint32_t, 1u>{});
-                if (fmt != PF_WIDE)
+                if (pf_rank_bytes(fmt))
                     for (uint32_t r = tid; r < nr; r += IG_BLOCK) {
                         const uint32_t dd = sdst[w0 + r];
                         uint8_t* rd = (dd & RUN_LOCAL) ? a.ranks + (size_t)slot * a.cap_rows + (size_t)base + (dd & ~RUN_LOCAL)
@@ -610,7 +671,7 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
                     st_wt8(dst + q, stage[q]);
                 }
             }
-            if (fmt != PF_WIDE) {
+            if (pf_rank_bytes(fmt)) {
                 uint8_t* rd = a.ranks + (size_t)slot * a.cap_rows + (size_t)base + w0;  // 16-B aligned
                 for (uint32_t q = 16 * tid; q < nr; q += 16 * IG_BLOCK) {
                     if (q + 16 <= nr) {
@@ -628,13 +689,8 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
     // wave reductions first: one LDS atomic per wave, not 3 x 512 on the same three words (they
     // serialise: ~10 us of a CFG2 launch)
     {
-        const int64_t wm = wave_min_i64(lmin);
-        uint32_t wd = ldrop, wr = lrows;
-#pragma unroll
-        for (int k = 32; k > 0; k >>= 1) {
-            wd += __shfl_xor(wd, k, 64);
-            wr += __shfl_xor(wr, k, 64);
-        }
+        const int64_t wm = wred_min_i64(lmin);
+        const uint32_t wd = wred_sum_u32(ldrop), wr = wred_sum_u32(lrows);
         if ((tid & 63) == 0) {
             if (wm != INT64_MAX) __hip_atomic_fetch_min(s_min, wm, __ATOMIC_RELAXED, LDS_SCOPE);
             if (wd) atomicAdd(s_drop, (unsigned long long)wd);
@@ -650,8 +706,11 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
         __hip_atomic_store(&a.chunk_stats[CS_WORDS * c + 3], (int64_t)total, __ATOMIC_RELAXED, DEV_SCOPE);
         // bytes of partial rows (+ rank bytes) this chunk wrote, and whether they are compact
         __hip_atomic_store(&a.chunk_stats[CS_WORDS * c + 4],
-                           (int64_t)total * (8 * PWX + (fmt != PF_WIDE ? 1 : 0)) | ((int64_t)(fmt != PF_WIDE) << 40),
+                           (int64_t)total * (8 * PWX + (pf_rank_bytes(fmt) ? 1 : 0)) | ((int64_t)(fmt != PF_WIDE) << 40),
                            __ATOMIC_RELAXED, DEV_SCOPE);
+        if (pk_stats)
+#pragma unroll
+            for (int q = 0; q < 4; q++) __hip_atomic_store(&a.chunk_stats[CS_WORDS * c + 8 + q], s_pk[q], __ATOMIC_RELAXED, DEV_SCOPE);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         *s_last = grid_last_wg(a.tickets->c[0]);
     }
@@ -665,14 +724,11 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
         q += __hip_atomic_load(&a.chunk_stats[CS_WORDS * i + 3], __ATOMIC_RELAXED, DEV_SCOPE);
         y += __hip_atomic_load(&a.chunk_stats[CS_WORDS * i + 4], __ATOMIC_RELAXED, DEV_SCOPE);  // no carry: < 2^40 per chunk
     }
-    m = wave_min_i64(m);
-#pragma unroll
-    for (int k = 32; k > 0; k >>= 1) {
-        d += (int64_t)__shfl_xor((long long)d, k, 64);
-        r += (int64_t)__shfl_xor((long long)r, k, 64);
-        q += (int64_t)__shfl_xor((long long)q, k, 64);
-        y += (int64_t)__shfl_xor((long long)y, k, 64);
-    }
+    m = wred_min_i64(m);
+    d = wred_sum_i64(d);
+    r = wred_sum_i64(r);
+    q = wred_sum_i64(q);
+    y = wred_sum_i64(y);
     int64_t* red = (int64_t*)area;  // [5][IG_BLOCK / 64]
     constexpr int NWV = IG_BLOCK / 64;
     if ((tid & 63) == 0) {
@@ -704,8 +760,58 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
         if (fold) ctrl->fold_skip = q * 50 > r * 49;  // folded away fewer than 2 % of the rows
         ctrl->push_count += 1;
         ctrl->late_dropped += (uint64_t)d;
-        kt_end(a.kt);
     }
+    if (pk_stats) {  // (uniform) the push's key and accumulator ranges -> the next epoch's PF_PACK fields
+        int64_t kmn = INT64_MAX, kmx = INT64_MIN, vmn = INT64_MAX, vmx = INT64_MIN;
+        for (int64_t i = tid; i < (int64_t)gridDim.x; i += IG_BLOCK) {
+            const int64_t* cs = a.chunk_stats + CS_WORDS * i + 8;
+            kmn = min(kmn, __hip_atomic_load(&cs[0], __ATOMIC_RELAXED, DEV_SCOPE));
+            kmx = max(kmx, __hip_atomic_load(&cs[1], __ATOMIC_RELAXED, DEV_SCOPE));
+            vmn = min(vmn, __hip_atomic_load(&cs[2], __ATOMIC_RELAXED, DEV_SCOPE));
+            vmx = max(vmx, __hip_atomic_load(&cs[3], __ATOMIC_RELAXED, DEV_SCOPE));
+        }
+        kmn = wred_min_i64(kmn);
+        kmx = wred_max_i64(kmx);
+        vmn = wred_min_i64(vmn);
+        vmx = wred_max_i64(vmx);
+        __syncthreads();  // tid 0 is done with red
+        if ((tid & 63) == 0) {
+            red[tid >> 6] = kmn;
+            red[NWV + (tid >> 6)] = kmx;
+            red[2 * NWV + (tid >> 6)] = vmn;
+            red[3 * NWV + (tid >> 6)] = vmx;
+        }
+        __syncthreads();
+        if (tid == 0) {
+#pragma unroll 1
+            for (int v = 1; v < NWV; v++) {
+                kmn = min(kmn, red[v]);
+                kmx = max(kmx, red[NWV + v]);
+                vmn = min(vmn, red[2 * NWV + v]);
+                vmx = max(vmx, red[3 * NWV + v]);
+            }
+            if (slot == 0) {  // this push opened the flush epoch with the parameters it read
+                ctrl->pk_cur_k = pk_k;
+                ctrl->pk_cur_v = pk_v;
+                ctrl->pk_cur_bits = pk_bits;
+            }
+            if (kmn <= kmx) {  // rows seen: fields twice the measured spans (kb + rb + vb = 64, 2 <= rb <= 8)
+                const uint64_t ks = (uint64_t)kmx - (uint64_t)kmn, vs = (uint64_t)vmx - (uint64_t)vmn;
+                const uint32_t kb = (ks ? 64u - (uint32_t)__clzll((long long)ks) : 1u) + 1u;
+                uint32_t vb = (vs ? 64u - (uint32_t)__clzll((long long)vs) : 1u) + 1u;
+                if (kb + vb + 2u <= 64u) {
+                    const uint32_t rb = min(64u - kb - vb, 8u);
+                    vb = 64u - kb - rb;  // the spare bits widen the accumulator field (sums drift)
+                    ctrl->pk_next_k = (int64_t)((uint64_t)kmn - ((((1ull << kb) - 1ull) - ks) >> 1));
+                    ctrl->pk_next_v = (int64_t)((uint64_t)vmn - ((((1ull << vb) - 1ull) - vs) >> 1));
+                    ctrl->pk_next_bits = kb | (rb << 8) | (vb << 16) | PK_OK;
+                } else {
+                    ctrl->pk_next_bits = 0;
+                }
+            }
+        }
+    }
+    if (tid == 0) kt_end(a.kt);
 }
 
 template <int NV, int NW, bool X>

@@ -131,12 +131,22 @@ constexpr bool ig_runs_fit(int n_isb, int block, int rpt, int nw) {
 constexpr uint32_t PF_WIDE = 0;    // (key, sliceEnd, acc[nw])
 constexpr uint32_t PF_NARROW = 1;  // (key, acc[nw]) + rank byte
 constexpr uint32_t PF_UNIT = 2;    // (key) + rank byte; acc = 1
+// (runs, one integer accumulator word) one 8-B word per partial: the key and the accumulator as
+// offsets from the flush epoch's bases and the slice as a rank from its rank base,
+//   (key - kbase) << (64 - kb) | rank << vb | (acc - vbase)
+// with kb / rb / vb bits (Ctrl::pk_cur_*; the rank base is slot_base[0], the epoch's first push's).
+// The bases come from the previous push's key and accumulator ranges (2x headroom); a chunk with a
+// row outside them writes PF_WIDE rows into its own region instead.
+constexpr uint32_t PF_PACK = 3;
 constexpr int64_t PF_MAX_RANK = 255;
+constexpr uint32_t PK_OK = 1u << 31;  // Ctrl::pk_*_bits: kb | rb << 8 | vb << 16 | PK_OK
 __host__ __device__ inline uint32_t cell_count(uint32_t v) { return (v >> 16) & 0x3FFFu; }
 __host__ __device__ inline uint32_t cell_start(uint32_t v) { return v & 0xFFFFu; }
 __host__ __device__ inline uint32_t cell_fmt(uint32_t v) { return v >> 30; }
 // words per row of a format
 __host__ __device__ inline int pf_stride(uint32_t fmt, int nw) { return fmt == PF_WIDE ? 2 + nw : fmt == PF_NARROW ? 1 + nw : 1; }
+// a compact format with a side array of rank bytes
+__host__ __device__ inline bool pf_rank_bytes(uint32_t fmt) { return fmt == PF_NARROW || fmt == PF_UNIT; }
 
 // Accumulator word operations.  Every built-in aggregate maps to 1 or 2 words, except SQL
 // MIN/MAX(DOUBLE), whose strict-comparison-in-arrival-order semantics need a small word group.
@@ -310,6 +320,12 @@ struct Ctrl {
     uint32_t kr_epoch;       // mark epoch of the current collection
     int32_t kr_gc;           // a collection runs in the current advance (set by k_kr_gc_begin)
     int64_t kr_collections;  // collections so far
+    // PF_PACK parameters (IngestArgs::pack): pk_next_* measured by the last push (its key and
+    // accumulator ranges), taken by the next flush epoch's first push (slot 0) into pk_cur_*, which
+    // every push of the epoch and the merge that flushes them decode with
+    int64_t pk_next_k, pk_next_v;
+    int64_t pk_cur_k, pk_cur_v;
+    uint32_t pk_next_bits, pk_cur_bits;  // kb | rb << 8 | vb << 16 | PK_OK
 };
 
 // Window / slice description shared by both kernels (SliceAssigners.java).
@@ -491,7 +507,7 @@ struct AggDesc {
     int32_t by_prev;          // minBy / maxBy: the W_BYPREV word (-1: not a minBy / maxBy layout)
 };
 
-constexpr int CS_WORDS = 8;  // IngestArgs::chunk_stats words per chunk
+constexpr int CS_WORDS = 12;  // IngestArgs::chunk_stats words per chunk
 struct IngestArgs {
     const int64_t* key;
     const int64_t* ts;
@@ -512,7 +528,7 @@ struct IngestArgs {
     int32_t* slot_nch;     // [FW_MAX_PENDING] chunks of each pending push
     int64_t max_nch;       // cell_pad(chunks per slot): cells per superbucket per slot
     int64_t* chunk_stats;  // [n_chunks][CS_WORDS]: min target slice, dropped rows, accepted rows, partials,
-                           // partial bytes | compact << 40
+                           // partial bytes | compact << 40, -, -, -, key min / max, accumulator min / max
     Tickets* tickets;
     int64_t n_chunks;
     int64_t* treq;         // timer requests: (key, window, sb) triples
@@ -550,6 +566,7 @@ struct IngestArgs {
     int32_t* slot_fmt;     // [FW_MAX_PENDING]: the run rows' format (PF_*) of each push
     int64_t run_rows;      // rows per slot: n_isb * RUN_X * sub_cap
     int32_t sub_cap;       // rows per sub-run
+    int32_t pack;          // PF_PACK run rows allowed (runs, one integer word; fw_api.hip plans it)
 };
 // Development ablations and phase stamps (FW_ABLATE) are compiled into the kernels only in a
 // diagnostic build (make DIAG=1): in the production build their checks fold away, so the hot loops
@@ -571,6 +588,8 @@ constexpr int AB_M_NO_FOLDOP = 1024; // merge: insert the partials but skip the 
 constexpr int AB_GSTAMPS = 256;      // merge: with AB_STAMPS, stamps 2/4/7 = thread 0 gather loads/probe/fold
 constexpr int AB_M_NO_EMIT = 4096;  // merge: fire without writing result rows (diagnostic)
 constexpr int AB_FSTAMPS = 8192;    // merge: per-lane cycles of fire_one's parts into stamps[8..11]
+constexpr int AB_IG_LINEAR = 16384;  // ingest (runs): store every staged row at its chunk position (no scatter)
+constexpr int AB_IG_NO_GSTORE = 32768;  // ingest: stage the rows in LDS but issue no global store
 constexpr int N_STAMPS = 16;
 
 struct MergeArgs {

@@ -291,11 +291,65 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
     for (int d = 32; d > 0; d >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, d, 64));
     return v;
 }
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, d, 64));
+    return v;
+}
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
     return v;
 }
+// Whole-wave reductions on DPP (no LDS): butterfly inside each 16-lane row (quad perms, half-row and
+// row mirrors), then row_bcast:15 / row_bcast:31 carry the rows into lane 63, read back as a scalar.
+// Every lane of the wave must be active.  (The __shfl_xor butterflies above go through
+// ds_bpermute: six dependent LDS round trips per 32-bit step.)
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t old, uint64_t v) {
+    const uint32_t lo = dpp_u32<CTRL, RM>((uint32_t)old, (uint32_t)v);
+    const uint32_t hi = dpp_u32<CTRL, RM>((uint32_t)(old >> 32), (uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T wred(T v, T ident, Op op) {
+    if constexpr (sizeof(T) == 8) {
+        v = op(v, (T)dpp_u64<0xB1, 0xf>((uint64_t)ident, (uint64_t)v));   // quad_perm [1,0,3,2]
+        v = op(v, (T)dpp_u64<0x4E, 0xf>((uint64_t)ident, (uint64_t)v));   // quad_perm [2,3,0,1]
+        v = op(v, (T)dpp_u64<0x141, 0xf>((uint64_t)ident, (uint64_t)v));  // row_half_mirror
+        v = op(v, (T)dpp_u64<0x140, 0xf>((uint64_t)ident, (uint64_t)v));  // row_mirror
+        v = op(v, (T)dpp_u64<0x142, 0xa>((uint64_t)ident, (uint64_t)v));  // row_bcast:15 -> rows 1, 3
+        v = op(v, (T)dpp_u64<0x143, 0xc>((uint64_t)ident, (uint64_t)v));  // row_bcast:31 -> rows 2, 3
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, 63);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), 63);
+        return (T)(((uint64_t)hi << 32) | lo);
+    } else {
+        v = op(v, (T)dpp_u32<0xB1, 0xf>((uint32_t)ident, (uint32_t)v));
+        v = op(v, (T)dpp_u32<0x4E, 0xf>((uint32_t)ident, (uint32_t)v));
+        v = op(v, (T)dpp_u32<0x141, 0xf>((uint32_t)ident, (uint32_t)v));
+        v = op(v, (T)dpp_u32<0x140, 0xf>((uint32_t)ident, (uint32_t)v));
+        v = op(v, (T)dpp_u32<0x142, 0xa>((uint32_t)ident, (uint32_t)v));
+        v = op(v, (T)dpp_u32<0x143, 0xc>((uint32_t)ident, (uint32_t)v));
+        return (T)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    }
+}
+__device__ __forceinline__ int64_t wred_min_i64(int64_t v) {
+    return wred<int64_t>(v, INT64_MAX, [](int64_t a, int64_t b) { return a < b ? a : b; });
+}
+__device__ __forceinline__ int64_t wred_max_i64(int64_t v) {
+    return wred<int64_t>(v, INT64_MIN, [](int64_t a, int64_t b) { return a > b ? a : b; });
+}
+__device__ __forceinline__ uint32_t wred_sum_u32(uint32_t v) {
+    return wred<uint32_t>(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
+}
+__device__ __forceinline__ int64_t wred_sum_i64(int64_t v) {
+    return wred<int64_t>(v, 0, [](int64_t a, int64_t b) { return a + b; });
+}
+
 // slot claim for the active lanes of a wave: one atomicAdd on *ctr, each lane gets base + rank
 __device__ __forceinline__ int32_t wave_claim(int32_t* ctr) {
     const uint64_t act = __ballot(1);

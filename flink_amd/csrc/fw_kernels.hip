@@ -123,6 +123,8 @@ __global__ void k_init_ctrl(Ctrl* c) {
         c->kr_epoch = 0;
         c->kr_gc = 0;
         c->kr_collections = 0;
+        c->pk_next_k = c->pk_next_v = c->pk_cur_k = c->pk_cur_v = 0;
+        c->pk_next_bits = c->pk_cur_bits = 0;  // no PF_PACK until a push has measured its ranges
     }
 }
 

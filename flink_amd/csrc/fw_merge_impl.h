@@ -912,6 +912,33 @@ __device__ __forceinline__ CellGroup cell_group(uint32_t v, int f, int64_t CH) {
 constexpr int GF_PASS = 1;
 constexpr int GF_COMPACT = 2;
 
+// PF_PACK rows (fw_internal.h): the flush epoch's fields and bases, and one row decoded into the
+// PF_WIDE layout (key, sliceEnd, acc)
+struct PackDec {
+    int64_t kbase, vbase, rbase;
+    uint32_t ksh, rb, vb;
+};
+__device__ __forceinline__ PackDec pack_dec(const MergeArgs& a) {
+    PackDec d;
+    const uint32_t bits = __hip_atomic_load(&a.ctrl->pk_cur_bits, __ATOMIC_RELAXED, DEV_SCOPE);
+    d.kbase = __hip_atomic_load(&a.ctrl->pk_cur_k, __ATOMIC_RELAXED, DEV_SCOPE);
+    d.vbase = __hip_atomic_load(&a.ctrl->pk_cur_v, __ATOMIC_RELAXED, DEV_SCOPE);
+    d.rbase = a.slot_base[0];
+    d.ksh = 64u - (bits & 255u);
+    d.rb = (bits >> 8) & 255u;
+    d.vb = (bits >> 16) & 255u;
+    return d;
+}
+template <int PW>
+__device__ __forceinline__ void unpack_row(const PackDec& d, uint64_t w, int64_t interval, uint64_t (&row)[PW]) {
+    static_assert(PW == 3, "PF_PACK rows carry one accumulator word");
+    row[0] = (uint64_t)d.kbase + (w >> d.ksh);
+    const uint32_t rank = (uint32_t)(w >> d.vb) & ((1u << d.rb) - 1u);
+    // rank * interval < 2^31 (IngestArgs::rank_lim)
+    row[1] = (uint64_t)(d.rbase + (int64_t)(rank * (uint32_t)interval));
+    row[2] = (uint64_t)d.vbase + (w & ((1ull << d.vb) - 1ull));
+}
+
 template <int NW, int GU, int GF>
 __device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t pi, const CellGroup& g, uint32_t r0,
                                                     int sb, uint64_t (&row)[GU][2 + NW]) {
@@ -931,6 +958,9 @@ __device__ __forceinline__ uint32_t load_group_rows(const MergeArgs& a, int64_t 
         const uint32_t fmt = (uint32_t)__shfl((int)g.fmt, lo, 64);
         if (!CR || fmt == PF_WIDE) {
             load_words<PW>(seg + (size_t)rg * PW, row[u]);
+        } else if (NW == 1 && fmt == PF_PACK) {
+            const uint32_t within = rg & ((1u << a.ch_log2) - 1u);
+            if constexpr (NW == 1) unpack_row(pack_dec(a), seg[(size_t)(rg - within) * PW + within], a.win.interval, row[u]);
         } else {
             // a compact chunk fills the front of its PF_WIDE-sized region
             const uint32_t within = rg & ((1u << a.ch_log2) - 1u);
@@ -1016,6 +1046,8 @@ __device__ __forceinline__ uint32_t load_run_rows(const MergeArgs& a, const RunS
     const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)r0_);
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readfirstlane((int)g.tot);
     const uint32_t last = min(r0 + (uint32_t)(64 * GU), tot) - 1u;  // the block's last row (tot > 0)
+    PackDec pk{};
+    if constexpr (CR && NW == 1) pk = pack_dec(a);
     const uint32_t first = min(r0, tot - 1u);  // a block past the end re-reads the last row
     int cur = 0;
 #pragma unroll
@@ -1047,7 +1079,7 @@ __device__ __forceinline__ uint32_t load_run_rows(const MergeArgs& a, const RunS
 #pragma unroll
     for (int u = 0; u < GU; u++) {
         const uint32_t ri = adj[u] + x[u];  // row index in its push's run region
-        const uint32_t p = pf[u] & 15u, fmt = pf[u] >> 4;
+        const uint32_t p = pf[u] & 15u, fmt = (pf[u] >> 4) & 3u;
         const uint64_t* base = a.runs + (size_t)p * a.run_rows * PW;
         if (!CR || fmt == PF_WIDE) {
             // plain 8-B loads straight into the row's registers: no lane-parity selects, so the
@@ -1055,6 +1087,8 @@ __device__ __forceinline__ uint32_t load_run_rows(const MergeArgs& a, const RunS
             const uint64_t* q = base + (size_t)ri * PW;
 #pragma unroll
             for (int w = 0; w < PW; w++) row[u][w] = q[w];
+        } else if (NW == 1 && fmt == PF_PACK) {
+            if constexpr (NW == 1) unpack_row(pk, base[ri], a.win.interval, row[u]);
         } else {
             const uint32_t rank = a.run_ranks[(size_t)p * a.run_rows + ri];
             row[u][1] = (uint64_t)(a.slot_base[p] + (int64_t)(rank * (uint32_t)a.win.interval));

@@ -146,15 +146,24 @@ class WindowOperator:
             return ids
         return np.array([self._kstr[int(i)] for i in ids], dtype=object)
 
+    def _intern_batch(self, keys):
+        """a batch of STRING keys -> (device ids, String.hashCodes): each distinct String of the batch is
+        looked up once.  The table grows with the distinct Strings the operator has seen (ids are not
+        reused: a long-running, high-cardinality String stream holds every String it ever saw)."""
+        uniq, inv = np.unique(np.asarray([str(k) for k in keys], dtype=object), return_inverse=True)
+        ids = np.empty(len(uniq), np.int64)
+        hashes = np.empty(len(uniq), np.int32)
+        for i, k in enumerate(uniq.tolist()):
+            ids[i], hashes[i] = self._intern(k)
+        return ids[inv], hashes[inv]
+
     def process_batch(self, keys, timestamps, values, key_hashes=None, records=None):
         """processElement for a batch; ``records``: the elements themselves (record-shaped
         operator), kept until the device says which ones are first elements of a window.  A
         STRING-keyed operator takes its keys as Python strings."""
         seq0 = self.handle.push_seq
         if self.key_type == "STRING":
-            pairs = [self._intern(str(k)) for k in keys]
-            keys = np.array([p[0] for p in pairs], dtype=np.int64)
-            key_hashes = np.array([p[1] for p in pairs], dtype=np.int32)
+            keys, key_hashes = self._intern_batch(keys) if len(keys) else (np.empty(0, np.int64), np.empty(0, np.int32))
         self.handle.push_host(keys, timestamps, [values], key_hashes)
         self._keep(seq0, records, len(keys))
 
@@ -236,23 +245,32 @@ class WindowOperator:
 
     def snapshot_state(self) -> bytes:
         """The device blob; a record-shaped operator appends the first elements it keeps (the
-        reference's window state holds them: HeapReducingState's value is value1)."""
-        if self.field is None:
+        reference's window state holds them: HeapReducingState's value is value1), a STRING-keyed
+        one the Strings behind its device key ids (the blob holds ids)."""
+        if self.field is None and self.key_type != "STRING":
             return self.handle.snapshot()
-        self.handle.flush()                          # prepareSnapshotPreBarrier
-        self._first_elements(np.empty(0, np.int64), True)  # the flush's retains; batches flushed
+        if self.field is not None:
+            self.handle.flush()                          # prepareSnapshotPreBarrier
+            self._first_elements(np.empty(0, np.int64), True)  # the flush's retains; batches flushed
         blob = self.handle.snapshot()
-        side = json.dumps([[o, [_enc_field(x) for x in r], c] for o, (r, c) in self._retained.items()]).encode()
-        return struct.pack("<q", len(blob)) + blob + side
+        side = {"retained": [[o, [_enc_field(x) for x in r], c] for o, (r, c) in self._retained.items()]}
+        if self.key_type == "STRING":
+            side["strings"] = self._kstr
+        return struct.pack("<q", len(blob)) + blob + json.dumps(side).encode()
 
     def initialize_state(self, blob: bytes):
-        if self.field is None:
+        if self.field is None and self.key_type != "STRING":
             self.handle.restore(blob)
             return
         n = struct.unpack_from("<q", blob, 0)[0]
         self.handle.restore(blob[8:8 + n])
-        self._retained = {o: [tuple(_dec_field(x) for x in r), c] for o, r, c in json.loads(blob[8 + n:].decode())}
+        side = json.loads(blob[8 + n:].decode())
+        self._retained = {o: [tuple(_dec_field(x) for x in r), c] for o, r, c in side["retained"]}
         self._pending.clear()
+        if self.key_type == "STRING":  # the same ids as the snapshotting operator's
+            self._kstr = list(side["strings"])
+            self._kid = {k: i for i, k in enumerate(self._kstr)}
+            self._khash = [heap_state.java_string_hash(k) for k in self._kstr]
 
     # ---- the heap keyed-state backend's key-group bytes (heap_state.py) -------------------------
     def _cleanup_time(self, end):

@@ -304,3 +304,44 @@ def test_gloo_device_valve_holds_watermark_until_overflow_round():
     expect[0] = expect[1] = -(1 << 63)  # step 0 is Long.MIN_VALUE; step 1 overflows and holds it
     assert res[0][2] == expect
     assert res[0][3] == n_batches // 2
+
+
+def _worker_rank_load(rank, port, n_batches, n, out_q):
+    """bench.rank_load on CPU: each rank routes its slice of every batch by destination subtask
+    (the oracle's computeKeyGroupRangeForOperatorIndex) and the collective returns the job-wide shares."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        import bench
+        from oracle.oracle import operator_indices
+        owned = torch.zeros(WORLD, dtype=torch.int64)
+        for b in range(n_batches):
+            k, _, _ = _stream(rank, b, n)
+            owned += torch.bincount(torch.from_numpy(operator_indices(abi.KEYHASH_BINROW_BIGINT, k, 128, WORLD)).long(),
+                                    minlength=WORLD)
+        out_q.put((rank, bench.rank_load(owned, 0.5 + rank, 100 * (rank + 1), WORLD)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_rank_load_fields_sum_to_all_events():
+    """The N > 1 BENCH line's per-rank block (bench.rank_load): present on every
+    rank, the per-subtask event shares sum to N * B * steps, the imbalance is max / mean of them, and
+    every rank's wall clock and ingested partials are gathered."""
+    n_batches, n = 3, 4096
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_rank_load, args=(r, port, n_batches, n, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    r = res[0]
+    ev = r["events_owned_per_rank"]
+    assert len(ev) == WORLD and sum(ev) == r["events_total"] == WORLD * n_batches * n
+    assert min(ev) > 0 and r["key_group_imbalance_max_over_mean"] == pytest.approx(max(ev) / (sum(ev) / WORLD))
+    assert r["rank_elapsed_s"] == [0.5, 1.5] and r["partials_ingested_per_rank"] == [100, 200]

@@ -303,3 +303,45 @@ def test_string_keys_route_by_java_hash_across_subtasks():
         b.close()
     a.close()
     assert got == want
+
+
+@pytest.mark.parametrize("shaped", [True, False], ids=["record_shaped", "key_value"])
+def test_string_key_snapshot_restores_into_fresh_operator(shaped):
+    """snapshot_state / initialize_state of a STRING-keyed operator: the device blob holds
+    interned ids, so the snapshot carries the id -> String table and a fresh operator resumes with the
+    same Strings -- a String first seen after the restore gets a new id, not one of the restored ones."""
+    from flink_amd.datastream.heap_state import TupleSerializer
+    from flink_amd.datastream.window_operator import WindowOperator
+    from flink_amd.datastream.windowing import EventTimeTrigger, TumblingEventTimeWindows
+
+    def op():
+        kw = dict(field=1, record_serializer=TupleSerializer.of("STRING", "INT")) if shaped else {}
+        return WindowOperator(TumblingEventTimeWindows.of(3000), EventTimeTrigger(), ("sum", "INT"), key_type="STRING",
+                              state_capacity=1 << 12, max_batch_rows=1 << 12, output_capacity=1 << 12, **kw).open()
+    rng = np.random.default_rng(11)
+    names = [f"k{i}" for i in range(40)]
+    keys = [names[j] for j in rng.integers(0, 40, 500)]
+    ts = rng.integers(0, 6000, 500).astype(np.int64)
+    vals = rng.integers(0, 50, 500).astype(np.int64)
+    recs = lambda ks, vs: [(k, int(v)) for k, v in zip(ks, vs)] if shaped else None
+    a = op()
+    a.process_batch(keys[:300], ts[:300], vals[:300], records=recs(keys[:300], vals[:300]))
+    blob = a.snapshot_state()
+    a.close()
+    b = op()  # fresh: no Strings interned yet
+    b.initialize_state(blob)
+    late_keys = keys[300:] + ["new-key"]
+    late_ts = np.concatenate([ts[300:], np.array([100], np.int64)])
+    late_vals = np.concatenate([vals[300:], np.array([7], np.int64)])
+    b.process_batch(late_keys, late_ts, late_vals, records=recs(late_keys, late_vals))
+    got = {}
+    for wm in (2999, 5999):
+        r = b.process_watermark(wm)
+        for k, v, t in zip(r["key"], r["value"], r["timestamp"]):
+            got[(k, int(t))] = int(np.int32(np.int64(v)))
+    want = {}
+    for k, t, v in zip(keys + ["new-key"], np.concatenate([ts, [100]]), np.concatenate([vals, [7]])):
+        e = (k, (int(t) // 3000) * 3000 + 2999)
+        want[e] = want.get(e, 0) + int(v)
+    assert got == want
+    b.close()

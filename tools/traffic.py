@@ -55,6 +55,8 @@ def main():
     ing_w = sum(wv["k_ingest"]) / len(wv["k_ingest"]) * 1024.0
     res = {
         "workload": wl,
+        "n_gpus": 1,            # tools/measure.sh runs the PMC passes at N = 1 with the default plan
+        "plan": "one-phase",
         "k_ingest_hbm_bytes_per_launch": ing_f * read_scale + ing_w,
         "k_ingest_read_bytes_per_launch": ing_f * read_scale,
         "k_ingest_write_bytes_per_launch": ing_w,

@@ -53,11 +53,9 @@ __device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t* wsum, 
 }
 
 // X: the configuration has nullable columns or words that read arrival ordinals (gates, ordinals)
-#ifndef FW_IG_MINW
-#define FW_IG_MINW 4  // waves per SIMD the register budget must allow (development A/B builds override)
-#endif
 template <int NV, int NW, int RPT, bool X, int IG_BLOCK>
-__global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
+// (launch bounds: 4 waves per SIMD, 128 VGPRs)
+__global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int CH = IG_BLOCK * RPT;
     constexpr int NSUB = RPT / IG_SRPT;
     constexpr int NVR = NV > 0 ? NV : 1;
@@ -199,13 +197,17 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
     // `slow` and takes the general path below, entered only by waves that have such a row: the
     // per-row divergent branches of the general path cost as many scalar instructions as the
     // vector work itself.
-    const bool simple = fast && !a.win.ds && !a.global && a.win.tz.n == 0;
+    // (simple_l: the launch's part of it -- the push formats below depend on the launch only, so every
+    // chunk agrees on them; a chunk too far off for the 32-bit path sends every row down the general
+    // path, which keeps the slice end in the row: PF_WIDE)
+    const bool simple_l = a.win.fast32 && !a.win.ds && !a.global && a.win.tz.n == 0;
+    const bool simple = fast && simple_l;
     // compact partial rows (PF_NARROW / PF_UNIT) count slices from the push's rank base: the first
     // slice end that is not fired at the current watermark (every row that is not late ends at or
     // after it); the merge kernel reads it from slot_base
     // (planned for COUNT(*)-only layouts, fw_api.hip: the variants with wider accumulators carry
     // none of this code, which would cost them registers)
-    const bool nar = CAN_COMPACT && a.narrow && simple && cur_wm != INT64_MIN;
+    const bool nar = CAN_COMPACT && a.narrow && simple_l && cur_wm != INT64_MIN;
     uint32_t slow = simple ? 0u : valid;
     // record words: the word op is uniform, so it is resolved once per launch into a mode and
     // the rows only select (no per-row switch over the op)
@@ -464,7 +466,7 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
     bool wide = wide_row || !nar;
     const bool runs = a.runs != nullptr && sort;
     // PF_PACK push: runs, the epoch's parameters valid, every row on the common path's slice grid
-    const bool pk = pk_stats && runs && (pk_bits & PK_OK) && simple && cur_wm != INT64_MIN;
+    const bool pk = pk_stats && runs && (pk_bits & PK_OK) && simple_l && cur_wm != INT64_MIN;
     const uint32_t pk_kb = pk_bits & 255u, pk_rb = (pk_bits >> 8) & 255u, pk_vb = (pk_bits >> 16) & 255u;
     // (re-read here rather than kept live through the fold: the watermark does not change during a push);
     // a PF_PACK push counts ranks from the epoch's rank base (slot 0's, every later row's slice end is >= it)
@@ -631,21 +633,21 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
 #pragma unroll
                             for (uint32_t k = 0; k < P / 2; k++) {
                                 const ulonglong2 x = *(const ulonglong2*)(src + 2 * k);
-                                st_wt16(dst + 2 * k, x.x, x.y);
+                                st16(dst + 2 * k, x.x, x.y);
                             }
                         } else {
                             uint64_t v[P];
 #pragma unroll
                             for (uint32_t k = 0; k < P; k++) v[k] = src[k];
                             if constexpr (P == 1) {
-                                st_wt8(dst, v[0]);
+                                st8(dst, v[0]);
                             } else {  // the lone 8-B word first or last, so the pairs are 16-B aligned
                                 const bool odd = ((uintptr_t)dst & 8) != 0;
-                                st_wt8(odd ? dst : dst + (P - 1), odd ? v[0] : v[P - 1]);
+                                st8(odd ? dst : dst + (P - 1), odd ? v[0] : v[P - 1]);
                                 uint64_t* q = dst + (odd ? 1 : 0);
 #pragma unroll
                                 for (uint32_t k = 0; k < (P - 1) / 2; k++)
-                                    st_wt16(q + 2 * k, odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
+                                    st16(q + 2 * k, odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
                             }
                         }
                     }
@@ -666,9 +668,9 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
             for (uint32_t q = 2 * tid; q < nwords; q += 2 * IG_BLOCK) {
                 if (q + 1 < nwords) {
                     const ulonglong2 x = *(const ulonglong2*)(stage + q);
-                    st_wt16(dst + q, x.x, x.y);
+                    st16(dst + q, x.x, x.y);
                 } else {
-                    st_wt8(dst + q, stage[q]);
+                    st8(dst + q, stage[q]);
                 }
             }
             if (pf_rank_bytes(fmt)) {
@@ -795,20 +797,7 @@ __global__ __launch_bounds__(IG_BLOCK, FW_IG_MINW) void k_ingest(IngestArgs a) {
                 ctrl->pk_cur_v = pk_v;
                 ctrl->pk_cur_bits = pk_bits;
             }
-            if (kmn <= kmx) {  // rows seen: fields twice the measured spans (kb + rb + vb = 64, 2 <= rb <= 8)
-                const uint64_t ks = (uint64_t)kmx - (uint64_t)kmn, vs = (uint64_t)vmx - (uint64_t)vmn;
-                const uint32_t kb = (ks ? 64u - (uint32_t)__clzll((long long)ks) : 1u) + 1u;
-                uint32_t vb = (vs ? 64u - (uint32_t)__clzll((long long)vs) : 1u) + 1u;
-                if (kb + vb + 2u <= 64u) {
-                    const uint32_t rb = min(64u - kb - vb, 8u);
-                    vb = 64u - kb - rb;  // the spare bits widen the accumulator field (sums drift)
-                    ctrl->pk_next_k = (int64_t)((uint64_t)kmn - ((((1ull << kb) - 1ull) - ks) >> 1));
-                    ctrl->pk_next_v = (int64_t)((uint64_t)vmn - ((((1ull << vb) - 1ull) - vs) >> 1));
-                    ctrl->pk_next_bits = kb | (rb << 8) | (vb << 16) | PK_OK;
-                } else {
-                    ctrl->pk_next_bits = 0;
-                }
-            }
+            ctrl->pk_next_bits = pack_fields(kmn, kmx, vmn, vmx, &ctrl->pk_next_k, &ctrl->pk_next_v, ctrl->pk_next_bits);
         }
     }
     if (tid == 0) kt_end(a.kt);

@@ -30,32 +30,19 @@ constexpr int IG_HDR_WORDS = 16;                // 8-B words of per-chunk counte
 constexpr int ig_hist_words(int n_sb) { return ((n_sb + 7) >> 3) << 1; }  // u16 counters, 16-B multiple
 // rows per thread by accumulator words and loaded value columns (template NV): the chunk's rows
 // and partials stay in registers (<= 128 VGPRs)
-#ifndef FW_IG_RPT2
-#define FW_IG_RPT2 8    // rows per thread, <= 2 words (development A/B builds override)
-#endif
-#ifndef FW_IG_BLK2
-#define FW_IG_BLK2 512  // workgroup size, <= 2 words
-#endif
-constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? FW_IG_RPT2 : nw <= 4 ? 4 : 2; }
-constexpr int ig_block(int nw, int nv) { return (nv > 4 || nw > 2) ? 1024 : FW_IG_BLK2; }
-#ifndef FW_IG_LDS2_KB
-#define FW_IG_LDS2_KB 78  // LDS of a 512-thread ingest workgroup (two per CU)
-#endif
-constexpr int ig_lds(int block) { return block == 1024 ? 156 * 1024 : FW_IG_LDS2_KB * 1024; }
+constexpr int ig_rpt(int nw, int nv) { return nv > 4 ? 2 : nw <= 2 ? 8 : nw <= 4 ? 4 : 2; }
+constexpr int ig_block(int nw, int nv) { return (nv > 4 || nw > 2) ? 1024 : 512; }
+constexpr int ig_lds(int block) { return block == 1024 ? 156 * 1024 : 78 * 1024; }  // (two 512-thread workgroups per CU)
 // the template NV of a count of loaded value columns
 constexpr int ig_nv(int nv) { return nv <= 2 ? nv : nv <= 4 ? 4 : 8; }
 // LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)
 constexpr int ig_slots(int nw) { return nw <= 2 ? 1024 : nw <= 4 ? 512 : 256; }
 constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw); }
 
-// ---- merge/fire (K4+K5): one 1024-thread workgroup per superbucket
-#ifndef FW_MG_BLOCK
-#define FW_MG_BLOCK 1024
-#endif
-constexpr int MG_BLOCK = FW_MG_BLOCK;
-// merge workgroups per CU: 512-thread workgroups share a CU two at a time (each with half the LDS:
-// half the entries per superbucket, twice the superbuckets), so one's gather overlaps the other's fire
-constexpr int MG_PER_CU = MG_BLOCK == 512 ? 2 : 1;
+// ---- merge/fire (K4+K5): persistent 1024-thread workgroups, one per CU (the LDS entry table fills
+// it).  Two 512-thread workgroups per CU with half the entries each were measured out (rounds 2-5:
+// half the LDS entries per superbucket, twice the superbuckets; CFG2 flush 127 -> 165 us)
+constexpr int MG_BLOCK = 1024;
 constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a time per pending push (one per thread)
 // LDS slice-state capacity (entries) per superbucket by accumulator words
 // (kind: FW_WIN_* of a SQL operator, KIND_DSWIN (3) for DataStream windows).  One accumulator word
@@ -63,23 +50,16 @@ constexpr int MG_CELL_GROUP = 1024;             // cells (chunks) scanned at a t
 // window kinds that keep several slices per key (HOP, CUMULATE, DataStream panes) keep 4096 entries
 // of capacity with a 2x index.
 constexpr int mg_entries(int nw, int kind) {
-    if (kind == 4) return (nw <= 1 ? 1536 : 768) / MG_PER_CU;  // KIND_HOPB: HB_R slots of nw words per entry
-    return (nw <= 1 ? (kind == FW_WIN_TUMBLE ? 3072 : 4096) : nw <= 4 ? 2048 : 1024) / MG_PER_CU;
+    if (kind == 4) return nw <= 1 ? 1536 : 768;  // KIND_HOPB: HB_R slots of nw words per entry
+    return nw <= 1 ? (kind == FW_WIN_TUMBLE ? 3072 : 4096) : nw <= 4 ? 2048 : 1024;
 }
 // LDS index slots of a table of E entries with NW accumulator words: a power of two, 4E when it
 // fits beside the entries in a workgroup's LDS, else the largest that does
 constexpr int mg_idx_slots(int nw, int e) {
     const int entry_bytes = 8 + 8 + 4 + 8 * nw + 2;  // key, slice, flag, acc, due
-#ifndef FW_LEAN
-#define FW_LEAN 0
-#endif
-    const int spare_bytes = FW_LEAN ? 64 * (4 + 8 * nw) : 0;  // the per-lane spare flag / acc columns (StateLds)
-    const int room = (158 * 1024 / MG_PER_CU - e * entry_bytes - spare_bytes) / 4;
-#ifndef FW_IDX_MULT
-#define FW_IDX_MULT 4  // index slots per entry aimed at (development A/B builds override)
-#endif
+    const int room = (158 * 1024 - e * entry_bytes) / 4;
     int n = 1;
-    while (n < FW_IDX_MULT * e) n <<= 1;
+    while (n < 4 * e) n <<= 1;  // 4 index slots per entry aimed at
     while (n > room) n >>= 1;
     return n;
 }

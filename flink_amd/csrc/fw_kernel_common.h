@@ -250,39 +250,11 @@ __device__ __forceinline__ uint32_t index_hash(int64_t k, int64_t s) {
     return h ^ (h >> 13);
 }
 
-// Write-through stores for the bulk outputs a later kernel reads (partial rows, state write-back):
-// global_store ... sc1 leaves no dirty line in the XCD's L2 (MI355X_MICROARCH.md, store flavours:
-// sc1 drops the line, a 16-B sc1 store costs what a plain one does), so the kernel boundary that
-// follows has no ~100 MB of dirty lines to write back before the next kernel starts.  Off: measured
-// (round 5, CFG2/CFG4) the sc1 stores made the ingest store phase 1.1-2x slower (CFG2 runs ingest 67 ->
-// 116 us, CFG4 78 -> 152 us) and the step gaps did not shrink; kept as an A/B knob.
-#ifndef FW_WT
-#define FW_WT 0
-#endif
-typedef unsigned int fw_u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int fw_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void st_wt16(void* p, uint64_t lo, uint64_t hi) {
-#if FW_WT
-    fw_u32x4 w;
-    w.x = (unsigned)lo;
-    w.y = (unsigned)(lo >> 32);
-    w.z = (unsigned)hi;
-    w.w = (unsigned)(hi >> 32);
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
-#else
-    *(ulonglong2*)p = make_ulonglong2(lo, hi);
-#endif
-}
-__device__ __forceinline__ void st_wt8(void* p, uint64_t v) {
-#if FW_WT
-    fw_u32x2 w;
-    w.x = (unsigned)v;
-    w.y = (unsigned)(v >> 32);
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
-#else
-    *(uint64_t*)p = v;
-#endif
-}
+// 16-B and 8-B stores of the bulk outputs (partial rows, state write-back, result slabs).  Plain
+// stores: write-through (sc1) versions, to spare the kernel boundary the dirty L2 lines, were measured
+// out in round 5 (CFG2 runs ingest 67 -> 116 us, CFG4 78 -> 152 us; the step gaps did not shrink).
+__device__ __forceinline__ void st16(void* p, uint64_t lo, uint64_t hi) { *(ulonglong2*)p = make_ulonglong2(lo, hi); }
+__device__ __forceinline__ void st8(void* p, uint64_t v) { *(uint64_t*)p = v; }
 
 // wave-level reductions: one LDS atomic per wave instead of one per lane (same-address LDS
 // atomics serialise lane by lane)
@@ -348,6 +320,24 @@ __device__ __forceinline__ uint32_t wred_sum_u32(uint32_t v) {
 }
 __device__ __forceinline__ int64_t wred_sum_i64(int64_t v) {
     return wred<int64_t>(v, 0, [](int64_t a, int64_t b) { return a + b; });
+}
+
+// PF_PACK fields for the next flush epoch from a push's key and accumulator ranges (fw_internal.h):
+// each field twice the measured span (kb + rb + vb = 64, 2 <= rb <= 8, the spare bits widen the
+// accumulator field: sums drift), the bases centred on the ranges.  Returns the fields word (0: the
+// spans do not fit one word); no rows seen (kmn > kmx): the previous word stands.
+__device__ __forceinline__ uint32_t pack_fields(int64_t kmn, int64_t kmx, int64_t vmn, int64_t vmx, int64_t* kbase,
+                                                int64_t* vbase, uint32_t prev) {
+    if (kmn > kmx) return prev;
+    const uint64_t ks = (uint64_t)kmx - (uint64_t)kmn, vs = (uint64_t)vmx - (uint64_t)vmn;
+    const uint32_t kb = (ks ? 64u - (uint32_t)__clzll((long long)ks) : 1u) + 1u;
+    uint32_t vb = (vs ? 64u - (uint32_t)__clzll((long long)vs) : 1u) + 1u;
+    if (kb + vb + 2u > 64u) return 0u;
+    const uint32_t rb = min(64u - kb - vb, 8u);
+    vb = 64u - kb - rb;
+    *kbase = (int64_t)((uint64_t)kmn - ((((1ull << kb) - 1ull) - ks) >> 1));
+    *vbase = (int64_t)((uint64_t)vmn - ((((1ull << vb) - 1ull) - vs) >> 1));
+    return kb | (rb << 8) | (vb << 16) | PK_OK;
 }
 
 // slot claim for the active lanes of a wave: one atomicAdd on *ctr, each lane gets base + rank

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         const int lane = tid & 63, wv = tid >> 6;
         auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
         // this lane's cell word of its wave's first group in push 0 (the next push's is loaded at the top
-        // of each push's loop, FW_MG_ROLL)
+        // of each push's loop)
         uint32_t v_first = 0;
         if (do_flush && !a.runs && lane < gather_group((int)cell_pad(a.slot_nch[0])))
             v_first = cell_at(0, wv * gather_group((int)cell_pad(a.slot_nch[0])) + lane);
@@ -234,10 +234,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
             }
         }
         __syncthreads();
-        // ---- flush: every pending partial (key, sliceEnd, acc) folds into its block's slot.  One
-        // accumulator word (COUNT(*)): software-pipelined over the wave's blocks of rows, as in
-        // k_merge_fire (the next block's rows in flight while the current one folds)
-        constexpr bool PIPE = FW_MG_PIPE && FW_MG_PIPE1 && NWP == 1;
+        // ---- flush: every pending partial (key, sliceEnd, acc) folds into its block's slot (the
+        // software-pipelined gather of k_merge_fire was measured out here: round 3)
         const bool gather = do_flush && !(FW_ABL(a) & AB_M_NO_GATHER);
         if (gather && a.runs) {  // runs (IngestArgs::runs), then the rows chunks kept in their regions
             auto fold_rows = [&](auto& row, uint32_t live) __attribute__((always_inline)) {
@@ -267,91 +265,12 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
                     atomicOr(&S.flag[e], F_ACC | (1u << (HB_MASK_SHIFT + sl)));
                 });
             };
-            gather_runs<NWP, GU, GF, FW_MG_PIPE1 != 0 ? 2 : 1>(a, sb, pend, fold_rows);
+            gather_runs<NWP, GU, GF, 1>(a, sb, pend, fold_rows);
             uint32_t ovf = run_overflow(a, sb, pend);
             while (ovf) {
                 const int pi = __ffs(ovf) - 1;
                 ovf &= ovf - 1;
                 gather_cells_push<NWP, GU, GF>(a, sb, pi, fold_rows);
-            }
-        } else if (PIPE && gather) {
-            constexpr int GP = GU;  // two full blocks fit beside the block-state code
-            auto ngroups_of = [&](int64_t p) {
-                const int nc = (int)cell_pad(a.slot_nch[p]);
-                return nc / gather_group(nc);
-            };
-            auto norm = [&](int64_t& p, int& q) {
-                while (p < pend && q >= ngroups_of(p)) {
-                    p++;
-                    q = wv;
-                }
-            };
-            auto fpos = [&](int64_t p, int q) { return q * gather_group((int)cell_pad(a.slot_nch[p])) + lane; };
-            auto cword = [&](int64_t p, int q) -> uint32_t {
-                return lane < gather_group((int)cell_pad(a.slot_nch[p])) ? cell_at(p, fpos(p, q)) : 0u;
-            };
-            CellGroup cg;
-            cg.tot = cg.excl = cg.adj = cg.fmt = 0;
-            int64_t cp = 0;
-            uint32_t r0 = 0;
-            int64_t np = 0;
-            int nq = wv;
-            norm(np, nq);
-            uint32_t vn = np < pend ? ((np == 0 && nq == wv) ? v_first : cword(np, nq)) : 0u;
-            auto next_block = [&]() -> bool {
-                r0 += 64 * GP;
-                while (r0 >= cg.tot) {
-                    if (np >= pend) return false;
-                    const uint32_t vc = vn;
-                    const int f = fpos(np, nq);
-                    cp = np;
-                    nq += MG_BLOCK / 64;
-                    norm(np, nq);
-                    vn = np < pend ? cword(np, nq) : 0u;
-                    cg = cell_group(vc, f, CH);
-                    r0 = 0;
-                }
-                return true;
-            };
-            auto process = [&](auto& row, uint32_t live) {
-                constexpr int GX = std::extent<std::remove_reference_t<decltype(row)>>::value;
-                int ge[GX], slot[GX];
-                {
-                    int64_t gk[GX], gb[GX];
-#pragma unroll
-                    for (int u = 0; u < GX; u++) {
-                        gk[u] = (int64_t)row[u][0];
-                        gb[u] = hb_block_of(win, (int64_t)row[u][1]);
-                        slot[u] = hb_slot_of(win, (int64_t)row[u][1], gb[u]);
-                        row[u][1] = (uint64_t)gb[u];
-                    }
-                    probe_batch<NA, E, GX>(S, gk, gb, ge);
-                }
-                static_for<GX>([&](auto UU) {
-                    constexpr int u = decltype(UU)::value;
-                    if (!((live >> u) & 1u)) return;
-                    int e = ge[u];
-                    if (e < 0) e = hb_find_or_insert<NWP, E, OPS>(S, (int64_t)row[u][0], (int64_t)row[u][1], a.wd);
-                    if (e < 0) return;  // state overflow (flagged)
-                    const int sl = slot[u];
-#pragma unroll
-                    for (int w = 0; w < NWP; w++)
-                        if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[sl * NWP + w][e], row[u][2 + w]);
-                    atomicOr(&S.flag[e], F_ACC | (1u << (HB_MASK_SHIFT + sl)));
-                });
-            };
-            uint64_t ra[GP][PW], rb[GP][PW];
-            uint32_t la = 0, lb = 0;
-            bool ha = next_block();
-            if (ha) la = load_group_rows<NWP, GP, GF>(a, cp, cg, r0, sb, ra);
-            while (ha) {  // unrolled by two: the buffers alternate without copies
-                const bool hb = next_block();
-                if (hb) lb = load_group_rows<NWP, GP, GF>(a, cp, cg, r0, sb, rb);
-                process(ra, la);
-                if (!hb) break;
-                ha = next_block();
-                if (ha) la = load_group_rows<NWP, GP, GF>(a, cp, cg, r0, sb, ra);
-                process(rb, lb);
             }
         } else if (gather) {
             for (int64_t pi = 0; pi < pend; pi++) {
@@ -360,8 +279,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
                 const int ngroups = ncell / G;
                 for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                     const int f = g * G + lane;
-                    const uint32_t v = lane >= G ? 0u : (g == wv && (FW_MG_ROLL || pi == 0)) ? v_first : cell_at(pi, f);
-                    if (FW_MG_ROLL && g == wv) {  // the next push's first cell word, in flight during this push
+                    const uint32_t v = lane >= G ? 0u : g == wv ? v_first : cell_at(pi, f);
+                    if (g == wv) {  // the next push's first cell word, in flight during this push
                         v_first = 0;
                         if (pi + 1 < pend) {
                             const int G1 = gather_group((int)cell_pad(a.slot_nch[pi + 1]));

@@ -9,21 +9,14 @@ namespace fw {
 // ======================================================================================
 // K4+K5: merge pending partials into the HBM slice-state table, fire due timers
 // ======================================================================================
-#ifndef FW_LEAN
-#define FW_LEAN 0  // branch-free first probes and folds in the SQL gathers (fold_block; A/B, off: measured
-                   // neutral on CFG2 / CFG4 and 3 % slower on CFG5 -- DESIGN.md 4)
-#endif
-// One spare accumulator / flag column per lane beyond the E entries (MG_SPARE): the branch-free fold
-// (fold_block) sends a lane's row that is not a first-probe hit there instead of masking the lane off.
-constexpr int MG_SPARE = FW_LEAN ? 64 : 0;
 template <int NW, int E>
 struct StateLds {
     static constexpr int NI = mg_idx_slots(NW, E);  // 4E slots where they fit (mg_idx_slots)
     uint32_t idx[NI];      // open-addressing index: 0 empty, 1 claiming, 2+e entry e
     int64_t key[E];
     int64_t slice[E];
-    uint32_t flag[E + MG_SPARE];
-    uint64_t acc[NW][E + MG_SPARE];
+    uint32_t flag[E];
+    uint64_t acc[NW][E];
     uint16_t due[E];       // entries whose timer is due at this watermark (each fires once)
     int32_t ndue;
     int32_t n;             // entries in use
@@ -67,18 +60,17 @@ __device__ __forceinline__ void load_words(const uint64_t* p, uint64_t (&o)[W]) 
         }
     }
 }
-// (write-through: the state rows are read by the next flush, not by this kernel -- st_wt16)
 template <int W>
 __device__ __forceinline__ void store_words(uint64_t* p, const uint64_t (&v)[W]) {
     if constexpr (W % 2 == 0) {
 #pragma unroll
-        for (int k = 0; k < W / 2; k++) st_wt16(p + 2 * k, v[2 * k], v[2 * k + 1]);
+        for (int k = 0; k < W / 2; k++) st16(p + 2 * k, v[2 * k], v[2 * k + 1]);
     } else {
         const bool odd = ((uintptr_t)p & 8) != 0;
-        st_wt8(odd ? p : p + (W - 1), odd ? v[0] : v[W - 1]);
+        st8(odd ? p : p + (W - 1), odd ? v[0] : v[W - 1]);
         uint64_t* q = p + (odd ? 1 : 0);
 #pragma unroll
-        for (int k = 0; k < (W - 1) / 2; k++) st_wt16(q + 2 * k, odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
+        for (int k = 0; k < (W - 1) / 2; k++) st16(q + 2 * k, odd ? v[2 * k + 1] : v[2 * k], odd ? v[2 * k + 2] : v[2 * k + 1]);
     }
 }
 
@@ -243,48 +235,6 @@ __device__ __forceinline__ uint32_t insert_fresh(StateLds<NW, E>& S, const WordD
     return miss & ~won;
 }
 
-// Branch-free first probes and folds of a block of GX rows per lane (SQL TUMBLE / CUMULATE / HOP
-// slices; not DataStream windows): every lane issues the index reads of all its rows, then the entry
-// reads, then folds each row -- a first-probe hit into its entry, any other row (not live, home slot
-// empty, collision, insertion in flight) into the lane's spare column, so no row masks a lane off
-// and the hot path runs without exec-mask branches.  Returns the live rows the first probe did not
-// decide (bit u) with ge[u] = -1 (home slot empty: insert_fresh may claim it) or -2 (probe further).
-template <int NW, int E, int GX, uint32_t OPS, typename Row, typename FlagsOf>
-__device__ __forceinline__ uint32_t fold_block(StateLds<NW, E>& S, const WordDesc& wd, const Row& row, uint32_t live,
-                                               int* ge, const FlagsOf& flags_of) {
-    static_assert(MG_SPARE >= 64 || GX < 0, "fold_block needs the spare columns (FW_LEAN)");
-    constexpr uint32_t MASK = StateLds<NW, E>::NI - 1;
-    const uint32_t spare = (uint32_t)E + (uint32_t)(threadIdx.x & 63);
-    uint32_t st[GX];
-#pragma unroll
-    for (int u = 0; u < GX; u++)
-        st[u] = __hip_atomic_load(&S.idx[index_hash((int64_t)row[u][0], (int64_t)row[u][1]) & MASK], __ATOMIC_RELAXED,
-                                  LDS_SCOPE);
-    int64_t kk[GX], ss[GX];
-    uint32_t ei[GX];
-#pragma unroll
-    for (int u = 0; u < GX; u++) {
-        ei[u] = min(st[u] - 2u, (uint32_t)(E - 1));
-        kk[u] = S.key[ei[u]];
-        ss[u] = S.slice[ei[u]];
-    }
-    uint32_t miss = 0;
-#pragma unroll
-    for (int u = 0; u < GX; u++) {
-        const bool lv = (live >> u) & 1u;
-        const bool hit = lv && st[u] >= 2u && st[u] - 2u < (uint32_t)E && kk[u] == (int64_t)row[u][0] &&
-                         ss[u] == (int64_t)row[u][1];
-        const uint32_t t = hit ? ei[u] : spare;
-#pragma unroll
-        for (int w = 0; w < NW; w++)
-            if (word_on<OPS>(wd, w)) lds_fold(word_op<OPS>(wd, w), &S.acc[w][t], row[u][2 + w]);
-        atomicOr(&S.flag[t], flags_of((int64_t)row[u][1]));
-        ge[u] = hit ? (int)ei[u] : st[u] == 0u ? -1 : -2;
-        miss |= (uint32_t)(lv && !hit) << u;
-    }
-    return miss;
-}
-
 // register an event-time timer on entry e; a timer that is already due at this watermark joins
 // the due list (an entry's timer fires at most once per advance: its timestamp is its slice end)
 template <int NW, int E>
@@ -299,25 +249,12 @@ __device__ __forceinline__ void set_timer(StateLds<NW, E>& S, int e, int64_t W, 
 // The fire passes deal n items (due entries, HOP block entries) to the 1024 threads in passes of
 // 1024, in thread order: the lanes of a wave take consecutive items, and consecutive entries sit in
 // consecutive LDS words, so the fire's entry reads are bank-conflict free.  Round 4's lane-major
-// dealing (l * 16 + w, FW_QLANE 1: every wave busy when fewer items than threads) put a wave's lanes
+// dealing (l * 16 + w: every wave busy when fewer items than threads) put a wave's lanes
 // 16 entries apart, 32-way conflicts on every 8-byte entry read; measured round 5: thread order
 // CFG3 merge 267 -> 248 us, CFG5 317 -> 300, CFG4 196 -> 187, CFG2 131 -> 127 us per flush; blocks
-// of consecutive items for every wave (FW_QLANE 2) landed in between.
-#ifndef FW_QLANE
-#define FW_QLANE 0  // 0: thread order; 1: lane-major; 2: blocks of consecutive items per wave (A/B)
-#endif
+// of consecutive items for every wave landed in between.
 __device__ __forceinline__ int fire_deal(int b0, int n, int tid) {
-#if FW_QLANE == 2
-    const int rem = n - b0;
-    if (rem >= MG_BLOCK) return b0 + tid;
-    const int per = (rem + MG_BLOCK / 64 - 1) / (MG_BLOCK / 64);
-    const int l = tid & 63;
-    return l < per ? b0 + (tid >> 6) * per + l : n;
-#elif FW_QLANE == 1
-    return b0 + (tid & 63) * (MG_BLOCK / 64) + (tid >> 6);
-#else
     return b0 + tid;
-#endif
 }
 
 // Emission is atomic-free at device scope: each superbucket appends to its own output slab
@@ -343,9 +280,9 @@ __device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_
     if (FW_ABL(a) & AB_M_NO_EMIT) return;
     const int64_t i = claim_out_row(a, sb, s_emit);
     if (i < 0) return;
-    st_wt8(&a.out_key[i], (uint64_t)key);
-    st_wt8(&a.out_ws[i], (uint64_t)window_start_of(a.win, we));
-    st_wt8(&a.out_we[i], (uint64_t)we);
+    st8(&a.out_key[i], (uint64_t)key);
+    st8(&a.out_ws[i], (uint64_t)window_start_of(a.win, we));
+    st8(&a.out_we[i], (uint64_t)we);
     uint32_t nm = 0;
     for (int g = 0; g < a.ad.n; g++) {
         const int32_t kind = a.ad.kind[g], type = a.ad.type[g];
@@ -388,9 +325,9 @@ __device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_
                 break;
             }
         }
-        st_wt8(&a.out_val[g][i], ((nm >> g) & 1u) ? 0ull : v);  // a NULL's value word is 0
+        st8(&a.out_val[g][i], ((nm >> g) & 1u) ? 0ull : v);  // a NULL's value word is 0
     }
-    if (a.ad.first_word >= 0) st_wt8(&a.out_val[a.ad.n][i], acc[a.ad.first_word]);  // value1's arrival ordinal
+    if (a.ad.first_word >= 0) st8(&a.out_val[a.ad.n][i], acc[a.ad.first_word]);  // value1's arrival ordinal
     a.out_null[i] = nm;
 }
 
@@ -849,31 +786,13 @@ __device__ __forceinline__ void merge_ticket(const MergeArgs& a, int64_t W) {
 }
 
 // rows of one cell loaded together in the gather (VGPR budget of the 1024-thread workgroup)
-#ifndef FW_MG_PIPE
-#define FW_MG_PIPE 1  // software-pipelined gather for one-word layouts (0: the plain loop, A/B)
-#endif
-#ifndef FW_MG_PIPE1
-#define FW_MG_PIPE1 0  // ... also for one-word layouts and HOP block state (A/B: CFG2 slower with half blocks)
-#endif
-// (measured against the round-3 sizes: one word 3 rows per lane instead of 4 -- CFG2 flush 176 ->
-// 167 us, CFG3 274 -> 266 us; two words 2 instead of 3 -- CFG4 203 -> 191 us; four words stay at 2)
-#ifndef FW_GU1
-#define FW_GU1 3
-#endif
-#ifndef FW_GU2
-#define FW_GU2 2
-#endif
-#ifndef FW_GU4
-#define FW_GU4 2
-#endif
+// rows per lane per gather pass by accumulator words (measured against the round-3 sizes: one word
+// 3 rows per lane instead of 4 -- CFG2 flush 176 -> 167 us, CFG3 274 -> 266 us; two words 2 instead
+// of 3 -- CFG4 203 -> 191 us; four words stay at 2)
 constexpr int mg_rows_in_flight(int nw) {
-    return MG_BLOCK < 512 ? (nw <= 1 ? 2 * FW_GU1 : nw <= 2 ? 2 * FW_GU2 : nw <= 4 ? 2 * FW_GU4 : 2)
-                          : (nw <= 1 ? FW_GU1 : nw <= 2 ? FW_GU2 : nw <= 4 ? FW_GU4 : 1);
+    return nw <= 1 ? 3 : nw <= 2 ? 2 : nw <= 4 ? 2 : 1;
 }
 
-#ifndef FW_MG_ROLL
-#define FW_MG_ROLL 1
-#endif
 
 // ---- the gather's view of the pending partials.  A wave takes a group of up to 64 consecutive
 // cells of one push slot (lane l holds cell word v of flat cell position f), scans their row
@@ -1277,7 +1196,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
     const int lane = tid & 63, wv = tid >> 6;
     auto gather_group = [](int ncell) { return min(64, ncell / (MG_BLOCK / 64)); };
     // this lane's cell word of its wave's first group in push 0, loaded beside the state; each
-    // push's loop then loads the next push's first cell word before it gathers (FW_MG_ROLL), so that
+    // push's loop then loads the next push's first cell word before it gathers, so that
     // round trip overlaps the current push's rows
     uint32_t v_first = 0;
     if (gather && !a.runs && lane < gather_group((int)cell_pad(a.slot_nch[0])))
@@ -1330,7 +1249,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
     // software-pipelined over the wave's blocks of rows -- the next block's rows (and the next
     // group's cell word) are in flight while the current block is probed and folded.  Two blocks of
     // GU / 2 rows per lane take the registers of one block of GU rows.
-    constexpr bool PIPE = FW_MG_PIPE && (NW >= 2 || FW_MG_PIPE1) && NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
+    // (one-word layouts lost with half-size blocks: round 3, CFG2 merge 69.7 -> 74.1 us per step)
+    constexpr bool PIPE = NW >= 2 && NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
     if (gather && a.runs) {
         // runs (IngestArgs::runs): the superbucket's rows of every pending push as RUN_X contiguous
         // stretches per push, then the rows chunks kept in their own regions (overflow)
@@ -1397,12 +1317,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                     });
                     return rest;
                 };
-#if FW_LEAN
-                uint32_t miss = fold_block<NW, E, GX, OPS>(S, a.wd, row, live, ge, flags_of);
-                (void)probe_fold;
-#else
                 uint32_t miss = probe_fold(live);
-#endif
                 gstamp(4);
                 const bool gcount = (FW_ABL(a) & AB_GSTAMPS) && stm.on && (tid >> 6) == 0;  // wave 0's row census
                 if (gcount) {
@@ -1455,20 +1370,14 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
         };
         // TUMBLE / CUMULATE up to 4 words: software-pipelined (two blocks in flight); the others
         // (HOP chains, DataStream windows) leave no registers for a second block
-        constexpr bool RP = FW_MG_PIPE && NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
-#ifndef FW_GR
-#define FW_GR 0  // rows per lane per pipelined block (0: planned below)
-#endif
-#ifndef FW_GD
-#define FW_GD 0  // blocks in the pipelined gather's ring (0: planned below)
-#endif
+        constexpr bool RP = NW <= 4 && (KIND == FW_WIN_TUMBLE || KIND == FW_WIN_CUMULATE);
         // one-word TUMBLE: one block of 4 rows per lane (measured round 5, CFG2 runs flush 144.5 ->
         // 128.7 us; 3 rows: 131.8, 2 rows: 133.3, 5 rows: 130.1, 6 rows: 141.7; the freed registers go to the probe loop); CFG4 (two
         // words, 197 -> 201 us) and CFG5 (CUMULATE, 322 -> 370 us) keep two blocks of half of
         // mg_rows_in_flight
         constexpr bool ONE_BLOCK = NW == 1 && KIND == FW_WIN_TUMBLE;
-        constexpr int GR = !RP ? GU : FW_GR > 0 ? FW_GR : ONE_BLOCK ? 4 : GU / 2 > 0 ? GU / 2 : 1;
-        constexpr int GD = !RP ? 1 : FW_GD > 0 ? FW_GD : ONE_BLOCK ? 1 : 2;
+        constexpr int GR = !RP ? GU : ONE_BLOCK ? 4 : GU / 2 > 0 ? GU / 2 : 1;
+        constexpr int GD = !RP ? 1 : ONE_BLOCK ? 1 : 2;
         const uint64_t gl0 = gst ? __builtin_amdgcn_s_memtime() : 0;
         gather_runs<NW, GR, GF, GD>(a, sb, pend, fold_rows);
         if (gst) stm.acc[13] += __builtin_amdgcn_s_memtime() - gl0;
@@ -1536,9 +1445,6 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                 return;
             }
             int ge[GX];
-#if FW_LEAN
-            uint32_t miss = fold_block<NW, E, GX, OPS>(S, a.wd, row, live, ge, flags_of);
-#else
             {
                 int64_t gk[GX], gs[GX];
 #pragma unroll
@@ -1563,7 +1469,6 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                     if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
                 atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
             });
-#endif
             while (miss) {
                 const int um = __ffs(miss) - 1;
                 miss &= miss - 1;
@@ -1606,8 +1511,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
             for (int g = wv; g < ngroups; g += MG_BLOCK / 64) {
                 const int f = g * G + lane;
                 uint64_t gc0 = gst ? __builtin_amdgcn_s_memtime() : 0;
-                const uint32_t v = lane >= G ? 0u : (g == wv && (FW_MG_ROLL || pi == 0)) ? v_first : cell_at(pi, f);
-                    if (FW_MG_ROLL && g == wv) {  // the next push's first cell word, in flight during this push
+                const uint32_t v = lane >= G ? 0u : g == wv ? v_first : cell_at(pi, f);
+                    if (g == wv) {  // the next push's first cell word, in flight during this push
                         v_first = 0;
                         if (pi + 1 < pend) {
                             const int G1 = gather_group((int)cell_pad(a.slot_nch[pi + 1]));
@@ -1657,15 +1562,6 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                         return fired ? F_ACC : (F_ACC | F_TIMER);
                     };
                     int ge[GU];
-#if FW_LEAN
-                    uint32_t miss = fold_block<NW, E, GU, OPS>(S, a.wd, row, live, ge, flags_of);
-                    if (gst) {
-                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        const uint64_t g1 = __builtin_amdgcn_s_memtime();
-                        stm.acc[4] += g1 - g0;
-                        g0 = g1;
-                    }
-#else
                     {
                         int64_t gk[GU], gs[GU];
 #pragma unroll
@@ -1696,7 +1592,6 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_fire(MergeArgs a) {
                             if (word_on<OPS>(a.wd, w)) lds_fold(word_op<OPS>(a.wd, w), &S.acc[w][e], row[u][2 + w]);
                         atomicOr(&S.flag[e], flags_of((int64_t)row[u][1]));
                     });
-#endif
                     const uint64_t gm0 = gst ? __builtin_amdgcn_s_memtime() : 0;
                     while (miss) {  // the wave loops max(popcount) times, not GU times
                         const int um = __ffs(miss) - 1;
@@ -1950,7 +1845,7 @@ static unsigned merge_grid(int n_sb) {
             hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             n_cu = 256;
     }
-    return (unsigned)(n_sb < n_cu * MG_PER_CU ? n_sb : n_cu * MG_PER_CU);
+    return (unsigned)(n_sb < n_cu ? n_sb : n_cu);
 }
 
 // the accumulator layouts with a compiled variant per accumulator width (the others, and every SQL

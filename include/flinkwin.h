@@ -533,8 +533,10 @@ int fw_restore_key_group_heap(fw_handle* h, const void* buf, int64_t size, const
    next_push_seq, after which the handle's arrival ordinals continue.  v8: key_hash -- for a
    FW_KEYHASH_PRECOMPUTED handle (keys the shim interns, e.g. String keys: key = the interned id,
    key_hash = String.hashCode) the key's hash, which routes the restored window exactly as the
-   ingest routes the key's records; ignored for LONG / INT keys; 0 on snapshot (the shim knows its
-   keys' hashes). */
+   ingest routes the key's records; ignored for LONG / INT keys; 0 on snapshot: the state keeps no
+   hash per entry (the shim knows its keys' hashes), so a caller that restores a snapshotted array
+   into a FW_KEYHASH_PRECOMPUTED handle must fill key_hash back in first -- an unfilled array is
+   refused (FW_E_INVALID) for every key whose hash 0 does not route to the key group. */
 enum { FW_DSW_CONTENTS = 1, FW_DSW_TRIGGER = 2, FW_DSW_CLEANUP = 4 };
 typedef struct {
     int64_t key;

@@ -345,3 +345,44 @@ def test_string_key_snapshot_restores_into_fresh_operator(shaped):
         want[e] = want.get(e, 0) + int(v)
     assert got == want
     b.close()
+
+
+def test_precomputed_hash_round_trip_needs_hashes_refilled():
+    """fw_ds_snapshot_key_group reports key_hash 0 for FW_KEYHASH_PRECOMPUTED handles:
+    restoring the unmodified array into a fresh handle is refused for a key group that hash 0 does not
+    route to; with the keys' hashes filled back in the same array restores and fires the same sums."""
+    from flink_amd.datastream.heap_state import java_string_hash
+    from flink_amd.datastream.window_operator import WindowOperator
+    from flink_amd.datastream.windowing import EventTimeTrigger, TumblingEventTimeWindows
+    from flink_amd._native import FlinkWinError
+    from flink_amd import _native
+
+    def op():
+        return WindowOperator(TumblingEventTimeWindows.of(3000), EventTimeTrigger(), ("sum", "INT"), key_type="STRING",
+                              state_capacity=1 << 12, max_batch_rows=1 << 12, output_capacity=1 << 12).open()
+    kg0 = _native.lib().fw_host_key_group(abi.KEYHASH_PRECOMPUTED, 0, 0, 128)
+    names = [n for n in (f"s{i}" for i in range(400))
+             if _native.lib().fw_host_key_group(abi.KEYHASH_PRECOMPUTED, 0, java_string_hash(n), 128) != kg0]
+    kg = _native.lib().fw_host_key_group(abi.KEYHASH_PRECOMPUTED, 0, java_string_hash(names[0]), 128)
+    keys = [n for n in names if _native.lib().fw_host_key_group(abi.KEYHASH_PRECOMPUTED, 0, java_string_hash(n), 128) == kg]
+    a = op()
+    a.process_batch(keys * 3, np.array([100, 200, 300] * len(keys), np.int64)[:3 * len(keys)],
+                    np.arange(3 * len(keys), dtype=np.int64))
+    w = a.handle.ds_key_group_windows(kg)
+    assert len(w) == len(keys) and (w["key_hash"] == 0).all()
+    b = op()
+    with pytest.raises(FlinkWinError):
+        b.handle.ds_restore_key_group_windows(kg, w, a.handle.push_seq)
+    b.close()
+    c = op()
+    w2 = w.copy()
+    w2["key_hash"] = [java_string_hash(a._kstr[int(k)]) for k in w["key"]]
+    c.handle.ds_restore_key_group_windows(kg, w2, a.handle.push_seq)
+    c.handle.advance(2999)
+    r = c.handle.results(reset=True)
+    want = {}
+    for i, k in enumerate(keys * 3):
+        want[int(a._kid[k])] = want.get(int(a._kid[k]), 0) + i
+    assert dict(zip(r["key"].tolist(), [int(np.int32(np.int64(v))) for v in r["values"][0]])) == want
+    c.close()
+    a.close()

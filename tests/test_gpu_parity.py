@@ -759,15 +759,21 @@ def test_partition_packed_equals_partition_by_dest():
         o += int(cnt[d])
 
 
+@pytest.mark.parametrize("delivery", ["kernel", "dma"])
 @pytest.mark.parametrize("depth", [1, 2])
 @pytest.mark.parametrize("name", ["sql_tumble_int_aggs", "sql_hop", "sql_tumble_double", "ds_sliding_max"])
-def test_async_results_pipeline_matches_oracle(name, depth):
+def test_async_results_pipeline_matches_oracle(name, depth, delivery, monkeypatch):
     """fw_results_async / fw_results_ready: watermark b's rows are collected into pinned host memory
     while batch b + 1 is pushed (three pushes per watermark through the double-buffered staging)
     and read ``depth`` steps later (the oldest outstanding collection first) -- the same rows as
-    the oracle's, watermark by watermark.  A fourth outstanding collection is refused."""
+    the oracle's, watermark by watermark.  A fourth outstanding collection is refused.  ``dma``:
+    the rows cross by hipMemcpyAsync on the D2H stream instead of the copy kernel (FW_AR_KERNEL=0:
+    the early copy started by the next call, the wait before a buffer is reused, the synchronous
+    copy in fw_results_ready)."""
     from flink_amd.runtime.handle import WindowAggHandle
     from oracle.oracle import OracleOperator
+    if delivery == "dma":
+        monkeypatch.setenv("FW_AR_KERNEL", "0")
     kw = CASES[name]
     cfg = _cfg(kw)
     dc = _double_cols(kw)

@@ -5,7 +5,7 @@ test-side oracle wrapper can build the same ``fw_config`` structure.
 """
 import ctypes as C
 
-FW_ABI_VERSION = 9
+FW_ABI_VERSION = 10
 FW_MAX_AGGS = 8
 FW_MAX_COLS = 8
 

@@ -175,7 +175,6 @@ struct fw_handle {
     int32_t* state_count = nullptr;
     int64_t* sb_min_timer = nullptr;
     int64_t* out_key = nullptr;
-    int64_t* out_ws = nullptr;
     int64_t* out_we = nullptr;
     uint64_t* out_val[FW_MAX_AGGS] = {};
     uint32_t* out_null = nullptr;
@@ -810,7 +809,6 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->sb_min_timer, h->ks.n_sb))) return rc;
     const size_t orows = (size_t)h->ks.n_sb * h->slab_cap + h->out_cap;
     if ((rc = dalloc(&h->out_key, orows))) return rc;
-    if ((rc = dalloc(&h->out_ws, orows))) return rc;
     if ((rc = dalloc(&h->out_we, orows))) return rc;
     if ((rc = dalloc(&h->out_null, orows))) return rc;
     for (int g = 0; g < h->n_out; g++)
@@ -964,7 +962,6 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.local = h->cfg.agg_phase == FW_PHASE_LOCAL;
     a.chunk_rows = (int32_t)h->chunk_rows;
     a.out_key = h->out_key;
-    a.out_ws = h->out_ws;
     a.out_we = h->out_we;
     for (int g = 0; g < FW_MAX_AGGS; g++) a.out_val[g] = h->out_val[g] ? h->out_val[g] : h->out_val[0];
     a.out_null = h->out_null;
@@ -1224,7 +1221,6 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->state_count);
     hipFree(h->sb_min_timer);
     hipFree(h->out_key);
-    hipFree(h->out_ws);
     hipFree(h->out_we);
     hipFree(h->out_null);
     for (int g = 0; g < FW_MAX_AGGS; g++) hipFree(h->out_val[g]);
@@ -1564,7 +1560,8 @@ int fw_results(fw_handle* h, fw_result* out, int copy_to_host) {
     ca.n_aggs = h->n_out;
     ca.slab_cap = h->slab_cap;
     ca.out_key = h->out_key;
-    ca.out_ws = h->out_ws;
+    ca.win = device_win(h);
+    ca.local_out = h->cfg.agg_phase == FW_PHASE_LOCAL;
     ca.out_we = h->out_we;
     ca.out_null = h->out_null;
     for (int g = 0; g < h->n_out; g++) {
@@ -1671,7 +1668,8 @@ int fw_results_async(fw_handle* h) {
     ca.n_aggs = h->n_out;
     ca.slab_cap = h->slab_cap;
     ca.out_key = h->out_key;
-    ca.out_ws = h->out_ws;
+    ca.win = device_win(h);
+    ca.local_out = h->cfg.agg_phase == FW_PHASE_LOCAL;
     ca.out_we = h->out_we;
     ca.out_null = h->out_null;
     for (int g = 0; g < h->n_out; g++) {
@@ -1723,7 +1721,7 @@ int fw_results_device_segments(fw_handle* h, fw_result_segments* out) {
     out->counts = h->sb_out;
     out->cols.n = (int64_t)h->ks.n_sb * h->slab_cap + h->out_cap;
     out->cols.key = h->out_key;
-    out->cols.window_start = h->out_ws;
+    out->cols.window_start = nullptr;  // v10: derived from window_end (flinkwin.h)
     out->cols.window_end = h->out_we;
     for (int g = 0; g < nv; g++) out->cols.values[g] = (int64_t*)h->out_val[g];
     if (nv < na) out->cols.first_ord = (int64_t*)h->out_val[nv];
@@ -1750,7 +1748,8 @@ int fw_results_device(fw_handle* h, fw_result* out, int64_t** d_n) {
         ca.n_aggs = h->n_out;
         ca.slab_cap = h->slab_cap;
         ca.out_key = h->out_key;
-        ca.out_ws = h->out_ws;
+        ca.win = device_win(h);
+    ca.local_out = h->cfg.agg_phase == FW_PHASE_LOCAL;
         ca.out_we = h->out_we;
         ca.out_null = h->out_null;
         for (int g = 0; g < h->n_out; g++) {

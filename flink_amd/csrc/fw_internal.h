@@ -594,7 +594,6 @@ struct MergeArgs {
     int32_t local;           // LOCAL phase: emit every gathered (key, slice) partial, keep no state
     int32_t chunk_rows;      // rows per ingest chunk (IG_BLOCK * ig_rpt): the cells' row stride
     int64_t* out_key;        // output slabs: [n_sb][slab_cap] rows, then out_cap overflow rows
-    int64_t* out_ws;
     int64_t* out_we;
     uint64_t* out_val[FW_MAX_AGGS];
     uint32_t* out_null;
@@ -645,7 +644,8 @@ struct CompactArgs {
     int32_t n_aggs;
     int64_t slab_cap;
     const int64_t* out_key;
-    const int64_t* out_ws;
+    WinDesc win;             // window_start = window_start_of(window_end) (LOCAL phase: = window_end)
+    int32_t local_out;
     const int64_t* out_we;
     const uint64_t* out_val[FW_MAX_AGGS];
     const uint32_t* out_null;

@@ -65,8 +65,9 @@ __global__ __launch_bounds__(BLOCK) void k_compact(CompactArgs a, int32_t R) {
             const int64_t d = dst0 + i, sidx = src0 + i;
             if (d >= a.res_cap) break;
             a.res_key[d] = a.out_key[sidx];
-            a.res_ws[d] = a.out_ws[sidx];
-            a.res_we[d] = a.out_we[sidx];
+            const int64_t we = a.out_we[sidx];
+            a.res_ws[d] = a.local_out ? we : window_start_of(a.win, we);  // SliceAssigner.getWindowStart
+            a.res_we[d] = we;
             a.res_null[d] = a.out_null[sidx];
             for (int g = 0; g < a.n_aggs; g++) a.res_val[g][d] = a.out_val[g][sidx];
         }

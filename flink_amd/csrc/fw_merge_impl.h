@@ -281,7 +281,7 @@ __device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_
     const int64_t i = claim_out_row(a, sb, s_emit);
     if (i < 0) return;
     st8(&a.out_key[i], (uint64_t)key);
-    st8(&a.out_ws[i], (uint64_t)window_start_of(a.win, we));
+    // (no window_start column: it is window_start_of(window_end), derived where rows are read)
     st8(&a.out_we[i], (uint64_t)we);
     uint32_t nm = 0;
     for (int g = 0; g < a.ad.n; g++) {
@@ -334,13 +334,12 @@ __device__ __forceinline__ void emit_row(const MergeArgs& a, int sb, int32_t* s_
 // LOCAL phase output (LocalAggCombiner.combine :69-97 -> output(key, window, acc)): one row per
 // (key, sliceEnd) of the flush holding the local accumulator fields of every aggregate in order
 // (COUNT(*) / COUNT: count; SUM, MIN, MAX: value, NULL-able; AVG: sum, count), window_end =
-// window_start = sliceEnd.  The GLOBAL phase ingests exactly these columns.
+// sliceEnd (window_start = sliceEnd too, derived by the readers).  The GLOBAL phase ingests exactly these columns.
 template <int NW, bool Q>
 __device__ __forceinline__ void emit_partial(const MergeArgs& a, int sb, int32_t* s_emit, int64_t key, int64_t se, const uint64_t* acc) {
     const int64_t i = claim_out_row(a, sb, s_emit);
     if (i < 0) return;
     a.out_key[i] = key;
-    a.out_ws[i] = se;
     a.out_we[i] = se;
     uint32_t nm = 0;
     int j = 0;

@@ -276,12 +276,26 @@ class WindowAggHandle:
         check(lib().fw_results_device_segments(self._h, C.byref(seg)))
         return seg
 
+    def _window_starts(self, window_end):
+        """ABI v10: segments carry no window_start; it is SliceAssigner.getWindowStart(window_end),
+        computed by the library's own host helper (fw_host_time_op 4) once per distinct window end
+        (the LOCAL phase's rows are slices: start = end)."""
+        if self.cfg.agg_phase == abi.PHASE_LOCAL or window_end.size == 0:
+            return window_end.copy()
+        ends, inv = np.unique(window_end, return_inverse=True)
+        starts = np.empty_like(ends)
+        v = C.c_int64()
+        for i, e in enumerate(ends.tolist()):
+            check(lib().fw_host_time_op(C.byref(self.cfg), 4, int(e), C.byref(v)))
+            starts[i] = v.value
+        return starts[inv.reshape(-1)]
+
     def segments_to_host(self, seg):
         """The rows of a result_segments() description as the dict results() returns (host copies,
         after the handle's stream drains; for tests and tools -- a device consumer reads the
         segments in place)."""
         self.sync()
-        cols = {"key": seg.cols.key, "window_start": seg.cols.window_start, "window_end": seg.cols.window_end}
+        cols = {"key": seg.cols.key, "window_end": seg.cols.window_end}
         out = {k: [] for k in cols}
         out["values"] = [[] for _ in range(self.n_aggs)]
         out["null_mask"] = []
@@ -306,6 +320,7 @@ class WindowAggHandle:
         def cat(xs, dt):
             return np.concatenate(xs) if xs else np.empty(0, dt)
         res = {k: cat(out[k], np.int64) for k in cols}
+        res["window_start"] = self._window_starts(res["window_end"])
         res["values"] = [cat(v, np.int64) for v in out["values"]]
         res["null_mask"] = cat(out["null_mask"], np.uint32)
         if ds:

@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define FW_ABI_VERSION 9
+#define FW_ABI_VERSION 10
 #define FW_MAX_AGGS 8
 #define FW_MAX_COLS 8
 
@@ -419,7 +419,12 @@ int fw_results_device(fw_handle* h, fw_result* out, int64_t** d_n);
    kernels, so read it (and the rows) on the handle's stream (fw_get_stream) or after it, before
    the next call that can run a merge (see FW_ERRF_OUTPUT below).  n_segments = 0 when nothing was emitted since the last
    collection.  The rows count as consumed.  fw_results / fw_results_device compact the same rows
-   into one contiguous set (a copy of every row). */
+   into one contiguous set (a copy of every row).
+   v10: cols.window_start is NULL.  The merge stores no window start (8 B less per row); a row's
+   start is SliceAssigner.getWindowStart(window_end): window_end - size for TUMBLE / HOP (and the
+   DataStream assigners), getWindowStartWithOffset(window_end - 1, offset, size) for CUMULATE, and
+   window_end itself for a LOCAL phase (its rows are slices).  fw_host_time_op(cfg, 4, we) computes
+   it on the host; fw_results / fw_results_device fill window_start as before. */
 typedef struct {
     int64_t n_segments;
     int64_t seg_cap;

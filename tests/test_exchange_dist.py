@@ -345,3 +345,80 @@ def test_bench_rank_load_fields_sum_to_all_events():
     assert len(ev) == WORLD and sum(ev) == r["events_total"] == WORLD * n_batches * n
     assert min(ev) > 0 and r["key_group_imbalance_max_over_mean"] == pytest.approx(max(ev) / (sum(ev) / WORLD))
     assert r["rank_elapsed_s"] == [0.5, 1.5] and r["partials_ingested_per_rank"] == [100, 200]
+
+
+SIZES_GROWING = [2000, 2600, 3400, 4400, 5700, 1500]  # +30 % a step, then a small step
+
+
+def _worker_growing_shares(rank, port, out_q):
+    """The device-counted packed exchange with the segment size LEARNED (capacity=None: the previous
+    step's agreed largest share + KeyByExchange.headroom): batches growing ~30 % a step overflow their
+    segments on every step after the first, so the overflow round and the held watermark repeat on
+    consecutive steps (settle-time advance under repeated overflow)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from flink_amd.runtime.exchange import KeyByExchange
+
+        ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+        got, wms, agreed, caps, prev_px, prev_wm = [], [], [], [], None, None
+
+        def take(rows_, w):
+            sp = rows_.view(-1, w)
+            got.extend(zip(sp[:, 0].tolist(), sp[:, 1].tolist(), sp[:, 2].tolist()))
+
+        for b, n in enumerate(SIZES_GROWING):
+            if prev_px is not None:
+                spill = prev_px.settle()
+                agreed.append(prev_px.agreed_watermark)
+                if spill is not None:
+                    take(spill, prev_px.row_words)
+            k, t, v = _stream(rank, b, n)
+            px = ex.exchange_packed_async(torch.from_numpy(k), torch.from_numpy(t), [torch.from_numpy(v)])
+            cap = px.rows.numel() // (WORLD * px.row_words)
+            caps.append(cap)
+            seg = px.rows.view(WORLD, cap, px.row_words)
+            keep = torch.arange(cap)[None, :] < px.recv_counts.clamp(max=cap)[:, None]
+            take(seg[keep].reshape(-1), px.row_words)
+            wm = px.finish_device(T0 + b * 3000 - 3000 + 500 * rank, prev_wm)
+            wms.append(int(wm.item()))
+            prev_px, prev_wm = px, wm
+        spill = prev_px.settle()
+        agreed.append(prev_px.agreed_watermark)
+        if spill is not None:
+            take(spill, prev_px.row_words)
+        out_q.put((rank, sorted(got), wms, agreed, caps, ex.spill_rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_learned_segments_repeated_overflow():
+    from oracle.oracle import operator_indices
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_growing_shares, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # row parity: every row reached its key group's subtask exactly once, through 4 overflow rounds
+    for r in range(WORLD):
+        want = []
+        for b, n in enumerate(SIZES_GROWING):
+            for src in range(WORLD):
+                k, t, v = _stream(src, b, n)
+                m = operator_indices(abi.KEYHASH_BINROW_BIGINT, k, 128, WORLD) == r
+                want += zip(k[m].tolist(), t[m].tolist(), v[m].tolist())
+        assert res[r][1] == sorted(want)
+    wm = [T0 + b * 3000 - 3000 for b in range(len(SIZES_GROWING))]
+    for r in range(WORLD):
+        _, _, wms, agreed, caps, spills = res[r]
+        assert caps == res[0][4]  # every subtask picked the same (learned) segment size
+        assert caps[1] < caps[2] < caps[3] < caps[4]  # ... tracking the growing share
+        assert spills == 4  # steps 1..4 overflowed, step 5 (small) did not
+        assert agreed == wm  # the valve's minimum every step
+        # the device watermark holds at the last non-overflowing step's, then catches up
+        assert wms == [wm[0]] * 5 + [wm[5]]

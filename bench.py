@@ -522,7 +522,9 @@ def main():
     # the flushes really read: every partial row the ingest wrote (partials_merged * w_partial).
     mg_ms, mg_n = kt["merge"]
     w_entry = 8 * (3 + wl["nw"])
-    w_out = 8 * (3 + len(wl["aggs"])) + 4
+    # an emitted row as the merge writes it: key, window_end, one word per aggregate, the NULL mask
+    # (no window_start since ABI v10: readers derive it from window_end)
+    w_out = 8 * (2 + len(wl["aggs"])) + 4
     live = st["live_state_entries"]
     fired_total = st["num_fired_windows"]
     merged_share = st["partials_merged"] / max(st["partials_emitted"], 1)  # batches flushed by the end

@@ -174,6 +174,8 @@ struct fw_handle {
     uint64_t* state = nullptr;
     int32_t* state_count = nullptr;
     int64_t* sb_min_timer = nullptr;
+    uint8_t* sb_nar = nullptr;  // HOP block state: superbucket written in the narrow layout
+    bool hb_narrow = true;       // (FW_HB_NARROW=0: every write-back wide, development A/B)
     int64_t* out_key = nullptr;
     int64_t* out_we = nullptr;
     uint64_t* out_val[FW_MAX_AGGS] = {};
@@ -582,6 +584,7 @@ int validate_and_plan(fw_handle* h) {
     // SQL HOP with few slices per window and plain accumulators keeps block state (k_merge_hopb):
     // one entry per (key, HB_R consecutive slices) instead of one per (key, slice)
     const char* hb_env = getenv("FW_HOPB");
+    if (const char* nv = getenv("FW_HB_NARROW")) h->hb_narrow = atoi(nv) != 0;
     w.hopb = c.api == FW_API_SQL && c.window_kind == FW_WIN_HOP && c.agg_phase != FW_PHASE_LOCAL && !wd.has_q &&
              h->nw_t <= 2 && w.n_slices <= HB_R && !(hb_env && atoi(hb_env) == 0);
     if (w.hopb) {
@@ -807,6 +810,7 @@ int allocate(fw_handle* h) {
     if ((rc = dalloc(&h->state, (size_t)h->ks.n_sb * h->cap_e * PWE))) return rc;
     if ((rc = dalloc(&h->state_count, h->ks.n_sb))) return rc;
     if ((rc = dalloc(&h->sb_min_timer, h->ks.n_sb))) return rc;
+    if ((rc = dalloc(&h->sb_nar, h->ks.n_sb))) return rc;
     const size_t orows = (size_t)h->ks.n_sb * h->slab_cap + h->out_cap;
     if ((rc = dalloc(&h->out_key, orows))) return rc;
     if ((rc = dalloc(&h->out_we, orows))) return rc;
@@ -835,6 +839,7 @@ int allocate(fw_handle* h) {
     HIP_TRY(hipMemsetAsync(h->sb_out, 0, sizeof(int32_t) * (h->ks.n_sb + 1), h->stream));
     HIP_TRY(hipMemsetAsync(h->sb_fired, 0, sizeof(uint32_t) * h->ks.n_sb, h->stream));
     HIP_TRY(hipMemsetAsync(h->state_count, 0, sizeof(int32_t) * h->ks.n_sb, h->stream));
+    HIP_TRY(hipMemsetAsync(h->sb_nar, 0, h->ks.n_sb, h->stream));
     std::vector<int64_t> inf(h->ks.n_sb, INT64_MAX);
     HIP_TRY(hipMemcpyAsync(h->sb_min_timer, inf.data(), sizeof(int64_t) * h->ks.n_sb, hipMemcpyHostToDevice, h->stream));
     HIP_TRY(launch_init_ctrl(h->ctrl, h->stream));
@@ -951,6 +956,8 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.state = h->state;
     a.state_count = h->state_count;
     a.sb_min_timer = h->sb_min_timer;
+    a.sb_nar = h->sb_nar;
+    a.hb_narrow = h->win.hopb && h->hb_narrow;
     a.n_sb = h->ks.n_sb;
     a.cap_e = h->cap_e;
     a.win = device_win(h);
@@ -1133,6 +1140,36 @@ int push_key_rows(fw_handle* h, int64_t n, const int64_t* d_off, const uint8_t* 
     return push(h, n, h->d_kid, ts, h->d_khash, vals, nulls);
 }
 
+// the first n entries of superbucket sb, in the wide layout (key, slice, flags, words) whatever the
+// layout the last write-back chose (HOP block state may be narrow, hb_narrow_words)
+int state_rows_to_host(const fw_handle* h, size_t sb, int64_t n, uint64_t* out) {
+    const int pwe = h->pwe;
+    const uint64_t* src = h->state + sb * h->cap_e * pwe;
+    uint8_t nar = 0;
+    if (h->win.hopb) HIP_TRY(hipMemcpy(&nar, h->sb_nar + sb, 1, hipMemcpyDeviceToHost));
+    if (!nar) {
+        HIP_TRY(hipMemcpy(out, src, (size_t)n * pwe * 8, hipMemcpyDeviceToHost));
+        return FW_OK;
+    }
+    const int nw = h->nw_t, pwn = hb_narrow_words(nw);
+    std::vector<uint64_t> tmp((size_t)n * pwn);
+    HIP_TRY(hipMemcpy(tmp.data(), src, tmp.size() * 8, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++) {
+        uint32_t q[2 * 16];
+        memcpy(q, tmp.data() + (size_t)i * pwn, (size_t)pwn * 8);
+        uint64_t* e = out + (size_t)i * pwe;
+        e[0] = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+        e[1] = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
+        e[2] = q[4];
+        const uint32_t mask = q[4] >> HB_MASK_SHIFT;
+        for (int s = 0; s < HB_R; s++)
+            for (int x = 0; x < nw; x++)
+                e[3 + s * nw + x] = ((mask >> s) & 1u) ? (uint64_t)(int64_t)(int32_t)q[5 + s * nw + x]
+                                    : x < h->wd.nw ? word_identity(h->wd.op[x]) : 0;
+    }
+    return FW_OK;
+}
+
 // earliest watermark-visible time of an entry's timers, as a window end (is_fired(x, W) <=> due):
 // the maxTimestamp timer at its window end, a DataStream cleanup timer at cleanupTime + 1
 int64_t entry_timer_end(const fw_handle* h, int64_t slice, uint64_t flags) {
@@ -1220,6 +1257,7 @@ int fw_destroy(fw_handle* h) {
     hipFree(h->state);
     hipFree(h->state_count);
     hipFree(h->sb_min_timer);
+    hipFree(h->sb_nar);
     hipFree(h->out_key);
     hipFree(h->out_we);
     hipFree(h->out_null);
@@ -1514,7 +1552,7 @@ int fw_advance(fw_handle* h, int64_t watermark) {
     int rc = launch_merge(h, watermark, 0);
     if (rc) return rc;
     if (h->keyrow)  // key rows no state / partial / timer request / unread result holds any more
-        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->ks.n_sb, h->cap_e, h->pwe,
+        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->sb_nar, hb_narrow_words(h->nw_t), h->ks.n_sb, h->cap_e, h->pwe,
                                   2 + h->nw_t, h->parts, h->cap_rows, h->treq, h->out_key, h->sb_out, h->slab_cap,
                                   h->stream));
     if (watermark > h->host_cur) h->host_cur = watermark;
@@ -1532,7 +1570,7 @@ int fw_advance_device(fw_handle* h, const int64_t* d_watermark) {
     h->merge_seq++;
     h->reset_pending = false;
     if (h->keyrow)
-        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->ks.n_sb, h->cap_e, h->pwe,
+        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->sb_nar, hb_narrow_words(h->nw_t), h->ks.n_sb, h->cap_e, h->pwe,
                                   2 + h->nw_t, h->parts, h->cap_rows, h->treq, h->out_key, h->sb_out, h->slab_cap,
                                   h->stream));
     return FW_OK;
@@ -2120,7 +2158,7 @@ int fw_snapshot(fw_handle* h, void* buf, int64_t capacity, int64_t* size) {
         uint64_t* e = ent.data();
         for (int s = 0; s < nsb; s++) {
             if (!cnt[s]) continue;
-            HIP_TRY(hipMemcpy(e, h->state + (size_t)s * h->cap_e * pwe, (size_t)cnt[s] * pwe * 8, hipMemcpyDeviceToHost));
+            if ((rc = state_rows_to_host(h, (size_t)s, cnt[s], e))) return rc;
             e += (size_t)cnt[s] * pwe;
         }
     }
@@ -2186,6 +2224,7 @@ int fw_restore(fw_handle* h, const void* buf, int64_t size) {
         e += (size_t)cnt[s] * pwe;
     }
     HIP_TRY(hipMemcpy(h->state_count, cnt.data(), 4ll * nsb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(h->sb_nar, 0, (size_t)nsb));  // restored entries are in the wide layout
     HIP_TRY(hipMemcpy(h->sb_min_timer, mins.data(), 8ll * nsb, hipMemcpyHostToDevice));
     Ctrl c;
     HIP_TRY(hipMemcpy(&c, h->ctrl, sizeof c, hipMemcpyDeviceToHost));  // the key-row allocator survives
@@ -2260,7 +2299,7 @@ int fw_snapshot_key_group(fw_handle* h, int32_t key_group, void* buf, int64_t ca
     for (int q = 0; q < nsub; q++) {
         if (!cnt[q]) continue;
         const size_t sb = ((size_t)li << L) + q;
-        HIP_TRY(hipMemcpy(e, h->state + sb * h->cap_e * pwe, (size_t)cnt[q] * pwe * 8, hipMemcpyDeviceToHost));
+        if ((rc = state_rows_to_host(h, sb, cnt[q], e))) return rc;
         for (int i = 0; i < cnt[q]; i++) e[(size_t)i * pwe + 2] = (uint32_t)e[(size_t)i * pwe + 2] | ((uint64_t)q << 32);
         e += (size_t)cnt[q] * pwe;
     }
@@ -2352,6 +2391,7 @@ int fw_restore_key_group(fw_handle* h, const void* buf, int64_t size) {
         const size_t sb = ((size_t)li << L) + q;
         HIP_TRY(hipMemcpy(h->state + (sb * h->cap_e + cnt[q]) * pwe, per[q].data(), (size_t)n * pwe * 8,
                           hipMemcpyHostToDevice));
+        HIP_TRY(hipMemset(h->sb_nar + sb, 0, 1));  // (the superbucket held no entries: cnt[q] == 0)
         for (int64_t i = 0; i < n; i++)
             mins[q] = std::min(mins[q], entry_timer_end(h, (int64_t)per[q][(size_t)i * pwe + 1], per[q][(size_t)i * pwe + 2]));
         cnt[q] += (int32_t)n;

@@ -138,6 +138,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
     constexpr int NA = HB_R * NWP;  // ring words per entry
     constexpr int PW = 2 + NWP;     // partial row words
     constexpr int PWE = 3 + NA;     // state entry words
+    constexpr int PWN = hb_narrow_words(NWP);  // ... in the narrow layout
     const int64_t CH = a.chunk_rows;
     constexpr int GU = mg_rows_in_flight(NWP);
     __shared__ StateLds<NA, E> S;
@@ -214,16 +215,37 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         }
         __syncthreads();
         const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
+        const bool nar_in = a.sb_nar[sb] != 0;  // (uniform) the layout the last write-back chose
         if ((FW_ABL(a) & AB_M_NO_LOAD) && tid == 0) S.n = 0;  // (diagnostic ablations: timing only)
         if (!(FW_ABL(a) & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
-            uint64_t p[PWE];
-            load_words<PWE>(st + (size_t)e * PWE, p);
-            const int64_t k = (int64_t)p[0], bs = (int64_t)p[1];
+            int64_t k, bs;
+            if (nar_in) {
+                uint64_t p[PWN];
+                load_words<PWN>(st + (size_t)e * PWN, p);
+                k = (int64_t)p[0];
+                bs = (int64_t)p[1];
+                const uint32_t fl = (uint32_t)p[2];
+                S.flag[e] = fl;
+                const uint32_t mask = fl >> HB_MASK_SHIFT;
+#pragma unroll
+                for (int i = 0; i < NA; i++) {
+                    const int x = 5 + i;  // the slot word's 32-bit index in the entry
+                    const uint32_t v32 = (x & 1) ? (uint32_t)(p[x >> 1] >> 32) : (uint32_t)p[x >> 1];
+                    const int w = i % NWP;
+                    S.acc[i][e] = ((mask >> (i / NWP)) & 1u) ? (uint64_t)(int64_t)(int32_t)v32
+                                  : word_on<OPS>(a.wd, w) ? word_identity(word_op<OPS>(a.wd, w)) : 0;
+                }
+            } else {
+                uint64_t p[PWE];
+                load_words<PWE>(st + (size_t)e * PWE, p);
+                k = (int64_t)p[0];
+                bs = (int64_t)p[1];
+                S.flag[e] = (uint32_t)p[2];
+#pragma unroll
+                for (int i = 0; i < NA; i++) S.acc[i][e] = p[3 + i];
+            }
             S.key[e] = k;
             S.slice[e] = bs;
-            S.flag[e] = (uint32_t)p[2];
-#pragma unroll
-            for (int i = 0; i < NA; i++) S.acc[i][e] = p[3 + i];
             uint32_t h = index_hash(k, bs) & (StateLds<NA, E>::NI - 1);
             for (;;) {
                 uint32_t expect = 0;
@@ -334,50 +356,84 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
             if ((tid & 63) == 0 && nf) atomicAdd(&s_fired, nf);
         }
         // ---- write back: a slice is dropped once its last window has fired (clearWindow); an
-        // entry without live slices is dropped
+        // entry without live slices is dropped.  Pass 1 expires the slices (the entry's flags in LDS)
+        // and votes on the narrow layout; pass 2 writes the live entries in the layout chosen.
         if (tid == 0) {
             s_nlive = 0;
             s_newmin = INT64_MAX;
         }
-        __syncthreads();
+        __syncthreads();  // (the fire reads neighbouring entries' flags, which pass 1 rewrites)
         const int n = min(S.n, E);
         uint64_t* so = a.state + (size_t)sb * a.cap_e * PWE;
         int64_t lnm = INT64_MAX;
         // the first window end that is not fired at w_new (UTC: the slice grid point above w_new + 1)
         const int64_t e_min = win.tz.n == 0 ? slice_end_of(win, wadd(w_new, 1)) : INT64_MIN;
+        bool fits = a.hb_narrow != 0;
         for (int e = tid; e < n; e += MG_BLOCK) {
             const int64_t bs = S.slice[e];
             uint32_t mask = S.flag[e] >> HB_MASK_SHIFT;
-            uint64_t p[PWE];
-#pragma unroll
-            for (int i = 0; i < NA; i++) p[3 + i] = S.acc[i][e];
             int64_t first = INT64_MAX;
 #pragma unroll
             for (int i = 0; i < HB_R; i++) {
                 if (!((mask >> i) & 1u)) continue;
                 const int64_t se = wadd(bs, (int64_t)(i + 1) * win.interval);
                 if (win_fired(win, wadd(se, wsub(win.size, win.interval)), w_new)) {
-                    mask &= ~(1u << i);  // its last window fired: expired
+                    mask &= ~(1u << i);  // its last window fired: expired (its words: identity, below)
+                } else {
+                    if (first == INT64_MAX) first = se;
 #pragma unroll
-                    for (int w = 0; w < NWP; w++)
-                        p[3 + i * NWP + w] = word_on<OPS>(a.wd, w) ? word_identity(word_op<OPS>(a.wd, w)) : 0;
-                } else if (first == INT64_MAX) {
-                    first = se;
+                    for (int w = 0; w < NWP; w++) {
+                        const int64_t v = (int64_t)S.acc[i * NWP + w][e];
+                        fits &= v == (int64_t)(int32_t)v;
+                    }
                 }
             }
+            S.flag[e] = F_ACC | (mask << HB_MASK_SHIFT);
+            if (mask) lnm = min(lnm, max(first, e_min));  // no window of this entry is due before it
+        }
+        const bool nar_out = __syncthreads_and(fits) != 0;
+        for (int e = tid; e < n; e += MG_BLOCK) {
+            const uint32_t fl = S.flag[e];
+            const uint32_t mask = fl >> HB_MASK_SHIFT;
             if (!mask) continue;
             const int pos = wave_claim(&s_nlive);
-            p[0] = (uint64_t)S.key[e];
-            p[1] = (uint64_t)bs;
-            p[2] = (uint64_t)(F_ACC | (mask << HB_MASK_SHIFT));
-            if (!(FW_ABL(a) & AB_M_NO_WB)) store_words<PWE>(so + (size_t)pos * PWE, p);
-            lnm = min(lnm, max(first, e_min));  // no window of this entry is due before it
+            if (FW_ABL(a) & AB_M_NO_WB) continue;
+            if (nar_out) {
+                uint32_t q[2 * PWN];
+                const uint64_t k = (uint64_t)S.key[e], bs = (uint64_t)S.slice[e];
+                q[0] = (uint32_t)k;
+                q[1] = (uint32_t)(k >> 32);
+                q[2] = (uint32_t)bs;
+                q[3] = (uint32_t)(bs >> 32);
+                q[4] = fl;
+#pragma unroll
+                for (int i = 0; i < NA; i++) q[5 + i] = ((mask >> (i / NWP)) & 1u) ? (uint32_t)S.acc[i][e] : 0u;
+#pragma unroll
+                for (int i = 5 + NA; i < 2 * PWN; i++) q[i] = 0u;
+                uint64_t p[PWN];
+#pragma unroll
+                for (int i = 0; i < PWN; i++) p[i] = (uint64_t)q[2 * i] | ((uint64_t)q[2 * i + 1] << 32);
+                store_words<PWN>(so + (size_t)pos * PWN, p);
+            } else {
+                uint64_t p[PWE];
+                p[0] = (uint64_t)S.key[e];
+                p[1] = (uint64_t)S.slice[e];
+                p[2] = (uint64_t)fl;
+#pragma unroll
+                for (int i = 0; i < NA; i++) {
+                    const int w = i % NWP;
+                    p[3 + i] = ((mask >> (i / NWP)) & 1u) ? S.acc[i][e]
+                               : word_on<OPS>(a.wd, w) ? word_identity(word_op<OPS>(a.wd, w)) : 0;
+                }
+                store_words<PWE>(so + (size_t)pos * PWE, p);
+            }
         }
         lnm = wave_min_i64(lnm);
         if ((tid & 63) == 0 && lnm != INT64_MAX) __hip_atomic_fetch_min(&s_newmin, lnm, __ATOMIC_RELAXED, LDS_SCOPE);
         __syncthreads();
         if (tid == 0) {
             a.state_count[sb] = s_nlive;
+            a.sb_nar[sb] = nar_out ? 1 : 0;
             a.sb_min_timer[sb] = s_newmin;
             a.sb_out[sb] = min(s_emit, a.slab_cap);
             if (s_fired) a.sb_fired[sb] += s_fired;

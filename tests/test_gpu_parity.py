@@ -1001,3 +1001,28 @@ def test_restore_into_same_handle_drops_pending_pushes(layout, monkeypatch):
         _compare(_rows(g.results(reset=True), cfg, set()), _rows(o.results(clear=True), cfg, set()), set(), f"batch {bi}")
     assert g.stats()["error_flags"] == 0
     g.close()
+
+
+# HOP block state in the narrow layout (k_merge_hopb: a superbucket whose every slot word with data
+# fits int32 is written back as 7 / 11 words instead of 11 / 19) and back: some batches carry values
+# past 2^31 (and sums that pass it by accumulation), so superbuckets switch layouts from flush to flush;
+# a snapshot / restore in the middle reads narrow and wide superbuckets back.  COUNT(*) + SUM and
+# COUNT(*) + MIN (whose empty slots hold the identity Long.MAX_VALUE, restored on load).
+@pytest.mark.parametrize("agg", [abi.AGG_SUM, abi.AGG_MIN, abi.AGG_MAX])
+@pytest.mark.parametrize("narrow", ["1", "0"])
+def test_hop_block_state_narrow_and_wide_layouts(agg, narrow, monkeypatch):
+    monkeypatch.setenv("FW_HB_NARROW", narrow)
+    kw = dict(window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000, count_star_index=0,
+              aggs=[(abi.AGG_COUNT_STAR, 0, I64), (agg, 0, I64)])
+    batches = _stream(4242 + agg, 24000, 400, ooo=12000, step_ms=4500, n_wm=24)
+    out = []
+    for b, (k, t, iv, dv, wm) in enumerate(batches):
+        iv = iv.copy()
+        if b % 6 == 2:  # a few keys with values past int32
+            sel = (k // 7919) % 7 == 0
+            iv[sel] = iv[sel] * (1 << 33) + (1 << 40)
+        elif b % 6 == 4:  # sums past int32 by accumulation (each value < 2^31)
+            iv[:] = (1 << 30) + iv
+        out.append((k, t, iv, dv, wm))
+    for snap in (None, 11):
+        _run_both(_cfg(kw), out, _double_cols(kw), snapshot_at=snap)

@@ -175,7 +175,7 @@ struct fw_handle {
     int32_t* state_count = nullptr;
     int64_t* sb_min_timer = nullptr;
     uint8_t* sb_nar = nullptr;  // HOP block state: superbucket written in the narrow layout
-    bool hb_narrow = true;       // (FW_HB_NARROW=0: every write-back wide, development A/B)
+    int hb_narrow = 2;           // narrowest HOP block layout level (FW_HB_NARROW=0/1: development A/B)
     int64_t* out_key = nullptr;
     int64_t* out_we = nullptr;
     uint64_t* out_val[FW_MAX_AGGS] = {};
@@ -584,7 +584,7 @@ int validate_and_plan(fw_handle* h) {
     // SQL HOP with few slices per window and plain accumulators keeps block state (k_merge_hopb):
     // one entry per (key, HB_R consecutive slices) instead of one per (key, slice)
     const char* hb_env = getenv("FW_HOPB");
-    if (const char* nv = getenv("FW_HB_NARROW")) h->hb_narrow = atoi(nv) != 0;
+    if (const char* nv = getenv("FW_HB_NARROW")) h->hb_narrow = std::min(std::max(atoi(nv), 0), 2);
     w.hopb = c.api == FW_API_SQL && c.window_kind == FW_WIN_HOP && c.agg_phase != FW_PHASE_LOCAL && !wd.has_q &&
              h->nw_t <= 2 && w.n_slices <= HB_R && !(hb_env && atoi(hb_env) == 0);
     if (w.hopb) {
@@ -957,7 +957,7 @@ MergeArgs merge_args(fw_handle* h, int64_t wm, int force) {
     a.state_count = h->state_count;
     a.sb_min_timer = h->sb_min_timer;
     a.sb_nar = h->sb_nar;
-    a.hb_narrow = h->win.hopb && h->hb_narrow;
+    a.hb_narrow = h->win.hopb ? h->hb_narrow : 0;
     a.n_sb = h->ks.n_sb;
     a.cap_e = h->cap_e;
     a.win = device_win(h);
@@ -1151,21 +1151,33 @@ int state_rows_to_host(const fw_handle* h, size_t sb, int64_t n, uint64_t* out) 
         HIP_TRY(hipMemcpy(out, src, (size_t)n * pwe * 8, hipMemcpyDeviceToHost));
         return FW_OK;
     }
-    const int nw = h->nw_t, pwn = hb_narrow_words(nw);
+    const int nw = h->nw_t, pwn = hb_narrow_words(nw, nar), sbytes = hb_slot_bytes(nar);
     std::vector<uint64_t> tmp((size_t)n * pwn);
     HIP_TRY(hipMemcpy(tmp.data(), src, tmp.size() * 8, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; i++) {
-        uint32_t q[2 * 16];
-        memcpy(q, tmp.data() + (size_t)i * pwn, (size_t)pwn * 8);
+        const uint8_t* q = (const uint8_t*)(tmp.data() + (size_t)i * pwn);
         uint64_t* e = out + (size_t)i * pwe;
-        e[0] = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
-        e[1] = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
-        e[2] = q[4];
-        const uint32_t mask = q[4] >> HB_MASK_SHIFT;
+        uint32_t fl;
+        memcpy(&e[0], q, 8);
+        memcpy(&e[1], q + 8, 8);
+        memcpy(&fl, q + 16, 4);
+        e[2] = fl;
+        const uint32_t mask = fl >> HB_MASK_SHIFT;
         for (int s = 0; s < HB_R; s++)
-            for (int x = 0; x < nw; x++)
-                e[3 + s * nw + x] = ((mask >> s) & 1u) ? (uint64_t)(int64_t)(int32_t)q[5 + s * nw + x]
-                                    : x < h->wd.nw ? word_identity(h->wd.op[x]) : 0;
+            for (int x = 0; x < nw; x++) {
+                const uint8_t* f = q + 20 + sbytes * (s * nw + x);
+                int64_t v;
+                if (sbytes == 4) {
+                    int32_t t;
+                    memcpy(&t, f, 4);
+                    v = t;
+                } else {
+                    int16_t t;
+                    memcpy(&t, f, 2);
+                    v = t;
+                }
+                e[3 + s * nw + x] = ((mask >> s) & 1u) ? (uint64_t)v : x < h->wd.nw ? word_identity(h->wd.op[x]) : 0;
+            }
     }
     return FW_OK;
 }
@@ -1552,7 +1564,7 @@ int fw_advance(fw_handle* h, int64_t watermark) {
     int rc = launch_merge(h, watermark, 0);
     if (rc) return rc;
     if (h->keyrow)  // key rows no state / partial / timer request / unread result holds any more
-        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->sb_nar, hb_narrow_words(h->nw_t), h->ks.n_sb, h->cap_e, h->pwe,
+        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->sb_nar, h->nw_t, h->ks.n_sb, h->cap_e, h->pwe,
                                   2 + h->nw_t, h->parts, h->cap_rows, h->treq, h->out_key, h->sb_out, h->slab_cap,
                                   h->stream));
     if (watermark > h->host_cur) h->host_cur = watermark;
@@ -1570,7 +1582,7 @@ int fw_advance_device(fw_handle* h, const int64_t* d_watermark) {
     h->merge_seq++;
     h->reset_pending = false;
     if (h->keyrow)
-        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->sb_nar, hb_narrow_words(h->nw_t), h->ks.n_sb, h->cap_e, h->pwe,
+        HIP_TRY(launch_kr_collect(h->kr, h->ctrl, h->state, h->state_count, h->sb_nar, h->nw_t, h->ks.n_sb, h->cap_e, h->pwe,
                                   2 + h->nw_t, h->parts, h->cap_rows, h->treq, h->out_key, h->sb_out, h->slab_cap,
                                   h->stream));
     return FW_OK;

@@ -337,11 +337,14 @@ struct WinDesc {
 constexpr int KIND_DSWIN = 3;
 constexpr int KIND_HOPB = 4;  // SQL HOP, block state (fw_merge_hopb.h)
 constexpr int HB_R = 8;       // slices per HOP block entry
-// Narrow HOP block entry (k_merge_hopb write-back, per superbucket: every slot word with data fits
-// int32): 32-bit words key lo/hi, block start lo/hi, flags, then the HB_R * nw slot words as int32
-// (a slot without data -- its mask bit clear -- holds the word's identity, restored on load).
-// 7 words instead of 11 for one accumulator word, 11 instead of 19 for two.
-constexpr int hb_narrow_words(int nw) { return (20 + 4 * HB_R * nw + 7) / 8; }
+// Narrow HOP block entries (k_merge_hopb write-back, per superbucket: every slot word with data fits
+// the level's width): key (8 B), block start (8 B), flags (4 B), then the HB_R * nw slot words as
+// int32 (level 1) or int16 (level 2), zero-padded to whole 8-byte words.  A slot without data -- its
+// mask bit clear -- holds the word's identity, restored on load.  One accumulator word: 11 words
+// wide, 7 at level 1, 5 at level 2; two: 19, 11, 7.
+constexpr int HB_LEVELS = 3;  // 0: wide (3 + HB_R * nw words), 1: int32 slots, 2: int16 slots
+constexpr int hb_slot_bytes(int level) { return level == 1 ? 4 : 2; }
+constexpr int hb_narrow_words(int nw, int level = 1) { return (20 + hb_slot_bytes(level) * HB_R * nw + 7) / 8; }
 constexpr uint32_t HB_MASK_SHIFT = 8;  // block entry flag bits 8.. : slot i holds data
 
 // TimeWindowUtil.isWindowFired in the window's shift zone (UTC when tz.n == 0)
@@ -590,8 +593,8 @@ struct MergeArgs {
     uint64_t* state;         // [n_sb][cap_e][3 + nw] words: key, slice, flags, acc...
     int32_t* state_count;    // live entries per superbucket
     int64_t* sb_min_timer;   // min windowEnd with a timer per superbucket (INT64_MAX: none)
-    uint8_t* sb_nar;         // HOP block state: the superbucket's entries are in the narrow layout (hb_narrow_words)
-    int32_t hb_narrow;       // HOP block state: a write-back may choose the narrow layout
+    uint8_t* sb_nar;         // HOP block state: the superbucket's layout level (0 wide, 1 / 2 narrow: hb_narrow_words)
+    int32_t hb_narrow;       // HOP block state: the narrowest layout level a write-back may choose (0..2)
     int32_t n_sb;
     int32_t cap_e;
     WinDesc win;
@@ -730,7 +733,7 @@ int key_row_desc(const fw_key_field* fields, int32_t n_fields, KeyRowDesc* d);
 hipError_t launch_kr_intern(const KeyRowTable& t, Ctrl* c, int64_t n, const int64_t* off, const uint8_t* bytes,
                             int64_t* out_id, int32_t* out_hash, hipStream_t s);
 hipError_t launch_kr_collect(const KeyRowTable& t, Ctrl* c, const uint64_t* state, const int32_t* state_count,
-                             const uint8_t* sb_nar, int32_t pwn,
+                             const uint8_t* sb_nar, int32_t hb_nw,
                              int32_t n_sb, int32_t cap_e, int32_t pwe, int32_t pw, const uint64_t* parts,
                              int64_t cap_rows, const int64_t* treq, const int64_t* out_key, const int32_t* sb_out,
                              int64_t slab_cap, hipStream_t s);

@@ -129,8 +129,8 @@ struct KrMarkArgs {
     Ctrl* c;
     const uint64_t* state;  // [n_sb][cap_e][pwe]
     const int32_t* state_count;
-    const uint8_t* sb_nar;  // HOP block state: superbucket b's entries are pwn words (key first either way)
-    int32_t pwn;
+    const uint8_t* sb_nar;  // HOP block state: superbucket b's layout level (hb_narrow_words; key first in every layout)
+    int32_t hb_nw;
     int32_t n_sb, cap_e, pwe, pw;
     const uint64_t* parts;  // FW_MAX_PENDING slots of cap_rows rows of pw words
     int64_t cap_rows;
@@ -150,7 +150,8 @@ __global__ void k_kr_gc_mark(KrMarkArgs a) {
     if (b < a.n_sb) {
         const int32_t n = a.state_count[b];
         const uint64_t* st = a.state + (size_t)b * a.cap_e * a.pwe;
-        const int stride = a.sb_nar && a.sb_nar[b] ? a.pwn : a.pwe;
+        const int lv = a.sb_nar ? a.sb_nar[b] : 0;
+        const int stride = lv ? hb_narrow_words(a.hb_nw, lv) : a.pwe;
         for (int e = threadIdx.x; e < n; e += blockDim.x) kr_mark(a.t, c, (int64_t)st[(size_t)e * stride], ep);
         const int32_t no = min((int64_t)a.sb_out[b], a.slab_cap);
         for (int r = threadIdx.x; r < no; r += blockDim.x) kr_mark(a.t, c, a.out_key[b * a.slab_cap + r], ep);
@@ -234,12 +235,12 @@ hipError_t launch_kr_intern(const KeyRowTable& t, Ctrl* c, int64_t n, const int6
 }
 
 hipError_t launch_kr_collect(const KeyRowTable& t, Ctrl* c, const uint64_t* state, const int32_t* state_count,
-                             const uint8_t* sb_nar, int32_t pwn,
+                             const uint8_t* sb_nar, int32_t hb_nw,
                              int32_t n_sb, int32_t cap_e, int32_t pwe, int32_t pw, const uint64_t* parts,
                              int64_t cap_rows, const int64_t* treq, const int64_t* out_key, const int32_t* sb_out,
                              int64_t slab_cap, hipStream_t s) {
     hipLaunchKernelGGL(k_kr_gc_begin, dim3(1), dim3(64), 0, s, t, c);
-    KrMarkArgs a{t, c, state, state_count, sb_nar, pwn, n_sb, cap_e, pwe, pw, parts, cap_rows, treq, out_key, sb_out, slab_cap};
+    KrMarkArgs a{t, c, state, state_count, sb_nar, hb_nw, n_sb, cap_e, pwe, pw, parts, cap_rows, treq, out_key, sb_out, slab_cap};
     hipLaunchKernelGGL(k_kr_gc_mark, dim3((unsigned)n_sb + 256), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_kr_gc_reset_free, dim3(1), dim3(64), 0, s, c);
     const unsigned g = (unsigned)std::min<int64_t>(4096, (std::max(t.n_slots, t.cap_ids) + 255) / 256);

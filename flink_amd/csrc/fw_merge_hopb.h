@@ -65,6 +65,47 @@ __device__ int hb_find_or_insert(StateLds<HB_R * NWP, E>& S, int64_t k, int64_t 
     return -1;
 }
 
+// a narrow entry (hb_narrow_words, level L) <-> the LDS entry
+template <int NWP, int E, uint32_t OPS, int L>
+__device__ __forceinline__ void hb_load_narrow(const MergeArgs& a, const uint64_t* src, StateLds<HB_R * NWP, E>& S, int e,
+                                               int64_t* k, int64_t* bs) {
+    constexpr int NA = HB_R * NWP, PN = hb_narrow_words(NWP, L), SB = hb_slot_bytes(L);
+    uint64_t p[PN];
+    load_words<PN>(src, p);
+    *k = (int64_t)p[0];
+    *bs = (int64_t)p[1];
+    const uint32_t fl = (uint32_t)p[2];
+    S.flag[e] = fl;
+    const uint32_t mask = fl >> HB_MASK_SHIFT;
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+        const int b = 20 + SB * i;  // the slot's byte offset in the entry
+        const uint64_t raw = p[b >> 3] >> (8 * (b & 7));
+        const int64_t v = SB == 4 ? (int64_t)(int32_t)(uint32_t)raw : (int64_t)(int16_t)(uint16_t)raw;
+        const int w = i % NWP;
+        S.acc[i][e] = ((mask >> (i / NWP)) & 1u) ? (uint64_t)v
+                      : word_on<OPS>(a.wd, w) ? word_identity(word_op<OPS>(a.wd, w)) : 0;
+    }
+}
+template <int NWP, int E, int L>
+__device__ __forceinline__ void hb_store_narrow(uint64_t* dst, const StateLds<HB_R * NWP, E>& S, int e, uint32_t fl) {
+    constexpr int NA = HB_R * NWP, PN = hb_narrow_words(NWP, L), SB = hb_slot_bytes(L);
+    const uint32_t mask = fl >> HB_MASK_SHIFT;
+    uint64_t p[PN];
+#pragma unroll
+    for (int i = 0; i < PN; i++) p[i] = 0;
+    p[0] = (uint64_t)S.key[e];
+    p[1] = (uint64_t)S.slice[e];
+    p[2] = (uint64_t)fl;
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+        const int b = 20 + SB * i;
+        const uint64_t v = ((mask >> (i / NWP)) & 1u) ? (S.acc[i][e] & (SB == 4 ? 0xFFFFFFFFull : 0xFFFFull)) : 0ull;
+        p[b >> 3] |= v << (8 * (b & 7));
+    }
+    store_words<PN>(dst, p);
+}
+
 // block start of a slice end and the slice's slot in it
 __device__ __forceinline__ int64_t hb_block_of(const WinDesc& w, int64_t se) {
     return window_start(wsub(se, 1), w.offset, w.hb_span_div);
@@ -138,7 +179,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
     constexpr int NA = HB_R * NWP;  // ring words per entry
     constexpr int PW = 2 + NWP;     // partial row words
     constexpr int PWE = 3 + NA;     // state entry words
-    constexpr int PWN = hb_narrow_words(NWP);  // ... in the narrow layout
+    constexpr int PW1 = hb_narrow_words(NWP, 1), PW2 = hb_narrow_words(NWP, 2);  // ... in the narrow layouts
     const int64_t CH = a.chunk_rows;
     constexpr int GU = mg_rows_in_flight(NWP);
     __shared__ StateLds<NA, E> S;
@@ -215,26 +256,14 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         }
         __syncthreads();
         const uint64_t* st = a.state + (size_t)sb * a.cap_e * PWE;
-        const bool nar_in = a.sb_nar[sb] != 0;  // (uniform) the layout the last write-back chose
+        const int lv_in = a.sb_nar[sb];  // (uniform) the layout the last write-back chose
         if ((FW_ABL(a) & AB_M_NO_LOAD) && tid == 0) S.n = 0;  // (diagnostic ablations: timing only)
         if (!(FW_ABL(a) & AB_M_NO_LOAD)) for (int e = tid; e < n0; e += MG_BLOCK) {
             int64_t k, bs;
-            if (nar_in) {
-                uint64_t p[PWN];
-                load_words<PWN>(st + (size_t)e * PWN, p);
-                k = (int64_t)p[0];
-                bs = (int64_t)p[1];
-                const uint32_t fl = (uint32_t)p[2];
-                S.flag[e] = fl;
-                const uint32_t mask = fl >> HB_MASK_SHIFT;
-#pragma unroll
-                for (int i = 0; i < NA; i++) {
-                    const int x = 5 + i;  // the slot word's 32-bit index in the entry
-                    const uint32_t v32 = (x & 1) ? (uint32_t)(p[x >> 1] >> 32) : (uint32_t)p[x >> 1];
-                    const int w = i % NWP;
-                    S.acc[i][e] = ((mask >> (i / NWP)) & 1u) ? (uint64_t)(int64_t)(int32_t)v32
-                                  : word_on<OPS>(a.wd, w) ? word_identity(word_op<OPS>(a.wd, w)) : 0;
-                }
+            if (lv_in == 2) {
+                hb_load_narrow<NWP, E, OPS, 2>(a, st + (size_t)e * PW2, S, e, &k, &bs);
+            } else if (lv_in == 1) {
+                hb_load_narrow<NWP, E, OPS, 1>(a, st + (size_t)e * PW1, S, e, &k, &bs);
             } else {
                 uint64_t p[PWE];
                 load_words<PWE>(st + (size_t)e * PWE, p);
@@ -368,7 +397,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         int64_t lnm = INT64_MAX;
         // the first window end that is not fired at w_new (UTC: the slice grid point above w_new + 1)
         const int64_t e_min = win.tz.n == 0 ? slice_end_of(win, wadd(w_new, 1)) : INT64_MIN;
-        bool fits = a.hb_narrow != 0;
+        bool fits = a.hb_narrow >= 1, fits16 = a.hb_narrow >= 2;  // every live slot word fits int32 / int16
         for (int e = tid; e < n; e += MG_BLOCK) {
             const int64_t bs = S.slice[e];
             uint32_t mask = S.flag[e] >> HB_MASK_SHIFT;
@@ -385,35 +414,25 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
                     for (int w = 0; w < NWP; w++) {
                         const int64_t v = (int64_t)S.acc[i * NWP + w][e];
                         fits &= v == (int64_t)(int32_t)v;
+                        fits16 &= v == (int64_t)(int16_t)v;
                     }
                 }
             }
             S.flag[e] = F_ACC | (mask << HB_MASK_SHIFT);
             if (mask) lnm = min(lnm, max(first, e_min));  // no window of this entry is due before it
         }
-        const bool nar_out = __syncthreads_and(fits) != 0;
+        const bool f32 = __syncthreads_and(fits) != 0;
+        const int lv_out = __syncthreads_and(fits16) ? 2 : f32 ? 1 : 0;
         for (int e = tid; e < n; e += MG_BLOCK) {
             const uint32_t fl = S.flag[e];
             const uint32_t mask = fl >> HB_MASK_SHIFT;
             if (!mask) continue;
             const int pos = wave_claim(&s_nlive);
             if (FW_ABL(a) & AB_M_NO_WB) continue;
-            if (nar_out) {
-                uint32_t q[2 * PWN];
-                const uint64_t k = (uint64_t)S.key[e], bs = (uint64_t)S.slice[e];
-                q[0] = (uint32_t)k;
-                q[1] = (uint32_t)(k >> 32);
-                q[2] = (uint32_t)bs;
-                q[3] = (uint32_t)(bs >> 32);
-                q[4] = fl;
-#pragma unroll
-                for (int i = 0; i < NA; i++) q[5 + i] = ((mask >> (i / NWP)) & 1u) ? (uint32_t)S.acc[i][e] : 0u;
-#pragma unroll
-                for (int i = 5 + NA; i < 2 * PWN; i++) q[i] = 0u;
-                uint64_t p[PWN];
-#pragma unroll
-                for (int i = 0; i < PWN; i++) p[i] = (uint64_t)q[2 * i] | ((uint64_t)q[2 * i + 1] << 32);
-                store_words<PWN>(so + (size_t)pos * PWN, p);
+            if (lv_out == 2) {
+                hb_store_narrow<NWP, E, 2>(so + (size_t)pos * PW2, S, e, fl);
+            } else if (lv_out == 1) {
+                hb_store_narrow<NWP, E, 1>(so + (size_t)pos * PW1, S, e, fl);
             } else {
                 uint64_t p[PWE];
                 p[0] = (uint64_t)S.key[e];
@@ -433,7 +452,7 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         __syncthreads();
         if (tid == 0) {
             a.state_count[sb] = s_nlive;
-            a.sb_nar[sb] = nar_out ? 1 : 0;
+            a.sb_nar[sb] = (uint8_t)lv_out;
             a.sb_min_timer[sb] = s_newmin;
             a.sb_out[sb] = min(s_emit, a.slab_cap);
             if (s_fired) a.sb_fired[sb] += s_fired;

@@ -1003,13 +1003,13 @@ def test_restore_into_same_handle_drops_pending_pushes(layout, monkeypatch):
     g.close()
 
 
-# HOP block state in the narrow layout (k_merge_hopb: a superbucket whose every slot word with data
-# fits int32 is written back as 7 / 11 words instead of 11 / 19) and back: some batches carry values
+# HOP block state in the narrow layouts (k_merge_hopb: a superbucket whose every slot word with data
+# fits int16 / int32 is written back as 5 / 7 words instead of 11, 7 / 11 instead of 19) and back: some batches carry values
 # past 2^31 (and sums that pass it by accumulation), so superbuckets switch layouts from flush to flush;
 # a snapshot / restore in the middle reads narrow and wide superbuckets back.  COUNT(*) + SUM and
 # COUNT(*) + MIN (whose empty slots hold the identity Long.MAX_VALUE, restored on load).
 @pytest.mark.parametrize("agg", [abi.AGG_SUM, abi.AGG_MIN, abi.AGG_MAX])
-@pytest.mark.parametrize("narrow", ["1", "0"])
+@pytest.mark.parametrize("narrow", ["2", "1", "0"])
 def test_hop_block_state_narrow_and_wide_layouts(agg, narrow, monkeypatch):
     monkeypatch.setenv("FW_HB_NARROW", narrow)
     kw = dict(window_kind=abi.WIN_HOP, size_ms=6000, slide_ms=2000, count_star_index=0,

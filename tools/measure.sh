@@ -12,9 +12,11 @@ PMC_WLS=${PMC_WLS:-"cfg2"}
 BENCH_WLS=${BENCH_WLS:-"cfg2 cfg3 cfg4 cfg5"}
 mkdir -p "$OUT/profiles"
 cd /tmp && export TMPDIR=/tmp
+if [ -z "$SKIP_DEFAULT" ]; then
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_default" -o run \
   -- python3 "$R/bench.py" > "$OUT/bench_default.json" 2> "$OUT/prof_default.log" || { tail -20 "$OUT/prof_default.log"; exit 1; }
 cat "$OUT/bench_default.json"
+fi
 for w in $PMC_WLS; do
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$w" -o run \
     -- python3 "$R/bench.py" --workload "$w" --steps 6 --warmup 1 --no-cpu-baseline --calibrate-traffic > "$OUT/pmc_fetch_$w.log" 2>&1 || { tail -20 "$OUT/pmc_fetch_$w.log"; exit 1; }

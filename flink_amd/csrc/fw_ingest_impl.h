@@ -11,10 +11,10 @@ namespace fw {
 // One workgroup of ig_block(nw, nv) threads (512 for <= 2 accumulator words, two per CU; 1024 for
 // wider accumulators, one per CU) owns a chunk of CH = block*RPT rows (4096 either way) and keeps
 // all of them in registers (row j*block + tid, coalesced column loads, every load of the chunk in
-// flight at once).  The chunk is folded in fold sub-tiles of IG_SUB rows: rows with equal (key, slice) meet
-// in an LDS slot table whose owner is the lowest row index hashing to the slot (so a hot key,
-// which occurs early, keeps its slot); the owner ends up holding the folded partial in its
-// registers.  The surviving partials are then ranked per superbucket with LDS atomics, the
+// flight at once).  The chunk is folded sub-tile by sub-tile (IG_SRPT rows per thread): rows with
+// equal (key, slice) meet in one LDS slot table for the chunk whose owner is the lowest row index
+// hashing to the slot (so a hot key, which occurs early, keeps its slot); the owner ends up holding
+// the folded partial in its registers.  The surviving partials are then ranked per superbucket with LDS atomics, the
 // per-superbucket counts are scanned, and every partial is stored at
 //     parts[slot][c*CH + start(sb) + rank]
 // so each (superbucket, chunk) cell is contiguous.  The cell table (cell_index: XCD-tiled
@@ -374,51 +374,55 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     const uint32_t valid_unfolded = valid;
     const bool do_fold = fold && !(FW_ABL(a) & AB_NO_FOLD);
     if (!do_fold) __syncthreads();  // the header and histogram are initialised (the fold's first barrier does it)
-    // ---- K3: fold equal (key, slice) rows, one 1024-row sub-tile at a time
-    if (do_fold) static_for<NSUB>([&](auto S) {
-        constexpr int s = decltype(S)::value;
-        uint32_t rh[IG_SRPT];
-        __syncthreads();  // previous sub-tile's owners are done with claim/cacc
+    // ---- K3: fold equal (key, slice) rows over the whole chunk, IG_SRPT rows per thread at a time.
+    // The slot table lives for the chunk: a slot's owner is the lowest row index hashing to it (the
+    // first occurrence -- a hot key keeps its slot), so a later sub-tile's rows fold into owners of
+    // earlier sub-tiles too; owners take their folded partials back once, after the last sub-tile.
+    if (do_fold) {
         for (int h = tid; h < SL; h += IG_BLOCK) claim[h] = 0xFFFFFFFFu;
-        __syncthreads();
-        static_for<IG_SRPT>([&](auto Q) {
-            constexpr int q = decltype(Q)::value;
-            constexpr int j = s * IG_SRPT + q;
-            rh[q] = fold_slot(rm[j], rs[j], SL);
-            if (valid & (1u << j)) atomicMin(&claim[rh[q]], (uint32_t)(j * IG_BLOCK + tid));
-        });
-        __syncthreads();
-        static_for<IG_SRPT>([&](auto Q) {  // slot owners publish their (key, slice) and partial
-            constexpr int q = decltype(Q)::value;
-            constexpr int j = s * IG_SRPT + q;
-            if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
-            ckey[rh[q]] = rk[j];
-            cslice[rh[q]] = rs[j];
+        static_for<NSUB>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            uint32_t rh[IG_SRPT];
+            __syncthreads();  // the table is reset / the previous sub-tile's folds are done
+            static_for<IG_SRPT>([&](auto Q) {
+                constexpr int q = decltype(Q)::value;
+                constexpr int j = s * IG_SRPT + q;
+                rh[q] = fold_slot(rm[j], rs[j], SL);
+                if (valid & (1u << j)) atomicMin(&claim[rh[q]], (uint32_t)(j * IG_BLOCK + tid));
+            });
+            __syncthreads();
+            static_for<IG_SRPT>([&](auto Q) {  // this sub-tile's new owners publish their (key, slice) and partial
+                constexpr int q = decltype(Q)::value;
+                constexpr int j = s * IG_SRPT + q;
+                if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
+                ckey[rh[q]] = rk[j];
+                cslice[rh[q]] = rs[j];
 #pragma unroll
-            for (int w = 0; w < NW; w++) cacc[w * SL + rh[q]] = racc[j][w];
+                for (int w = 0; w < NW; w++) cacc[w * SL + rh[q]] = racc[j][w];
+            });
+            __syncthreads();
+            static_for<IG_SRPT>([&](auto Q) {  // everyone else folds into a matching owner
+                constexpr int q = decltype(Q)::value;
+                constexpr int j = s * IG_SRPT + q;
+                const uint32_t h = rh[q];
+                if (!(valid & (1u << j)) || claim[h] == (uint32_t)(j * IG_BLOCK + tid)) return;
+                if (ckey[h] == rk[j] && cslice[h] == rs[j]) {
+#pragma unroll
+                    for (int w = 0; w < NW; w++)
+                        if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w * SL + h], racc[j][w]);
+                    valid &= ~(1u << j);
+                }
+            });
         });
         __syncthreads();
-        static_for<IG_SRPT>([&](auto Q) {  // everyone else folds into a matching owner
-            constexpr int q = decltype(Q)::value;
-            constexpr int j = s * IG_SRPT + q;
-            const uint32_t h = rh[q];
-            if (!(valid & (1u << j)) || claim[h] == (uint32_t)(j * IG_BLOCK + tid)) return;
-            if (ckey[h] == rk[j] && cslice[h] == rs[j]) {
+        static_for<RPT>([&](auto J) {  // owners take the folded partial back (slot recomputed: no registers held)
+            constexpr int j = decltype(J)::value;
+            const uint32_t h = fold_slot(rm[j], rs[j], SL);
+            if (!(valid & (1u << j)) || claim[h] != (uint32_t)(j * IG_BLOCK + tid)) return;
 #pragma unroll
-                for (int w = 0; w < NW; w++)
-                    if (w < a.wd.nw) lds_fold(a.wd.op[w], &cacc[w * SL + h], racc[j][w]);
-                valid &= ~(1u << j);
-            }
+            for (int w = 0; w < NW; w++) racc[j][w] = cacc[w * SL + h];
         });
-        __syncthreads();
-        static_for<IG_SRPT>([&](auto Q) {  // owners take the folded partial back
-            constexpr int q = decltype(Q)::value;
-            constexpr int j = s * IG_SRPT + q;
-            if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
-#pragma unroll
-            for (int w = 0; w < NW; w++) racc[j][w] = cacc[w * SL + rh[q]];
-        });
-    });
+    }
     // PF_UNIT needs a chunk in which no row folded into another: one LDS flag store per wave that folded
     if (a.narrow == 2 && do_fold && __ballot(valid != valid_unfolded) && (tid & 63) == 0) *s_folded = 1u;
     // ---- PF_PACK (runs, one integer word, no NULLs / ordinals): every push measures the key and

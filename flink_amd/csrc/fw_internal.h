@@ -35,8 +35,10 @@ constexpr int ig_block(int nw, int nv) { return (nv > 4 || nw > 2) ? 1024 : 512;
 constexpr int ig_lds(int block) { return block == 1024 ? 156 * 1024 : 78 * 1024; }  // (two 512-thread workgroups per CU)
 // the template NV of a count of loaded value columns
 constexpr int ig_nv(int nv) { return nv <= 2 ? nv : nv <= 4 ? 4 : 8; }
-// LDS fold slots per sub-tile (direct mapped; a collision just leaves the row unfolded)
-constexpr int ig_slots(int nw) { return nw <= 2 ? 1024 : nw <= 4 ? 512 : 256; }
+// LDS fold slots per chunk (direct mapped; a collision just leaves the row unfolded).  The
+// 1024-thread variants (> 2 words) have a CU's LDS to themselves: 2048 / 1024 slots (round 6; 512 /
+// 256 before, and per 2048-row sub-tile)
+constexpr int ig_slots(int nw) { return nw <= 2 ? 1024 : nw <= 4 ? 2048 : 1024; }
 constexpr int ig_fold_bytes(int nw) { return ig_slots(nw) * (4 + 8 + 8 + 8 * nw); }
 
 // ---- merge/fire (K4+K5): persistent 1024-thread workgroups, one per CU (the LDS entry table fills

@@ -41,7 +41,10 @@ _AGG = {"sum": abi.AGG_SUM, "min": abi.AGG_MIN, "max": abi.AGG_MAX, "count": abi
 _BY = ("minBy", "maxBy")
 # STRING keys (keyBy a String field): the operator interns each String to a dense int64 id -- the
 # device key -- and hands the device its String.hashCode, which routes it exactly as
-# KeyGroupRangeAssignment.assignToKeyGroup(key) does (FW_KEYHASH_PRECOMPUTED)
+# KeyGroupRangeAssignment.assignToKeyGroup(key) does (FW_KEYHASH_PRECOMPUTED).  Ids are never
+# reused: the table holds every distinct String the operator has seen (and is saved with each
+# snapshot), so its host memory grows with the stream's key cardinality, not with the live windows.
+# A stream with unbounded String cardinality should stay on the reference operator.
 _KEY = {"LONG": abi.KEYHASH_LONG, "INT": abi.KEYHASH_INT, "HOST_HASHED": abi.KEYHASH_PRECOMPUTED,
         "STRING": abi.KEYHASH_PRECOMPUTED}
 _TYPE = {"LONG": abi.T_I64, "INT": abi.T_I32, "DOUBLE": abi.T_F64}

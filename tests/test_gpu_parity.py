@@ -198,6 +198,40 @@ def test_hot_keys_fold_in_lds_cache():
     _run_both(_cfg(kw), batches, set())
 
 
+# The ingest fold keeps one slot table per chunk (round 6): rows of a later sub-tile fold into
+# owners an earlier sub-tile published, and the 1024-thread variants (3-8 words) have 2048 / 1024
+# slots.  Zipf keys put the same hot (key, slice) groups in every sub-tile of every chunk; the
+# layouts cover the 512-thread and both 1024-thread variants, NULL gates and the DOUBLE MIN/MAX word
+# groups whose fold keeps arrival order (ordinals).
+FOLD_LAYOUTS = {
+    "cfg5_4words": dict(window_kind=abi.WIN_CUMULATE, size_ms=8000, slide_ms=2000, count_star_index=0,
+                        aggs=[(abi.AGG_COUNT_STAR, 0, I64), (abi.AGG_SUM, 0, I64), (abi.AGG_MIN, 0, I64),
+                              (abi.AGG_MAX, 0, I64)]),
+    "tumble_2words": dict(window_kind=abi.WIN_TUMBLE, size_ms=4000,
+                          aggs=[(abi.AGG_SUM, 0, I64), (abi.AGG_MAX, 0, I64)]),
+    "null_double_minmax": NULL_CASES["tumble"],
+    "hop_null_double": NULL_CASES["hop"],
+}
+
+
+@pytest.mark.parametrize("name", sorted(FOLD_LAYOUTS))
+def test_chunk_fold_across_sub_tiles_matches_oracle(name):
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    kw = FOLD_LAYOUTS[name]
+    batches, nulls = [], []
+    for b in range(8):
+        n = 40000 + 977 * b  # ragged: a partial last chunk
+        keys = np.minimum(rng.zipf(1.2, n), 20000).astype(np.int64)
+        ts = 1_600_000_000_000 + b * 1500 + rng.integers(0, 1500, n)
+        dv = rng.integers(-3, 4, n).astype(np.float64)  # many ties, signed zeros
+        dv[rng.random(n) < 0.05] = -0.0
+        batches.append((keys, ts.astype(np.int64), rng.integers(-50, 50, n), dv, 1_600_000_000_000 + b * 1500 + 700))
+        nulls.append({0: (rng.random(n) < 0.1).astype(np.uint8), 1: (rng.random(n) < 0.1).astype(np.uint8)})
+    has_nulls = name.startswith(("null", "hop_null"))
+    _run_both(_cfg(kw, nullable_cols=[0, 1]) if has_nulls else _cfg(kw), batches, _double_cols(kw),
+              nulls=nulls if has_nulls else None)
+
+
 def test_int_sum_wraps_like_java():
     cfg = _cfg(dict(window_kind=abi.WIN_TUMBLE, size_ms=1000, aggs=[(abi.AGG_SUM, 0, I32), (abi.AGG_SUM, 1, I64)]),
                value_col_types=[I32, I64])

@@ -11,7 +11,7 @@ namespace fw {
 // One workgroup of ig_block(nw, nv) threads (512 for <= 2 accumulator words, two per CU; 1024 for
 // wider accumulators, one per CU) owns a chunk of CH = block*RPT rows (4096 either way) and keeps
 // all of them in registers (row j*block + tid, coalesced column loads, every load of the chunk in
-// flight at once).  The chunk is folded sub-tile by sub-tile (IG_SRPT rows per thread): rows with
+// flight at once).  The chunk is folded sub-tile by sub-tile (SRPT rows per thread): rows with
 // equal (key, slice) meet in one LDS slot table for the chunk whose owner is the lowest row index
 // hashing to the slot (so a hot key, which occurs early, keeps its slot); the owner ends up holding
 // the folded partial in its registers.  The surviving partials are then ranked per superbucket with LDS atomics, the
@@ -57,12 +57,15 @@ template <int NV, int NW, int RPT, bool X, int IG_BLOCK>
 // (launch bounds: 4 waves per SIMD, 128 VGPRs)
 __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     constexpr int CH = IG_BLOCK * RPT;
-    constexpr int NSUB = RPT / IG_SRPT;
+    // fold sub-tile: IG_SRPT rows per thread where the registers are tight (512 threads, 8 rows), the
+    // whole chunk at once for the 1024-thread variants (3 barriers per chunk instead of 7)
+    constexpr int SRPT = IG_BLOCK >= 1024 ? RPT : IG_SRPT;
+    constexpr int NSUB = RPT / SRPT;
     constexpr int NVR = NV > 0 ? NV : 1;
     constexpr int PW = 2 + NW;
     constexpr int SL = ig_slots(NW);
     constexpr bool CAN_COMPACT = NW == 1;  // compact partial rows (PF_NARROW / PF_UNIT)
-    static_assert(RPT % IG_SRPT == 0, "fold sub-tiles must tile the chunk");
+    static_assert(RPT % SRPT == 0, "fold sub-tiles must tile the chunk");
     // dynamic LDS only (16-B aligned base, G17): [header 16 words][hist: n_sb u16, padded to
     // 16 B][area: fold table, later the store stage]
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
     const uint32_t valid_unfolded = valid;
     const bool do_fold = fold && !(FW_ABL(a) & AB_NO_FOLD);
     if (!do_fold) __syncthreads();  // the header and histogram are initialised (the fold's first barrier does it)
-    // ---- K3: fold equal (key, slice) rows over the whole chunk, IG_SRPT rows per thread at a time.
+    // ---- K3: fold equal (key, slice) rows over the whole chunk, SRPT rows per thread at a time.
     // The slot table lives for the chunk: a slot's owner is the lowest row index hashing to it (the
     // first occurrence -- a hot key keeps its slot), so a later sub-tile's rows fold into owners of
     // earlier sub-tiles too; owners take their folded partials back once, after the last sub-tile.
@@ -382,18 +385,18 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
         for (int h = tid; h < SL; h += IG_BLOCK) claim[h] = 0xFFFFFFFFu;
         static_for<NSUB>([&](auto S) {
             constexpr int s = decltype(S)::value;
-            uint32_t rh[IG_SRPT];
+            uint32_t rh[SRPT];
             __syncthreads();  // the table is reset / the previous sub-tile's folds are done
-            static_for<IG_SRPT>([&](auto Q) {
+            static_for<SRPT>([&](auto Q) {
                 constexpr int q = decltype(Q)::value;
-                constexpr int j = s * IG_SRPT + q;
+                constexpr int j = s * SRPT + q;
                 rh[q] = fold_slot(rm[j], rs[j], SL);
                 if (valid & (1u << j)) atomicMin(&claim[rh[q]], (uint32_t)(j * IG_BLOCK + tid));
             });
             __syncthreads();
-            static_for<IG_SRPT>([&](auto Q) {  // this sub-tile's new owners publish their (key, slice) and partial
+            static_for<SRPT>([&](auto Q) {  // this sub-tile's new owners publish their (key, slice) and partial
                 constexpr int q = decltype(Q)::value;
-                constexpr int j = s * IG_SRPT + q;
+                constexpr int j = s * SRPT + q;
                 if (!(valid & (1u << j)) || claim[rh[q]] != (uint32_t)(j * IG_BLOCK + tid)) return;
                 ckey[rh[q]] = rk[j];
                 cslice[rh[q]] = rs[j];
@@ -401,9 +404,9 @@ __global__ __launch_bounds__(IG_BLOCK, 4) void k_ingest(IngestArgs a) {
                 for (int w = 0; w < NW; w++) cacc[w * SL + rh[q]] = racc[j][w];
             });
             __syncthreads();
-            static_for<IG_SRPT>([&](auto Q) {  // everyone else folds into a matching owner
+            static_for<SRPT>([&](auto Q) {  // everyone else folds into a matching owner
                 constexpr int q = decltype(Q)::value;
-                constexpr int j = s * IG_SRPT + q;
+                constexpr int j = s * SRPT + q;
                 const uint32_t h = rh[q];
                 if (!(valid & (1u << j)) || claim[h] == (uint32_t)(j * IG_BLOCK + tid)) return;
                 if (ckey[h] == rk[j] && cslice[h] == rs[j]) {

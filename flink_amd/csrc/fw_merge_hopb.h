@@ -139,7 +139,17 @@ __device__ __forceinline__ uint32_t hb_fire_entry(const MergeArgs& a, int64_t W,
     int prev = -2, next = -2;  // neighbouring blocks' entries, looked up on first need
     if (FW_ABL(a) & AB_M_NO_HASH) prev = next = -1;  // (diagnostic: fire without neighbour lookups)
     uint32_t nf = 0;
-    for (int j = 0; j < HB_R + n - 1; j++) {
+    // UTC: the due window ends lie in (w_old + 1, W + 1], so only the candidates j in
+    // [floor((w_old - bs) / slide), floor((W - bs + 1) / slide)] -- a superset by at most one on
+    // each side; the exact test below still decides -- need a look (about 2 + advance / slide of
+    // the 12, the rest of the loop's iterations cost as much as the windows it fires)
+    int j0 = 0, j1 = HB_R + n - 2;
+    if (w.tz.n == 0) {
+        if (W < bs) return 0;  // every candidate window end is >= bs + slide > W + 1
+        j1 = (int)min((uint64_t)j1, udiv((uint64_t)W - (uint64_t)bs + 1u, w.slice_div));
+        if (w_old >= bs) j0 = (int)min((uint64_t)(HB_R + n - 1), udiv((uint64_t)w_old - (uint64_t)bs, w.slice_div));
+    }
+    for (int j = j0; j <= j1; j++) {
         const int64_t we = wadd(bs, (int64_t)(j + 1) * w.interval);
         if (!win_fired(w, we, W) || win_fired(w, we, w_old)) continue;  // not due in this advance
         // the window's slots: j, j-1, ..., j-n+1 (newest first); < 0: previous block, >= HB_R: next

@@ -1157,15 +1157,17 @@ int state_rows_to_host(const fw_handle* h, size_t sb, int64_t n, uint64_t* out) 
     for (int64_t i = 0; i < n; i++) {
         const uint8_t* q = (const uint8_t*)(tmp.data() + (size_t)i * pwn);
         uint64_t* e = out + (size_t)i * pwe;
-        uint32_t fl;
+        uint32_t bi;
+        uint16_t fl;
         memcpy(&e[0], q, 8);
-        memcpy(&e[1], q + 8, 8);
-        memcpy(&fl, q + 16, 4);
+        memcpy(&bi, q + 8, 4);  // block index: block start = index * hb_span + offset
+        memcpy(&fl, q + 12, 2);
+        e[1] = (uint64_t)wadd((int64_t)bi * h->win.hb_span, h->win.offset);
         e[2] = fl;
-        const uint32_t mask = fl >> HB_MASK_SHIFT;
+        const uint32_t mask = (uint32_t)fl >> HB_MASK_SHIFT;
         for (int s = 0; s < HB_R; s++)
             for (int x = 0; x < nw; x++) {
-                const uint8_t* f = q + 20 + sbytes * (s * nw + x);
+                const uint8_t* f = q + HB_HDR_BYTES + sbytes * (s * nw + x);
                 int64_t v;
                 if (sbytes == 4) {
                     int32_t t;

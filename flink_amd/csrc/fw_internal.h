@@ -340,13 +340,15 @@ constexpr int KIND_DSWIN = 3;
 constexpr int KIND_HOPB = 4;  // SQL HOP, block state (fw_merge_hopb.h)
 constexpr int HB_R = 8;       // slices per HOP block entry
 // Narrow HOP block entries (k_merge_hopb write-back, per superbucket: every slot word with data fits
-// the level's width): key (8 B), block start (8 B), flags (4 B), then the HB_R * nw slot words as
-// int32 (level 1) or int16 (level 2), zero-padded to whole 8-byte words.  A slot without data -- its
-// mask bit clear -- holds the word's identity, restored on load.  One accumulator word: 11 words
-// wide, 7 at level 1, 5 at level 2; two: 19, 11, 7.
+// the level's width and every block start is (block index) * hb_span + offset with a block index
+// below 2^31): key (8 B), block index (4 B), flags (2 B: F_ACC | slot mask << 8), then the HB_R * nw
+// slot words as int32 (level 1) or int16 (level 2), zero-padded to whole 8-byte words.  A slot
+// without data -- its mask bit clear -- holds the word's identity, restored on load.  One
+// accumulator word: 11 words wide, 6 at level 1, 4 at level 2; two: 19, 10, 6.
 constexpr int HB_LEVELS = 3;  // 0: wide (3 + HB_R * nw words), 1: int32 slots, 2: int16 slots
+constexpr int HB_HDR_BYTES = 14;  // narrow entry header: key, block index, flags
 constexpr int hb_slot_bytes(int level) { return level == 1 ? 4 : 2; }
-constexpr int hb_narrow_words(int nw, int level = 1) { return (20 + hb_slot_bytes(level) * HB_R * nw + 7) / 8; }
+constexpr int hb_narrow_words(int nw, int level = 1) { return (HB_HDR_BYTES + hb_slot_bytes(level) * HB_R * nw + 7) / 8; }
 constexpr uint32_t HB_MASK_SHIFT = 8;  // block entry flag bits 8.. : slot i holds data
 
 // TimeWindowUtil.isWindowFired in the window's shift zone (UTC when tz.n == 0)

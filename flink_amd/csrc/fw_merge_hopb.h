@@ -73,13 +73,13 @@ __device__ __forceinline__ void hb_load_narrow(const MergeArgs& a, const uint64_
     uint64_t p[PN];
     load_words<PN>(src, p);
     *k = (int64_t)p[0];
-    *bs = (int64_t)p[1];
-    const uint32_t fl = (uint32_t)p[2];
+    *bs = wadd((int64_t)(uint32_t)p[1] * a.win.hb_span, a.win.offset);  // the block index
+    const uint32_t fl = (uint32_t)(p[1] >> 32) & 0xFFFFu;
     S.flag[e] = fl;
     const uint32_t mask = fl >> HB_MASK_SHIFT;
 #pragma unroll
     for (int i = 0; i < NA; i++) {
-        const int b = 20 + SB * i;  // the slot's byte offset in the entry
+        const int b = HB_HDR_BYTES + SB * i;  // the slot's byte offset in the entry
         const uint64_t raw = p[b >> 3] >> (8 * (b & 7));
         const int64_t v = SB == 4 ? (int64_t)(int32_t)(uint32_t)raw : (int64_t)(int16_t)(uint16_t)raw;
         const int w = i % NWP;
@@ -88,18 +88,18 @@ __device__ __forceinline__ void hb_load_narrow(const MergeArgs& a, const uint64_
     }
 }
 template <int NWP, int E, int L>
-__device__ __forceinline__ void hb_store_narrow(uint64_t* dst, const StateLds<HB_R * NWP, E>& S, int e, uint32_t fl) {
+__device__ __forceinline__ void hb_store_narrow(const WinDesc& w, uint64_t* dst, const StateLds<HB_R * NWP, E>& S, int e, uint32_t fl) {
     constexpr int NA = HB_R * NWP, PN = hb_narrow_words(NWP, L), SB = hb_slot_bytes(L);
     const uint32_t mask = fl >> HB_MASK_SHIFT;
     uint64_t p[PN];
 #pragma unroll
     for (int i = 0; i < PN; i++) p[i] = 0;
     p[0] = (uint64_t)S.key[e];
-    p[1] = (uint64_t)S.slice[e];
-    p[2] = (uint64_t)fl;
+    // the block index (the write-back checked that it fits 31 bits) and the 16 flag bits
+    p[1] = udiv((uint64_t)wsub(S.slice[e], w.offset), w.hb_span_div) | ((uint64_t)(fl & 0xFFFFu) << 32);
 #pragma unroll
     for (int i = 0; i < NA; i++) {
-        const int b = 20 + SB * i;
+        const int b = HB_HDR_BYTES + SB * i;
         const uint64_t v = ((mask >> (i / NWP)) & 1u) ? (S.acc[i][e] & (SB == 4 ? 0xFFFFFFFFull : 0xFFFFull)) : 0ull;
         p[b >> 3] |= v << (8 * (b & 7));
     }
@@ -411,6 +411,8 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
         for (int e = tid; e < n; e += MG_BLOCK) {
             const int64_t bs = S.slice[e];
             uint32_t mask = S.flag[e] >> HB_MASK_SHIFT;
+            // the narrow header keeps the block index in 31 bits (bs >= offset)
+            if (mask && udiv((uint64_t)wsub(bs, win.offset), win.hb_span_div) >= (1ull << 31)) fits = fits16 = false;
             int64_t first = INT64_MAX;
 #pragma unroll
             for (int i = 0; i < HB_R; i++) {
@@ -440,9 +442,9 @@ __global__ __launch_bounds__(MG_BLOCK, 4) void k_merge_hopb(MergeArgs a) {
             const int pos = wave_claim(&s_nlive);
             if (FW_ABL(a) & AB_M_NO_WB) continue;
             if (lv_out == 2) {
-                hb_store_narrow<NWP, E, 2>(so + (size_t)pos * PW2, S, e, fl);
+                hb_store_narrow<NWP, E, 2>(win, so + (size_t)pos * PW2, S, e, fl);
             } else if (lv_out == 1) {
-                hb_store_narrow<NWP, E, 1>(so + (size_t)pos * PW1, S, e, fl);
+                hb_store_narrow<NWP, E, 1>(win, so + (size_t)pos * PW1, S, e, fl);
             } else {
                 uint64_t p[PWE];
                 p[0] = (uint64_t)S.key[e];

@@ -38,7 +38,7 @@ from .._native import check, lib
 
 
 class KeyByExchange:
-    def __init__(self, key_hash_kind, max_parallelism=128, group=None):
+    def __init__(self, key_hash_kind, max_parallelism=128, group=None, force_collectives=False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -46,7 +46,11 @@ class KeyByExchange:
         self.max_p = max_parallelism
         self._ws = None
         self._cpu_group = None
-        if self.world > 1 and dist.get_backend(group) != "gloo":
+        # the packed exchange's collectives (all-to-all, valve all-reduce, overflow round) run when
+        # there is more than one subtask; force_collectives runs them for one subtask too, so the
+        # RCCL branches execute on a one-GPU box (tests/test_gpu_multirank.py)
+        self.collectives = self.world > 1 or (force_collectives and dist.is_initialized())
+        if self.collectives and dist.get_backend(group) != "gloo":
             # the watermark valve's host-side group over the same ranks (collective creation:
             # every rank builds the exchange at the same point)
             ranks = dist.get_process_group_ranks(group) if group is not None else None
@@ -240,10 +244,10 @@ class KeyByExchange:
                 o += c
             spill = torch.cat(sp).reshape(-1) if sp else torch.zeros(0, dtype=torch.int64)
             counts_h, part_done, counts_d = counts, None, counts
-        stage = key.is_cuda and p > 1 and dist.get_backend(self.group) != "nccl"
+        stage = key.is_cuda and self.collectives and dist.get_backend(self.group) != "nccl"
         mv = (lambda x: x.cpu()) if stage else (lambda x: x)
         back = (lambda x: x.to(dev)) if stage else (lambda x: x)
-        if p > 1:
+        if self.collectives:
             rc = torch.empty_like(mv(counts))
             dist.all_to_all_single(rc, mv(counts), group=self.group)
             s_ = mv(send)
@@ -258,7 +262,7 @@ class KeyByExchange:
         """One host all-reduce for the overflow decision, the watermark valve's minimum and the
         largest per-destination share."""
         wm = None if watermark is None else int(watermark)
-        if self.world == 1:
+        if not self.collectives:
             return overflow, wm, int(share)
         g = self.group if self._cpu_group is None else self._cpu_group
         # ~w (= -w - 1) reverses the int64 order with no overflow (-Long.MIN_VALUE would): MAX of ~w is ~MIN
@@ -347,7 +351,7 @@ class PackedExchange:
         t = torch.stack([(self._counts_d > self._cap).any().to(torch.int64),
                          torch.full((), ~int(watermark), dtype=torch.int64, device=dev),
                          self._counts_d.max() if self._counts_d.numel() else torch.zeros((), dtype=torch.int64, device=dev)])
-        if ex.world > 1:
+        if ex.collectives:
             if self._counts_d.is_cuda and dist.get_backend(ex.group) == "nccl":
                 dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ex.group)
             else:  # gloo moves host tensors (the one-GPU rehearsal and the CPU tests)
@@ -395,7 +399,7 @@ class PackedExchange:
         out_spill = None
         if any_over:
             ex.spill_rounds += 1
-            if ex.world == 1:
+            if not ex.collectives:
                 out_spill = self._spill[:over[0] * w] if over[0] else None
             else:
                 g = ex._cpu_group if ex._cpu_group is not None else ex.group

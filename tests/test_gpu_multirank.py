@@ -118,14 +118,17 @@ def _rows(res, n_aggs):
             for i in range(len(res["key"]))]
 
 
-def _worker(rank, port, name, out_q):
+def _worker(rank, port, name, out_q, world=WORLD, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        if backend == "nccl":  # RCCL: the device all-to-all and the device valve's all-reduce
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         from flink_amd.runtime.exchange import KeyByExchange
         from flink_amd.runtime.handle import WindowAggHandle
         from flink_amd.table.two_phase import TwoPhaseWindowAgg
@@ -133,9 +136,9 @@ def _worker(rank, port, name, out_q):
         sc = SCENARIOS[name]
         kw = sc["kw"]
         vt = kw["value_col_types"][0]
-        cfg = _cfg(kw, WORLD, rank)
+        cfg = _cfg(kw, world, rank)
         n_aggs = cfg.n_aggs
-        ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+        ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128, force_collectives=backend == "nccl")
         share_sizing = sc.get("cap") == "share"
         if share_sizing:
             ex.headroom = sc["headroom"]
@@ -157,7 +160,7 @@ def _worker(rank, port, name, out_q):
                 if px_prev is not None:
                     settle(px_prev)
                 k, t, v = (torch.from_numpy(x).to(dev) for x in _stream(sc["dist"], vt, rank, b, N_ROWS))
-                cap = None if share_sizing else ex.segment_capacity(N_ROWS, WORLD) if b % 2 == 0 else N_ROWS // (4 * WORLD)
+                cap = None if share_sizing else ex.segment_capacity(N_ROWS, world) if b % 2 == 0 else N_ROWS // (4 * world)
                 px = ex.exchange_packed_async(k, t, [v], capacity=cap)
                 h.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
                 received += int(px.recv_counts.clamp(max=px._cap).sum())
@@ -176,7 +179,7 @@ def _worker(rank, port, name, out_q):
             for b in range(N_BATCHES):
                 k, t, v = (torch.from_numpy(x).to(dev) for x in _stream(sc["dist"], vt, rank, b, N_ROWS))
                 # odd steps: segments of a quarter of the even share -> the overflow round carries the rest
-                cap = None if share_sizing else ex.segment_capacity(N_ROWS, WORLD) if b % 2 == 0 else N_ROWS // (4 * WORLD)
+                cap = None if share_sizing else ex.segment_capacity(N_ROWS, world) if b % 2 == 0 else N_ROWS // (4 * world)
                 px = ex.exchange_packed_async(k, t, [v], capacity=cap)
                 h.push_device_packed_segments(px.recv_counts, px.rows, px.row_words)
                 spill, wm = px.finish(watermark=_proposed_wm(b, rank))
@@ -218,8 +221,9 @@ def _worker(rank, port, name, out_q):
             st["error_flags"] |= tp.local.stats()["error_flags"]
             tp.close()
         torch.cuda.synchronize()
-        lo, hi = (rank * 128 + WORLD - 1) // WORLD, ((rank + 1) * 128 - 1) // WORLD
+        lo, hi = (rank * 128 + world - 1) // world, ((rank + 1) * 128 - 1) // world
         out_q.put((rank, dict(rows=rows, wms=wms, received=received, spill_rounds=ex.spill_rounds,
+                              backend=dist.get_backend(), collectives=ex.collectives,
                               late=st["num_late_records_dropped"], err=st["error_flags"], kg=(lo, hi))))
     except Exception as e:  # reported to the parent, which fails the test with it
         import traceback
@@ -235,29 +239,29 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(name):
+def _run_ranks(name, world=WORLD, backend="gloo"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, name, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, name, q, world, backend)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        res = dict(q.get(timeout=180) for _ in range(WORLD))
+        res = dict(q.get(timeout=180) for _ in range(world))
     finally:
         for p in procs:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(WORLD):
+    for r in range(world):
         assert "error" not in res[r], f"rank {r}: {res[r]['error']}"
     for p in procs:
         assert p.exitcode == 0
     return res
 
 
-def _oracle_rows(name, wms):
+def _oracle_rows(name, wms, world=WORLD):
     """One unsharded operator (parallelism 1) over the global stream and the valve's watermarks."""
     from oracle.oracle import OracleOperator
     sc = SCENARIOS[name]
@@ -266,7 +270,7 @@ def _oracle_rows(name, wms):
     op = OracleOperator(_cfg(kw, 1, 0))
     want = []
     for b in range(N_BATCHES):
-        cols = [_stream(sc["dist"], vt, r, b, N_ROWS) for r in range(WORLD)]
+        cols = [_stream(sc["dist"], vt, r, b, N_ROWS) for r in range(world)]
         op.process_batch(np.concatenate([c[0] for c in cols]), np.concatenate([c[1] for c in cols]),
                          [np.concatenate([c[2] for c in cols])])
         op.process_watermark(wms[b])
@@ -327,3 +331,42 @@ def test_two_ranks_union_equals_unsharded_oracle(name):
     _compare(got, want, double_cols, name)
     if sc["plan"] == "one":  # (two-phase: the GLOBAL operator counts late partial rows, not records)
         assert res[0]["late"] + res[1]["late"] == late
+
+
+# The RCCL branches of the exchange on hardware: one rank over the nccl backend (RCCL) on the box's one
+# GPU -- RCCL does not put two ranks on one device, so the two-rank scenarios above run over gloo.
+# force_collectives keeps the collectives a single subtask would skip: the packed all-to-all moves
+# device buffers unstaged through RCCL, the device valve's all-reduce runs in RCCL and
+# fw_advance_device reads its result, and the overflow round's device all-to-all runs too; with one
+# subtask the all-to-all is the rank's own segment, the forced-small segments still overflow, and
+# the results must equal the unsharded oracle.
+RCCL_SCENARIOS = ["one_phase_hop_device_valve", "one_phase_tumble_double_share_sizing_device_valve",
+                  "two_phase_cumulate_zipf_device_valve", "one_phase_hop"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name", RCCL_SCENARIOS)
+def test_rccl_single_rank_exchange_equals_oracle(name):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _run_ranks(name, world=1, backend="nccl")
+    assert res[0]["backend"] == "nccl" and res[0]["collectives"]  # the RCCL branches ran
+    sc = SCENARIOS[name]
+    wms = res[0]["wms"][:N_BATCHES]
+    if sc.get("valve") == "device":
+        held = [b for b in range(N_BATCHES) if wms[b] != _proposed_wm(b, 0)]
+        assert all(wms[b] == (wms[b - 1] if b else -(1 << 63)) for b in held)
+    else:
+        assert wms == [_proposed_wm(b, 0) for b in range(N_BATCHES)]
+    assert res[0]["err"] == 0
+    assert res[0]["spill_rounds"] > 0
+    if sc["plan"] == "one":
+        assert res[0]["received"] == N_BATCHES * N_ROWS
+    want, late = _oracle_rows(name, wms, world=1)
+    kw = sc["kw"]
+    double_cols = {a for a, (k, c, t) in enumerate(kw["aggs"]) if t == F64 and k in (abi.AGG_SUM, abi.AGG_AVG)}
+    assert len(want) > 1000
+    _compare(res[0]["rows"], want, double_cols, name)
+    if sc["plan"] == "one":
+        assert res[0]["late"] == late

@@ -183,6 +183,9 @@ def main():
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="rehearsal: run one rank (torch.distributed.run --nproc-per-node 1) through the N > 1 "
+                         "code path and its collectives (RCCL with --dist-backend nccl)")
     ap.add_argument("--cpu-sample", type=int, default=4 * B, help="events for the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="CPU baseline subtasks (threads), capped at the usable CPUs; 16 = the GPU box's "
@@ -241,7 +244,10 @@ def main():
         gpu = local % torch.cuda.device_count()
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
+    # --force-collectives: one rank through the N > 1 code path (process group, packed exchange and
+    # valve collectives, per-rank load), so the RCCL branches run on a one-GPU box; never the value
+    dpath = world > 1 or args.force_collectives
+    if dpath:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -275,11 +281,11 @@ def main():
 
     # ---------------- keyBy exchange (N > 1): device partition + RCCL all-to-all ------------
     from flink_amd.runtime.exchange import KeyByExchange
-    ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128)
+    ex = KeyByExchange(abi.KEYHASH_BINROW_BIGINT, 128, force_collectives=args.force_collectives)
 
     def exchange(b):
         """Untimed helper (G_b count): the plain exchange, exact row counts."""
-        if world == 1:
+        if not dpath:
             return gk[b], gt[b], gv[b]
         k, t, v = ex.exchange(gk[b], gt[b], [gv[b]] if nv else [])
         return k, t, (v[0] if nv else None)
@@ -290,7 +296,7 @@ def main():
     # and the watermark valve share one all-reduce per step
     def push_step(b, handle):
         """Ingest step b; returns the watermark to advance to (the valve's minimum over subtasks)."""
-        if world == 1:
+        if not dpath:
             if isinstance(handle, WindowAggHandle):
                 # the batches were generated and synchronised before the timed region: the C-ABI
                 # push as a JNI shim makes it, without torch stream events
@@ -452,7 +458,7 @@ def main():
         hw.close()
     h = make_op(cfg)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dpath:
         dist.barrier()
     torch.cuda.synchronize(dev)
     # per-launch kernel times over the timed region: in-kernel device-clock stamps (block 0's start
@@ -464,12 +470,12 @@ def main():
     t_issued = time.perf_counter() - t0  # host time to enqueue the K steps
     h.sync()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dpath:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     elapsed_own = elapsed
-    if world > 1:
+    if dpath:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -484,7 +490,7 @@ def main():
     # .computeKeyGroupRangeForOperatorIndex :93-106, as KeyGroupStreamPartitioner.selectChannel routes
     # them) -- and every rank's own timed wall clock; the shares sum to N * B * steps
     ranks = None
-    if world > 1:
+    if dpath:
         cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
         owned = torch.zeros(world, dtype=torch.int64, device=dev)
         kg_b = torch.empty(B, dtype=torch.int32, device=dev)
@@ -547,7 +553,7 @@ def main():
         # counters measured on this exact run shape only: same workload, GPU count and plan (files
         # written before round 6 carry neither field: tools/measure.sh ran them at N = 1, one-phase)
         if (tj.get("workload") == args.workload and tj.get("n_gpus", 1) == world
-                and tj.get("plan", "one-phase") == plan_name):
+                and tj.get("plan", "one-phase") == plan_name and not (world == 1 and dpath)):
             traffic = tj.get("k_ingest_hbm_bytes_per_launch")
             traffic_m = tj.get("k_merge_fire_hbm_bytes_per_launch")
             traffic_src = os.path.relpath(tpath, ROOT) if tpath.startswith(ROOT) else tpath
@@ -560,7 +566,7 @@ def main():
     # watermark's rows are collected into pinned host memory by fw_results_async and read
     # --e2e-depth steps later (fw_results_ready).  Reported beside the device-resident `value`, never as it.
     e2e = None
-    if world == 1 and not args.no_e2e and args.e2e_steps > 0:
+    if not dpath and not args.no_e2e and args.e2e_steps > 0:
         from concurrent.futures import ThreadPoolExecutor
         from flink_amd.runtime.handle import _np_view
         ns = min(args.e2e_steps, gk.shape[0])
@@ -668,7 +674,7 @@ def main():
                "delta32_columns": [n for i, n in enumerate(["key", "ts", "value"]) if delta_cols >> i & 1]}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not dpath and not args.no_cpu_baseline:
         try:
             host_cpus = len(os.sched_getaffinity(0))
         except AttributeError:
@@ -694,7 +700,7 @@ def main():
                        "keys_total": keys_total, "rate_per_gpu_ev_s": wl["rate"],
                        "state_per_key_hint": wl["state_per_key"],
                        "parallelism": f"key-group sharded x{world}" + (
-                           "" if world == 1 else " + RCCL all-to-all" if args.dist_backend == "nccl"
+                           "" if not dpath else " + RCCL all-to-all" if args.dist_backend == "nccl"
                            else " + gloo all-to-all (rehearsal, shared GPU)"),
                        "max_parallelism": 128, "superbuckets": st["num_superbuckets"],
                        "result_sink": {"segments": "each watermark's rows left in the merge's device slabs and "
@@ -703,7 +709,10 @@ def main():
                                        "compact": "each watermark's rows compacted into contiguous device columns "
                                                   "(fw_results_device)",
                                        "discard": "dropped (fw_results_reset)"}[args.sink],
-                       "exchange": None if world == 1 else {
+                       "rehearsal": ("one rank through the N > 1 code path (--force-collectives): its "
+                                     "all-to-all is the rank's own segment; not a scaling measurement")
+                                    if world == 1 and dpath else None,
+                       "exchange": None if not dpath else {
                            "kind": "packed padded all-to-all, segments of the previous step's agreed largest "
                                    "share + 3 % (first step: even share + 25 %)",
                            "watermark_valve": ("device all-reduce (overflow, watermark, share) -> fw_advance_device"
@@ -752,7 +761,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     h.close()
-    if world > 1:
+    if dpath:
         dist.destroy_process_group()
 
 

@@ -54,6 +54,8 @@ def lib():
         "fw_partition_packed": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, i64, vp]),
         "fw_partition_packed_spill": (i32, [vp, vp, vp, vp, i32, i64, i32, i32, i32, i64, vp, vp, vp, vp, i64, vp]),
         "fw_partition_packed_spill_dn": (i32, [vp, vp, vp, vp, i32, i64, vp, i32, i32, i32, i64, vp, vp, vp, vp, i64, vp]),
+        "fw_valve_local": (i32, [vp, i32, i64, i64, vp, vp]),
+        "fw_valve_select": (i32, [vp, vp, vp, vp]),
         "fw_advance": (i32, [vp, i64]),
         "fw_advance_device": (i32, [vp, vp]),
         "fw_flush": (i32, [vp]),
@@ -110,6 +112,7 @@ EXPORTED = ["fw_create", "fw_destroy", "fw_last_error", "fw_abi_version", "fw_de
             "fw_get_kernel_times", "fw_snapshot", "fw_restore", "fw_snapshot_key_group", "fw_restore_key_group",
             "fw_snapshot_key_group_heap", "fw_restore_key_group_heap", "fw_ds_snapshot_key_group", "fw_ds_restore_key_group", "fw_results_device_segments", "fw_key_row_hash", "fw_host_key_row_hash",
             "fw_assign_key_groups", "fw_partition_by_dest", "fw_partition_packed", "fw_partition_packed_spill", "fw_partition_packed_spill_dn", "fw_partition_workspace_bytes",
+            "fw_valve_local", "fw_valve_select",
             "fw_generate", "fw_host_key_group", "fw_host_assign_key_groups", "fw_host_window_start",
             "fw_host_next_trigger_watermark", "fw_host_time_op", "fw_late_records", "fw_first_element_events",
             "fw_push_device_key_rows", "fw_key_row_images", "fw_host_key_row_image_lengths", "fw_host_key_row_images",

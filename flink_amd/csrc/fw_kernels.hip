@@ -228,6 +228,11 @@ __global__ void k_key_groups(const int64_t* key, const int32_t* kh, int64_t n, i
 
 constexpr int PART_TILE = 4096;
 constexpr int PART_MAXP = 64;
+// value-column pointers of the partition kernels, passed by value (no per-call pointer-array copy)
+struct PartCols {
+    const uint64_t* in[FW_MAX_COLS];
+    uint64_t* out[FW_MAX_COLS];
+};
 
 __global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, const int32_t* kh, int64_t n, int32_t kind,
                                                      int32_t max_p, int32_t p, uint32_t* counts,
@@ -248,34 +253,62 @@ __global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, const i
     if (tid < p) counts[(size_t)blockIdx.x * p + tid] = h[tid];
 }
 
-// one block: offsets[blk][d] = sum_{d'<d} total(d') + sum_{b'<blk} counts[b'][d]
-__global__ __launch_bounds__(BLOCK) void k_part_scan(uint32_t* counts, int64_t nblk, int32_t p, int64_t* totals) {
-    __shared__ uint64_t tot[PART_MAXP];
+// one block: offsets[blk][d] = sum_{d'<d} total(d') + sum_{b'<blk} counts[b'][d].  Thread (seg, d)
+// sums destination d's counts over a contiguous range of tiles, the per-destination segment sums are
+// scanned in LDS, and each thread rewrites its range from its running offset (a serial loop over
+// every tile per destination took 155 us for 1024 tiles)
+constexpr int PSCAN_T = 1024;
+__global__ __launch_bounds__(PSCAN_T) void k_part_scan(uint32_t* counts, int64_t nblk, int32_t p, int64_t* totals) {
+    __shared__ uint64_t part[PSCAN_T];  // [seg][d] sums, then their exclusive prefix per destination
+    __shared__ uint64_t base[PART_MAXP];
     const int tid = threadIdx.x;
-    if (tid < p) {
-        uint64_t s = 0;
-        for (int64_t b = 0; b < nblk; b++) s += counts[b * p + tid];
-        tot[tid] = s;
+    const int S = PSCAN_T / p;  // segments per destination
+    const int d = tid % p, seg = tid / p;
+    const int64_t per = (nblk + S - 1) / S;
+    const int64_t b0 = min(nblk, (int64_t)seg * per), b1 = min(nblk, b0 + per);
+    uint64_t sum = 0;
+    if (seg < S)
+        for (int64_t b = b0; b < b1; b++) sum += counts[b * p + d];
+    part[tid] = sum;
+    __syncthreads();
+    // inclusive scan of each destination's segment sums (stride p: part[seg * p + d]), log2(S) rounds
+    for (int off = p; off < S * p; off <<= 1) {
+        const uint64_t v = (tid < S * p && tid >= off) ? part[tid - off] : 0;
+        __syncthreads();
+        if (tid < S * p) part[tid] += v;
+        __syncthreads();
+    }
+    if (tid < p) {  // destination tid's total: its last segment's inclusive sum
+        const uint64_t tot = part[(S - 1) * p + tid];
+        totals[tid] = (int64_t)tot;
+        base[tid] = tot;
+    }
+    if (seg < S) sum = part[tid] - sum;  // this segment's exclusive offset within its destination
+    __syncthreads();
+    if (tid == 0) {  // destinations' bases: the totals of the destinations before them
+        uint64_t r = 0;
+        for (int x = 0; x < p; x++) {
+            const uint64_t t = base[x];
+            base[x] = r;
+            r += t;
+        }
     }
     __syncthreads();
-    if (tid < p) {
-        uint64_t base = 0;
-        for (int d = 0; d < tid; d++) base += tot[d];
-        uint64_t run = base;
-        for (int64_t b = 0; b < nblk; b++) {
-            const uint32_t v = counts[b * p + tid];
-            counts[b * p + tid] = (uint32_t)run;  // fits: n < 2^32 per call
+    if (seg < S) {
+        uint64_t run = base[d] + sum;
+        for (int64_t b = b0; b < b1; b++) {
+            const uint32_t v = counts[b * p + d];
+            counts[b * p + d] = (uint32_t)run;  // fits: n < 2^32 per call
             run += v;
         }
-        totals[tid] = (int64_t)tot[tid];
     }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, const int32_t* kh, const int64_t* ts,
-                                                        const uint64_t* const* vals,
+                                                        PartCols cols,
                                                         int32_t ncols, int64_t n, int32_t kind, int32_t max_p,
                                                         int32_t p, const uint32_t* offsets, int64_t* okey, int64_t* ots,
-                                                        uint64_t* const* ovals, int64_t* orows = nullptr,
+                                                        int64_t* orows = nullptr,
                                                         int64_t seg_len = 0, const int64_t* totals = nullptr,
                                                         int64_t* spill = nullptr, const int64_t* n_dev = nullptr) {
     if (n_dev) n = min(n, *n_dev);
@@ -337,12 +370,12 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
             if (o) {
                 o[0] = k;
                 o[1] = ts[i];
-                for (int c = 0; c < ncols; c++) o[2 + c] = (int64_t)vals[c][i];
+                for (int c = 0; c < ncols; c++) o[2 + c] = (int64_t)cols.in[c][i];
             }
         } else if (d >= 0) {
             okey[pos] = k;
             ots[pos] = ts[i];
-            for (int c = 0; c < ncols; c++) ovals[c][pos] = vals[c][i];
+            for (int c = 0; c < ncols; c++) cols.out[c][pos] = cols.in[c][i];
         }
         __syncthreads();  // h updated before the next pass reads it; wc free to overwrite
     }
@@ -461,22 +494,17 @@ extern "C" int fw_partition_by_dest(const int64_t* d_key, const int32_t* d_key_h
     }
     const int64_t nblk = (n + PART_TILE - 1) / PART_TILE;
     uint32_t* counts = (uint32_t*)d_workspace;
-    // value-column pointer arrays live in the workspace tail (device-visible)
-    const uint64_t** dv = (const uint64_t**)((char*)d_workspace + nblk * parallelism * 4);
-    dv = (const uint64_t**)(((uintptr_t)dv + 15) & ~(uintptr_t)15);
-    uint64_t** dov = (uint64_t**)(dv + FW_MAX_COLS);
-    const void* hv[2 * FW_MAX_COLS] = {nullptr};
+    PartCols pc{};
     for (int c = 0; c < n_cols; c++) {
-        hv[c] = d_values[c];
-        hv[FW_MAX_COLS + c] = d_out_values[c];
+        pc.in[c] = (const uint64_t*)d_values[c];
+        pc.out[c] = (uint64_t*)d_out_values[c];
     }
-    if (hipMemcpyAsync(dv, hv, sizeof(hv), hipMemcpyHostToDevice, s) != hipSuccess) return FW_E_DEVICE;
     hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, n, key_hash_kind,
                        max_parallelism, parallelism, counts);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(BLOCK), 0, s, counts, nblk, parallelism, d_counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PSCAN_T), 0, s, counts, nblk, parallelism, d_counts);
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, d_ts,
-                       (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
-                       d_out_key, d_out_ts, (uint64_t* const*)dov);
+                       pc, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
+                       d_out_key, d_out_ts);
     return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
 }
 
@@ -530,18 +558,51 @@ static int partition_packed(const int64_t* d_key, const int32_t* d_key_hash, con
     }
     const int64_t nblk = (n + PART_TILE - 1) / PART_TILE;
     uint32_t* counts = (uint32_t*)d_workspace;
-    const uint64_t** dv = (const uint64_t**)((char*)d_workspace + nblk * parallelism * 4);
-    dv = (const uint64_t**)(((uintptr_t)dv + 15) & ~(uintptr_t)15);
-    const void* hv[2 * FW_MAX_COLS] = {nullptr};
-    for (int c = 0; c < n_cols; c++) hv[c] = d_values[c];
-    if (hipMemcpyAsync(dv, hv, sizeof(hv), hipMemcpyHostToDevice, s) != hipSuccess) return FW_E_DEVICE;
+    PartCols pc{};
+    for (int c = 0; c < n_cols; c++) pc.in[c] = (const uint64_t*)d_values[c];
     hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, n, key_hash_kind,
                        max_parallelism, parallelism, counts, d_n);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(BLOCK), 0, s, counts, nblk, parallelism, d_counts);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(PSCAN_T), 0, s, counts, nblk, parallelism, d_counts);
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nblk), dim3(BLOCK), 0, s, d_key, d_key_hash, d_ts,
-                       (const uint64_t* const*)dv, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
-                       (int64_t*)nullptr, (int64_t*)nullptr, (uint64_t* const*)nullptr, d_out_rows, seg_len,
+                       pc, n_cols, n, key_hash_kind, max_parallelism, parallelism, counts,
+                       (int64_t*)nullptr, (int64_t*)nullptr, d_out_rows, seg_len,
                        (const int64_t*)d_counts, d_spill_rows, d_n);
+    return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
+}
+
+// Device watermark valve (PackedExchange.finish_device): the subtask's [overflow flag, ~watermark,
+// largest per-destination share] in one kernel, and after the all-reduce the valve's watermark in
+// another (a dozen small torch kernels before, ~55 us per step)
+__global__ void k_valve_local(const int64_t* counts, int32_t p, int64_t cap, int64_t watermark, int64_t* out3) {
+    const int tid = threadIdx.x;  // one wave: p <= PART_MAXP = 64
+    const int64_t c = tid < p ? counts[tid] : 0;
+    int64_t m = c;
+    uint64_t over = __ballot(tid < p && c > cap);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) m = max(m, (int64_t)__shfl_xor(m, d, 64));
+    if (tid == 0) {
+        out3[0] = over != 0;
+        out3[1] = ~watermark;  // bitwise NOT reverses the int64 order (Long.MIN_VALUE travels too)
+        out3[2] = m;
+    }
+}
+__global__ void k_valve_select(const int64_t* agreed3, const int64_t* prev, int64_t* wm) {
+    if (threadIdx.x == 0) *wm = agreed3[0] > 0 ? (prev ? *prev : INT64_MIN) : ~agreed3[1];
+}
+
+extern "C" int fw_valve_local(const int64_t* d_counts, int32_t parallelism, int64_t cap, int64_t watermark,
+                              int64_t* d_out3, void* stream) {
+    if (parallelism <= 0 || parallelism > PART_MAXP || !d_counts || !d_out3) return FW_E_INVALID;
+    hipLaunchKernelGGL(k_valve_local, dim3(1), dim3(64), 0, (hipStream_t)stream, d_counts, parallelism, cap, watermark,
+                       d_out3);
+    return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
+}
+
+extern "C" int fw_valve_select(const int64_t* d_agreed3, const int64_t* d_prev_watermark, int64_t* d_watermark,
+                               void* stream) {
+    if (!d_agreed3 || !d_watermark) return FW_E_INVALID;
+    hipLaunchKernelGGL(k_valve_select, dim3(1), dim3(64), 0, (hipStream_t)stream, d_agreed3, d_prev_watermark,
+                       d_watermark);
     return hipGetLastError() == hipSuccess ? FW_OK : FW_E_DEVICE;
 }
 

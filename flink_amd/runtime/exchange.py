@@ -348,9 +348,14 @@ class PackedExchange:
         exchange (it also agrees on the next device-counted segment size)."""
         ex = self.ex
         dev = self._counts_d.device
-        t = torch.stack([(self._counts_d > self._cap).any().to(torch.int64),
-                         torch.full((), ~int(watermark), dtype=torch.int64, device=dev),
-                         self._counts_d.max() if self._counts_d.numel() else torch.zeros((), dtype=torch.int64, device=dev)])
+        if self._counts_d.is_cuda and 0 < self._counts_d.numel() <= 64:  # one kernel for the three words
+            t = torch.empty(3, dtype=torch.int64, device=dev)
+            check(lib().fw_valve_local(self._counts_d.data_ptr(), self._counts_d.numel(), int(self._cap), int(watermark),
+                                       t.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+        else:
+            t = torch.stack([(self._counts_d > self._cap).any().to(torch.int64),
+                             torch.full((), ~int(watermark), dtype=torch.int64, device=dev),
+                             self._counts_d.max() if self._counts_d.numel() else torch.zeros((), dtype=torch.int64, device=dev)])
         if ex.collectives:
             if self._counts_d.is_cuda and dist.get_backend(ex.group) == "nccl":
                 dist.all_reduce(t, op=dist.ReduceOp.MAX, group=ex.group)
@@ -366,7 +371,12 @@ class PackedExchange:
             self._agreed_h.copy_(t, non_blocking=True)
             self._agreed_ev = torch.cuda.Event()
             self._agreed_ev.record(torch.cuda.current_stream(dev))
-        if prev_watermark is None:  # nothing advanced yet: an overflowing first step holds at Long.MIN_VALUE
+        if t.is_cuda:  # nothing advanced yet (prev None): an overflowing first step holds at Long.MIN_VALUE
+            wm = torch.empty(1, dtype=torch.int64, device=dev)
+            check(lib().fw_valve_select(t.data_ptr(), None if prev_watermark is None else prev_watermark.data_ptr(),
+                                        wm.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+            return wm
+        if prev_watermark is None:
             prev_watermark = torch.full((1,), -(1 << 63), dtype=torch.int64, device=dev)
         return torch.where(t[0:1] > 0, prev_watermark, torch.bitwise_not(t[1:2]))
 

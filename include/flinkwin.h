@@ -634,6 +634,17 @@ int fw_partition_packed_spill_dn(const int64_t* d_key, const int32_t* d_key_hash
                                  int32_t key_hash_kind, int32_t max_parallelism, int32_t parallelism, int64_t seg_len,
                                  int64_t* d_out_rows, int64_t* d_spill_rows, int64_t* d_counts, void* d_workspace,
                                  int64_t workspace_bytes, void* stream);
+/* The device watermark valve (StatusWatermarkValve.java:153, the min over input channels) around one
+   all-reduce (MAX) of three int64 words per subtask.  fw_valve_local writes this subtask's words:
+   [d_counts[d] > cap for any destination d, ~watermark (bitwise NOT reverses the int64 order), the
+   largest d_counts[d]] (parallelism <= 64).  After the all-reduce, fw_valve_select writes the valve's
+   watermark: the previous one (*d_prev_watermark, or Long.MIN_VALUE when NULL) while any subtask's
+   segments overflowed -- its overflow round must arrive before the watermark passes it -- else the
+   minimum, ~agreed[1].  fw_advance_device reads it from device memory.  Both are stream-ordered and
+   never wait on the host. */
+int fw_valve_local(const int64_t* d_counts, int32_t parallelism, int64_t cap, int64_t watermark, int64_t* d_out3,
+                   void* stream);
+int fw_valve_select(const int64_t* d_agreed3, const int64_t* d_prev_watermark, int64_t* d_watermark, void* stream);
 
 /* Synthetic Nexmark-shaped generator: event i in [i0, i0+n). */
 typedef struct {

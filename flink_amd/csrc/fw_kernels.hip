@@ -238,17 +238,25 @@ __global__ __launch_bounds__(BLOCK) void k_part_hist(const int64_t* key, const i
                                                      int32_t max_p, int32_t p, uint32_t* counts,
                                                      const int64_t* n_dev = nullptr) {
     __shared__ uint32_t h[PART_MAXP];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     if (n_dev) n = min(n, *n_dev);  // a row count known only on the device (<= the launch's n)
     if (tid < PART_MAXP) h[tid] = 0;
     __syncthreads();
+    // counted per wave with ballots (lane d keeps destination d's count): one LDS add per wave and
+    // destination instead of a same-address LDS atomic per row
+    uint32_t mine = 0;
     const int64_t b = (int64_t)blockIdx.x * PART_TILE;
-    for (int j = tid; j < PART_TILE; j += BLOCK) {
-        const int64_t i = b + j;
-        if (i >= n) break;
-        const int32_t g = key_group_for_hash(java_key_hash(kind, key[i], kh ? kh[i] : 0), max_p);
-        atomicAdd(&h[operator_for_key_group(max_p, p, g)], 1u);
+    for (int j = tid - lane; j < PART_TILE; j += BLOCK) {
+        const int64_t i = b + j + lane;
+        int32_t d = -1;
+        if (j + lane < PART_TILE && i < n)
+            d = operator_for_key_group(max_p, p, key_group_for_hash(java_key_hash(kind, key[i], kh ? kh[i] : 0), max_p));
+        for (int dd = 0; dd < p; dd++) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(d == dd));
+            if (lane == dd) mine += c;
+        }
     }
+    if (lane < p && mine) atomicAdd(&h[lane], mine);
     __syncthreads();
     if (tid < p) counts[(size_t)blockIdx.x * p + tid] = h[tid];
 }

@@ -342,14 +342,28 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
     }
     const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t b = (int64_t)blockIdx.x * PART_TILE;
+    // every column of a pass is loaded one pass ahead (the next pass's loads are in flight while this
+    // pass ranks, waits at its barriers and stores): one exposed load round trip per block, not two
+    // per pass
+    int64_t ck = 0, ct = 0, nk = 0, nt = 0;
+    int32_t ch = 0, nh = 0;
+    uint64_t cv[FW_MAX_COLS], nv[FW_MAX_COLS];
+    auto load_pass = [&](int64_t i, int64_t& k_, int64_t& t_, int32_t& h_, uint64_t (&v_)[FW_MAX_COLS]) {
+        if (i >= n) return;
+        k_ = key[i];
+        t_ = ts[i];
+        h_ = kh ? kh[i] : 0;
+#pragma unroll
+        for (int c = 0; c < FW_MAX_COLS; c++)
+            if (c < ncols) v_[c] = cols.in[c][i];
+    };
+    load_pass(b + tid, ck, ct, ch, cv);
     for (int j0 = 0; j0 < PART_TILE; j0 += BLOCK) {
         const int64_t i = b + j0 + tid;
+        if (j0 + BLOCK < PART_TILE) load_pass(i + BLOCK, nk, nt, nh, nv);
         int32_t d = -1;
-        int64_t k = 0;
-        if (i < n) {
-            k = key[i];
-            d = operator_for_key_group(max_p, p, key_group_for_hash(java_key_hash(kind, k, kh ? kh[i] : 0), max_p));
-        }
+        const int64_t k = ck;
+        if (i < n) d = operator_for_key_group(max_p, p, key_group_for_hash(java_key_hash(kind, k, ch), max_p));
         uint32_t rank = 0;
         for (int dd = 0; dd < p; dd++) {
             const uint64_t m = __ballot(d == dd);
@@ -377,15 +391,24 @@ __global__ __launch_bounds__(BLOCK) void k_part_scatter(const int64_t* key, cons
                                       : nullptr;
             if (o) {
                 o[0] = k;
-                o[1] = ts[i];
-                for (int c = 0; c < ncols; c++) o[2 + c] = (int64_t)cols.in[c][i];
+                o[1] = ct;
+#pragma unroll
+                for (int c = 0; c < FW_MAX_COLS; c++)
+                    if (c < ncols) o[2 + c] = (int64_t)cv[c];
             }
         } else if (d >= 0) {
             okey[pos] = k;
-            ots[pos] = ts[i];
-            for (int c = 0; c < ncols; c++) cols.out[c][pos] = cols.in[c][i];
+            ots[pos] = ct;
+#pragma unroll
+            for (int c = 0; c < FW_MAX_COLS; c++)
+                if (c < ncols) cols.out[c][pos] = cv[c];
         }
         __syncthreads();  // h updated before the next pass reads it; wc free to overwrite
+        ck = nk;
+        ct = nt;
+        ch = nh;
+#pragma unroll
+        for (int c = 0; c < FW_MAX_COLS; c++) cv[c] = nv[c];
     }
 }
 
